@@ -1,0 +1,162 @@
+/*
+ * klf.h — C ABI of the MI355X log-filter engine (libklf.so).
+ *
+ * This is the seam klogs' Go host binds through cgo.  It replaces
+ * the byte sink `writeLogToDisk(logs io.ReadCloser, logFile *os.File)`
+ * (/root/reference/cmd/root.go:359-374, called from streamLog at :337) for streams the
+ * host now fetches with Timestamps=true and without SinceSeconds/TailLines
+ * (getLopOpts, cmd/root.go:201-221).  The filtering kubelet used to do server-side
+ * (k8s v1.30.3 logs.go ReadLogs / tail.go FindTailLineStartIndex) runs here, on the GPU,
+ * with the exact semantics of SPEC.md.
+ *
+ * Conventions: every function returns 0 (KLF_OK) or a negative KLF_E* code; no C++
+ * types, no HIP types (streams are passed as void*).  Pointers handed in are not
+ * retained after return unless stated (cgo pointer rules).  Views handed out stay valid
+ * until the owning object is freed.
+ *
+ * Threading: klf_stage may be called concurrently for DIFFERENT stream ids (one
+ * goroutine per container stream, cmd/root.go:249/:261); everything else is
+ * single-caller per engine.
+ */
+#ifndef KLF_H
+#define KLF_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes ---------------------------------------------------------------- */
+#define KLF_OK 0
+#define KLF_EINVAL -1      /* bad argument (null pointer, bad id, tail < -1, ...)      */
+#define KLF_ENOMEM -2      /* host or device allocation failed                          */
+#define KLF_EHIP -3        /* a HIP runtime call failed (no device, launch error, ...)  */
+#define KLF_EPATTERN -4    /* a --match pattern is outside the supported RE2 subset     */
+#define KLF_ETOOBIG -5     /* pattern set exceeds engine limits                         */
+#define KLF_ESTATE -6      /* call out of order (e.g. stage after run without reset)    */
+
+/* ---- instants ------------------------------------------------------------------- */
+/* An absolute UTC instant: seconds since the Unix epoch + nanoseconds in [0, 1e9).
+ * Comparisons are lexicographic (Go time.Time.Before). */
+typedef struct klf_time {
+  int64_t sec;
+  int32_t nsec;
+  int32_t _reserved;
+} klf_time;
+
+/* Go's zero time.Time, 0001-01-01T00:00:00Z: kubelet's `since` when SinceSeconds is
+ * unset (logs.go NewLogOptions); pass it for "no --since". */
+#define KLF_GO_ZERO_TIME_SEC (-62135596800LL)
+
+/* ---- patterns ------------------------------------------------------------------- */
+#define KLF_PAT_LITERAL 0 /* --grep: Go bytes.Contains(content, p)                      */
+#define KLF_PAT_REGEX 1   /* --match: Go regexp.Match(p, content), SPEC.md S5 subset     */
+
+typedef struct klf_pattern {
+  const uint8_t* bytes;
+  uint32_t len;
+  uint32_t kind; /* KLF_PAT_* */
+} klf_pattern;
+
+/* ---- engine --------------------------------------------------------------------- */
+typedef struct klf_config {
+  int32_t device;          /* HIP device ordinal (one process per GPU)                 */
+  uint32_t n_patterns;     /* OR'ed; 0 = no grep stage                                 */
+  const klf_pattern* patterns;
+  void* hip_stream;        /* hipStream_t to launch on; NULL = engine-owned stream      */
+  uint64_t staging_hint;   /* expected total staged bytes (pre-reserve), 0 = none       */
+} klf_config;
+
+typedef struct klf_engine klf_engine;
+
+/* Compiles the pattern set once (replaces nothing in the reference: --grep/--match are
+ * new flags added at cmd/root.go:485-497). */
+int klf_open(const klf_config* cfg, klf_engine** out);
+void klf_close(klf_engine* e);
+/* Human-readable detail of the last error on this engine (e.g. the pattern error). */
+const char* klf_last_error(const klf_engine* e);
+const char* klf_strerror(int code);
+
+/* ---- host staging path (what the cgo glue calls) -------------------------------- */
+/* Appends n bytes of stream `stream_id`'s body (chunks arrive in order).  Replaces the
+ * io.Copy in writeLogToDisk (cmd/root.go:366).  Ids are dense, 0-based, caller-chosen
+ * (the stream-table order of getPodLogs, cmd/root.go:240-262). */
+int klf_stage(klf_engine* e, uint32_t stream_id, const uint8_t* p, size_t n);
+/* Declares stream ids [0, n_streams) (streams never staged are empty). */
+int klf_set_streams(klf_engine* e, uint32_t n_streams);
+/* Drops all staged bytes (engine and compiled patterns stay). */
+int klf_reset(klf_engine* e);
+
+typedef struct klf_filter {
+  klf_time since;   /* lines with ts.Before(since) are dropped (S3)                    */
+  int64_t tail;     /* -1 = all, else >= 0 (S4)                                        */
+  uint32_t flags;   /* reserved, 0                                                     */
+  uint32_t _reserved;
+} klf_filter;
+
+typedef struct klf_counts {
+  uint64_t lines;      /* all lines (a trailing fragment counts)                       */
+  uint64_t parsed;     /* lines with a valid RFC3339Nano prefix                       */
+  uint64_t since_ok;   /* parsed lines with ts >= since                               */
+  uint64_t matched;    /* |G|: matching parsed lines (all lines without patterns)     */
+  uint64_t selected;   /* emitted lines                                               */
+  uint64_t out_bytes;  /* emitted bytes                                               */
+} klf_counts;
+
+typedef struct klf_result klf_result;
+
+/* Runs the whole filter over the staged streams (H2D, kernels, counts D2H).  Called
+ * once after wg.Wait() (cmd/root.go:470). */
+int klf_run(klf_engine* e, const klf_filter* f, klf_result** out);
+
+/* ---- device-resident path (bench / callers that already hold bytes in HBM) ------- */
+/* Device layout helper: segment base offsets (256-B aligned, in stream order) and the
+ * total device bytes to allocate (includes tail slack the kernels may over-read). */
+int klf_layout(uint32_t n_streams, const uint64_t* lens, uint64_t* seg_base,
+               uint64_t* total_alloc);
+/* Runs over streams already laid out in device memory at d_bytes + seg_base[i]
+ * (d_bytes must be a device allocation of >= total_alloc bytes from klf_layout). */
+int klf_run_device(klf_engine* e, const uint8_t* d_bytes, uint32_t n_streams,
+                   const uint64_t* seg_base, const uint64_t* lens, const klf_filter* f,
+                   klf_result** out);
+
+/* ---- results -------------------------------------------------------------------- */
+/* Selected bytes of one stream (host view, D2H on first access). */
+int klf_result_stream(klf_result* r, uint32_t stream_id, const uint8_t** bytes,
+                      uint64_t* len, klf_counts* counts);
+/* Line-start offsets of one stream: n_lines+1 u64 (last = stream length). */
+int klf_result_lines(klf_result* r, uint32_t stream_id, const uint64_t** off,
+                     uint64_t* n_lines);
+/* Match bitmap of one stream (bit l LSB-first in byte l>>3); *nbytes = ceil(lines/8).
+ * Returns KLF_EINVAL when the engine has no patterns. */
+int klf_result_match_bits(klf_result* r, uint32_t stream_id, const uint8_t** bits,
+                          uint64_t* nbytes);
+/* Device views (no copy): the concatenated output and the stream's [off, len) in it. */
+int klf_result_device_out(klf_result* r, uint32_t stream_id, const uint8_t** d_out,
+                          uint64_t* off, uint64_t* len);
+/* Per-stage device time of the run in ms, HIP events on the launch stream:
+ * [0] scan kernel (newline + line index + timestamp + since + fused literal grep),
+ * [1] general pattern matcher, [2] counts + tail + window prefix, [3] compaction,
+ * [4] total device time, [5] workspace memsets.  n = number of entries written. */
+int klf_result_timing(const klf_result* r, double* ms, uint32_t cap, uint32_t* n);
+/* Totals across streams. */
+int klf_result_totals(const klf_result* r, klf_counts* totals);
+void klf_result_free(klf_result* r);
+
+/* ---- host-side helpers mirroring cmd/root.go (no GPU needed) ---------------------- */
+/* Go time.Parse(time.RFC3339Nano, s) restated (SPEC.md S2); 0 = ok. */
+int klf_parse_rfc3339nano(const uint8_t* s, size_t n, klf_time* out);
+
+/* ---- test hooks (host only, no GPU): the compiled pattern tables run on the CPU ---- */
+/* Compiles `pats` and reports the matcher mode: 0 none, 1 never, 2 all, 3 single
+ * literal (fused scan), 4 general (AC + Glushkov).  err receives the compile message. */
+int klf_debug_compile(const klf_pattern* pats, uint32_t n, uint32_t* mode, char* err, size_t err_cap);
+/* Runs the compiled tables (the exact recurrences the GPU matcher runs) on one content. */
+int klf_debug_match(const klf_pattern* pats, uint32_t n, const uint8_t* content, size_t len, int* match);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* KLF_H */

@@ -1,0 +1,612 @@
+// klf_engine.cpp — the C ABI of include/klf.h: staging, device workspace, the run,
+// result views.  One engine = one GPU = one HIP stream (one process per GPU; the
+// multi-GPU split happens above, in the host, by stream sharding — DESIGN.md §5).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/klf.h"
+#include "klf_kernels.hpp"
+#include "klf_patterns.hpp"
+#include "klf_ts.hpp"
+
+using klf::SegDesc;
+using klf::SegOut;
+
+namespace {
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  hipError_t ensure(size_t bytes) {
+    if (bytes <= cap && p) return hipSuccess;
+    if (p) { (void)hipFree(p); p = nullptr; cap = 0; }
+    size_t want = std::max<size_t>(bytes, 256);
+    hipError_t e = hipMalloc(&p, want);
+    if (e == hipSuccess) cap = want;
+    return e;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+  template <class T>
+  T* as() const { return static_cast<T*>(p); }
+};
+
+uint64_t align_up(uint64_t x, uint64_t a) { return (x + a - 1) / a * a; }
+
+}  // namespace
+
+struct klf_engine {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  bool own_stream = false;
+  int num_cus = 256;
+  klf::CompiledSet cs;
+  std::string err;
+  uint64_t gen = 0;
+  // staging (host path)
+  std::mutex mu;
+  std::vector<std::vector<uint8_t>> staged;
+  // device pattern tables
+  DevBuf d_lit, d_ac_class, d_ac_next, d_ac_accept, d_rx_class, d_rx_b, d_rx_follow, d_rx_vec, d_rx_flags;
+  klf::DevPatterns dpats;
+  // workspace
+  DevBuf d_batch, d_segs, d_status, d_cstatus, d_counters, d_line_off, d_meta, d_bits, d_tile_cnt,
+      d_segout, d_wpre, d_out;
+  hipEvent_t ev[6] = {};
+};
+
+struct klf_result {
+  klf_engine* e = nullptr;
+  uint64_t gen = 0;
+  uint32_t n_streams = 0;
+  std::vector<int64_t> seg_of;       // stream id -> segment (-1 = empty stream)
+  std::vector<SegOut> so;            // per segment
+  std::vector<uint64_t> seg_base;    // per segment (device byte offset)
+  bool has_bits = false;
+  uint64_t total_lines = 0, total_out = 0;
+  double ms[6] = {0, 0, 0, 0, 0, 0};
+  // lazily filled host copies
+  bool have_out = false, have_lines = false, have_bits = false;
+  std::vector<uint8_t> out;
+  std::vector<uint64_t> line_off;
+  std::vector<uint32_t> bits;
+  std::vector<std::vector<uint8_t>> stream_bits;
+  std::vector<uint8_t> have_stream_bits;
+};
+
+static int set_err(klf_engine* e, int code, const std::string& m) {
+  if (e) e->err = m;
+  return code;
+}
+static int hip_err(klf_engine* e, hipError_t h, const char* where) {
+  return set_err(e, KLF_EHIP, std::string(where) + ": " + hipGetErrorString(h));
+}
+#define HIPCHK(e, x, where) do { hipError_t _h = (x); if (_h != hipSuccess) return hip_err(e, _h, where); } while (0)
+
+extern "C" const char* klf_strerror(int code) {
+  switch (code) {
+    case KLF_OK: return "ok";
+    case KLF_EINVAL: return "invalid argument";
+    case KLF_ENOMEM: return "out of memory";
+    case KLF_EHIP: return "HIP runtime error";
+    case KLF_EPATTERN: return "pattern outside the supported RE2 subset";
+    case KLF_ETOOBIG: return "pattern set exceeds engine limits";
+    case KLF_ESTATE: return "call out of order";
+    default: return "unknown error";
+  }
+}
+
+extern "C" const char* klf_last_error(const klf_engine* e) { return e ? e->err.c_str() : ""; }
+
+template <class T>
+static hipError_t upload(DevBuf& b, const std::vector<T>& v, hipStream_t st) {
+  hipError_t h = b.ensure(std::max<size_t>(v.size() * sizeof(T), 16));
+  if (h != hipSuccess || v.empty()) return h;
+  h = hipMemcpyAsync(b.p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice, st);
+  if (h != hipSuccess) return h;
+  return hipStreamSynchronize(st);
+}
+
+extern "C" int klf_open(const klf_config* cfg, klf_engine** out) {
+  if (!cfg || !out || (cfg->n_patterns && !cfg->patterns)) return KLF_EINVAL;
+  *out = nullptr;
+  auto* e = new (std::nothrow) klf_engine();
+  if (!e) return KLF_ENOMEM;
+  // 1) patterns (host only; errors surface before any device work)
+  std::vector<std::vector<uint8_t>> pats;
+  std::vector<uint32_t> kinds;
+  for (uint32_t i = 0; i < cfg->n_patterns; ++i) {
+    const klf_pattern& p = cfg->patterns[i];
+    if (p.len && !p.bytes) { delete e; return KLF_EINVAL; }
+    pats.emplace_back(p.bytes, p.bytes + p.len);
+    kinds.push_back(p.kind);
+  }
+  int code = KLF_OK;
+  std::string err;
+  if (!klf::compile_set(pats, kinds, e->cs, err, code)) {
+    // keep the engine alive so the caller can read klf_last_error; report failure
+    e->err = err;
+    *out = e;
+    return code;
+  }
+  // 2) device
+  e->device = cfg->device;
+  hipError_t h = hipSetDevice(cfg->device);
+  if (h != hipSuccess) { e->err = std::string("hipSetDevice: ") + hipGetErrorString(h); *out = e; return KLF_EHIP; }
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, cfg->device) == hipSuccess && prop.multiProcessorCount > 0)
+    e->num_cus = prop.multiProcessorCount;
+  if (cfg->hip_stream) {
+    e->stream = static_cast<hipStream_t>(cfg->hip_stream);
+  } else {
+    h = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking);
+    if (h != hipSuccess) { e->err = "hipStreamCreate failed"; *out = e; return KLF_EHIP; }
+    e->own_stream = true;
+  }
+  for (auto& x : e->ev) {
+    h = hipEventCreate(&x);
+    if (h != hipSuccess) { e->err = "hipEventCreate failed"; *out = e; return KLF_EHIP; }
+  }
+  // 3) pattern tables to the device
+  const auto& cs = e->cs;
+  hipStream_t st = e->stream;
+  if (cs.mode == klf::CompiledSet::kLiteral1) {
+    h = upload(e->d_lit, cs.literal, st);
+    if (h != hipSuccess) { *out = e; return hip_err(e, h, "upload literal"); }
+  } else if (cs.mode == klf::CompiledSet::kGeneral) {
+    klf::DevPatterns& P = e->dpats;
+    if (cs.ac_states) {
+      if ((h = upload(e->d_ac_class, cs.ac_class, st)) != hipSuccess ||
+          (h = upload(e->d_ac_next, cs.ac_next, st)) != hipSuccess ||
+          (h = upload(e->d_ac_accept, cs.ac_accept, st)) != hipSuccess) {
+        *out = e;
+        return hip_err(e, h, "upload AC tables");
+      }
+      P.ac_class = e->d_ac_class.as<uint8_t>();
+      P.ac_next = e->d_ac_next.as<uint32_t>();
+      P.ac_accept = e->d_ac_accept.as<uint8_t>();
+      P.ac_states = cs.ac_states;
+      P.ac_classes = cs.ac_classes;
+    }
+    if (cs.rx_count) {
+      std::vector<uint64_t> vec;  // first | last | init0 | end, each [rx_count]
+      vec.insert(vec.end(), cs.rx_first.begin(), cs.rx_first.end());
+      vec.insert(vec.end(), cs.rx_last.begin(), cs.rx_last.end());
+      vec.insert(vec.end(), cs.rx_init0.begin(), cs.rx_init0.end());
+      vec.insert(vec.end(), cs.rx_end.begin(), cs.rx_end.end());
+      if ((h = upload(e->d_rx_class, cs.rx_class, st)) != hipSuccess ||
+          (h = upload(e->d_rx_b, cs.rx_b, st)) != hipSuccess ||
+          (h = upload(e->d_rx_follow, cs.rx_follow, st)) != hipSuccess ||
+          (h = upload(e->d_rx_vec, vec, st)) != hipSuccess ||
+          (h = upload(e->d_rx_flags, cs.rx_flags, st)) != hipSuccess) {
+        *out = e;
+        return hip_err(e, h, "upload regex tables");
+      }
+      const uint64_t* v = e->d_rx_vec.as<uint64_t>();
+      P.rx_class = e->d_rx_class.as<uint8_t>();
+      P.rx_b = e->d_rx_b.as<uint64_t>();
+      P.rx_follow = e->d_rx_follow.as<uint64_t>();
+      P.rx_first = v;
+      P.rx_last = v + cs.rx_count;
+      P.rx_init0 = v + 2 * cs.rx_count;
+      P.rx_end = v + 3 * cs.rx_count;
+      P.rx_flags = e->d_rx_flags.as<uint32_t>();
+      P.rx_count = cs.rx_count;
+      P.rx_classes = cs.rx_classes;
+    }
+  }
+  if (cfg->staging_hint) e->staged.reserve(16);
+  *out = e;
+  return KLF_OK;
+}
+
+extern "C" void klf_close(klf_engine* e) {
+  if (!e) return;
+  if (e->stream) (void)hipStreamSynchronize(e->stream);
+  for (DevBuf* b : {&e->d_lit, &e->d_ac_class, &e->d_ac_next, &e->d_ac_accept, &e->d_rx_class, &e->d_rx_b,
+                    &e->d_rx_follow, &e->d_rx_vec, &e->d_rx_flags, &e->d_batch, &e->d_segs, &e->d_status,
+                    &e->d_cstatus, &e->d_counters, &e->d_line_off, &e->d_meta, &e->d_bits, &e->d_tile_cnt,
+                    &e->d_segout, &e->d_wpre, &e->d_out})
+    b->release();
+  for (auto& x : e->ev)
+    if (x) (void)hipEventDestroy(x);
+  if (e->own_stream && e->stream) (void)hipStreamDestroy(e->stream);
+  delete e;
+}
+
+// ------------------------------------------------------------------------ staging ---
+
+extern "C" int klf_set_streams(klf_engine* e, uint32_t n) {
+  if (!e) return KLF_EINVAL;
+  std::lock_guard<std::mutex> g(e->mu);
+  if (n < e->staged.size()) return set_err(e, KLF_ESTATE, "cannot shrink the stream table; klf_reset first");
+  e->staged.resize(n);
+  return KLF_OK;
+}
+
+extern "C" int klf_stage(klf_engine* e, uint32_t id, const uint8_t* p, size_t n) {
+  if (!e || (n && !p)) return KLF_EINVAL;
+  std::vector<uint8_t>* dst;
+  {
+    std::lock_guard<std::mutex> g(e->mu);
+    if (id >= e->staged.size()) e->staged.resize((size_t)id + 1);
+    dst = &e->staged[id];
+  }
+  // different ids never share a vector; the outer vector only grows under the lock and
+  // callers declare the table with klf_set_streams before staging concurrently.
+  try {
+    dst->insert(dst->end(), p, p + n);
+  } catch (...) {
+    return KLF_ENOMEM;
+  }
+  return KLF_OK;
+}
+
+extern "C" int klf_reset(klf_engine* e) {
+  if (!e) return KLF_EINVAL;
+  std::lock_guard<std::mutex> g(e->mu);
+  e->staged.clear();
+  return KLF_OK;
+}
+
+extern "C" int klf_layout(uint32_t n, const uint64_t* lens, uint64_t* seg_base, uint64_t* total) {
+  if ((n && (!lens || !seg_base)) || !total) return KLF_EINVAL;
+  uint64_t off = 0;
+  for (uint32_t i = 0; i < n; ++i) {
+    seg_base[i] = off;
+    off = align_up(off + lens[i], klf::kSegAlign);
+  }
+  *total = off + klf::kAllocSlack;
+  return KLF_OK;
+}
+
+// -------------------------------------------------------------------------- run ---
+
+static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_streams, const uint64_t* seg_base,
+                           const uint64_t* lens, const klf_filter* f, klf_result** out) {
+  if (!e || !f || !out || (n_streams && (!seg_base || !lens))) return KLF_EINVAL;
+  if (f->tail < -1) return set_err(e, KLF_EINVAL, "tail must be >= -1");
+  if (f->since.nsec < 0 || f->since.nsec >= 1000000000) return set_err(e, KLF_EINVAL, "since.nsec out of range");
+  *out = nullptr;
+  HIPCHK(e, hipSetDevice(e->device), "hipSetDevice");
+  auto* r = new (std::nothrow) klf_result();
+  if (!r) return KLF_ENOMEM;
+  r->e = e;
+  r->gen = ++e->gen;
+  r->n_streams = n_streams;
+  r->seg_of.assign(n_streams, -1);
+  const auto mode = e->cs.mode;
+  r->has_bits = mode != klf::CompiledSet::kNone;
+
+  std::vector<SegDesc> segs;
+  uint64_t total_bytes = 0, ntiles = 0, cap = 0;
+  for (uint32_t i = 0; i < n_streams; ++i) {
+    if (!lens[i]) continue;
+    if (seg_base[i] % klf::kSegAlign) { delete r; return set_err(e, KLF_EINVAL, "seg_base must be 256-B aligned"); }
+    SegDesc d;
+    d.base = seg_base[i];
+    d.len = lens[i];
+    d.tile0 = (uint32_t)ntiles;
+    d.ntiles = (uint32_t)((lens[i] + klf::kTile - 1) / klf::kTile);
+    r->seg_of[i] = (int64_t)segs.size();
+    segs.push_back(d);
+    r->seg_base.push_back(d.base);
+    ntiles += d.ntiles;
+    total_bytes += lens[i];
+    cap += lens[i] / 32 + 2;  // kubelet lines carry a >= 31-byte prefix; overflow -> exact rerun
+  }
+  if (ntiles >= (1ull << 32)) { delete r; return set_err(e, KLF_EINVAL, "batch too large"); }
+  const uint32_t nsegs = (uint32_t)segs.size();
+  if (nsegs == 0) { *out = r; return KLF_OK; }
+
+  hipStream_t st = e->stream;
+  HIPCHK(e, e->d_segs.ensure(nsegs * sizeof(SegDesc)), "alloc segs");
+  HIPCHK(e, hipMemcpyAsync(e->d_segs.p, segs.data(), nsegs * sizeof(SegDesc), hipMemcpyHostToDevice, st), "H2D segs");
+  HIPCHK(e, e->d_status.ensure(ntiles * 8), "alloc status");
+  HIPCHK(e, e->d_counters.ensure(64), "alloc counters");
+  HIPCHK(e, e->d_tile_cnt.ensure(ntiles * 8), "alloc tile counters");
+  HIPCHK(e, e->d_segout.ensure(nsegs * sizeof(SegOut)), "alloc segout");
+  HIPCHK(e, e->d_wpre.ensure((nsegs + 1) * 8), "alloc wpre");
+  HIPCHK(e, e->d_out.ensure(total_bytes + 64), "alloc out");
+
+  for (int attempt = 0; attempt < 2; ++attempt) {
+    const uint64_t max_cblocks = cap / klf::kCompactLines + 2;
+    HIPCHK(e, e->d_line_off.ensure((cap + nsegs + 1) * 8), "alloc line_off");
+    HIPCHK(e, e->d_meta.ensure(cap * 2 + 16), "alloc meta");
+    HIPCHK(e, e->d_bits.ensure((cap / 32 + 1) * 4), "alloc bits");
+    HIPCHK(e, e->d_cstatus.ensure(max_cblocks * 2 * 8), "alloc cstatus");
+    klf::RunArgs a{};
+    a.bytes = d_bytes;
+    a.segs = e->d_segs.as<SegDesc>();
+    a.nsegs = nsegs;
+    a.ntiles = (uint32_t)ntiles;
+    a.since_sec = f->since.sec;
+    a.since_nsec = f->since.nsec;
+    a.tail = f->tail;
+    a.grep_mode = (uint32_t)mode;
+    a.lit = e->d_lit.as<uint8_t>();
+    a.lit_len = (uint32_t)e->cs.literal.size();
+    a.pats = e->dpats;
+    a.status = e->d_status.as<uint64_t>();
+    a.cstatus = e->d_cstatus.as<uint64_t>();
+    a.counters = e->d_counters.as<uint32_t>();
+    a.line_off = e->d_line_off.as<uint64_t>();
+    a.meta = e->d_meta.as<uint16_t>();
+    a.bits = e->d_bits.as<uint32_t>();
+    a.cap_lines = cap;
+    a.tile_cnt = e->d_tile_cnt.as<uint32_t>();
+    a.segout = e->d_segout.as<SegOut>();
+    a.wpre = e->d_wpre.as<uint64_t>();
+    a.out = e->d_out.as<uint8_t>();
+    a.max_cblocks = (uint32_t)max_cblocks;
+    HIPCHK(e, klf::launch_pipeline(a, st, e->ev, e->num_cus), "launch");
+    r->so.resize(nsegs);
+    uint32_t counters[8];
+    HIPCHK(e, hipMemcpyAsync(r->so.data(), e->d_segout.p, nsegs * sizeof(SegOut), hipMemcpyDeviceToHost, st), "D2H segout");
+    HIPCHK(e, hipMemcpyAsync(counters, e->d_counters.p, sizeof(counters), hipMemcpyDeviceToHost, st), "D2H counters");
+    HIPCHK(e, hipStreamSynchronize(st), "sync");
+    if (counters[2] & 2u) { delete r; return set_err(e, KLF_EHIP, "look-back spin timeout"); }
+    if (counters[2] & 1u) {  // more lines than the capacity estimate: rerun with the exact count
+      cap = r->so[nsegs - 1].line_hi + 2;
+      continue;
+    }
+    break;
+  }
+  float ms;
+  for (int k = 0; k < 4; ++k)  // scan, match, tail stage, compaction
+    if (hipEventElapsedTime(&ms, e->ev[k + 1], e->ev[k + 2]) == hipSuccess) r->ms[k] = ms;
+  if (hipEventElapsedTime(&ms, e->ev[0], e->ev[5]) == hipSuccess) r->ms[4] = ms;
+  if (hipEventElapsedTime(&ms, e->ev[0], e->ev[1]) == hipSuccess) r->ms[5] = ms;
+  r->total_lines = r->so[nsegs - 1].line_hi;
+  for (auto& s : r->so) r->total_out = std::max(r->total_out, s.out_hi);
+  *out = r;
+  return KLF_OK;
+}
+
+extern "C" int klf_run_device(klf_engine* e, const uint8_t* d_bytes, uint32_t n, const uint64_t* seg_base,
+                              const uint64_t* lens, const klf_filter* f, klf_result** out) {
+  return run_device_impl(e, d_bytes, n, seg_base, lens, f, out);
+}
+
+extern "C" int klf_run(klf_engine* e, const klf_filter* f, klf_result** out) {
+  if (!e || !f || !out) return KLF_EINVAL;
+  HIPCHK(e, hipSetDevice(e->device), "hipSetDevice");
+  std::lock_guard<std::mutex> g(e->mu);
+  const uint32_t n = (uint32_t)e->staged.size();
+  std::vector<uint64_t> lens(n), base(n);
+  for (uint32_t i = 0; i < n; ++i) lens[i] = e->staged[i].size();
+  uint64_t total = 0;
+  klf_layout(n, lens.data(), base.data(), &total);
+  HIPCHK(e, e->d_batch.ensure(total), "alloc batch");
+  for (uint32_t i = 0; i < n; ++i)
+    if (lens[i])
+      HIPCHK(e, hipMemcpyAsync(e->d_batch.as<uint8_t>() + base[i], e->staged[i].data(), lens[i], hipMemcpyHostToDevice,
+                               e->stream), "H2D stream");
+  return run_device_impl(e, e->d_batch.as<uint8_t>(), n, base.data(), lens.data(), f, out);
+}
+
+// ---------------------------------------------------------------------- results ---
+
+static int check_result(klf_result* r, uint32_t id) {
+  if (!r || id >= r->n_streams) return KLF_EINVAL;
+  if (r->e->gen != r->gen) return KLF_ESTATE;  // workspace reused by a later run
+  return KLF_OK;
+}
+
+static void fill_counts(const klf_result* r, int64_t s, const uint64_t len, klf_counts* c) {
+  if (!c) return;
+  memset(c, 0, sizeof(*c));
+  if (s < 0) return;
+  const SegOut& so = r->so[s];
+  const auto mode = r->e->cs.mode;
+  c->lines = so.line_hi - so.line_lo;
+  c->parsed = so.parsed;
+  c->since_ok = so.since_ok;
+  c->matched = mode == klf::CompiledSet::kNone ? c->lines : so.matched;
+  c->selected = so.sel_hi - so.sel_lo;
+  c->out_bytes = len;
+}
+
+extern "C" int klf_result_stream(klf_result* r, uint32_t id, const uint8_t** bytes, uint64_t* len, klf_counts* counts) {
+  int rc = check_result(r, id);
+  if (rc) return rc;
+  klf_engine* e = r->e;
+  if (!r->have_out) {
+    r->out.resize(r->total_out + 1);
+    if (r->total_out) {
+      HIPCHK(e, hipMemcpyAsync(r->out.data(), e->d_out.p, r->total_out, hipMemcpyDeviceToHost, e->stream), "D2H out");
+      HIPCHK(e, hipStreamSynchronize(e->stream), "sync");
+    }
+    r->have_out = true;
+  }
+  const int64_t s = r->seg_of[id];
+  uint64_t n = 0, off = 0;
+  if (s >= 0) { off = r->so[s].out_lo; n = r->so[s].out_hi - r->so[s].out_lo; }
+  if (bytes) *bytes = r->out.data() + off;
+  if (len) *len = n;
+  fill_counts(r, s, n, counts);
+  return KLF_OK;
+}
+
+extern "C" int klf_result_lines(klf_result* r, uint32_t id, const uint64_t** off, uint64_t* n_lines) {
+  int rc = check_result(r, id);
+  if (rc) return rc;
+  klf_engine* e = r->e;
+  const int64_t s = r->seg_of[id];
+  static const uint64_t kZero = 0;
+  if (s < 0) {
+    if (off) *off = &kZero;
+    if (n_lines) *n_lines = 0;
+    return KLF_OK;
+  }
+  if (!r->have_lines) {
+    const size_t nwords = r->total_lines + r->so.size();
+    r->line_off.resize(nwords);
+    HIPCHK(e, hipMemcpyAsync(r->line_off.data(), e->d_line_off.p, nwords * 8, hipMemcpyDeviceToHost, e->stream), "D2H lines");
+    HIPCHK(e, hipStreamSynchronize(e->stream), "sync");
+    r->have_lines = true;
+  }
+  if (off) *off = r->line_off.data() + r->so[s].line_lo + (uint64_t)s;
+  if (n_lines) *n_lines = r->so[s].line_hi - r->so[s].line_lo;
+  return KLF_OK;
+}
+
+extern "C" int klf_result_match_bits(klf_result* r, uint32_t id, const uint8_t** bits, uint64_t* nbytes) {
+  int rc = check_result(r, id);
+  if (rc) return rc;
+  if (!r->has_bits) return KLF_EINVAL;
+  klf_engine* e = r->e;
+  if (!r->have_bits) {
+    const size_t nw = r->total_lines / 32 + 1;
+    r->bits.assign(nw, 0);
+    if (!r->so.empty()) {
+      HIPCHK(e, hipMemcpyAsync(r->bits.data(), e->d_bits.p, nw * 4, hipMemcpyDeviceToHost, e->stream), "D2H bits");
+      HIPCHK(e, hipStreamSynchronize(e->stream), "sync");
+    }
+    r->have_bits = true;
+    r->stream_bits.assign(r->n_streams, {});
+    r->have_stream_bits.assign(r->n_streams, 0);
+  }
+  if (!r->have_stream_bits[id]) {
+    const int64_t s = r->seg_of[id];
+    auto& v = r->stream_bits[id];
+    if (s >= 0) {
+      const uint64_t lo = r->so[s].line_lo, n = r->so[s].line_hi - lo;
+      v.assign((n + 7) / 8, 0);
+      for (uint64_t i = 0; i < n; ++i) {
+        const uint64_t l = lo + i;
+        if ((r->bits[l >> 5] >> (l & 31)) & 1u) v[i >> 3] |= (uint8_t)(1u << (i & 7));
+      }
+    }
+    r->have_stream_bits[id] = 1;
+  }
+  if (bits) *bits = r->stream_bits[id].data();
+  if (nbytes) *nbytes = r->stream_bits[id].size();
+  return KLF_OK;
+}
+
+extern "C" int klf_result_device_out(klf_result* r, uint32_t id, const uint8_t** d_out, uint64_t* off, uint64_t* len) {
+  int rc = check_result(r, id);
+  if (rc) return rc;
+  const int64_t s = r->seg_of[id];
+  if (d_out) *d_out = r->e->d_out.as<uint8_t>();
+  if (off) *off = s >= 0 ? r->so[s].out_lo : 0;
+  if (len) *len = s >= 0 ? r->so[s].out_hi - r->so[s].out_lo : 0;
+  return KLF_OK;
+}
+
+extern "C" int klf_result_timing(const klf_result* r, double* ms, uint32_t cap, uint32_t* n) {
+  if (!r || (cap && !ms)) return KLF_EINVAL;
+  const uint32_t k = std::min<uint32_t>(cap, 6);
+  for (uint32_t i = 0; i < k; ++i) ms[i] = r->ms[i];
+  if (n) *n = k;
+  return KLF_OK;
+}
+
+extern "C" int klf_result_totals(const klf_result* r, klf_counts* t) {
+  if (!r || !t) return KLF_EINVAL;
+  memset(t, 0, sizeof(*t));
+  for (uint32_t i = 0; i < r->n_streams; ++i) {
+    const int64_t s = r->seg_of[i];
+    if (s < 0) continue;
+    klf_counts c;
+    fill_counts(r, s, r->so[s].out_hi - r->so[s].out_lo, &c);
+    t->lines += c.lines;
+    t->parsed += c.parsed;
+    t->since_ok += c.since_ok;
+    t->matched += c.matched;
+    t->selected += c.selected;
+    t->out_bytes += c.out_bytes;
+  }
+  return KLF_OK;
+}
+
+extern "C" void klf_result_free(klf_result* r) { delete r; }
+
+// ---------------------------------------------------------------- host helpers ---
+
+extern "C" int klf_parse_rfc3339nano(const uint8_t* s, size_t n, klf_time* out) {
+  if (!s || !out) return KLF_EINVAL;
+  klf::TsResult r;
+  auto get = [&](uint32_t i) -> int { return i < n ? s[i] : -1; };
+  if (!klf::parse_rfc3339nano(get, r) || r.len != n) return KLF_EINVAL;
+  out->sec = r.sec;
+  out->nsec = r.nsec;
+  out->_reserved = 0;
+  return KLF_OK;
+}
+
+extern "C" int klf_debug_match(const klf_pattern* pats, uint32_t n, const uint8_t* content, size_t len, int* match) {
+  if ((n && !pats) || (len && !content) || !match) return KLF_EINVAL;
+  std::vector<std::vector<uint8_t>> ps;
+  std::vector<uint32_t> kinds;
+  for (uint32_t i = 0; i < n; ++i) {
+    ps.emplace_back(pats[i].bytes, pats[i].bytes + pats[i].len);
+    kinds.push_back(pats[i].kind);
+  }
+  klf::CompiledSet cs;
+  std::string err;
+  int code = KLF_OK;
+  if (!klf::compile_set(ps, kinds, cs, err, code)) return code;
+  bool hit = false;
+  switch (cs.mode) {
+    case klf::CompiledSet::kNone: case klf::CompiledSet::kAll: hit = true; break;
+    case klf::CompiledSet::kNever: hit = false; break;
+    case klf::CompiledSet::kLiteral1:
+      hit = std::search(content, content + len, cs.literal.begin(), cs.literal.end()) != content + len;
+      break;
+    case klf::CompiledSet::kGeneral: {
+      if (cs.ac_states) {  // run the same DFA tables the GPU runs
+        uint32_t st = 0;
+        for (size_t i = 0; i < len && !hit; ++i) {
+          st = cs.ac_next[(size_t)st * cs.ac_classes + cs.ac_class[content[i]]];
+          hit = cs.ac_accept[st] != 0;
+        }
+      }
+      for (uint32_t r = 0; r < cs.rx_count && !hit; ++r) {  // the GPU recurrence on host
+        const uint32_t fl = cs.rx_flags[r];
+        if (len == 0) { hit = fl & 2u; continue; }
+        if (fl & 1u) { hit = true; continue; }
+        uint64_t d = cs.rx_init0[r];
+        for (size_t i = 0; i < len && !hit; ++i) {
+          const uint64_t c = d & cs.rx_b[(size_t)r * cs.rx_classes + cs.rx_class[content[i]]];
+          if (c & cs.rx_last[r]) { hit = true; break; }
+          uint64_t nd = cs.rx_first[r];
+          for (int p = 0; p < 64; ++p)
+            if (c >> p & 1) nd |= cs.rx_follow[(size_t)r * 64 + p];
+          d = nd;
+        }
+        if (!hit) hit = (d & cs.rx_end[r]) != 0;
+      }
+      break;
+    }
+  }
+  *match = hit ? 1 : 0;
+  return KLF_OK;
+}
+
+extern "C" int klf_debug_compile(const klf_pattern* pats, uint32_t n, uint32_t* mode, char* err, size_t err_cap) {
+  if ((n && !pats) || !mode) return KLF_EINVAL;
+  std::vector<std::vector<uint8_t>> ps;
+  std::vector<uint32_t> kinds;
+  for (uint32_t i = 0; i < n; ++i) {
+    ps.emplace_back(pats[i].bytes, pats[i].bytes + pats[i].len);
+    kinds.push_back(pats[i].kind);
+  }
+  klf::CompiledSet cs;
+  std::string e;
+  int code = KLF_OK;
+  bool ok = klf::compile_set(ps, kinds, cs, e, code);
+  if (err && err_cap) { strncpy(err, e.c_str(), err_cap - 1); err[err_cap - 1] = 0; }
+  *mode = (uint32_t)cs.mode;
+  return ok ? KLF_OK : code;
+}

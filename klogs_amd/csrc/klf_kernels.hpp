@@ -1,0 +1,97 @@
+// klf_kernels.hpp — device-side data structures and host launchers of the filter path.
+// Kernels live in klf_kernels.hip; the engine (klf_engine.cpp) only sees this header.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace klf {
+
+// Work decomposition of the scan: a tile = 256 threads x 64 contiguous bytes.
+constexpr int kThreads = 256;
+constexpr int kBytesPerThread = 64;
+constexpr int kTile = kThreads * kBytesPerThread;  // 16 KiB
+constexpr int kHalo = 320;                          // LDS bytes past the tile (ts + literal window)
+constexpr int kMaxFusedLiteral = 256;
+constexpr uint64_t kSegAlign = 256;                 // segment base alignment in the batch buffer
+constexpr uint64_t kAllocSlack = kTile + kHalo + 1024;
+constexpr uint32_t kPlenEscape = 16383;             // meta plen field saturates here
+constexpr int kCompactLines = 1024;                 // lines per compaction block
+
+// One segment (= one non-empty stream) of the device batch.
+struct SegDesc {
+  uint64_t base;    // byte offset of the stream in the batch buffer (256-aligned)
+  uint64_t len;     // stream length (> 0)
+  uint32_t tile0;   // first global tile of the stream
+  uint32_t ntiles;  // ceil(len / kTile)
+};
+
+// Per-segment results, written by the kernels, read back by the host in one copy.
+struct SegOut {
+  uint64_t line_lo, line_hi;   // global line indices [lo, hi) of the stream
+  uint64_t parsed, since_ok, matched;
+  uint64_t win_lo, win_hi;     // candidate window after the tail rule
+  uint64_t sel_lo, sel_hi;     // selected-line chain values at the window ends
+  uint64_t out_lo, out_hi;     // output byte offsets [lo, hi) in the output buffer
+  uint64_t frag;               // 1 when the stream ends without '\n'
+};
+
+// Line-meta word (u16): bit0 parsed, bit1 since_ok, bits 2..15 content offset (plen),
+// saturating at kPlenEscape (then recomputed from the bytes).
+struct Meta {
+  static constexpr uint16_t kParsed = 1, kSince = 2;
+};
+
+enum GrepMode : uint32_t { kGrepNone = 0, kGrepNever = 1, kGrepAll = 2, kGrepLit1 = 3, kGrepGeneral = 4 };
+
+struct DevPatterns {  // device copies of CompiledSet tables (kGrepGeneral)
+  const uint8_t* ac_class = nullptr;
+  const uint32_t* ac_next = nullptr;
+  const uint8_t* ac_accept = nullptr;
+  uint32_t ac_states = 0, ac_classes = 0;
+  const uint8_t* rx_class = nullptr;
+  const uint64_t* rx_b = nullptr;
+  const uint64_t* rx_follow = nullptr;
+  const uint64_t* rx_first = nullptr;
+  const uint64_t* rx_last = nullptr;
+  const uint64_t* rx_init0 = nullptr;
+  const uint64_t* rx_end = nullptr;
+  const uint32_t* rx_flags = nullptr;
+  uint32_t rx_count = 0, rx_classes = 0;
+};
+
+struct RunArgs {
+  // batch
+  const uint8_t* bytes;
+  const SegDesc* segs;
+  uint32_t nsegs;
+  uint32_t ntiles;
+  // filter
+  int64_t since_sec;
+  int32_t since_nsec;
+  int64_t tail;
+  uint32_t grep_mode;
+  const uint8_t* lit;  // kGrepLit1 literal (device)
+  uint32_t lit_len;
+  DevPatterns pats;
+  // workspace (device)
+  uint64_t* status;     // [ntiles] scan look-back words
+  uint64_t* cstatus;    // [2 * max compaction blocks] compaction look-back words
+  uint32_t* counters;   // [8] tickets / flags: 0 scan ticket, 1 compact ticket, 2 overflow
+  uint64_t* line_off;   // [cap_lines + nsegs]
+  uint16_t* meta;       // [cap_lines]
+  uint32_t* bits;       // [cap_lines / 32 + 1]
+  uint64_t cap_lines;
+  uint32_t* tile_cnt;   // [ntiles * 2] parsed, since_ok
+  SegOut* segout;       // [nsegs]
+  uint64_t* wpre;       // [nsegs + 1] exclusive prefix of window sizes
+  uint8_t* out;         // output bytes (capacity >= total input)
+  uint32_t max_cblocks; // compaction look-back capacity
+};
+
+// Enqueues the whole pipeline on `stream`; `ev` (6 events) brackets the stages for
+// per-kernel timing: ev[0] start, ev[1] after the workspace memsets, ev[2] after the
+// scan, ev[3] after the general matcher, ev[4] after counts+tail+window prefix, ev[5]
+// after compaction.  Returns a hipError_t.
+hipError_t launch_pipeline(const RunArgs& a, hipStream_t stream, hipEvent_t* ev, int num_cus);
+
+}  // namespace klf

@@ -1,0 +1,791 @@
+// klf_patterns.cpp — Go RE2-subset parser, Glushkov construction, Aho-Corasick build.
+// See klf_patterns.hpp and SPEC.md S5 for the accepted syntax and semantics.
+#include "klf_patterns.hpp"
+
+#include <algorithm>
+#include <bitset>
+#include <cstring>
+#include <map>
+#include <queue>
+
+#include "../../include/klf.h"
+
+namespace klf {
+namespace {
+
+using ByteSet = std::bitset<256>;
+
+ByteSet range_set(int lo, int hi) {
+  ByteSet s;
+  for (int c = lo; c <= hi; ++c) s.set(c);
+  return s;
+}
+ByteSet perl_d() { return range_set('0', '9'); }
+ByteSet perl_w() { return range_set('0', '9') | range_set('A', 'Z') | range_set('a', 'z') | range_set('_', '_'); }
+ByteSet perl_s() {
+  ByteSet s;
+  for (int c : {'\t', '\n', '\f', '\r', ' '}) s.set(c);  // Go \s has no \v
+  return s;
+}
+ByteSet fold(const ByteSet& s) {
+  ByteSet o = s;
+  for (int c = 'A'; c <= 'Z'; ++c) {
+    if (s.test(c)) o.set(c + 32);
+    if (s.test(c + 32)) o.set(c);
+  }
+  return o;
+}
+
+struct RNode {
+  enum Kind { kEmpty, kSet, kCat, kAlt, kStar, kPlus, kQuest, kRepeat, kBot, kEot } k = kEmpty;
+  ByteSet set;
+  std::vector<int> kids;
+  int lo = 0, hi = 0;  // kRepeat; hi = -1 means unbounded
+};
+
+struct Flags {
+  bool i = false, s = false;
+};
+
+class Parser {
+ public:
+  Parser(const uint8_t* p, size_t n) : p_(p), n_(n) {}
+  std::vector<RNode> pool;
+  std::string err;
+
+  int parse() {
+    for (size_t k = 0; k < n_; ++k)
+      if (p_[k] >= 0x80) return fail("non-ASCII pattern bytes are outside the supported subset");
+    Flags f;
+    int r = alt(f);
+    if (r < 0) return r;
+    if (i_ < n_) return fail("unexpected )");
+    return r;
+  }
+
+ private:
+  const uint8_t* p_;
+  size_t n_;
+  size_t i_ = 0;
+
+  int fail(const char* m) {
+    if (err.empty()) err = m;
+    return -1;
+  }
+  int peek(size_t k = 0) const { return i_ + k < n_ ? p_[i_ + k] : -1; }
+  int mk(RNode::Kind k) {
+    RNode n;
+    n.k = k;
+    pool.push_back(n);
+    return (int)pool.size() - 1;
+  }
+  int mkset(const ByteSet& s) {
+    int x = mk(RNode::kSet);
+    pool[x].set = s;
+    return x;
+  }
+
+  int alt(Flags& f) {
+    std::vector<int> br;
+    int c = concat(f);
+    if (c < 0) return c;
+    br.push_back(c);
+    while (peek() == '|') {
+      ++i_;
+      c = concat(f);
+      if (c < 0) return c;
+      br.push_back(c);
+    }
+    if (br.size() == 1) return br[0];
+    int x = mk(RNode::kAlt);
+    pool[x].kids = br;
+    return x;
+  }
+
+  int concat(Flags& f) {
+    std::vector<int> items;
+    while (i_ < n_ && peek() != '|' && peek() != ')') {
+      bool flags_only = false;
+      int a = atom(f, flags_only);
+      if (a < 0 && !flags_only) return -1;
+      if (flags_only) continue;
+      a = repeat(a);
+      if (a < 0) return -1;
+      items.push_back(a);
+    }
+    if (items.empty()) return mk(RNode::kEmpty);
+    if (items.size() == 1) return items[0];
+    int x = mk(RNode::kCat);
+    pool[x].kids = items;
+    return x;
+  }
+
+  // {m}, {m,}, {m,n}; returns false (no consumption) when not a valid repeat spec.
+  bool braces(int& lo, int& hi, size_t& len) const {
+    size_t j = i_;
+    if (j >= n_ || p_[j] != '{') return false;
+    ++j;
+    size_t d0 = j;
+    long v = 0;
+    while (j < n_ && p_[j] >= '0' && p_[j] <= '9') { v = std::min(v * 10 + (p_[j] - '0'), 100000L); ++j; }
+    if (j == d0) return false;
+    lo = (int)v;
+    if (j < n_ && p_[j] == '}') { hi = lo; len = j + 1 - i_; return true; }
+    if (j >= n_ || p_[j] != ',') return false;
+    ++j;
+    size_t d1 = j;
+    v = 0;
+    while (j < n_ && p_[j] >= '0' && p_[j] <= '9') { v = std::min(v * 10 + (p_[j] - '0'), 100000L); ++j; }
+    if (j >= n_ || p_[j] != '}') return false;
+    hi = (j == d1) ? -1 : (int)v;
+    len = j + 1 - i_;
+    return true;
+  }
+
+  int repeat(int a) {
+    bool seen = false;
+    for (;;) {
+      int c = peek();
+      int k;
+      if (c == '*' || c == '+' || c == '?') {
+        if (seen) return fail("invalid nested repetition operator");
+        ++i_;
+        k = mk(c == '*' ? RNode::kStar : c == '+' ? RNode::kPlus : RNode::kQuest);
+        pool[k].kids = {a};
+      } else if (c == '{') {
+        int lo, hi;
+        size_t len;
+        if (!braces(lo, hi, len)) return a;  // Go: '{' is then a literal
+        if (seen) return fail("invalid nested repetition operator");
+        if (lo > 1000 || hi > 1000 || (hi >= 0 && hi < lo)) return fail("invalid repeat count");
+        i_ += len;
+        k = mk(RNode::kRepeat);
+        pool[k].kids = {a};
+        pool[k].lo = lo;
+        pool[k].hi = hi;
+      } else {
+        return a;
+      }
+      a = k;
+      seen = true;
+      if (peek() == '?') ++i_;  // lazy: same boolean match
+    }
+  }
+
+  int atom(Flags& f, bool& flags_only) {
+    int c = peek();
+    if (c == '*' || c == '+' || c == '?') return fail("missing argument to repetition operator");
+    if (c == '{') {
+      int lo, hi;
+      size_t len;
+      if (braces(lo, hi, len)) return fail("missing argument to repetition operator");
+    }
+    if (c == '(') return group(f, flags_only);
+    if (c == '[') {
+      ByteSet s;
+      if (!bracket(f, s)) return -1;
+      return mkset(s);
+    }
+    if (c == '.') {
+      ++i_;
+      ByteSet s;
+      s.set();
+      if (!f.s) s.reset('\n');
+      return mkset(s);
+    }
+    if (c == '^') { ++i_; return mk(RNode::kBot); }
+    if (c == '$') { ++i_; return mk(RNode::kEot); }
+    if (c == '\\') return escape_atom(f);
+    ++i_;
+    ByteSet s;
+    s.set(c);
+    return mkset(f.i ? fold(s) : s);
+  }
+
+  int group(Flags& f, bool& flags_only) {
+    ++i_;  // (
+    Flags inner = f;
+    if (peek() == '?') {
+      // named groups (?P<name>  (?<name>
+      size_t j = i_ + 1;
+      if (j < n_ && p_[j] == 'P') ++j;
+      if (j < n_ && p_[j] == '<') {
+        size_t k = j + 1;
+        while (k < n_ && (isalnum(p_[k]) || p_[k] == '_')) ++k;
+        if (k == j + 1 || k >= n_ || p_[k] != '>') return fail("invalid named capture");
+        i_ = k + 1;
+      } else {
+        // flags: (?imsU-imsU) or (?imsU-imsU:...)
+        size_t k = i_ + 1;
+        bool neg = false, saw = false, saw_neg_flag = false;
+        Flags nf = f;
+        for (;; ++k) {
+          if (k >= n_) return fail("missing closing )");
+          int ch = p_[k];
+          if (ch == 'i' || ch == 'm' || ch == 's' || ch == 'U') {
+            if (ch == 'i') nf.i = !neg;
+            if (ch == 's') nf.s = !neg;
+            saw = true;
+            if (neg) saw_neg_flag = true;
+          } else if (ch == '-') {
+            if (neg) return fail("invalid or unsupported Perl syntax");
+            neg = true;
+          } else if (ch == ':' || ch == ')') {
+            if (neg && !saw_neg_flag) return fail("invalid or unsupported Perl syntax");
+            if (ch == ')' && !saw) return fail("invalid or unsupported Perl syntax");
+            break;
+          } else {
+            return fail("invalid or unsupported Perl syntax");
+          }
+        }
+        if (p_[k] == ')') {  // flags for the rest of the current group
+          f = nf;
+          i_ = k + 1;
+          flags_only = true;
+          return -1;
+        }
+        inner = nf;
+        i_ = k + 1;
+      }
+    }
+    int r = alt(inner);
+    if (r < 0) return r;
+    if (peek() != ')') return fail("missing closing )");
+    ++i_;
+    return r;
+  }
+
+  // One escape; kind: 0 byte (v), 1 class (s), 2 assertion BOT, 3 assertion EOT.
+  bool escape(bool in_class, int& kind, int& v, ByteSet& s) {
+    ++i_;  // backslash
+    int c = peek();
+    if (c < 0) { fail("trailing backslash at end of expression"); return false; }
+    ++i_;
+    switch (c) {
+      case 'd': kind = 1; s = perl_d(); return true;
+      case 'w': kind = 1; s = perl_w(); return true;
+      case 's': kind = 1; s = perl_s(); return true;
+      case 'D': kind = 1; s = ~perl_d(); return true;
+      case 'W': kind = 1; s = ~perl_w(); return true;
+      case 'S': kind = 1; s = ~perl_s(); return true;
+      case 't': kind = 0; v = '\t'; return true;
+      case 'n': kind = 0; v = '\n'; return true;
+      case 'r': kind = 0; v = '\r'; return true;
+      case 'f': kind = 0; v = '\f'; return true;
+      case 'v': kind = 0; v = '\v'; return true;
+      case 'a': kind = 0; v = 7; return true;
+      default: break;
+    }
+    if (c == 'x') {
+      long val = 0;
+      if (peek() == '{') {
+        size_t j = i_ + 1, d0 = j;
+        while (j < n_ && isxdigit(p_[j]) && j - d0 < 8) { val = val * 16 + (isdigit(p_[j]) ? p_[j] - '0' : (tolower(p_[j]) - 'a' + 10)); ++j; }
+        if (j == d0 || j >= n_ || p_[j] != '}') { fail("invalid escape sequence"); return false; }
+        i_ = j + 1;
+      } else {
+        if (i_ + 2 > n_ || !isxdigit(p_[i_]) || !isxdigit(p_[i_ + 1])) { fail("invalid escape sequence"); return false; }
+        for (int k = 0; k < 2; ++k) val = val * 16 + (isdigit(p_[i_ + k]) ? p_[i_ + k] - '0' : (tolower(p_[i_ + k]) - 'a' + 10));
+        i_ += 2;
+      }
+      if (val >= 0x80) { fail("non-ASCII escapes are outside the supported subset"); return false; }
+      kind = 0; v = (int)val; return true;
+    }
+    if (c >= '0' && c <= '7') {
+      // Go parseEscape: a single non-zero digit would be a backreference.
+      if (c != '0' && !(peek() >= '0' && peek() <= '7')) { fail("invalid escape sequence"); return false; }
+      int val = c - '0';
+      for (int k = 0; k < 2 && peek() >= '0' && peek() <= '7'; ++k) { val = val * 8 + (peek() - '0'); ++i_; }
+      if (val >= 0x80) { fail("non-ASCII escapes are outside the supported subset"); return false; }
+      kind = 0; v = val; return true;
+    }
+    if (!in_class && c == 'A') { kind = 2; return true; }
+    if (!in_class && c == 'z') { kind = 3; return true; }
+    if (!isalnum(c)) { kind = 0; v = c; return true; }  // punctuation (and '_') is itself
+    fail("invalid or unsupported escape");
+    return false;
+  }
+
+  int escape_atom(Flags& f) {
+    if (peek(1) == 'Q') {  // \Q...\E
+      i_ += 2;
+      std::vector<int> items;
+      while (i_ < n_) {
+        if (p_[i_] == '\\' && i_ + 1 < n_ && p_[i_ + 1] == 'E') { i_ += 2; break; }
+        ByteSet s;
+        s.set(p_[i_]);
+        items.push_back(mkset(f.i ? fold(s) : s));
+        ++i_;
+      }
+      if (items.empty()) return mk(RNode::kEmpty);
+      if (items.size() == 1) return items[0];
+      int x = mk(RNode::kCat);
+      pool[x].kids = items;
+      return x;
+    }
+    int kind, v = 0;
+    ByteSet s;
+    if (!escape(false, kind, v, s)) return -1;
+    if (kind == 2) return mk(RNode::kBot);
+    if (kind == 3) return mk(RNode::kEot);
+    if (kind == 0) { s.reset(); s.set(v); }
+    return mkset(f.i ? fold(s) : s);
+  }
+
+  bool posix_class(ByteSet& out) {
+    // at "[:"; returns false (no consumption) when not a known [:name:]
+    size_t j = i_ + 2;
+    bool neg = false;
+    if (j < n_ && p_[j] == '^') { neg = true; ++j; }
+    size_t k = j;
+    while (k < n_ && p_[k] >= 'a' && p_[k] <= 'z') ++k;
+    if (k + 1 >= n_ || p_[k] != ':' || p_[k + 1] != ']') return false;
+    std::string name((const char*)p_ + j, k - j);
+    ByteSet s;
+    if (name == "alnum") s = range_set('0', '9') | range_set('A', 'Z') | range_set('a', 'z');
+    else if (name == "alpha") s = range_set('A', 'Z') | range_set('a', 'z');
+    else if (name == "ascii") s = range_set(0, 0x7f);
+    else if (name == "blank") { s.set('\t'); s.set(' '); }
+    else if (name == "cntrl") { s = range_set(0, 0x1f); s.set(0x7f); }
+    else if (name == "digit") s = range_set('0', '9');
+    else if (name == "graph") s = range_set(0x21, 0x7e);
+    else if (name == "lower") s = range_set('a', 'z');
+    else if (name == "print") s = range_set(0x20, 0x7e);
+    else if (name == "punct") s = range_set(0x21, 0x2f) | range_set(0x3a, 0x40) | range_set(0x5b, 0x60) | range_set(0x7b, 0x7e);
+    else if (name == "space") { for (int c : {9, 10, 11, 12, 13, 32}) s.set(c); }
+    else if (name == "upper") s = range_set('A', 'Z');
+    else if (name == "word") s = perl_w();
+    else if (name == "xdigit") s = range_set('0', '9') | range_set('A', 'F') | range_set('a', 'f');
+    else return false;
+    out |= neg ? ~s : s;
+    i_ = k + 2;
+    return true;
+  }
+
+  // class char: returns -2 on error, -3 when a set was added to `acc`, else the byte.
+  int class_char(ByteSet& acc) {
+    int c = peek();
+    if (c == '\\') {
+      int kind, v = 0;
+      ByteSet s;
+      if (!escape(true, kind, v, s)) return -2;
+      if (kind == 1) { acc |= s; return -3; }
+      return v;
+    }
+    ++i_;
+    return c;
+  }
+
+  bool bracket(const Flags& f, ByteSet& out) {
+    ++i_;  // [
+    bool neg = false;
+    if (peek() == '^') { neg = true; ++i_; }
+    ByteSet s;
+    bool first = true;
+    for (;;) {
+      int c = peek();
+      if (c < 0) { fail("missing closing ]"); return false; }
+      if (c == ']' && !first) { ++i_; break; }
+      first = false;
+      if (c == '[' && peek(1) == ':' && posix_class(s)) continue;
+      int lo = class_char(s);
+      if (lo == -2) return false;
+      if (lo == -3) continue;
+      if (peek() == '-' && peek(1) != ']' && peek(1) >= 0) {
+        ++i_;
+        ByteSet dummy;
+        int hi = class_char(dummy);
+        if (hi == -2) return false;
+        if (hi == -3 || hi < lo) { fail("invalid character class range"); return false; }
+        s |= range_set(lo, hi);
+      } else {
+        s.set(lo);
+      }
+    }
+    if (f.i) s = fold(s);
+    out = neg ? ~s : s;
+    return true;
+  }
+};
+
+// ---- repetition expansion + Glushkov -------------------------------------------------
+
+struct Builder {
+  std::vector<RNode>& pool;
+  int npos = 0;
+  std::string err;
+  explicit Builder(std::vector<RNode>& p) : pool(p) {}
+
+  int clone(int x) {
+    RNode n = pool[x];
+    for (int& k : n.kids) k = clone(k);
+    pool.push_back(n);
+    return (int)pool.size() - 1;
+  }
+
+  // Counts leaves (positions) after expansion without materialising it.
+  long count_pos(int x) const {
+    const RNode& n = pool[x];
+    switch (n.k) {
+      case RNode::kEmpty: return 0;
+      case RNode::kSet: case RNode::kBot: case RNode::kEot: return 1;
+      case RNode::kRepeat: {
+        long c = count_pos(n.kids[0]);
+        long reps = n.hi < 0 ? std::max(n.lo, 1) : n.hi;
+        return std::min(c * reps, 1L << 30);
+      }
+      default: {
+        long s = 0;
+        for (int k : n.kids) s = std::min(s + count_pos(k), 1L << 30);
+        return s;
+      }
+    }
+  }
+
+  int expand(int x) {
+    RNode n = pool[x];
+    if (n.k == RNode::kRepeat) {
+      int a = expand(n.kids[0]);
+      std::vector<int> items;
+      for (int r = 0; r < n.lo; ++r) items.push_back(r == 0 ? a : clone(a));
+      int used = n.lo;
+      if (n.hi < 0) {
+        int st = (int)pool.size();
+        RNode s;
+        s.k = RNode::kStar;
+        s.kids = {used == 0 ? a : clone(a)};
+        pool.push_back(s);
+        items.push_back(st);
+      } else if (n.hi > n.lo) {
+        // x{lo,hi} = x^lo (x(x(...)?)?)?  — nested optionals keep it linear
+        int tail = -1;
+        for (int r = n.hi - n.lo - 1; r >= 0; --r) {
+          int xr = (used == 0 && r == 0) ? a : clone(a);
+          int body = xr;
+          if (tail >= 0) {
+            RNode c;
+            c.k = RNode::kCat;
+            c.kids = {xr, tail};
+            pool.push_back(c);
+            body = (int)pool.size() - 1;
+          }
+          RNode q;
+          q.k = RNode::kQuest;
+          q.kids = {body};
+          pool.push_back(q);
+          tail = (int)pool.size() - 1;
+        }
+        items.push_back(tail);
+      }
+      if (items.empty()) {
+        RNode e;
+        e.k = RNode::kEmpty;
+        pool.push_back(e);
+        return (int)pool.size() - 1;
+      }
+      if (items.size() == 1) return items[0];
+      RNode c;
+      c.k = RNode::kCat;
+      c.kids = items;
+      pool.push_back(c);
+      return (int)pool.size() - 1;
+    }
+    for (size_t k = 0; k < n.kids.size(); ++k) {
+      int e = expand(n.kids[k]);
+      pool[x].kids[k] = e;
+    }
+    return x;
+  }
+
+  struct Info {
+    bool nullable;
+    uint64_t first, last;
+  };
+  std::vector<uint64_t> follow;
+  std::vector<ByteSet> pos_set;
+  uint64_t a_bot = 0, a_eot = 0;
+
+  Info glushkov(int x) {
+    const RNode& n = pool[x];
+    switch (n.k) {
+      case RNode::kEmpty: return {true, 0, 0};
+      case RNode::kSet: case RNode::kBot: case RNode::kEot: {
+        int p = npos++;
+        follow.push_back(0);
+        pos_set.push_back(n.k == RNode::kSet ? n.set : ByteSet());
+        if (n.k == RNode::kBot) a_bot |= 1ull << p;
+        if (n.k == RNode::kEot) a_eot |= 1ull << p;
+        return {false, 1ull << p, 1ull << p};
+      }
+      case RNode::kCat: {
+        Info acc{true, 0, 0};
+        bool firstk = true;
+        for (int k : n.kids) {
+          Info b = glushkov(k);
+          if (firstk) { acc = b; firstk = false; continue; }
+          for (int p = 0; p < 64; ++p)
+            if (acc.last >> p & 1) follow[p] |= b.first;
+          Info r;
+          r.nullable = acc.nullable && b.nullable;
+          r.first = acc.first | (acc.nullable ? b.first : 0);
+          r.last = b.last | (b.nullable ? acc.last : 0);
+          acc = r;
+        }
+        return acc;
+      }
+      case RNode::kAlt: {
+        Info acc{false, 0, 0};
+        for (int k : n.kids) {
+          Info b = glushkov(k);
+          acc.nullable = acc.nullable || b.nullable;
+          acc.first |= b.first;
+          acc.last |= b.last;
+        }
+        return acc;
+      }
+      case RNode::kStar: case RNode::kPlus: {
+        Info a = glushkov(n.kids[0]);
+        for (int p = 0; p < 64; ++p)
+          if (a.last >> p & 1) follow[p] |= a.first;
+        return {n.k == RNode::kStar ? true : a.nullable, a.first, a.last};
+      }
+      case RNode::kQuest: {
+        Info a = glushkov(n.kids[0]);
+        return {true, a.first, a.last};
+      }
+      default: return {true, 0, 0};
+    }
+  }
+};
+
+// Closure of an entered set at one boundary: assertion positions in `holds` pass and
+// enter their follow sets.  Returns the entered set; *acc = a passed position is final.
+uint64_t closure(uint64_t entered, uint64_t holds, const std::vector<uint64_t>& follow,
+                 uint64_t last, bool* acc) {
+  uint64_t passed = 0;
+  for (;;) {
+    uint64_t todo = entered & holds & ~passed;
+    if (!todo) break;
+    passed |= todo;
+    for (int p = 0; p < 64; ++p)
+      if (todo >> p & 1) entered |= follow[p];
+  }
+  if (acc) *acc = (passed & last) != 0;
+  return entered;
+}
+
+}  // namespace
+
+bool compile_regex(const uint8_t* pat, size_t n, GlushkovTables& out, std::string& err,
+                   int& err_code) {
+  Parser ps(pat, n);
+  int root = ps.parse();
+  if (root < 0) {
+    err = ps.err;
+    err_code = KLF_EPATTERN;
+    return false;
+  }
+  Builder b(ps.pool);
+  if (b.count_pos(root) > kMaxRegexPositions) {
+    err = "regex needs more than 64 Glushkov positions after {m,n} expansion";
+    err_code = KLF_ETOOBIG;
+    return false;
+  }
+  root = b.expand(root);
+  Builder::Info info = b.glushkov(root);
+  out = GlushkovTables();
+  out.npos = b.npos;
+  out.follow = b.follow;
+  out.first = info.first;
+  out.last = info.last;
+  for (auto& s : b.pos_set) {
+    std::vector<uint8_t> v(256);
+    for (int c = 0; c < 256; ++c) v[c] = s.test(c);
+    out.pos_bytes.push_back(v);
+  }
+  bool acc0 = false;
+  out.init0 = closure(info.first, b.a_bot, b.follow, info.last, &acc0);
+  out.accept_at_start = info.nullable || acc0;
+  bool acce = false;
+  closure(info.first, b.a_bot | b.a_eot, b.follow, info.last, &acce);
+  out.accept_empty = info.nullable || acce;
+  // end_accept: EOT positions from which a chain of EOT passes reaches `last`
+  uint64_t ea = 0;
+  for (;;) {
+    uint64_t nea = ea;
+    for (int p = 0; p < out.npos; ++p)
+      if ((b.a_eot >> p & 1) && (((info.last >> p) & 1) || (b.follow[p] & ea))) nea |= 1ull << p;
+    if (nea == ea) break;
+    ea = nea;
+  }
+  out.end_accept = ea;
+  return true;
+}
+
+bool glushkov_match(const GlushkovTables& g, const uint8_t* s, size_t n) {
+  if (n == 0) return g.accept_empty;
+  if (g.accept_at_start) return true;
+  uint64_t d = g.init0;
+  for (size_t i = 0; i < n; ++i) {
+    uint64_t c = 0;
+    for (int p = 0; p < g.npos; ++p)
+      if ((d >> p & 1) && g.pos_bytes[p][s[i]]) c |= 1ull << p;
+    if (c & g.last) return true;
+    uint64_t nd = g.first;
+    for (int p = 0; p < g.npos; ++p)
+      if (c >> p & 1) nd |= g.follow[p];
+    d = nd;
+  }
+  return (d & g.end_accept) != 0;
+}
+
+bool compile_set(const std::vector<std::vector<uint8_t>>& pats, const std::vector<uint32_t>& kinds,
+                 CompiledSet& out, std::string& err, int& err_code) {
+  out = CompiledSet();
+  if (pats.empty()) {
+    out.mode = CompiledSet::kNone;
+    return true;
+  }
+  if (pats.size() > (size_t)kMaxRegexes * 64) {
+    err = "too many patterns";
+    err_code = KLF_ETOOBIG;
+    return false;
+  }
+  std::vector<std::vector<uint8_t>> lits;
+  std::vector<GlushkovTables> rxs;
+  bool always = false;
+  for (size_t k = 0; k < pats.size(); ++k) {
+    if (kinds[k] == KLF_PAT_LITERAL) {
+      const auto& l = pats[k];
+      if (l.empty()) { always = true; continue; }  // bytes.Contains(x, "") == true
+      if (std::find(l.begin(), l.end(), (uint8_t)'\n') != l.end()) continue;  // never in content
+      lits.push_back(l);
+    } else if (kinds[k] == KLF_PAT_REGEX) {
+      GlushkovTables g;
+      if (!compile_regex(pats[k].data(), pats[k].size(), g, err, err_code)) {
+        err = "pattern " + std::to_string(k) + ": " + err;
+        return false;
+      }
+      if (g.accept_at_start && g.accept_empty) { always = true; continue; }
+      rxs.push_back(std::move(g));
+    } else {
+      err = "unknown pattern kind";
+      err_code = KLF_EINVAL;
+      return false;
+    }
+  }
+  if (rxs.size() > (size_t)kMaxRegexes) {
+    err = "more than 1024 regexes";
+    err_code = KLF_ETOOBIG;
+    return false;
+  }
+  if (always) { out.mode = CompiledSet::kAll; return true; }
+  // dedupe literals
+  std::sort(lits.begin(), lits.end());
+  lits.erase(std::unique(lits.begin(), lits.end()), lits.end());
+  if (lits.empty() && rxs.empty()) { out.mode = CompiledSet::kNever; return true; }
+  if (rxs.empty() && lits.size() == 1 && lits[0].size() <= 256) {
+    out.mode = CompiledSet::kLiteral1;
+    out.literal = lits[0];
+    return true;
+  }
+  out.mode = CompiledSet::kGeneral;
+
+  // ---- Aho-Corasick over the literals ----
+  if (!lits.empty()) {
+    out.ac_class.assign(256, 0);
+    int ncls = 1;
+    {
+      std::vector<bool> used(256, false);
+      for (auto& l : lits)
+        for (uint8_t c : l) used[c] = true;
+      for (int c = 0; c < 256; ++c)
+        if (used[c]) out.ac_class[c] = (uint8_t)std::min(ncls++, 255);
+      if (ncls > 256) { err = "literal alphabet too large"; err_code = KLF_ETOOBIG; return false; }
+    }
+    std::vector<std::map<int, int>> go(1);
+    std::vector<uint8_t> term(1, 0);
+    for (auto& l : lits) {
+      int s = 0;
+      for (uint8_t c : l) {
+        int cl = out.ac_class[c];
+        auto it = go[s].find(cl);
+        if (it == go[s].end()) {
+          go.push_back({});
+          term.push_back(0);
+          go[s][cl] = (int)go.size() - 1;
+          s = (int)go.size() - 1;
+        } else {
+          s = it->second;
+        }
+      }
+      term[s] = 1;
+    }
+    const size_t ns = go.size();
+    if (ns >= (1u << 31)) { err = "AC automaton too large"; err_code = KLF_ETOOBIG; return false; }
+    out.ac_states = (uint32_t)ns;
+    out.ac_classes = (uint32_t)ncls;
+    out.ac_next.assign(ns * ncls, 0);
+    out.ac_accept.assign(ns, 0);
+    std::vector<int> fail(ns, 0);
+    std::queue<int> q;
+    for (int c = 0; c < ncls; ++c) {
+      auto it = go[0].find(c);
+      int t = it == go[0].end() ? 0 : it->second;
+      out.ac_next[c] = (uint32_t)t;
+      if (t) { fail[t] = 0; q.push(t); }
+    }
+    out.ac_accept[0] = term[0];
+    while (!q.empty()) {
+      int s = q.front();
+      q.pop();
+      out.ac_accept[s] = term[s] | out.ac_accept[fail[s]];
+      for (int c = 0; c < ncls; ++c) {
+        auto it = go[s].find(c);
+        if (it != go[s].end()) {
+          int t = it->second;
+          fail[t] = (int)out.ac_next[(size_t)fail[s] * ncls + c];
+          out.ac_next[(size_t)s * ncls + c] = (uint32_t)t;
+          q.push(t);
+        } else {
+          out.ac_next[(size_t)s * ncls + c] = out.ac_next[(size_t)fail[s] * ncls + c];
+        }
+      }
+    }
+  }
+
+  // ---- regexes: shared byte classes by partition refinement ----
+  out.rx_count = (uint32_t)rxs.size();
+  if (!rxs.empty()) {
+    std::map<std::vector<uint64_t>, int> sig2cls;
+    out.rx_class.assign(256, 0);
+    const size_t words = rxs.size();
+    for (int c = 0; c < 256; ++c) {
+      std::vector<uint64_t> sig(words, 0);
+      for (size_t r = 0; r < rxs.size(); ++r)
+        for (int p = 0; p < rxs[r].npos; ++p)
+          if (rxs[r].pos_bytes[p][c]) sig[r] |= 1ull << p;
+      auto it = sig2cls.find(sig);
+      int cl;
+      if (it == sig2cls.end()) { cl = (int)sig2cls.size(); sig2cls[sig] = cl; }
+      else cl = it->second;
+      out.rx_class[c] = (uint8_t)cl;
+    }
+    out.rx_classes = (uint32_t)sig2cls.size();
+    out.rx_b.assign((size_t)rxs.size() * out.rx_classes, 0);
+    for (auto& kv : sig2cls)
+      for (size_t r = 0; r < rxs.size(); ++r) out.rx_b[r * out.rx_classes + kv.second] = kv.first[r];
+    out.rx_follow.assign((size_t)rxs.size() * 64, 0);
+    for (size_t r = 0; r < rxs.size(); ++r) {
+      for (int p = 0; p < rxs[r].npos; ++p) out.rx_follow[r * 64 + p] = rxs[r].follow[p];
+      out.rx_first.push_back(rxs[r].first);
+      out.rx_last.push_back(rxs[r].last);
+      out.rx_init0.push_back(rxs[r].init0);
+      out.rx_end.push_back(rxs[r].end_accept);
+      out.rx_flags.push_back((rxs[r].accept_at_start ? 1u : 0u) | (rxs[r].accept_empty ? 2u : 0u));
+    }
+  }
+  return true;
+}
+
+}  // namespace klf

@@ -1,0 +1,77 @@
+// klf_patterns.hpp — host-side compilation of --grep / --match pattern sets into the
+// tables the GPU matchers read.
+//
+//   * literals (Go bytes.Contains) -> one fused literal scan (single literal) or an
+//     Aho-Corasick DFA over byte classes (several literals);
+//   * regexes (Go regexp.Match, SPEC.md S5 RE2 subset) -> one Glushkov position
+//     automaton per regex, simulated bit-parallel (one 64-bit state word per regex).
+//
+// Zero-width assertions (^ $ \A \z) are Glushkov positions evaluated at text
+// boundaries; content never contains '\n', so only the two ends of the content can
+// satisfy them (SPEC.md S5).
+#pragma once
+#include <stdint.h>
+
+#include <string>
+#include <vector>
+
+namespace klf {
+
+constexpr int kMaxRegexPositions = 64;  // one u64 state word per regex
+constexpr int kMaxRegexes = 1024;
+
+struct GlushkovTables {
+  // per-position tables (bit p = position p)
+  std::vector<uint64_t> follow;  // [npos]
+  uint64_t first = 0;            // entered at every boundary (unanchored search)
+  uint64_t last = 0;             // a completed position in `last` = match
+  uint64_t init0 = 0;            // entered set at boundary 0 (BOT closure of first)
+  uint64_t end_accept = 0;       // entered at the end boundary -> match via EOT closure
+  bool accept_at_start = false;  // matches at boundary 0 of a non-empty content
+  bool accept_empty = false;     // matches the empty content
+  std::vector<std::vector<uint8_t>> pos_bytes;  // byte set (256 flags) per position
+  int npos = 0;
+};
+
+struct CompiledSet {
+  enum Mode : uint32_t {
+    kNone = 0,      // no patterns: G = every line
+    kNever = 1,     // patterns given but none can ever match content
+    kAll = 2,       // some pattern matches every content: G = parsed lines
+    kLiteral1 = 3,  // exactly one effective pattern, a literal of length 1..256
+    kGeneral = 4,   // AC over literals and/or Glushkov regexes
+  };
+  Mode mode = kNone;
+  std::vector<uint8_t> literal;  // kLiteral1
+
+  // kGeneral: Aho-Corasick over the literals (empty when no literal).
+  uint32_t ac_states = 0;
+  uint32_t ac_classes = 0;
+  std::vector<uint8_t> ac_class;    // [256] byte -> class
+  std::vector<uint32_t> ac_next;    // [states * classes]
+  std::vector<uint8_t> ac_accept;   // [states] 1 if a literal ends here (via fail links)
+
+  // kGeneral: regexes.  Byte classes shared by all regexes (partition refinement).
+  uint32_t rx_count = 0;
+  uint32_t rx_classes = 0;
+  std::vector<uint8_t> rx_class;      // [256]
+  std::vector<uint64_t> rx_b;         // [rx_count * rx_classes] positions accepting class
+  std::vector<uint64_t> rx_follow;    // [rx_count * 64]
+  std::vector<uint64_t> rx_first, rx_last, rx_init0, rx_end;  // [rx_count]
+  std::vector<uint32_t> rx_flags;     // bit0 accept_at_start, bit1 accept_empty
+};
+
+// Parses one Go-syntax regex (SPEC.md S5) and builds its Glushkov tables.
+// Returns false with `err` set for syntax outside the subset or > 64 positions.
+bool compile_regex(const uint8_t* pat, size_t n, GlushkovTables& out, std::string& err,
+                   int& err_code);
+
+// Compiles a whole OR'ed pattern set.  kinds[i]: 0 literal, 1 regex.
+bool compile_set(const std::vector<std::vector<uint8_t>>& pats, const std::vector<uint32_t>& kinds,
+                 CompiledSet& out, std::string& err, int& err_code);
+
+// Host reference simulation of one compiled regex on a content (used by unit tests of
+// the compiler through klf_debug_regex_match; the GPU kernel runs the same recurrence).
+bool glushkov_match(const GlushkovTables& g, const uint8_t* s, size_t n);
+
+}  // namespace klf

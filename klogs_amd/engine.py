@@ -1,0 +1,313 @@
+"""ctypes binding of the C ABI in ``include/klf.h`` (``klogs_amd/_lib/libklf.so``).
+
+This is the same surface the Go host binds through cgo; Python uses it
+for the tests and ``bench.py``.  There is deliberately no fallback: if the native
+library is missing, importing this module raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from dataclasses import dataclass
+from pathlib import Path
+from typing import Iterable, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+_LIB_DIR = Path(__file__).resolve().parent / "_lib"
+_LIB_PATH = _LIB_DIR / "libklf.so"
+
+KLF_OK = 0
+KLF_EINVAL = -1
+KLF_ENOMEM = -2
+KLF_EHIP = -3
+KLF_EPATTERN = -4
+KLF_ETOOBIG = -5
+KLF_ESTATE = -6
+KLF_PAT_LITERAL = 0
+KLF_PAT_REGEX = 1
+GO_ZERO_TIME = (-62135596800, 0)
+
+MODE_NAMES = {0: "none", 1: "never", 2: "all", 3: "literal1", 4: "general"}
+
+
+class KlfError(RuntimeError):
+    def __init__(self, code: int, msg: str = ""):
+        self.code = code
+        super().__init__(f"klf error {code}: {msg}")
+
+
+class _Time(C.Structure):
+    _fields_ = [("sec", C.c_int64), ("nsec", C.c_int32), ("_reserved", C.c_int32)]
+
+
+class _Pattern(C.Structure):
+    _fields_ = [("bytes", C.c_void_p), ("len", C.c_uint32), ("kind", C.c_uint32)]
+
+
+class _Config(C.Structure):
+    _fields_ = [("device", C.c_int32), ("n_patterns", C.c_uint32), ("patterns", C.POINTER(_Pattern)),
+                ("hip_stream", C.c_void_p), ("staging_hint", C.c_uint64)]
+
+
+class _Filter(C.Structure):
+    _fields_ = [("since", _Time), ("tail", C.c_int64), ("flags", C.c_uint32), ("_reserved", C.c_uint32)]
+
+
+class _Counts(C.Structure):
+    _fields_ = [("lines", C.c_uint64), ("parsed", C.c_uint64), ("since_ok", C.c_uint64),
+                ("matched", C.c_uint64), ("selected", C.c_uint64), ("out_bytes", C.c_uint64)]
+
+    def as_dict(self):
+        return {k: int(getattr(self, k)) for k, _ in self._fields_}
+
+
+# Every symbol include/klf.h declares, with its ctypes signature (checked by the CPU tests).
+SIGNATURES = {
+    "klf_open": (C.c_int, [C.POINTER(_Config), C.POINTER(C.c_void_p)]),
+    "klf_close": (None, [C.c_void_p]),
+    "klf_last_error": (C.c_char_p, [C.c_void_p]),
+    "klf_strerror": (C.c_char_p, [C.c_int]),
+    "klf_stage": (C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p, C.c_size_t]),
+    "klf_set_streams": (C.c_int, [C.c_void_p, C.c_uint32]),
+    "klf_reset": (C.c_int, [C.c_void_p]),
+    "klf_run": (C.c_int, [C.c_void_p, C.POINTER(_Filter), C.POINTER(C.c_void_p)]),
+    "klf_layout": (C.c_int, [C.c_uint32, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
+    "klf_run_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.POINTER(C.c_uint64),
+                                 C.POINTER(C.c_uint64), C.POINTER(_Filter), C.POINTER(C.c_void_p)]),
+    "klf_result_stream": (C.c_int, [C.c_void_p, C.c_uint32, C.POINTER(C.c_void_p), C.POINTER(C.c_uint64),
+                                    C.POINTER(_Counts)]),
+    "klf_result_lines": (C.c_int, [C.c_void_p, C.c_uint32, C.POINTER(C.c_void_p), C.POINTER(C.c_uint64)]),
+    "klf_result_match_bits": (C.c_int, [C.c_void_p, C.c_uint32, C.POINTER(C.c_void_p), C.POINTER(C.c_uint64)]),
+    "klf_result_device_out": (C.c_int, [C.c_void_p, C.c_uint32, C.POINTER(C.c_void_p), C.POINTER(C.c_uint64),
+                                        C.POINTER(C.c_uint64)]),
+    "klf_result_timing": (C.c_int, [C.c_void_p, C.POINTER(C.c_double), C.c_uint32, C.POINTER(C.c_uint32)]),
+    "klf_result_totals": (C.c_int, [C.c_void_p, C.POINTER(_Counts)]),
+    "klf_result_free": (None, [C.c_void_p]),
+    "klf_parse_rfc3339nano": (C.c_int, [C.c_void_p, C.c_size_t, C.POINTER(_Time)]),
+    "klf_debug_compile": (C.c_int, [C.POINTER(_Pattern), C.c_uint32, C.POINTER(C.c_uint32), C.c_char_p,
+                                    C.c_size_t]),
+    "klf_debug_match": (C.c_int, [C.POINTER(_Pattern), C.c_uint32, C.c_void_p, C.c_size_t,
+                                  C.POINTER(C.c_int)]),
+}
+
+
+def _load():
+    # One HIP runtime per process: when PyTorch is present its bundled libamdhip64.so.7
+    # must be the one libklf.so binds to (same SONAME), so device pointers and streams
+    # from torch are valid here.  Loading libklf first would pull /opt/rocm's runtime
+    # in beside torch's, and whichever initialises second sees no device.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+    if not _LIB_PATH.exists():
+        raise ImportError(f"{_LIB_PATH} is missing: build it with `python -m klogs_amd._build` "
+                          "(the filter has no CPU fallback)")
+    lib = C.CDLL(str(_LIB_PATH))
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    return lib
+
+
+_lib = _load()
+
+
+def lib():
+    return _lib
+
+
+def _check(rc: int, eng=None):
+    if rc != KLF_OK:
+        msg = _lib.klf_strerror(rc).decode()
+        if eng is not None:
+            detail = _lib.klf_last_error(eng).decode()
+            if detail:
+                msg += ": " + detail
+        raise KlfError(rc, msg)
+
+
+def _patterns(grep: Sequence[bytes], match: Sequence[bytes]):
+    items = [(bytes(g), KLF_PAT_LITERAL) for g in grep] + [(bytes(m), KLF_PAT_REGEX) for m in match]
+    keep = [C.create_string_buffer(b, len(b) or 1) for b, _ in items]
+    arr = (_Pattern * max(1, len(items)))()
+    for i, ((b, kind), buf) in enumerate(zip(items, keep)):
+        arr[i].bytes = C.cast(buf, C.c_void_p)
+        arr[i].len = len(b)
+        arr[i].kind = kind
+    return arr, len(items), keep
+
+
+def _filter(since: Optional[Tuple[int, int]], tail: int) -> _Filter:
+    f = _Filter()
+    s = GO_ZERO_TIME if since is None else since
+    f.since.sec, f.since.nsec = int(s[0]), int(s[1])
+    f.tail = int(tail)
+    return f
+
+
+def layout(lens: Sequence[int]) -> Tuple[np.ndarray, int]:
+    n = len(lens)
+    L = (C.c_uint64 * max(1, n))(*[int(x) for x in lens])
+    B = (C.c_uint64 * max(1, n))()
+    tot = C.c_uint64()
+    _check(_lib.klf_layout(n, L, B, C.byref(tot)))
+    return np.array(B[:n], dtype=np.uint64), int(tot.value)
+
+
+def parse_rfc3339nano(b: bytes) -> Optional[Tuple[int, int]]:
+    t = _Time()
+    buf = C.create_string_buffer(b, len(b) or 1)
+    rc = _lib.klf_parse_rfc3339nano(buf, len(b), C.byref(t))
+    return (t.sec, t.nsec) if rc == KLF_OK else None
+
+
+def debug_compile(grep=(), match=()) -> Tuple[int, str, str]:
+    arr, n, keep = _patterns(grep, match)
+    mode = C.c_uint32()
+    err = C.create_string_buffer(512)
+    rc = _lib.klf_debug_compile(arr, n, C.byref(mode), err, 512)
+    return rc, MODE_NAMES.get(mode.value, "?"), err.value.decode()
+
+
+def debug_match(content: bytes, grep=(), match=()) -> bool:
+    arr, n, keep = _patterns(grep, match)
+    m = C.c_int()
+    buf = C.create_string_buffer(content, len(content) or 1)
+    _check(_lib.klf_debug_match(arr, n, buf, len(content), C.byref(m)))
+    return bool(m.value)
+
+
+@dataclass
+class StreamOut:
+    out: bytes
+    counts: dict
+
+
+class Result:
+    def __init__(self, ptr: int, n_streams: int, eng):
+        self._p = C.c_void_p(ptr)
+        self.n_streams = n_streams
+        self._eng = eng
+
+    def stream(self, i: int) -> StreamOut:
+        p = C.c_void_p()
+        n = C.c_uint64()
+        c = _Counts()
+        _check(_lib.klf_result_stream(self._p, i, C.byref(p), C.byref(n), C.byref(c)))
+        data = C.string_at(p.value, n.value) if n.value else b""
+        return StreamOut(data, c.as_dict())
+
+    def lines(self, i: int) -> np.ndarray:
+        p = C.c_void_p()
+        n = C.c_uint64()
+        _check(_lib.klf_result_lines(self._p, i, C.byref(p), C.byref(n)))
+        cnt = n.value + 1
+        if n.value == 0:
+            return np.zeros(1, dtype=np.uint64) if p.value is None else np.frombuffer(
+                C.string_at(p.value, 8), dtype=np.uint64).copy()
+        return np.frombuffer(C.string_at(p.value, 8 * cnt), dtype=np.uint64).copy()
+
+    def match_bits(self, i: int) -> bytes:
+        p = C.c_void_p()
+        n = C.c_uint64()
+        _check(_lib.klf_result_match_bits(self._p, i, C.byref(p), C.byref(n)))
+        return C.string_at(p.value, n.value) if n.value else b""
+
+    def device_out(self, i: int) -> Tuple[int, int, int]:
+        p = C.c_void_p()
+        off = C.c_uint64()
+        n = C.c_uint64()
+        _check(_lib.klf_result_device_out(self._p, i, C.byref(p), C.byref(off), C.byref(n)))
+        return p.value or 0, off.value, n.value
+
+    def timing(self) -> List[float]:
+        ms = (C.c_double * 6)()
+        k = C.c_uint32()
+        _check(_lib.klf_result_timing(self._p, ms, 6, C.byref(k)))
+        return list(ms[: k.value])
+
+    def totals(self) -> dict:
+        c = _Counts()
+        _check(_lib.klf_result_totals(self._p, C.byref(c)))
+        return c.as_dict()
+
+    def free(self):
+        if self._p:
+            _lib.klf_result_free(self._p)
+            self._p = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+class Engine:
+    """One engine = one GPU (klf_open).  grep: literals (Go bytes.Contains); match: Go
+    regexp subset (SPEC.md S5)."""
+
+    def __init__(self, device: int = 0, grep: Iterable[bytes] = (), match: Iterable[bytes] = (),
+                 hip_stream: Optional[int] = None):
+        arr, n, self._keep = _patterns(list(grep), list(match))
+        cfg = _Config()
+        cfg.device = device
+        cfg.n_patterns = n
+        cfg.patterns = arr
+        cfg.hip_stream = hip_stream
+        h = C.c_void_p()
+        rc = _lib.klf_open(C.byref(cfg), C.byref(h))
+        self._h = h
+        if rc != KLF_OK:
+            msg = _lib.klf_strerror(rc).decode()
+            if h.value:
+                msg += ": " + _lib.klf_last_error(h).decode()
+                _lib.klf_close(h)
+                self._h = C.c_void_p()
+            raise KlfError(rc, msg)
+
+    def set_streams(self, n: int):
+        _check(_lib.klf_set_streams(self._h, n), self._h)
+
+    def stage(self, stream_id: int, data: bytes):
+        buf = C.create_string_buffer(data, len(data) or 1)
+        _check(_lib.klf_stage(self._h, stream_id, buf, len(data)), self._h)
+
+    def reset(self):
+        _check(_lib.klf_reset(self._h), self._h)
+
+    def run(self, since=None, tail: int = -1, n_streams: Optional[int] = None) -> Result:
+        f = _filter(since, tail)
+        r = C.c_void_p()
+        _check(_lib.klf_run(self._h, C.byref(f), C.byref(r)), self._h)
+        return Result(r.value or 0, n_streams if n_streams is not None else 0, self)
+
+    def run_device(self, d_ptr: int, seg_base: Sequence[int], lens: Sequence[int], since=None,
+                   tail: int = -1) -> Result:
+        n = len(lens)
+        B = (C.c_uint64 * max(1, n))(*[int(x) for x in seg_base])
+        L = (C.c_uint64 * max(1, n))(*[int(x) for x in lens])
+        f = _filter(since, tail)
+        r = C.c_void_p()
+        _check(_lib.klf_run_device(self._h, C.c_void_p(d_ptr), n, B, L, C.byref(f), C.byref(r)), self._h)
+        return Result(r.value or 0, n, self)
+
+    def close(self):
+        if self._h:
+            _lib.klf_close(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()

@@ -1,0 +1,97 @@
+"""HIP engine vs the oracles, through the C ABI (libklf.so) on the GPU."""
+import random
+
+import numpy as np
+import pytest
+
+import c_oracle as co
+import klf_oracle as po
+from klogs_amd import engine as E
+from klogs_amd import synth
+
+pytestmark = pytest.mark.gpu
+
+GZ = po.GO_ZERO_TIME
+
+
+def run_engine(streams, since=None, tail=-1, grep=(), match=()):
+    with E.Engine(0, grep=grep, match=match) as eng:
+        eng.set_streams(len(streams))
+        for i, s in enumerate(streams):
+            if s:
+                eng.stage(i, s)
+        r = eng.run(since=since, tail=tail, n_streams=len(streams))
+        res = []
+        for i in range(len(streams)):
+            so = r.stream(i)
+            bits = r.match_bits(i) if (grep or match) else None
+            res.append((so.out, r.lines(i), bits, so.counts))
+        r.free()
+        return res
+
+
+def check_against_c(streams, since, tail, grep):
+    got = run_engine(streams, since=since, tail=tail, grep=grep)
+    for i, s in enumerate(streams):
+        out, lo, bits, c = co.filter_stream(s, since or GZ, tail, list(grep))
+        g_out, g_lo, g_bits, g_c = got[i]
+        assert g_out == out, f"stream {i}: out differs ({len(g_out)} vs {len(out)})"
+        assert np.array_equal(g_lo, lo), f"stream {i}: line offsets differ"
+        if grep:
+            assert g_bits == bits, f"stream {i}: match bits differ"
+        for k in ("lines", "parsed", "since_ok", "selected", "out_bytes"):
+            assert g_c[k] == c[k], (i, k, g_c, c)
+        if grep:
+            assert g_c["matched"] == c["matched"], (i, g_c, c)
+
+
+@pytest.mark.parametrize("kind", [synth.TEXT, synth.JSON])
+@pytest.mark.parametrize("tail", [-1, 0, 1, 100])
+def test_single_stream_synthetic(gpu, kind, tail):
+    d = synth.generate(kind, 11, 0, 3_000_000)
+    check_against_c([d], (synth.T0 + 3300, 0), tail, [])
+    check_against_c([d], (synth.T0 + 3300, 0), tail, [synth.NEEDLE])
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_adversarial(gpu, seed):
+    rng = random.Random(seed)
+    d = synth.generate(synth.ADVERSARIAL, seed, 0, 4000, drop_final_nl=bool(seed & 1), permille=30)
+    for _ in range(6):
+        since = rng.choice([None, (synth.T0 + 1800, 0), (synth.T0 + 600, 123)])
+        tail = rng.choice([-1, 0, 1, 7, 3999, 10000])
+        grep = rng.choice([[], [synth.NEEDLE], [b"ms"], [b"Z "]])
+        check_against_c([d], since, tail, grep)
+
+
+def test_multi_stream_and_empty(gpu):
+    streams = [synth.generate(synth.TEXT, 5, i, 50_000 * (i % 4)) for i in range(9)]
+    streams.append(b"")
+    streams.append(b"no newline at all")
+    streams.append(b"\n\n\n")
+    streams.append(synth.generate(synth.ADVERSARIAL, 9, 2, 500, drop_final_nl=True))
+    for since, tail, grep in [(None, -1, []), ((synth.T0 + 1200, 0), 10, []), (None, 5, [synth.NEEDLE]),
+                              (None, 3, [b"pod"])]:
+        check_against_c(streams, since, tail, grep)
+
+
+def _golden():
+    import json
+    from pathlib import Path
+    g = Path(__file__).resolve().parent / "golden"
+    return g, json.loads((g / "manifest.json").read_text())["cases"]
+
+
+@pytest.mark.parametrize("idx", range(len(_golden()[1])))
+def test_golden_fixtures(gpu, idx):
+    g, cases = _golden()
+    c = cases[idx]
+    data = (g / c["input"]).read_bytes()
+    grep = [bytes.fromhex(x) for x in c["grep"]]
+    match = [bytes.fromhex(x) for x in c["match"]]
+    out, lo, bits, cnt = run_engine([data], since=tuple(c["since"]), tail=c["tail"], grep=grep, match=match)[0]
+    assert out == (g / c["expect_out"]).read_bytes(), c["name"]
+    assert lo.tolist() == np.load(g / c["expect_lines"]).tolist(), c["name"]
+    if c["expect_bits"] is not None:
+        assert bits.hex() == c["expect_bits"], c["name"]
+    assert [cnt["lines"], cnt["parsed"], cnt["since_ok"], cnt["matched"], cnt["selected"]] == c["expect_counts"]
