@@ -59,6 +59,8 @@ struct klf_engine {
   DevBuf d_lit, d_ac_class, d_ac_next, d_ac_accept, d_rx_class, d_rx_b, d_rx_follow, d_rx_vec, d_rx_flags;
   klf::DevPatterns dpats;
   // workspace
+  std::vector<SegDesc> last_segs;  // tile_seg cache key
+  DevBuf d_tile_seg;
   DevBuf d_batch, d_segs, d_status, d_cstatus, d_counters, d_line_off, d_meta, d_bits, d_tile_cnt,
       d_segout, d_wpre, d_out;
   hipEvent_t ev[6] = {};
@@ -215,7 +217,7 @@ extern "C" void klf_close(klf_engine* e) {
   for (DevBuf* b : {&e->d_lit, &e->d_ac_class, &e->d_ac_next, &e->d_ac_accept, &e->d_rx_class, &e->d_rx_b,
                     &e->d_rx_follow, &e->d_rx_vec, &e->d_rx_flags, &e->d_batch, &e->d_segs, &e->d_status,
                     &e->d_cstatus, &e->d_counters, &e->d_line_off, &e->d_meta, &e->d_bits, &e->d_tile_cnt,
-                    &e->d_segout, &e->d_wpre, &e->d_out})
+                    &e->d_segout, &e->d_wpre, &e->d_out, &e->d_tile_seg})
     b->release();
   for (auto& x : e->ev)
     if (x) (void)hipEventDestroy(x);
@@ -309,10 +311,17 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
   if (nsegs == 0) { *out = r; return KLF_OK; }
 
   hipStream_t st = e->stream;
-  HIPCHK(e, e->d_segs.ensure(nsegs * sizeof(SegDesc)), "alloc segs");
-  HIPCHK(e, hipMemcpyAsync(e->d_segs.p, segs.data(), nsegs * sizeof(SegDesc), hipMemcpyHostToDevice, st), "H2D segs");
+  bool same_layout = segs.size() == e->last_segs.size() && e->d_tile_seg.cap >= ntiles * 4 &&
+                     memcmp(segs.data(), e->last_segs.data(), segs.size() * sizeof(SegDesc)) == 0;
+  if (!same_layout) {
+    HIPCHK(e, e->d_segs.ensure(nsegs * sizeof(SegDesc)), "alloc segs");
+    HIPCHK(e, hipMemcpyAsync(e->d_segs.p, segs.data(), nsegs * sizeof(SegDesc), hipMemcpyHostToDevice, st),
+           "H2D segs");
+    HIPCHK(e, hipStreamSynchronize(st), "sync segs");
+    HIPCHK(e, e->d_tile_seg.ensure(ntiles * 4), "alloc tile_seg");
+  }
   HIPCHK(e, e->d_status.ensure(ntiles * 8), "alloc status");
-  HIPCHK(e, e->d_counters.ensure(64), "alloc counters");
+  HIPCHK(e, e->d_counters.ensure(klf::kNumCounters * 4), "alloc counters");
   HIPCHK(e, e->d_tile_cnt.ensure(ntiles * 8), "alloc tile counters");
   HIPCHK(e, e->d_segout.ensure(nsegs * sizeof(SegOut)), "alloc segout");
   HIPCHK(e, e->d_wpre.ensure((nsegs + 1) * 8), "alloc wpre");
@@ -329,6 +338,8 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
     a.segs = e->d_segs.as<SegDesc>();
     a.nsegs = nsegs;
     a.ntiles = (uint32_t)ntiles;
+    a.tile_seg = e->d_tile_seg.as<uint32_t>();
+    a.build_tiles = (!same_layout && attempt == 0) ? 1u : 0u;
     a.since_sec = f->since.sec;
     a.since_nsec = f->since.nsec;
     a.tail = f->tail;
@@ -354,7 +365,8 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
     HIPCHK(e, hipMemcpyAsync(r->so.data(), e->d_segout.p, nsegs * sizeof(SegOut), hipMemcpyDeviceToHost, st), "D2H segout");
     HIPCHK(e, hipMemcpyAsync(counters, e->d_counters.p, sizeof(counters), hipMemcpyDeviceToHost, st), "D2H counters");
     HIPCHK(e, hipStreamSynchronize(st), "sync");
-    if (counters[2] & 2u) { delete r; return set_err(e, KLF_EHIP, "look-back spin timeout"); }
+    e->last_segs = segs;
+    if (counters[2] & 2u) { delete r; e->last_segs.clear(); return set_err(e, KLF_EHIP, "look-back spin timeout"); }
     if (counters[2] & 1u) {  // more lines than the capacity estimate: rerun with the exact count
       cap = r->so[nsegs - 1].line_hi + 2;
       continue;

@@ -51,25 +51,24 @@ constexpr uint64_t kFlagMask = 3ull << 62;
 constexpr uint32_t kSpinLimit = 1u << 24;
 
 // ---- scan summary monoid -----------------------------------------------------------
-// (count of line-end events, IND = a line starts inside the span, S = a space was seen
-// since the current line's start, P = the current line's prefix parsed).
+// (count of line-end events, IND = a line starts inside the span, P = the line open at
+// the span's end has a parseable prefix).
 // combine(a, b) with a before b.  Packed u32 (thread/block level) and u64 (tiles).
-constexpr uint32_t kInd32 = 1u << 16, kS32 = 1u << 17, kP32 = 1u << 18;
+constexpr uint32_t kInd32 = 1u << 16, kP32 = 1u << 17;
 __device__ __forceinline__ uint32_t comb32(uint32_t a, uint32_t b) {
   const uint32_t cnt = (a & 0xFFFFu) + (b & 0xFFFFu);
-  const uint32_t sp = (b & kInd32) ? (b & (kS32 | kP32)) : (((a | b) & kS32) | (a & kP32));
-  return cnt | ((a | b) & kInd32) | sp;
+  const uint32_t pb = (b & kInd32) ? (b & kP32) : (a & kP32);
+  return cnt | ((a | b) & kInd32) | pb;
 }
 constexpr uint64_t kCnt64 = (1ull << 59) - 1;
-constexpr uint64_t kP64 = 1ull << 59, kS64 = 1ull << 60, kInd64 = 1ull << 61;
+constexpr uint64_t kP64 = 1ull << 59, kInd64 = 1ull << 61;
 __device__ __forceinline__ uint64_t comb64(uint64_t a, uint64_t b) {
   const uint64_t cnt = ((a & kCnt64) + (b & kCnt64)) & kCnt64;
-  const uint64_t sp = (b & kInd64) ? (b & (kS64 | kP64)) : (((a | b) & kS64) | (a & kP64));
-  return cnt | ((a | b) & kInd64) | sp;
+  const uint64_t pb = (b & kInd64) ? (b & kP64) : (a & kP64);
+  return cnt | ((a | b) & kInd64) | pb;
 }
 __device__ __forceinline__ uint64_t widen(uint32_t x) {
-  return (uint64_t)(x & 0xFFFFu) | ((x & kInd32) ? kInd64 : 0) | ((x & kS32) ? kS64 : 0) |
-         ((x & kP32) ? kP64 : 0);
+  return (uint64_t)(x & 0xFFFFu) | ((x & kInd32) ? kInd64 : 0) | ((x & kP32) ? kP64 : 0);
 }
 
 __device__ __forceinline__ uint32_t wave_incl_scan_summary(uint32_t x, int lane) {
@@ -97,34 +96,53 @@ __device__ __forceinline__ T wave_incl_scan_add(T x, int lane) {
   return x;
 }
 
-// Decoupled look-back of one tile over a chain of u64 words; returns the exclusive
-// prefix (no flag bits).  `agg` has no flag bits.  Spins are bounded: a timeout sets
-// counters[2] bit 1 so the host reports an error instead of the GPU hanging.
+// Decoupled look-back of one tile over a chain of u64 words, run by ONE WAVE: each
+// round reads 64 predecessors at once, waits until all of them have published
+// (aggregate or inclusive), stops at the nearest inclusive prefix and folds the window
+// with an ordered shuffle reduction (earlier tiles sit at higher lanes).  Returns the
+// exclusive prefix (no flag bits) in every lane.  `agg` has no flag bits.  Spins are
+// bounded: a timeout sets counters[2] bit 1 so the host reports an error instead of the
+// GPU hanging.
 template <class Comb>
-__device__ uint64_t lookback(uint64_t* st, uint32_t idx, uint64_t agg, uint64_t ident, Comb comb,
-                             uint32_t* err_flag) {
+__device__ uint64_t lookback_wave(uint64_t* st, uint32_t idx, uint64_t agg, uint64_t ident, Comb comb,
+                                  uint32_t* err_flag, int lane) {
   if (idx == 0) {
-    atomic_store_u64(&st[0], agg | kFlagP);
+    if (lane == 0) atomic_store_u64(&st[0], agg | kFlagP);
     return ident;
   }
-  atomic_store_u64(&st[idx], agg | kFlagA);
+  if (lane == 0) atomic_store_u64(&st[idx], agg | kFlagA);
   uint64_t acc = ident;
-  int64_t j = (int64_t)idx - 1;
+  int64_t hi = (int64_t)idx - 1;
   for (;;) {
-    uint64_t w;
+    const int64_t j = hi - lane;
+    uint64_t w = kFlagP | ident;  // before tile 0: acts as an empty inclusive prefix
+    bool ready = j < 0;
     uint32_t spins = 0;
-    while (((w = atomic_load_u64(&st[j])) & kFlagMask) == 0) {
-      __builtin_amdgcn_s_sleep(2);
+    for (;;) {
+      if (!ready) {
+        w = atomic_load_u64(&st[j]);
+        ready = (w & kFlagMask) != 0;
+      }
+      if (__all(ready)) break;
+      __builtin_amdgcn_s_sleep(1);
       if (++spins > kSpinLimit) {
-        atomicOr(err_flag, 2u);
-        break;
+        if (lane == 0) atomicOr(err_flag, 2u);
+        return acc;
       }
     }
-    acc = comb(w & ~kFlagMask, acc);
-    if ((w & kFlagMask) == kFlagP || spins > kSpinLimit || j == 0) break;
-    --j;
+    const uint64_t pmask = __ballot((w & kFlagMask) == kFlagP);
+    const int plane = pmask ? __ffsll((unsigned long long)pmask) - 1 : 64;
+    uint64_t v = lane <= plane ? (w & ~kFlagMask) : ident;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint64_t o = __shfl_down(v, d, 64);
+      if (lane + d < 64) v = comb(o, v);
+    }
+    acc = comb(__shfl(v, 0, 64), acc);
+    if (plane < 64) break;
+    hi -= 64;
   }
-  atomic_store_u64(&st[idx], comb(acc, agg) | kFlagP);
+  if (lane == 0) atomic_store_u64(&st[idx], comb(acc, agg) | kFlagP);
   return acc;
 }
 
@@ -178,6 +196,14 @@ struct GlobalBytes {
   }
 };
 
+// Cold-path parse (kept out of line so the hot loop's register budget stays at 64).
+__device__ __attribute__((noinline)) bool parse_at_cold(const uint8_t* lds, const uint8_t* seg, int64_t p0,
+                                                       int64_t rel_lo, int64_t seg_len, uint32_t* plen) {
+  TsResult r;
+  LineBytes gb{lds, seg, p0, rel_lo, seg_len};
+  return parse_line_prefix(gb, r, *plen);
+}
+
 __device__ __forceinline__ uint16_t make_meta(bool ok, bool since_ok, uint32_t plen) {
   if (!ok) return 0;
   const uint32_t pl = plen < kPlenEscape ? plen : kPlenEscape;
@@ -185,25 +211,163 @@ __device__ __forceinline__ uint16_t make_meta(bool ok, bool since_ok, uint32_t p
 }
 
 // ============================================================== K1: the scan kernel ==
-// One 256-thread workgroup per 16 KiB tile (persistent, tiles handed out by a ticket
-// counter so look-back predecessors are always running).  Thread t owns bytes
-// [64t, 64t+64) of the tile.
+// Persistent 256-thread workgroups, one 16 KiB tile at a time; thread t owns bytes
+// [64t, 64t+64).  Per tile:
+//   1. claim (ticket groups, below) and stage tile + halo in LDS;
+//   2. line-end events ('\n', and the stream's last byte) -> counts -> block reduce ->
+//      publish the tile's AGGREGATE immediately (the chain is a plain line count, so a
+//      successor's look-back never waits on our parsing);
+//   3. parse every line starting in the tile into LDS (meta + tile-relative offset);
+//   4. look-back -> the tile's first global line index;
+//   5. coalesced copy-out of line_off / meta; fused literal grep on the rare first+last
+//      byte candidates.  Whether a hit lies in the content (after the first ' ') comes
+//      from the line's plen; for a line begun in an earlier tile, from a backward scan
+//      to its start and a re-parse (rare).
+// Tiles with more than kMaxTileLines line starts (< 16 B per line: never kubelet
+// output) take a slower per-thread path with the same results.
+
+constexpr int kMaxTileLines = 1024;
+
+// 4-bit mask of the zero bytes of x (exact): bit k set iff byte k of x is 0.
+__device__ __forceinline__ uint32_t zmask4(uint32_t x) {
+  const uint32_t z = ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x | 0x7F7F7F7Fu);  // 0x80 per zero byte
+  return (z * 0x00204081u) >> 28;
+}
+__device__ __forceinline__ uint64_t eq_mask64_words(const uint32_t* w, uint32_t pat) {
+  uint32_t lo = 0, hi = 0;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) lo |= zmask4(w[j] ^ pat) << (4 * j);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) hi |= zmask4(w[8 + j] ^ pat) << (4 * j);
+  return ((uint64_t)hi << 32) | lo;
+}
+
+__global__ __launch_bounds__(256) void k_tiles(const SegDesc* segs, uint32_t nsegs, uint32_t ntiles,
+                                               uint32_t* tile_seg) {
+  for (uint32_t tile = blockIdx.x * 256 + threadIdx.x; tile < ntiles; tile += gridDim.x * 256)
+    tile_seg[tile] = find_seg_by_tile(segs, nsegs, tile);
+}
+
+// Canonical kubelet prefix "YYYY-MM-DDTHH:MM:SS.nnnnnnnnnZ " (k8s logs.go timeFormatOut):
+// 9 dword LDS reads instead of ~31 dependent byte reads.  Accepts exactly the inputs of
+// this shape the general parser accepts (same value); anything else -> general parser.
+__device__ __forceinline__ bool parse_fast_lds(const uint8_t* lds, uint32_t o, TsResult& r) {
+  const uint32_t* s32 = reinterpret_cast<const uint32_t*>(lds);
+  const uint32_t base = o >> 2, sh = (o & 3) * 8;
+  uint32_t w[8];
+  uint32_t prev = s32[base];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const uint32_t nx = s32[base + j + 1];
+    w[j] = sh ? (uint32_t)((((uint64_t)nx << 32) | prev) >> sh) : prev;
+    prev = nx;
+  }
+#define KLF_B(k) ((w[(k) >> 2] >> (8 * ((k) & 3))) & 0xFFu)
+  if (KLF_B(4) != '-' || KLF_B(7) != '-' || KLF_B(10) != 'T' || KLF_B(13) != ':' || KLF_B(16) != ':' ||
+      KLF_B(19) != '.' || KLF_B(29) != 'Z' || KLF_B(30) != ' ')
+    return false;
+  // digits, folded as they are read (no per-byte array: keeps the register budget)
+  bool ok = true;
+  auto dig = [&](int k) -> uint32_t {
+    const uint32_t v = KLF_B(k) - '0';
+    ok &= v < 10;
+    return v;
+  };
+  const int64_t year = dig(0) * 1000 + dig(1) * 100 + dig(2) * 10 + dig(3);
+  const int month = (int)(dig(5) * 10 + dig(6)), day = (int)(dig(8) * 10 + dig(9));
+  const int hour = (int)(dig(11) * 10 + dig(12)), minute = (int)(dig(14) * 10 + dig(15));
+  const int second = (int)(dig(17) * 10 + dig(18));
+  uint32_t ns = 0;
+#pragma unroll
+  for (int k = 20; k < 29; ++k) ns = ns * 10 + dig(k);
+#undef KLF_B
+  if (!ok) return false;
+  if (month < 1 || month > 12 || hour >= 24 || minute >= 60 || second >= 60) return false;
+  if (day < 1 || day > days_in_month(month, year)) return false;
+  r.sec = days_from_civil(year, month, day) * 86400 + hour * 3600 + minute * 60 + second;
+  r.nsec = (int32_t)ns;
+  r.len = 30;
+  return true;
+}
+
+// General RFC3339Nano parse, out of line: non-canonical prefixes are rare, and keeping the
+// byte-at-a-time parser out of the hot loop keeps the loop's register budget.
+__device__ __attribute__((noinline)) bool parse_general_cold(const uint8_t* lds, const uint8_t* segp, int64_t p0,
+                                                            int64_t rel_lo, int64_t seg_len, TsResult* r,
+                                                            uint32_t* plen) {
+  LineBytes gb{lds, segp, p0, rel_lo, seg_len};
+  return parse_line_prefix(gb, *r, *plen);
+}
+
+// Parse of the line starting at stream offset p0: fast path from LDS, else general.
+__device__ __forceinline__ bool parse_line_at(const uint8_t* lds, const uint8_t* segp, int64_t p0, int64_t rel_lo,
+                                              int64_t seg_len, int64_t ssec, int32_t snsec, bool* since_ok,
+                                              uint32_t* plen) {
+  TsResult r;
+  const int64_t o = p0 - rel_lo;
+  bool ok;
+  if (o >= 0 && o + 36 <= kTile + kHalo && p0 + 31 <= seg_len && parse_fast_lds(lds, (uint32_t)o, r)) {
+    ok = true;
+    *plen = 31;
+  } else {
+    LineBytes gb{lds, segp, p0, rel_lo, seg_len};
+    ok = parse_line_prefix(gb, r, *plen);
+  }
+  *since_ok = ok && !time_before(r.sec, r.nsec, ssec, snsec);
+  return ok;
+}
+
+// Rare path: content start of the line containing stream offset `pos` when that line
+// began before `rel_lo` (scan back for its '\n', then parse).  -1 if unparseable.
+__device__ __attribute__((noinline)) int64_t carried_content_start(const uint8_t* lds, const uint8_t* segp,
+                                                                  int64_t rel_lo, int64_t seg_len,
+                                                                  int64_t from) {
+  int64_t ls = 0;
+  for (int64_t q = from; q >= 0; --q) {
+    const int64_t o = q - rel_lo;
+    const uint8_t c = (o >= 0 && o < kTile + kHalo) ? lds[o] : segp[q];
+    if (c == '\n') { ls = q + 1; break; }
+  }
+  uint32_t plen = 0;
+  TsResult r;
+  LineBytes gb{lds, segp, ls, rel_lo, seg_len};
+  if (!parse_line_prefix(gb, r, plen)) return -1;
+  return ls + plen;
+}
+
+#ifndef KLF_ABLATE
+#define KLF_ABLATE 0
+#endif
+
+#ifndef KLF_SCAN_OCC
+#define KLF_SCAN_OCC 6
+#endif
 template <bool LIT>
-__global__ __launch_bounds__(kThreads) void k_scan(RunArgs a) {
+__global__ __launch_bounds__(kThreads, KLF_SCAN_OCC) void k_scan(RunArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t s_tile[kTile + kHalo];
-  __shared__ uint32_t s_wave[4];
+  __shared__ uint16_t s_meta[kMaxTileLines + 1];
+  __shared__ uint16_t s_loff[kMaxTileLines + 1];
+  __shared__ uint32_t s_wsum[4];
   __shared__ uint32_t s_red[4][2];
   __shared__ uint64_t s_excl;
   __shared__ uint32_t s_ticket;
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   uint32_t* err_flag = a.counters + 2;
-
+  // Ticket groups: group g hands out tiles g, g+G, g+2G, ... in claim order.  One atomic
+  // word saturates near 88 claims/us (MI355X_MICROARCH.md, row "dequeue"); G padded words
+  // keep claims off the critical path.  A tile is claimed only when it is about to be
+  // processed (a claimed-but-idle tile would stall every later look-back).  Deadlock-free
+  // while every group keeps a resident workgroup: the lowest unfinished tile is either
+  // being processed (its look-back needs only lower, finished tiles) or is the next
+  // claim of its group, whose workgroups are then idle and claim it.
+  const uint32_t g = blockIdx.x % kScanGroups;
+  uint32_t* ctr = a.counters + kCtrScanGroups + g * kCtrStride;
   for (;;) {
-    if (t == 0) s_ticket = atomicAdd(&a.counters[0], 1u);
+    if (t == 0) s_ticket = atomicAdd(ctr, 1u);
     __syncthreads();
-    const uint32_t tile = s_ticket;
+    const uint32_t tile = s_ticket * kScanGroups + g;
     if (tile >= a.ntiles) break;
-    const uint32_t s = find_seg_by_tile(a.segs, a.nsegs, tile);
+    const uint32_t s = a.tile_seg[tile];
     const SegDesc sd = a.segs[s];
     const int64_t rel_lo = (int64_t)(tile - sd.tile0) * kTile;
     const int64_t seg_len = (int64_t)sd.len;
@@ -212,129 +376,131 @@ __global__ __launch_bounds__(kThreads) void k_scan(RunArgs a) {
     const bool last = rel_lo + kTile >= seg_len;
     const uint8_t* segp = a.bytes + sd.base;
 
-    // ---- stage tile + halo in LDS (coalesced 16 B per lane) ----
+    // ---- 1. stage tile + halo in LDS (coalesced 16 B per lane) ----
     {
-      const uint4* g = reinterpret_cast<const uint4*>(segp + rel_lo);
+      const uint4* gp = reinterpret_cast<const uint4*>(segp + rel_lo);
       uint4* l = reinterpret_cast<uint4*>(s_tile);
 #pragma unroll
-      for (int v = 0; v < kTile / (kThreads * 16); ++v) l[v * kThreads + t] = g[v * kThreads + t];
-      if (t < kHalo / 16) l[kTile / 16 + t] = g[kTile / 16 + t];
+      for (int v = 0; v < kTile / (kThreads * 16); ++v) l[v * kThreads + t] = gp[v * kThreads + t];
+      if (t < kHalo / 16) l[kTile / 16 + t] = gp[kTile / 16 + t];
     }
     __syncthreads();
 
-    // ---- per-thread masks ----
-    uint32_t w[16];
+    // ---- 2. events of my 64 bytes -> counts -> publish the aggregate ----
+    const int64_t nvalid_s = tile_len - (int64_t)t * kBytesPerThread;
+    const int nvalid = nvalid_s <= 0 ? 0 : (nvalid_s >= 64 ? 64 : (int)nvalid_s);
+    const uint64_t vm = nvalid >= 64 ? ~0ull : ((1ull << nvalid) - 1);
+    const int64_t rel0 = rel_lo + (int64_t)t * kBytesPerThread;
+    uint64_t nl, cand = 0;
     {
+      uint32_t w[16];
       const uint4* l = reinterpret_cast<const uint4*>(s_tile + t * kBytesPerThread);
 #pragma unroll
       for (int v = 0; v < 4; ++v) {
         const uint4 x = l[v];
         w[4 * v] = x.x; w[4 * v + 1] = x.y; w[4 * v + 2] = x.z; w[4 * v + 3] = x.w;
       }
+      nl = eq_mask64_words(w, 0x0A0A0A0Au) & vm;
+      if (LIT) cand = eq_mask64_words(w, a.lit[0] * 0x01010101u) & vm;
     }
-    const int64_t nvalid_s = tile_len - (int64_t)t * kBytesPerThread;
-    const int nvalid = nvalid_s <= 0 ? 0 : (nvalid_s >= 64 ? 64 : (int)nvalid_s);
-    const uint64_t vm = nvalid >= 64 ? ~0ull : ((1ull << nvalid) - 1);
-    const int64_t rel0 = rel_lo + (int64_t)t * kBytesPerThread;  // stream offset of my byte 0
-    const uint64_t nl = eq_mask64(w, 0x0A0A0A0Au) & vm;
-    const uint64_t sp = LIT ? (eq_mask64(w, 0x20202020u) & vm) : 0;
     const bool has_end = last && nvalid > 0 && rel0 + nvalid == seg_len;
-    const int eb = nvalid - 1;  // bit of the stream's last byte when has_end
-    uint64_t ev = nl;
-    uint64_t starts = nl;
+    const int eb = nvalid - 1;
+    uint64_t ev = nl, starts = nl;
     if (has_end) {
       ev |= 1ull << eb;
       starts &= ~(1ull << eb);
     }
     const bool reset = first && t == 0;
-
-    // ---- parse the last line starting in my range (its P bit feeds the scan) ----
-    bool last_ok = false, last_since = false;
-    uint32_t last_plen = 0;
-    const bool any_start = starts != 0 || reset;
-    if (any_start) {
-      const int64_t p0 = starts ? rel0 + (63 - __clzll(starts)) + 1 : rel0;
-      TsResult r;
-      uint32_t plen = 0;
-      LineBytes gb{s_tile, segp, p0, rel_lo, seg_len};
-      last_ok = parse_line_prefix(gb, r, plen);
-      last_since = last_ok && !time_before(r.sec, r.nsec, a.since_sec, a.since_nsec);
-      last_plen = plen;
-    }
-    uint32_t summ = (uint32_t)__popcll(ev);
-    if (any_start) {
-      summ |= kInd32 | (last_ok ? kP32 : 0);
-      if (LIT) {
-        uint64_t after = sp;
-        if (starts) {
-          const int q = 63 - __clzll(starts);
-          after = q >= 63 ? 0 : (sp & ~((2ull << q) - 1));
-        }
-        if (after) summ |= kS32;
-      }
-    } else if (LIT && sp) {
-      summ |= kS32;
-    }
-
-    // ---- block scan of the summaries + tile look-back ----
-    const uint32_t incl = wave_incl_scan_summary(summ, lane);
-    uint32_t lane_excl = __shfl_up(incl, 1, 64);
-    if (lane == 0) lane_excl = 0;
-    if (lane == 63) s_wave[wv] = incl;
+    const uint32_t cnt = (uint32_t)__popcll(ev);
+    const uint32_t incl = wave_incl_scan_add(cnt, lane);
+    if (lane == 63) s_wsum[wv] = incl;
     __syncthreads();
     uint32_t wexcl = 0, agg = 0;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      if (k < wv) wexcl = comb32(wexcl, s_wave[k]);
-      agg = comb32(agg, s_wave[k]);
+      if (k < wv) wexcl += s_wsum[k];
+      agg += s_wsum[k];
     }
-    if (t == 0) s_excl = lookback(a.status, tile, widen(agg), 0ull, ScanComb(), err_flag);
-    __syncthreads();
-    const uint64_t X = comb64(s_excl, widen(comb32(wexcl, lane_excl)));
-    const uint64_t lines_before = X & kCnt64;
+    const uint32_t texcl = wexcl + incl - cnt;  // events of the tile before my bytes
+    const bool staged = agg <= (uint32_t)kMaxTileLines;
+    if (t == 0 && tile != 0) atomic_store_u64(&a.status[tile], (uint64_t)agg | kFlagA);
 
-    // ---- line starts: offsets, parse, meta ----
+    // ---- 3. parse the lines starting in my bytes (into LDS when the tile fits) ----
     uint32_t n_parsed = 0, n_since = 0;
-    uint64_t okmask = 0;  // bit q: the line started after event q parsed
-    bool reset_ok = false;
-    if (reset) {
-      const uint64_t l = lines_before;
-      if (l < a.cap_lines) {
-        a.line_off[l + s] = 0;
-        bool ok = last_ok, so = last_since;
-        uint32_t plen = last_plen;
-        if (starts) {  // the reset line is not my last start: parse it here
-          TsResult r;
-          LineBytes gb{s_tile, segp, rel0, rel_lo, seg_len};
-          ok = parse_line_prefix(gb, r, plen);
-          so = ok && !time_before(r.sec, r.nsec, a.since_sec, a.since_nsec);
-        }
-        a.meta[l] = make_meta(ok, so, plen);
+    if (staged) {
+      if (reset) {
+        bool so;
+        uint32_t plen = 0;
+        const bool ok = KLF_ABLATE >= 2 ? true : parse_line_at(s_tile, segp, rel0, rel_lo, seg_len, a.since_sec, a.since_nsec, &so, &plen);
+        s_meta[0] = make_meta(ok, so, plen);
+        s_loff[0] = 0;
         n_parsed += ok;
         n_since += so;
-        reset_ok = ok;
-      } else {
-        atomicOr(err_flag, 1u);
       }
-      a.segout[s].line_lo = l;
+      for (uint64_t m = starts; m;) {
+        const int q = __ffsll((unsigned long long)m) - 1;
+        m &= m - 1;
+        const uint32_t k = texcl + (uint32_t)__popcll(ev & ((2ull << q) - 1));
+        const int64_t p0 = rel0 + q + 1;
+        bool so = true;
+        uint32_t plen = 31;
+        const bool ok = KLF_ABLATE >= 2 ? true : parse_line_at(s_tile, segp, p0, rel_lo, seg_len, a.since_sec, a.since_nsec, &so, &plen);
+        s_meta[k] = make_meta(ok, so, plen);
+        s_loff[k] = (uint16_t)(p0 - rel_lo);
+        n_parsed += ok;
+        n_since += so;
+      }
     }
-    {
-      uint64_t m = starts;
-      const int qlast = starts ? 63 - __clzll(starts) : -1;
-      while (m) {
+
+    // ---- 4. look-back: global index of the tile's first line ----
+#if KLF_ABLATE >= 1
+    if (t == 0) s_excl = 0;
+#else
+    if (wv == 0) {
+      const uint64_t ex = lookback_wave(a.status, tile, (uint64_t)agg, 0ull, SumComb(), err_flag, lane);
+      if (lane == 0) s_excl = ex;
+    }
+#endif
+    __syncthreads();
+    const uint64_t tile_lines = s_excl;
+    const uint64_t lines_before = tile_lines + texcl;
+
+    // ---- 5. write-out ----
+    if (staged) {  // coalesced: local line k -> global tile_lines + k
+      const uint32_t k0 = first ? 0 : 1;
+      const bool tile_has_end = last;  // the stream's final event lies in this tile
+      const uint32_t k1 = tile_has_end ? agg : agg + 1;
+      for (uint32_t k = k0 + t; k < k1; k += kThreads) {
+        const uint64_t l = tile_lines + k;
+        if (l < a.cap_lines) {
+          a.meta[l] = s_meta[k];
+          a.line_off[l + s] = (uint64_t)rel_lo + s_loff[k];
+        } else {
+          atomicOr(err_flag, 1u);
+        }
+      }
+    } else {  // dense tile: parse and write per thread
+      if (reset) {
+        bool so;
+        uint32_t plen = 0;
+        const bool ok = parse_line_at(s_tile, segp, rel0, rel_lo, seg_len, a.since_sec, a.since_nsec, &so, &plen);
+        if (lines_before < a.cap_lines) {
+          a.line_off[lines_before + s] = 0;
+          a.meta[lines_before] = make_meta(ok, so, plen);
+        } else {
+          atomicOr(err_flag, 1u);
+        }
+        n_parsed += ok;
+        n_since += so;
+      }
+      for (uint64_t m = starts; m;) {
         const int q = __ffsll((unsigned long long)m) - 1;
         m &= m - 1;
         const uint64_t l = lines_before + (uint64_t)__popcll(ev & ((2ull << q) - 1));
         const int64_t p0 = rel0 + q + 1;
-        bool ok = last_ok, so = last_since;
-        uint32_t plen = last_plen;
-        if (q != qlast) {
-          TsResult r;
-          LineBytes gb{s_tile, segp, p0, rel_lo, seg_len};
-          ok = parse_line_prefix(gb, r, plen);
-          so = ok && !time_before(r.sec, r.nsec, a.since_sec, a.since_nsec);
-        }
-        if (ok) okmask |= 1ull << q;
+        bool so;
+        uint32_t plen = 0;
+        const bool ok = parse_line_at(s_tile, segp, p0, rel_lo, seg_len, a.since_sec, a.since_nsec, &so, &plen);
         if (l < a.cap_lines) {
           a.line_off[l + s] = (uint64_t)p0;
           a.meta[l] = make_meta(ok, so, plen);
@@ -345,31 +511,35 @@ __global__ __launch_bounds__(kThreads) void k_scan(RunArgs a) {
         n_since += so;
       }
     }
+    if (reset) a.segout[s].line_lo = lines_before;
     if (has_end) {
-      const uint64_t lend = lines_before + (uint64_t)__popcll(ev);
+      const uint64_t lend = lines_before + cnt;
       if (lend <= a.cap_lines) a.line_off[lend + s] = (uint64_t)seg_len;
       else atomicOr(err_flag, 1u);
       a.segout[s].line_hi = lend;
       a.segout[s].frag = (nl >> eb) & 1 ? 0 : 1;
     }
 
-    // ---- fused single-literal grep ----
-    if (LIT) {
+    // ---- fused single-literal grep (rare path: first-byte candidates) ----
+    if (LIT && cand) {
       const uint32_t m = a.lit_len;
-      const uint32_t c0 = a.lit[0] * 0x01010101u;
-      const uint32_t cl = a.lit[m - 1] * 0x01010101u;
-      uint64_t cand = eq_mask64(w, c0) & vm;
-      if (cand) {
+      {  // last-byte filter from the LDS window at +m-1 (word by word)
         const uint32_t off = (uint32_t)t * kBytesPerThread + m - 1;
         const uint32_t* s32 = reinterpret_cast<const uint32_t*>(s_tile);
-        const uint32_t base = off >> 2, sh = off & 3;
-        uint32_t r[17], wl[16];
+        const uint32_t base = off >> 2, sh = (off & 3) * 8;
+        const uint32_t pat = a.lit[m - 1] * 0x01010101u;
+        uint32_t prev = s32[base], lo = 0, hi = 0;
 #pragma unroll
-        for (int j = 0; j < 17; ++j) r[j] = s32[base + j];
-#pragma unroll
-        for (int j = 0; j < 16; ++j) wl[j] = __builtin_amdgcn_alignbyte(r[j + 1], r[j], sh);
-        cand &= eq_mask64(wl, cl);
+        for (int j = 0; j < 16; ++j) {
+          const uint32_t nx = s32[base + j + 1];
+          const uint32_t wj = sh ? (uint32_t)((((uint64_t)nx << 32) | prev) >> sh) : prev;
+          prev = nx;
+          if (j < 8) lo |= zmask4(wj ^ pat) << (4 * j);
+          else hi |= zmask4(wj ^ pat) << (4 * (j - 8));
+        }
+        cand &= ((uint64_t)hi << 32) | lo;
       }
+      int64_t carried_cs = -2;  // content start of the line carried into my bytes (lazy)
       while (cand) {
         const int b = __ffsll((unsigned long long)cand) - 1;
         cand &= cand - 1;
@@ -380,36 +550,42 @@ __global__ __launch_bounds__(kThreads) void k_scan(RunArgs a) {
         if (!eq) continue;
         const uint64_t below = b == 0 ? 0 : ((1ull << b) - 1);
         const uint64_t E = ev & below;
-        bool in_content, pok;
-        uint64_t l;
-        if (E) {
-          const int k = 63 - __clzll(E);
-          in_content = (sp & below & ~((2ull << k) - 1)) != 0;
-          pok = (okmask >> k) & 1;
-          l = lines_before + (uint64_t)__popcll(E);
-        } else if (reset) {
-          in_content = (sp & below) != 0;
-          pok = reset_ok;
-          l = lines_before;
+        int64_t cs;  // content start of the hit's line, -1 = unparseable
+        if (E || reset || (staged && (texcl > 0 || first))) {
+          // the line starts inside this tile: its local index is the events before it
+          const uint32_t kl = texcl + (uint32_t)__popcll(E);
+          const int64_t p0 = E ? rel0 + (63 - __clzll(E)) + 1 : (reset ? rel0 : -1);
+          if (staged) {
+            const uint16_t mt = s_meta[kl];
+            cs = (mt & Meta::kParsed) ? (int64_t)rel_lo + s_loff[kl] + (mt >> 2) : -1;
+          } else if (p0 >= 0) {
+            bool so;
+            uint32_t plen = 0;
+            cs = parse_line_at(s_tile, segp, p0, rel_lo, seg_len, 0, 0, &so, &plen) ? p0 + plen : -1;
+          } else {
+            if (carried_cs == -2) carried_cs = carried_content_start(s_tile, segp, rel_lo, seg_len, rel0 - 1);
+            cs = carried_cs;
+          }
         } else {
-          in_content = (X & kS64) || (sp & below) != 0;
-          pok = (X & kP64) != 0;
-          l = lines_before;
+          if (carried_cs == -2) carried_cs = carried_content_start(s_tile, segp, rel_lo, seg_len, rel0 - 1);
+          cs = carried_cs;
         }
-        if (in_content && pok && l < a.cap_lines) atomicOr(&a.bits[l >> 5], 1u << (l & 31));
+        if (cs >= 0 && pos >= cs && cs <= pos) {
+          const uint64_t l = lines_before + (uint64_t)__popcll(E);
+          if (l < a.cap_lines) atomicOr(&a.bits[l >> 5], 1u << (l & 31));
+        }
       }
     }
 
     // ---- per-tile counters ----
-    {
-      const uint32_t p = wave_sum(n_parsed), q = wave_sum(n_since);
-      if (lane == 0) { s_red[wv][0] = p; s_red[wv][1] = q; }
-      __syncthreads();
-      if (t == 0) {
-        a.tile_cnt[2 * (size_t)tile] = s_red[0][0] + s_red[1][0] + s_red[2][0] + s_red[3][0];
-        a.tile_cnt[2 * (size_t)tile + 1] = s_red[0][1] + s_red[1][1] + s_red[2][1] + s_red[3][1];
-      }
+    const uint32_t pp = wave_sum(n_parsed), qq = wave_sum(n_since);
+    if (lane == 0) { s_red[wv][0] = pp; s_red[wv][1] = qq; }
+    __syncthreads();
+    if (t == 0) {
+      a.tile_cnt[2 * (size_t)tile] = s_red[0][0] + s_red[1][0] + s_red[2][0] + s_red[3][0];
+      a.tile_cnt[2 * (size_t)tile + 1] = s_red[0][1] + s_red[1][1] + s_red[2][1] + s_red[3][1];
     }
+    __syncthreads();  // LDS is reused by the next tile
   }
 }
 
@@ -718,9 +894,10 @@ __global__ __launch_bounds__(kThreads) void k_compact(RunArgs a) {
       if (k < wv) { pb += s_wb[k]; pc += s_wc[k]; }
       tb += s_wb[k]; tc += s_wc[k];
     }
-    if (t == 0) {
-      s_exb = lookback(stb, blk, tb, 0ull, SumComb(), a.counters + 2);
-      s_exc = lookback(stc, blk, tc, 0ull, SumComb(), a.counters + 2);
+    if (wv == 0) {
+      const uint64_t xb = lookback_wave(stb, blk, tb, 0ull, SumComb(), a.counters + 2, lane);
+      const uint64_t xc = lookback_wave(stc, blk, tc, 0ull, SumComb(), a.counters + 2, lane);
+      if (lane == 0) { s_exb = xb; s_exc = xc; }
     }
     __syncthreads();
     uint64_t ob = s_exb + pb + ib - blen;  // my exclusive byte offset
@@ -755,17 +932,33 @@ hipError_t launch_pipeline(const RunArgs& a, hipStream_t st, hipEvent_t* ev, int
   hipError_t e;
 #define KLF_TRY(x) do { e = (x); if (e != hipSuccess) return e; } while (0)
   KLF_TRY(hipEventRecord(ev[0], st));
-  KLF_TRY(hipMemsetAsync(a.counters, 0, 8 * sizeof(uint32_t), st));
+  KLF_TRY(hipMemsetAsync(a.counters, 0, kNumCounters * sizeof(uint32_t), st));
   KLF_TRY(hipMemsetAsync(a.status, 0, (size_t)a.ntiles * 8, st));
   KLF_TRY(hipMemsetAsync(a.segout, 0, (size_t)a.nsegs * sizeof(SegOut), st));
   KLF_TRY(hipMemsetAsync(a.cstatus, 0, (size_t)a.max_cblocks * 2 * 8, st));
   if (a.grep_mode != kGrepNone) KLF_TRY(hipMemsetAsync(a.bits, 0, (size_t)(a.cap_lines / 32 + 1) * 4, st));
+  if (a.build_tiles) {
+    const uint32_t g = (a.ntiles + 255) / 256;
+    hipLaunchKernelGGL(k_tiles, dim3(g < 4096 ? g : 4096), dim3(256), 0, st, a.segs, a.nsegs, a.ntiles,
+                       a.tile_seg);
+    KLF_TRY(hipGetLastError());
+  }
   KLF_TRY(hipEventRecord(ev[1], st));
-  const uint32_t scan_grid = (uint32_t)(a.ntiles < (uint32_t)num_cus * 8 ? a.ntiles : num_cus * 8);
-  if (a.grep_mode == kGrepLit1)
-    hipLaunchKernelGGL(k_scan<true>, dim3(scan_grid), dim3(kThreads), 0, st, a);
-  else
-    hipLaunchKernelGGL(k_scan<false>, dim3(scan_grid), dim3(kThreads), 0, st, a);
+  {
+    int occ = 0;
+    if (a.grep_mode == kGrepLit1)
+      (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_scan<true>, kThreads, 0);
+    else
+      (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_scan<false>, kThreads, 0);
+    occ = occ < 1 ? 1 : (occ > 8 ? 8 : occ);
+    uint32_t grid = (uint32_t)(num_cus * occ);
+    grid = grid / kScanGroups * kScanGroups;
+    if (grid < kScanGroups) grid = kScanGroups;
+    if (a.grep_mode == kGrepLit1)
+      hipLaunchKernelGGL(k_scan<true>, dim3(grid), dim3(kThreads), 0, st, a);
+    else
+      hipLaunchKernelGGL(k_scan<false>, dim3(grid), dim3(kThreads), 0, st, a);
+  }
   KLF_TRY(hipGetLastError());
   KLF_TRY(hipEventRecord(ev[2], st));
   if (a.grep_mode == kGrepGeneral || a.grep_mode == kGrepAll) {

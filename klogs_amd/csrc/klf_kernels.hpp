@@ -16,6 +16,13 @@ constexpr uint64_t kSegAlign = 256;                 // segment base alignment in
 constexpr uint64_t kAllocSlack = kTile + kHalo + 1024;
 constexpr uint32_t kPlenEscape = 16383;             // meta plen field saturates here
 constexpr int kCompactLines = 1024;                 // lines per compaction block
+// Scan ticket groups: one counter per group, each on its own 256-B line.  Counters that
+// share a line serialise like a single word (measured on MI355X with
+// scripts/mb_stream.hip: 32 adjacent counters 2.6 TB/s, 128 padded counters 6.2 TB/s).
+constexpr uint32_t kScanGroups = 128;
+constexpr uint32_t kCtrStride = 64;                 // u32 words between group counters
+constexpr uint32_t kCtrScanGroups = 64;             // counters[64 + g * kCtrStride]
+constexpr uint32_t kNumCounters = kCtrScanGroups + kScanGroups * kCtrStride;
 
 // One segment (= one non-empty stream) of the device batch.
 struct SegDesc {
@@ -65,6 +72,8 @@ struct RunArgs {
   const SegDesc* segs;
   uint32_t nsegs;
   uint32_t ntiles;
+  uint32_t* tile_seg;   // [ntiles] tile -> segment (filled by k_tiles when build_tiles)
+  uint32_t build_tiles;
   // filter
   int64_t since_sec;
   int32_t since_nsec;
@@ -76,7 +85,8 @@ struct RunArgs {
   // workspace (device)
   uint64_t* status;     // [ntiles] scan look-back words
   uint64_t* cstatus;    // [2 * max compaction blocks] compaction look-back words
-  uint32_t* counters;   // [8] tickets / flags: 0 scan ticket, 1 compact ticket, 2 overflow
+  uint32_t* counters;   // [kNumCounters]: 1 compact ticket, 2 error flags, 3 compact blocks,
+                        // [8, 8+kScanGroups) scan ticket groups
   uint64_t* line_off;   // [cap_lines + nsegs]
   uint16_t* meta;       // [cap_lines]
   uint32_t* bits;       // [cap_lines / 32 + 1]

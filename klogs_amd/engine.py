@@ -14,7 +14,7 @@ from typing import Iterable, List, Optional, Sequence, Tuple
 
 import numpy as np
 
-_LIB_DIR = Path(__file__).resolve().parent / "_lib"
+_LIB_DIR = Path(os.environ.get("KLF_LIB_DIR", Path(__file__).resolve().parent / "_lib"))
 _LIB_PATH = _LIB_DIR / "libklf.so"
 
 KLF_OK = 0
