@@ -5,6 +5,8 @@
 
 #include <algorithm>
 #include <atomic>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -61,8 +63,9 @@ struct klf_engine {
   // workspace
   std::vector<SegDesc> last_segs;  // tile_seg cache key
   DevBuf d_tile_seg;
-  DevBuf d_batch, d_segs, d_status, d_cstatus, d_counters, d_line_off, d_meta, d_bits, d_tile_cnt,
-      d_segout, d_wpre, d_out;
+  DevBuf d_batch, d_segs, d_tstat, d_slots, d_pool, d_tile_base, d_bsum, d_cstatus, d_counters, d_line_off,
+      d_meta, d_bits, d_segout, d_wpre, d_out;
+  uint64_t pool_cap = 1 << 20;
   hipEvent_t ev[6] = {};
 };
 
@@ -162,7 +165,9 @@ extern "C" int klf_open(const klf_config* cfg, klf_engine** out) {
   const auto& cs = e->cs;
   hipStream_t st = e->stream;
   if (cs.mode == klf::CompiledSet::kLiteral1) {
-    h = upload(e->d_lit, cs.literal, st);
+    std::vector<uint8_t> padded = cs.literal;
+    padded.resize((cs.literal.size() + 3) / 4 * 4 + 4, 0);  // bytes, then dword view at +0
+    h = upload(e->d_lit, padded, st);
     if (h != hipSuccess) { *out = e; return hip_err(e, h, "upload literal"); }
   } else if (cs.mode == klf::CompiledSet::kGeneral) {
     klf::DevPatterns& P = e->dpats;
@@ -215,9 +220,9 @@ extern "C" void klf_close(klf_engine* e) {
   if (!e) return;
   if (e->stream) (void)hipStreamSynchronize(e->stream);
   for (DevBuf* b : {&e->d_lit, &e->d_ac_class, &e->d_ac_next, &e->d_ac_accept, &e->d_rx_class, &e->d_rx_b,
-                    &e->d_rx_follow, &e->d_rx_vec, &e->d_rx_flags, &e->d_batch, &e->d_segs, &e->d_status,
-                    &e->d_cstatus, &e->d_counters, &e->d_line_off, &e->d_meta, &e->d_bits, &e->d_tile_cnt,
-                    &e->d_segout, &e->d_wpre, &e->d_out, &e->d_tile_seg})
+                    &e->d_rx_follow, &e->d_rx_vec, &e->d_rx_flags, &e->d_batch, &e->d_segs, &e->d_tstat,
+                    &e->d_slots, &e->d_pool, &e->d_tile_base, &e->d_bsum, &e->d_cstatus, &e->d_counters,
+                    &e->d_line_off, &e->d_meta, &e->d_bits, &e->d_segout, &e->d_wpre, &e->d_out, &e->d_tile_seg})
     b->release();
   for (auto& x : e->ev)
     if (x) (void)hipEventDestroy(x);
@@ -320,9 +325,11 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
     HIPCHK(e, hipStreamSynchronize(st), "sync segs");
     HIPCHK(e, e->d_tile_seg.ensure(ntiles * 4), "alloc tile_seg");
   }
-  HIPCHK(e, e->d_status.ensure(ntiles * 8), "alloc status");
+  HIPCHK(e, e->d_tstat.ensure(ntiles * sizeof(klf::TileStat)), "alloc tstat");
+  HIPCHK(e, e->d_slots.ensure(ntiles * klf::kSlots * 4), "alloc slots");
+  HIPCHK(e, e->d_tile_base.ensure(ntiles * 8), "alloc tile_base");
+  HIPCHK(e, e->d_bsum.ensure((ntiles / 4096 + 2) * 8), "alloc bsum");
   HIPCHK(e, e->d_counters.ensure(klf::kNumCounters * 4), "alloc counters");
-  HIPCHK(e, e->d_tile_cnt.ensure(ntiles * 8), "alloc tile counters");
   HIPCHK(e, e->d_segout.ensure(nsegs * sizeof(SegOut)), "alloc segout");
   HIPCHK(e, e->d_wpre.ensure((nsegs + 1) * 8), "alloc wpre");
   HIPCHK(e, e->d_out.ensure(total_bytes + 64), "alloc out");
@@ -333,6 +340,7 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
     HIPCHK(e, e->d_meta.ensure(cap * 2 + 16), "alloc meta");
     HIPCHK(e, e->d_bits.ensure((cap / 32 + 1) * 4), "alloc bits");
     HIPCHK(e, e->d_cstatus.ensure(max_cblocks * 2 * 8), "alloc cstatus");
+    HIPCHK(e, e->d_pool.ensure(e->pool_cap * 4), "alloc pool");
     klf::RunArgs a{};
     a.bytes = d_bytes;
     a.segs = e->d_segs.as<SegDesc>();
@@ -346,15 +354,21 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
     a.grep_mode = (uint32_t)mode;
     a.lit = e->d_lit.as<uint8_t>();
     a.lit_len = (uint32_t)e->cs.literal.size();
+    a.lit_anchor = e->cs.literal_anchor;
+    a.lit_words = e->d_lit.as<uint32_t>();
     a.pats = e->dpats;
-    a.status = e->d_status.as<uint64_t>();
+    a.tstat = e->d_tstat.as<klf::TileStat>();
+    a.slots = e->d_slots.as<uint32_t>();
+    a.pool = e->d_pool.as<uint32_t>();
+    a.pool_cap = e->pool_cap;
+    a.tile_base = e->d_tile_base.as<uint64_t>();
+    a.bsum = e->d_bsum.as<uint64_t>();
     a.cstatus = e->d_cstatus.as<uint64_t>();
     a.counters = e->d_counters.as<uint32_t>();
     a.line_off = e->d_line_off.as<uint64_t>();
     a.meta = e->d_meta.as<uint16_t>();
     a.bits = e->d_bits.as<uint32_t>();
     a.cap_lines = cap;
-    a.tile_cnt = e->d_tile_cnt.as<uint32_t>();
     a.segout = e->d_segout.as<SegOut>();
     a.wpre = e->d_wpre.as<uint64_t>();
     a.out = e->d_out.as<uint8_t>();
@@ -367,11 +381,22 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
     HIPCHK(e, hipStreamSynchronize(st), "sync");
     e->last_segs = segs;
     if (counters[2] & 2u) { delete r; e->last_segs.clear(); return set_err(e, KLF_EHIP, "look-back spin timeout"); }
-    if (counters[2] & 1u) {  // more lines than the capacity estimate: rerun with the exact count
-      cap = r->so[nsegs - 1].line_hi + 2;
+    if (counters[2] & 1u) {  // more lines (or dense-tile slots) than estimated: rerun with exact sizes
+      cap = std::max<uint64_t>(cap, r->so[nsegs - 1].line_hi + 2);
+      e->pool_cap = std::max<uint64_t>(e->pool_cap, (uint64_t)counters[klf::kCtrPool] + 1024);
       continue;
     }
     break;
+  }
+  if (const char* path = getenv("KLF_TIMELINE_OUT")) {  // diagnostic builds only
+    std::vector<uint64_t> tl(300000 * 8);
+    if (klf::dump_timeline(tl.data(), tl.size() * 8) == hipSuccess) {
+      if (FILE* f = fopen(path, "wb")) {
+        fwrite(tl.data(), 8, std::min<size_t>(tl.size(), ntiles * 8), f);
+        fclose(f);
+      }
+      (void)klf::clear_timeline();
+    }
   }
   float ms;
   for (int k = 0; k < 4; ++k)  // scan, match, tail stage, compaction

@@ -18,6 +18,19 @@
 namespace klf {
 namespace {
 
+#ifndef KLF_TIMELINE
+#define KLF_TIMELINE 0
+#endif
+#if KLF_TIMELINE
+// Diagnostic build only: per tile {claim, loaded, A published, prefix known, done,
+// look-back rounds, spins, cu/xcc} stamps (s_memtime), dumped by the engine.
+__device__ uint64_t g_timeline[300000 * 8];
+__device__ uint32_t g_lb_rounds, g_lb_spins;
+#define KLF_STAMP(tile, k) do { if (threadIdx.x == 0 && (tile) < 300000) g_timeline[(size_t)(tile) * 8 + (k)] = __builtin_amdgcn_s_memtime(); } while (0)
+#else
+#define KLF_STAMP(tile, k) do { } while (0)
+#endif
+
 // ------------------------------------------------------------------ small helpers ---
 
 __device__ __forceinline__ uint32_t zero_bytes(uint32_t x) {
@@ -146,6 +159,67 @@ __device__ uint64_t lookback_wave(uint64_t* st, uint32_t idx, uint64_t agg, uint
   return acc;
 }
 
+// Wave-level decoupled look-back for a SUM chain (the scan's line counts): each lane
+// polls 4 consecutive predecessors, so one round covers 256 tiles.  With ~1500 tiles in
+// flight and a tile starting every ~10 ns, the nearest inclusive prefix trails by
+// ~(round-trip latency / 10 ns) tiles; a 64-wide window needed several dependent round
+// trips per tile, which fed back into a growing lag.  The aggregate must already be
+// published (flag A) unless idx == 0.  Returns the exclusive prefix in every lane.
+__device__ uint64_t lookback_wave_sum(uint64_t* st, uint32_t idx, uint64_t agg, uint32_t* err_flag, int lane) {
+  if (idx == 0) {
+    if (lane == 0) atomic_store_u64(&st[0], agg | kFlagP);
+    return 0;
+  }
+  uint64_t acc = 0;
+  int64_t hi = (int64_t)idx - 1;
+  for (;;) {
+    uint64_t w[4];
+    bool ready[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      w[k] = kFlagP;  // before tile 0: an empty inclusive prefix
+      ready[k] = hi - (4 * lane + k) < 0;
+    }
+    uint32_t spins = 0;
+    for (;;) {
+      bool all = true;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        if (!ready[k]) {
+          w[k] = atomic_load_u64(&st[hi - (4 * lane + k)]);
+          ready[k] = (w[k] & kFlagMask) != 0;
+        }
+        all &= ready[k];
+      }
+      if (__all(all)) break;
+      __builtin_amdgcn_s_sleep(1);
+      if (++spins > kSpinLimit) {
+        if (lane == 0) atomicOr(err_flag, 2u);
+        return acc;
+      }
+    }
+#if KLF_TIMELINE
+    if (lane == 0 && idx < 300000) { g_timeline[(size_t)idx * 8 + 5] += 1; g_timeline[(size_t)idx * 8 + 6] += spins; }
+#endif
+    // nearest inclusive prefix: smallest distance 4*lane + k with flag P
+    uint32_t d = 0xFFFFFFFFu;
+#pragma unroll
+    for (int k = 3; k >= 0; --k)
+      if ((w[k] & kFlagMask) == kFlagP) d = 4 * lane + k;
+#pragma unroll
+    for (int s = 32; s >= 1; s >>= 1) d = min(d, (uint32_t)__shfl_xor((int)d, s, 64));
+    uint64_t v = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if ((uint32_t)(4 * lane + k) <= d) v += w[k] & ~kFlagMask;
+    acc += wave_sum(v);
+    if (d != 0xFFFFFFFFu) break;
+    hi -= 256;
+  }
+  if (lane == 0) atomic_store_u64(&st[idx], (acc + agg) | kFlagP);
+  return acc;
+}
+
 struct SumComb {
   __device__ uint64_t operator()(uint64_t a, uint64_t b) const { return (a + b) & ~kFlagMask; }
 };
@@ -210,23 +284,20 @@ __device__ __forceinline__ uint16_t make_meta(bool ok, bool since_ok, uint32_t p
   return (uint16_t)(Meta::kParsed | (since_ok ? Meta::kSince : 0) | (pl << 2));
 }
 
-// ============================================================== K1: the scan kernel ==
-// Persistent 256-thread workgroups, one 16 KiB tile at a time; thread t owns bytes
-// [64t, 64t+64).  Per tile:
-//   1. claim (ticket groups, below) and stage tile + halo in LDS;
-//   2. line-end events ('\n', and the stream's last byte) -> counts -> block reduce ->
-//      publish the tile's AGGREGATE immediately (the chain is a plain line count, so a
-//      successor's look-back never waits on our parsing);
-//   3. parse every line starting in the tile into LDS (meta + tile-relative offset);
-//   4. look-back -> the tile's first global line index;
-//   5. coalesced copy-out of line_off / meta; fused literal grep on the rare first+last
-//      byte candidates.  Whether a hit lies in the content (after the first ' ') comes
-//      from the line's plen; for a line begun in an earlier tile, from a backward scan
-//      to its start and a re-parse (rare).
-// Tiles with more than kMaxTileLines line starts (< 16 B per line: never kubelet
-// output) take a slower per-thread path with the same results.
-
-constexpr int kMaxTileLines = 1024;
+// ============================================================== K1: the scan ==
+// Streaming scan with NO inter-workgroup waiting (MI355X measurements, DESIGN.md §4:
+// a decoupled look-back round costs ~5 us under full-chip streaming, which dominated
+// the single-pass kernel).  Three steps:
+//   K1a k_scan     static tile assignment; per 16 KiB tile: stage in LDS, line-end
+//                  events, parse every line starting in the tile (fast fixed-width path
+//                  for the kubelet prefix), fused literal grep; per-tile results are
+//                  STAGED as one packed u32 per line start in the tile's slot region
+//                  (dense tiles, > kSlots starts, take slots from an overflow pool).
+//   K1b/K1c        device scan of per-tile line counts -> tile line bases, stream line
+//                  ranges.
+//   K1d k_scatter  staged slots -> global line_off (u64) / meta (u16) / match bitmap.
+// Slot (u32): bits 0..14 line start offset inside the tile (0..16384), bit 15 literal
+// hit, bits 16..31 the line's meta word.
 
 // 4-bit mask of the zero bytes of x (exact): bit k set iff byte k of x is 0.
 __device__ __forceinline__ uint32_t zmask4(uint32_t x) {
@@ -317,56 +388,35 @@ __device__ __forceinline__ bool parse_line_at(const uint8_t* lds, const uint8_t*
   return ok;
 }
 
-// Rare path: content start of the line containing stream offset `pos` when that line
-// began before `rel_lo` (scan back for its '\n', then parse).  -1 if unparseable.
-__device__ __attribute__((noinline)) int64_t carried_content_start(const uint8_t* lds, const uint8_t* segp,
-                                                                  int64_t rel_lo, int64_t seg_len,
-                                                                  int64_t from) {
-  int64_t ls = 0;
-  for (int64_t q = from; q >= 0; --q) {
-    const int64_t o = q - rel_lo;
-    const uint8_t c = (o >= 0 && o < kTile + kHalo) ? lds[o] : segp[q];
-    if (c == '\n') { ls = q + 1; break; }
-  }
-  uint32_t plen = 0;
-  TsResult r;
-  LineBytes gb{lds, segp, ls, rel_lo, seg_len};
-  if (!parse_line_prefix(gb, r, plen)) return -1;
-  return ls + plen;
-}
-
-#ifndef KLF_ABLATE
-#define KLF_ABLATE 0
-#endif
-
 #ifndef KLF_SCAN_OCC
-#define KLF_SCAN_OCC 6
+#define KLF_SCAN_OCC 4
 #endif
 template <bool LIT>
 __global__ __launch_bounds__(kThreads, KLF_SCAN_OCC) void k_scan(RunArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t s_tile[kTile + kHalo];
-  __shared__ uint16_t s_meta[kMaxTileLines + 1];
-  __shared__ uint16_t s_loff[kMaxTileLines + 1];
+  __shared__ uint32_t s_slot[kSlots];  // line starts (offsets), then the parsed slots
   __shared__ uint32_t s_wsum[4];
   __shared__ uint32_t s_red[4][2];
-  __shared__ uint64_t s_excl;
-  __shared__ uint32_t s_ticket;
+  __shared__ uint32_t s_pool, s_carry;
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   uint32_t* err_flag = a.counters + 2;
-  // Ticket groups: group g hands out tiles g, g+G, g+2G, ... in claim order.  One atomic
-  // word saturates near 88 claims/us (MI355X_MICROARCH.md, row "dequeue"); G padded words
-  // keep claims off the critical path.  A tile is claimed only when it is about to be
-  // processed (a claimed-but-idle tile would stall every later look-back).  Deadlock-free
-  // while every group keeps a resident workgroup: the lowest unfinished tile is either
-  // being processed (its look-back needs only lower, finished tiles) or is the next
-  // claim of its group, whose workgroups are then idle and claim it.
-  const uint32_t g = blockIdx.x % kScanGroups;
-  uint32_t* ctr = a.counters + kCtrScanGroups + g * kCtrStride;
-  for (;;) {
-    if (t == 0) s_ticket = atomicAdd(ctr, 1u);
-    __syncthreads();
-    const uint32_t tile = s_ticket * kScanGroups + g;
-    if (tile >= a.ntiles) break;
+  // One tile ahead in registers: the next tile's 16 KiB (+ halo) is in flight while this
+  // tile is parsed (barriers here wait on LDS only, never on these loads).
+  static_assert(kTile == kThreads * 16 * 4, "prefetch holds 4 uint4 per thread");
+  auto tile_src = [&](uint32_t tl) -> const uint4* {
+    const uint32_t ss = a.tile_seg[tl];
+    const SegDesc d = a.segs[ss];
+    return reinterpret_cast<const uint4*>(a.bytes + d.base + (uint64_t)(tl - d.tile0) * kTile);
+  };
+  uint4 pf0, pf1, pf2, pf3, pfh = make_uint4(0, 0, 0, 0);  // named, not an array: stays in VGPRs
+  if (blockIdx.x < a.ntiles) {
+    const uint4* gp = tile_src(blockIdx.x);
+    pf0 = gp[t]; pf1 = gp[kThreads + t]; pf2 = gp[2 * kThreads + t]; pf3 = gp[3 * kThreads + t];
+    if (t < kHalo / 16) pfh = gp[kTile / 16 + t];
+  }
+  for (uint32_t tile = blockIdx.x; tile < a.ntiles; tile += gridDim.x) {
+    KLF_STAMP(tile, 0);
+    // descriptors are re-read (scalar, cached) rather than carried: fewer live SGPRs
     const uint32_t s = a.tile_seg[tile];
     const SegDesc sd = a.segs[s];
     const int64_t rel_lo = (int64_t)(tile - sd.tile0) * kTile;
@@ -376,45 +426,54 @@ __global__ __launch_bounds__(kThreads, KLF_SCAN_OCC) void k_scan(RunArgs a) {
     const bool last = rel_lo + kTile >= seg_len;
     const uint8_t* segp = a.bytes + sd.base;
 
-    // ---- 1. stage tile + halo in LDS (coalesced 16 B per lane) ----
+    // ---- stage this tile in LDS, then start loading the next one ----
     {
-      const uint4* gp = reinterpret_cast<const uint4*>(segp + rel_lo);
       uint4* l = reinterpret_cast<uint4*>(s_tile);
-#pragma unroll
-      for (int v = 0; v < kTile / (kThreads * 16); ++v) l[v * kThreads + t] = gp[v * kThreads + t];
-      if (t < kHalo / 16) l[kTile / 16 + t] = gp[kTile / 16 + t];
+      l[t] = pf0; l[kThreads + t] = pf1; l[2 * kThreads + t] = pf2; l[3 * kThreads + t] = pf3;
+      if (t < kHalo / 16) l[kTile / 16 + t] = pfh;
+      const uint32_t nx = tile + gridDim.x;
+      if (nx < a.ntiles) {
+        const uint4* gp = tile_src(nx);
+        pf0 = gp[t]; pf1 = gp[kThreads + t]; pf2 = gp[2 * kThreads + t]; pf3 = gp[3 * kThreads + t];
+        if (t < kHalo / 16) pfh = gp[kTile / 16 + t];
+      }
     }
+    if (t == 0) s_carry = 0;
     __syncthreads();
+    KLF_STAMP(tile, 1);
 
-    // ---- 2. events of my 64 bytes -> counts -> publish the aggregate ----
-    const int64_t nvalid_s = tile_len - (int64_t)t * kBytesPerThread;
-    const int nvalid = nvalid_s <= 0 ? 0 : (nvalid_s >= 64 ? 64 : (int)nvalid_s);
+    // ---- line-end events of my 64 bytes, literal anchor candidates ----
+    const int nvalid_s = (int)(tile_len - (int64_t)t * kBytesPerThread);
+    const int nvalid = nvalid_s <= 0 ? 0 : (nvalid_s >= 64 ? 64 : nvalid_s);
     const uint64_t vm = nvalid >= 64 ? ~0ull : ((1ull << nvalid) - 1);
-    const int64_t rel0 = rel_lo + (int64_t)t * kBytesPerThread;
+    const uint32_t toff0 = (uint32_t)t * kBytesPerThread;  // my first byte, tile-relative
     uint64_t nl, cand = 0;
     {
       uint32_t w[16];
-      const uint4* l = reinterpret_cast<const uint4*>(s_tile + t * kBytesPerThread);
+      const uint4* l = reinterpret_cast<const uint4*>(s_tile + toff0);
 #pragma unroll
       for (int v = 0; v < 4; ++v) {
         const uint4 x = l[v];
         w[4 * v] = x.x; w[4 * v + 1] = x.y; w[4 * v + 2] = x.z; w[4 * v + 3] = x.w;
       }
       nl = eq_mask64_words(w, 0x0A0A0A0Au) & vm;
-      if (LIT) cand = eq_mask64_words(w, a.lit[0] * 0x01010101u) & vm;
+      // literal anchor: the literal's rarest byte (chosen on the host), at offset lit_anchor
+      if (LIT) cand = eq_mask64_words(w, a.lit[a.lit_anchor] * 0x01010101u) & vm;
     }
-    const bool has_end = last && nvalid > 0 && rel0 + nvalid == seg_len;
+    const bool has_end = last && nvalid > 0 && rel_lo + toff0 + nvalid == seg_len;
     const int eb = nvalid - 1;
     uint64_t ev = nl, starts = nl;
     if (has_end) {
       ev |= 1ull << eb;
       starts &= ~(1ull << eb);
+      a.segout[s].frag = (nl >> eb) & 1 ? 0 : 1;
     }
-    const bool reset = first && t == 0;
+    KLF_STAMP(tile, 5);
     const uint32_t cnt = (uint32_t)__popcll(ev);
     const uint32_t incl = wave_incl_scan_add(cnt, lane);
     if (lane == 63) s_wsum[wv] = incl;
     __syncthreads();
+    KLF_STAMP(tile, 6);
     uint32_t wexcl = 0, agg = 0;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
@@ -422,170 +481,240 @@ __global__ __launch_bounds__(kThreads, KLF_SCAN_OCC) void k_scan(RunArgs a) {
       agg += s_wsum[k];
     }
     const uint32_t texcl = wexcl + incl - cnt;  // events of the tile before my bytes
-    const bool staged = agg <= (uint32_t)kMaxTileLines;
-    if (t == 0 && tile != 0) atomic_store_u64(&a.status[tile], (uint64_t)agg | kFlagA);
-
-    // ---- 3. parse the lines starting in my bytes (into LDS when the tile fits) ----
+    // Local line k = the line after the tile's k-th event (k = 0: the line open at the
+    // tile start).  Lines starting here: k in [k0, k1), slot j = k - k0.
+    const uint32_t k0 = first ? 0 : 1;
+    const uint32_t k1 = last ? agg : agg + 1;
+    const uint32_t nlines = k1 > k0 ? k1 - k0 : 0;
+    const bool dense = nlines > (uint32_t)kSlots;
+    if (dense) {
+      if (t == 0) {
+        const uint32_t pb = atomicAdd(&a.counters[kCtrPool], nlines);
+        s_pool = pb;
+        if ((uint64_t)pb + nlines > a.pool_cap) atomicOr(err_flag, 1u);
+      }
+      __syncthreads();
+    }
+    uint32_t* pool_dst = dense ? a.pool + s_pool : nullptr;
+    const bool pool_ok = !dense || (uint64_t)s_pool + nlines <= a.pool_cap;
+    // ---- parse every line starting in my bytes -> its slot (LDS, or the pool if dense) ----
+    // Each lane parses its own line starts: the starts are already in registers, and the
+    // timestamp bytes are in LDS, so no extra barrier or slot round trip is needed.
     uint32_t n_parsed = 0, n_since = 0;
-    if (staged) {
-      if (reset) {
-        bool so;
-        uint32_t plen = 0;
-        const bool ok = KLF_ABLATE >= 2 ? true : parse_line_at(s_tile, segp, rel0, rel_lo, seg_len, a.since_sec, a.since_nsec, &so, &plen);
-        s_meta[0] = make_meta(ok, so, plen);
-        s_loff[0] = 0;
-        n_parsed += ok;
-        n_since += so;
-      }
-      for (uint64_t m = starts; m;) {
-        const int q = __ffsll((unsigned long long)m) - 1;
-        m &= m - 1;
-        const uint32_t k = texcl + (uint32_t)__popcll(ev & ((2ull << q) - 1));
-        const int64_t p0 = rel0 + q + 1;
-        bool so = true;
-        uint32_t plen = 31;
-        const bool ok = KLF_ABLATE >= 2 ? true : parse_line_at(s_tile, segp, p0, rel_lo, seg_len, a.since_sec, a.since_nsec, &so, &plen);
-        s_meta[k] = make_meta(ok, so, plen);
-        s_loff[k] = (uint16_t)(p0 - rel_lo);
-        n_parsed += ok;
-        n_since += so;
-      }
+    auto put = [&](uint32_t j, uint32_t off) {
+      bool so;
+      uint32_t plen = 0;
+      const bool ok = parse_line_at(s_tile, segp, rel_lo + off, rel_lo, seg_len, a.since_sec, a.since_nsec, &so, &plen);
+      const uint32_t slot = off | ((uint32_t)make_meta(ok, so, plen) << 16);
+      if (!dense) s_slot[j] = slot;
+      else if (pool_ok) pool_dst[j] = slot;
+      n_parsed += ok;
+      n_since += so;
+    };
+    if (first && t == 0) put(0, 0);
+    for (uint64_t m = starts; m;) {
+      const int q = __ffsll((unsigned long long)m) - 1;
+      m &= m - 1;
+      put(texcl + (uint32_t)__popcll(ev & ((2ull << q) - 1)) - k0, toff0 + q + 1);
     }
-
-    // ---- 4. look-back: global index of the tile's first line ----
-#if KLF_ABLATE >= 1
-    if (t == 0) s_excl = 0;
-#else
-    if (wv == 0) {
-      const uint64_t ex = lookback_wave(a.status, tile, (uint64_t)agg, 0ull, SumComb(), err_flag, lane);
-      if (lane == 0) s_excl = ex;
-    }
-#endif
+    KLF_STAMP(tile, 7);
+    if (dense) __threadfence_block();
     __syncthreads();
-    const uint64_t tile_lines = s_excl;
-    const uint64_t lines_before = tile_lines + texcl;
+    KLF_STAMP(tile, 2);
 
-    // ---- 5. write-out ----
-    if (staged) {  // coalesced: local line k -> global tile_lines + k
-      const uint32_t k0 = first ? 0 : 1;
-      const bool tile_has_end = last;  // the stream's final event lies in this tile
-      const uint32_t k1 = tile_has_end ? agg : agg + 1;
-      for (uint32_t k = k0 + t; k < k1; k += kThreads) {
-        const uint64_t l = tile_lines + k;
-        if (l < a.cap_lines) {
-          a.meta[l] = s_meta[k];
-          a.line_off[l + s] = (uint64_t)rel_lo + s_loff[k];
-        } else {
-          atomicOr(err_flag, 1u);
-        }
+    // ---- fused single-literal grep ----
+    // Anchor hits are rare (the literal's rarest byte); each names a candidate start
+    // p = anchor - lit_anchor.  A tile owns the starts inside it: anchors of this tile
+    // whose start lies in the previous tile are left to that tile, which scans its halo.
+    if (LIT) {
+      const uint32_t m = a.lit_len, ka = a.lit_anchor;
+      uint64_t hcand = 0;  // halo anchors [kTile, kTile + ka) -> starts in this tile's tail
+      if (t == kThreads - 1 && ka > 0 && !last) {
+        for (uint32_t j = 0; j < ka; ++j)
+          if (s_tile[kTile + j] == a.lit[ka]) hcand |= 1ull << j;
       }
-    } else {  // dense tile: parse and write per thread
-      if (reset) {
-        bool so;
-        uint32_t plen = 0;
-        const bool ok = parse_line_at(s_tile, segp, rel0, rel_lo, seg_len, a.since_sec, a.since_nsec, &so, &plen);
-        if (lines_before < a.cap_lines) {
-          a.line_off[lines_before + s] = 0;
-          a.meta[lines_before] = make_meta(ok, so, plen);
-        } else {
-          atomicOr(err_flag, 1u);
-        }
-        n_parsed += ok;
-        n_since += so;
-      }
-      for (uint64_t m = starts; m;) {
-        const int q = __ffsll((unsigned long long)m) - 1;
-        m &= m - 1;
-        const uint64_t l = lines_before + (uint64_t)__popcll(ev & ((2ull << q) - 1));
-        const int64_t p0 = rel0 + q + 1;
-        bool so;
-        uint32_t plen = 0;
-        const bool ok = parse_line_at(s_tile, segp, p0, rel_lo, seg_len, a.since_sec, a.since_nsec, &so, &plen);
-        if (l < a.cap_lines) {
-          a.line_off[l + s] = (uint64_t)p0;
-          a.meta[l] = make_meta(ok, so, plen);
-        } else {
-          atomicOr(err_flag, 1u);
-        }
-        n_parsed += ok;
-        n_since += so;
-      }
-    }
-    if (reset) a.segout[s].line_lo = lines_before;
-    if (has_end) {
-      const uint64_t lend = lines_before + cnt;
-      if (lend <= a.cap_lines) a.line_off[lend + s] = (uint64_t)seg_len;
-      else atomicOr(err_flag, 1u);
-      a.segout[s].line_hi = lend;
-      a.segout[s].frag = (nl >> eb) & 1 ? 0 : 1;
-    }
-
-    // ---- fused single-literal grep (rare path: first-byte candidates) ----
-    if (LIT && cand) {
-      const uint32_t m = a.lit_len;
-      {  // last-byte filter from the LDS window at +m-1 (word by word)
-        const uint32_t off = (uint32_t)t * kBytesPerThread + m - 1;
-        const uint32_t* s32 = reinterpret_cast<const uint32_t*>(s_tile);
-        const uint32_t base = off >> 2, sh = (off & 3) * 8;
-        const uint32_t pat = a.lit[m - 1] * 0x01010101u;
-        uint32_t prev = s32[base], lo = 0, hi = 0;
-#pragma unroll
-        for (int j = 0; j < 16; ++j) {
-          const uint32_t nx = s32[base + j + 1];
-          const uint32_t wj = sh ? (uint32_t)((((uint64_t)nx << 32) | prev) >> sh) : prev;
-          prev = nx;
-          if (j < 8) lo |= zmask4(wj ^ pat) << (4 * j);
-          else hi |= zmask4(wj ^ pat) << (4 * (j - 8));
-        }
-        cand &= ((uint64_t)hi << 32) | lo;
-      }
-      int64_t carried_cs = -2;  // content start of the line carried into my bytes (lazy)
-      while (cand) {
-        const int b = __ffsll((unsigned long long)cand) - 1;
-        cand &= cand - 1;
-        const int64_t pos = rel0 + b;
-        if (pos + (int64_t)m > seg_len) continue;
-        bool eq = true;
-        for (uint32_t k = 1; k + 1 < m && eq; ++k) eq = s_tile[t * kBytesPerThread + b + k] == a.lit[k];
-        if (!eq) continue;
-        const uint64_t below = b == 0 ? 0 : ((1ull << b) - 1);
-        const uint64_t E = ev & below;
-        int64_t cs;  // content start of the hit's line, -1 = unparseable
-        if (E || reset || (staged && (texcl > 0 || first))) {
-          // the line starts inside this tile: its local index is the events before it
-          const uint32_t kl = texcl + (uint32_t)__popcll(E);
-          const int64_t p0 = E ? rel0 + (63 - __clzll(E)) + 1 : (reset ? rel0 : -1);
-          if (staged) {
-            const uint16_t mt = s_meta[kl];
-            cs = (mt & Meta::kParsed) ? (int64_t)rel_lo + s_loff[kl] + (mt >> 2) : -1;
-          } else if (p0 >= 0) {
-            bool so;
-            uint32_t plen = 0;
-            cs = parse_line_at(s_tile, segp, p0, rel_lo, seg_len, 0, 0, &so, &plen) ? p0 + plen : -1;
-          } else {
-            if (carried_cs == -2) carried_cs = carried_content_start(s_tile, segp, rel_lo, seg_len, rel0 - 1);
-            cs = carried_cs;
+      for (int pass = 0; pass < 2; ++pass) {
+        uint64_t cm = pass == 0 ? cand : hcand;
+        const int64_t abase = pass == 0 ? rel_lo + toff0 : rel_lo + kTile;
+        while (cm) {
+          const int b = __ffsll((unsigned long long)cm) - 1;
+          cm &= cm - 1;
+          const int64_t pos = abase + b - (int64_t)ka;  // candidate literal start
+          if (pos < rel_lo || pos >= rel_lo + tile_len || pos + (int64_t)m > seg_len) continue;
+          bool eq = true;
+          {
+            const int64_t o0 = pos - rel_lo;
+            if (o0 + (int64_t)m + 4 <= kTile + kHalo) {  // 4 bytes per LDS read
+              const uint32_t* s32 = reinterpret_cast<const uint32_t*>(s_tile);
+              const uint32_t sh = (uint32_t)(o0 & 3) * 8;
+              uint32_t wi = (uint32_t)(o0 >> 2);
+              uint32_t prev = s32[wi];
+              for (uint32_t k = 0; k < m && eq; k += 4) {
+                const uint32_t nx = s32[++wi];
+                const uint32_t got = sh ? (uint32_t)((((uint64_t)nx << 32) | prev) >> sh) : prev;
+                prev = nx;
+                const uint32_t nb = m - k < 4 ? m - k : 4;
+                const uint32_t msk = nb == 4 ? 0xFFFFFFFFu : ((1u << (8 * nb)) - 1);
+                eq = ((got ^ a.lit_words[k >> 2]) & msk) == 0;
+              }
+            } else {
+              for (uint32_t k = 0; k < m && eq; ++k) {
+                const int64_t o = o0 + k;
+                const uint8_t c = o < kTile + kHalo ? s_tile[o] : segp[pos + k];
+                eq = c == a.lit[k];
+              }
+            }
           }
-        } else {
-          if (carried_cs == -2) carried_cs = carried_content_start(s_tile, segp, rel_lo, seg_len, rel0 - 1);
-          cs = carried_cs;
-        }
-        if (cs >= 0 && pos >= cs && cs <= pos) {
-          const uint64_t l = lines_before + (uint64_t)__popcll(E);
-          if (l < a.cap_lines) atomicOr(&a.bits[l >> 5], 1u << (l & 31));
+          if (!eq) continue;
+          // the hit's line: last staged line start at or before pos (binary search)
+          const uint32_t off = (uint32_t)(pos - rel_lo);
+          if (!pool_ok) continue;
+          auto slot_at = [&](int i) -> uint32_t { return dense ? pool_dst[i] : s_slot[i]; };
+          int lo = 0, hi = (int)nlines;  // find count of slots with start <= off
+          while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if ((slot_at(mid) & 0x7FFFu) <= off) lo = mid + 1; else hi = mid;
+          }
+          if (lo > 0) {  // the line starts in this tile: its slot says where content starts
+            const uint32_t v = slot_at(lo - 1);
+            const uint32_t mt = v >> 16;
+            if ((mt & Meta::kParsed) && off >= (v & 0x7FFFu) + (mt >> 2)) {
+              if (!dense) atomicOr(&s_slot[lo - 1], 0x8000u);
+              else atomicOr(&pool_dst[lo - 1], 0x8000u);
+            }
+          } else {  // carried in from an earlier tile: k_scatter decides (furthest hit wins)
+            atomicMax(&s_carry, off + 1);
+          }
         }
       }
     }
 
-    // ---- per-tile counters ----
+    KLF_STAMP(tile, 3);
+    // ---- per-tile record + staged slots out ----
     const uint32_t pp = wave_sum(n_parsed), qq = wave_sum(n_since);
     if (lane == 0) { s_red[wv][0] = pp; s_red[wv][1] = qq; }
     __syncthreads();
-    if (t == 0) {
-      a.tile_cnt[2 * (size_t)tile] = s_red[0][0] + s_red[1][0] + s_red[2][0] + s_red[3][0];
-      a.tile_cnt[2 * (size_t)tile + 1] = s_red[0][1] + s_red[1][1] + s_red[2][1] + s_red[3][1];
+    if (!dense) {
+      uint32_t* dst = a.slots + (size_t)tile * kSlots;
+      for (uint32_t j = t; j < nlines; j += kThreads) dst[j] = s_slot[j];
     }
+    if (t == 0) {
+      TileStat ts;
+      ts.events = agg;
+      ts.flags = (dense ? 1u : 0u) | (s_carry ? 2u : 0u);
+      ts.carry_off = s_carry;  // furthest literal hit in the carried-in line, + 1
+      ts.parsed = s_red[0][0] + s_red[1][0] + s_red[2][0] + s_red[3][0];
+      ts.since_ok = s_red[0][1] + s_red[1][1] + s_red[2][1] + s_red[3][1];
+      ts.pool_base = dense ? s_pool : 0;
+      ts.pad[0] = ts.pad[1] = 0;
+      a.tstat[tile] = ts;
+    }
+    KLF_STAMP(tile, 4);
     __syncthreads();  // LDS is reused by the next tile
+  }
+}
+
+// ---- K1b/K1c: tile line bases (exclusive scan of TileStat.events) -------------------
+constexpr int kTilesPerScanBlock = 4096;  // 256 threads x 16 tiles
+
+__global__ __launch_bounds__(256) void k_tsum(RunArgs a) {
+  __shared__ uint64_t s_w[4];
+  const uint32_t t0 = blockIdx.x * kTilesPerScanBlock + threadIdx.x * 16;
+  uint64_t v = 0;
+  for (int j = 0; j < 16; ++j)
+    if (t0 + j < a.ntiles) v += a.tstat[t0 + j].events;
+  v = wave_sum(v);
+  if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) a.bsum[blockIdx.x] = s_w[0] + s_w[1] + s_w[2] + s_w[3];
+}
+
+__global__ __launch_bounds__(256) void k_tbase(RunArgs a) {
+  __shared__ uint64_t s_w[4];
+  __shared__ uint64_t s_base;
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  {  // prefix of the preceding blocks' sums
+    uint64_t v = 0;
+    for (uint32_t b = t; b < blockIdx.x; b += 256) v += a.bsum[b];
+    v = wave_sum(v);
+    if (lane == 0) s_w[wv] = v;
+    __syncthreads();
+    if (t == 0) s_base = s_w[0] + s_w[1] + s_w[2] + s_w[3];
+    __syncthreads();
+  }
+  const uint32_t t0 = blockIdx.x * kTilesPerScanBlock + t * 16;
+  uint32_t ev[16];
+  uint64_t v = 0;
+  for (int j = 0; j < 16; ++j) {
+    ev[j] = t0 + j < a.ntiles ? a.tstat[t0 + j].events : 0;
+    v += ev[j];
+  }
+  const uint64_t inc = wave_incl_scan_add(v, lane);
+  if (lane == 63) s_w[wv] = inc;
+  __syncthreads();
+  uint64_t pre = s_base;
+  for (int k = 0; k < wv; ++k) pre += s_w[k];
+  uint64_t b = pre + inc - v;
+  for (int j = 0; j < 16; ++j) {
+    const uint32_t tile = t0 + j;
+    if (tile >= a.ntiles) break;
+    a.tile_base[tile] = b;
+    const uint32_t s = a.tile_seg[tile];
+    if (tile == a.segs[s].tile0) a.segout[s].line_lo = b;
+    if (tile == a.segs[s].tile0 + a.segs[s].ntiles - 1) a.segout[s].line_hi = b + ev[j];
+    b += ev[j];
+  }
+}
+
+// ---- K1d: scatter staged slots into the global line arrays --------------------------
+// One wave per tile (4 tiles per workgroup iteration), lanes over the tile's lines.
+__global__ __launch_bounds__(256) void k_scatter(RunArgs a) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  uint32_t* err_flag = a.counters + 2;
+  for (uint32_t tile = blockIdx.x * 4 + wv; tile < a.ntiles; tile += gridDim.x * 4) {
+    const TileStat ts = a.tstat[tile];
+    const uint32_t s = a.tile_seg[tile];
+    const SegDesc sd = a.segs[s];
+    const int64_t rel_lo = (int64_t)(tile - sd.tile0) * kTile;
+    const bool first = rel_lo == 0, last = rel_lo + kTile >= (int64_t)sd.len;
+    const uint32_t k0 = first ? 0 : 1, k1 = last ? ts.events : ts.events + 1;
+    const uint32_t n = k1 > k0 ? k1 - k0 : 0;
+    const uint64_t base = a.tile_base[tile];
+    const uint32_t* src = (ts.flags & 1u) ? a.pool + ts.pool_base : a.slots + (size_t)tile * kSlots;
+    for (uint32_t j = lane; j < n; j += 64) {
+      const uint32_t sl = src[j];
+      const uint64_t l = base + k0 + j;
+      if (l >= a.cap_lines) { atomicOr(err_flag, 1u); continue; }
+      a.line_off[l + s] = (uint64_t)rel_lo + (sl & 0x7FFFu);
+      a.meta[l] = (uint16_t)(sl >> 16);
+      if (sl & 0x8000u) atomicOr(&a.bits[l >> 5], 1u << (l & 31));
+    }
+    if (lane == 0) {
+      if ((ts.flags & 2u) && base < a.cap_lines) {
+        // literal hit inside the line carried in from an earlier tile: that line's start
+        // is the last staged start of the nearest earlier tile of the stream that has one
+        int64_t cs = -1;
+        for (uint32_t pt = tile; pt > sd.tile0;) {
+          --pt;
+          const TileStat pst = a.tstat[pt];
+          const int64_t prel = (int64_t)(pt - sd.tile0) * kTile;
+          const uint32_t pk0 = prel == 0 ? 0 : 1;
+          const uint32_t pn = pst.events + 1 > pk0 ? pst.events + 1 - pk0 : 0;  // never the stream's last tile
+          if (pn == 0) continue;
+          const uint32_t* psrc = (pst.flags & 1u) ? a.pool + pst.pool_base : a.slots + (size_t)pt * kSlots;
+          const uint32_t v = psrc[pn - 1];
+          const uint32_t mt = v >> 16;
+          if (mt & Meta::kParsed) cs = prel + (int64_t)(v & 0x7FFFu) + (mt >> 2);
+          break;
+        }
+        if (cs >= 0 && rel_lo + (int64_t)ts.carry_off - 1 >= cs) atomicOr(&a.bits[base >> 5], 1u << (base & 31));
+      }
+      if (last) {
+        const uint64_t lend = base + ts.events;
+        if (lend <= a.cap_lines) a.line_off[lend + s] = sd.len;
+        else atomicOr(err_flag, 1u);
+      }
+    }
   }
 }
 
@@ -690,8 +819,8 @@ __global__ __launch_bounds__(256) void k_count(RunArgs a, uint32_t nblk_tiles, u
     const uint32_t tile = blockIdx.x * 256 + threadIdx.x;
     const uint32_t tclamp = tile < a.ntiles ? tile : a.ntiles - 1;
     const uint32_t s = find_seg_by_tile(a.segs, a.nsegs, tclamp);
-    const uint64_t p = tile < a.ntiles ? a.tile_cnt[2 * (size_t)tile] : 0;
-    const uint64_t q = tile < a.ntiles ? a.tile_cnt[2 * (size_t)tile + 1] : 0;
+    const uint64_t p = tile < a.ntiles ? a.tstat[tile].parsed : 0;
+    const uint64_t q = tile < a.ntiles ? a.tstat[tile].since_ok : 0;
     seg_reduce_add(s, p, &a.segout[0].parsed, stride, s_seg, s_acc);
     seg_reduce_add(s, q, &a.segout[0].since_ok, stride, s_seg, s_acc);
   } else {
@@ -928,12 +1057,30 @@ __global__ __launch_bounds__(kThreads) void k_compact(RunArgs a) {
 
 }  // namespace
 
+hipError_t dump_timeline(void* host, size_t bytes) {
+#if KLF_TIMELINE
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_timeline), bytes, 0, hipMemcpyDeviceToHost);
+#else
+  (void)host; (void)bytes;
+  return hipErrorNotSupported;
+#endif
+}
+hipError_t clear_timeline() {
+#if KLF_TIMELINE
+  void* p;
+  hipError_t e = hipGetSymbolAddress(&p, HIP_SYMBOL(g_timeline));
+  if (e != hipSuccess) return e;
+  return hipMemset(p, 0, sizeof(uint64_t) * 300000 * 8);
+#else
+  return hipSuccess;
+#endif
+}
+
 hipError_t launch_pipeline(const RunArgs& a, hipStream_t st, hipEvent_t* ev, int num_cus) {
   hipError_t e;
 #define KLF_TRY(x) do { e = (x); if (e != hipSuccess) return e; } while (0)
   KLF_TRY(hipEventRecord(ev[0], st));
   KLF_TRY(hipMemsetAsync(a.counters, 0, kNumCounters * sizeof(uint32_t), st));
-  KLF_TRY(hipMemsetAsync(a.status, 0, (size_t)a.ntiles * 8, st));
   KLF_TRY(hipMemsetAsync(a.segout, 0, (size_t)a.nsegs * sizeof(SegOut), st));
   KLF_TRY(hipMemsetAsync(a.cstatus, 0, (size_t)a.max_cblocks * 2 * 8, st));
   if (a.grep_mode != kGrepNone) KLF_TRY(hipMemsetAsync(a.bits, 0, (size_t)(a.cap_lines / 32 + 1) * 4, st));
@@ -952,12 +1099,20 @@ hipError_t launch_pipeline(const RunArgs& a, hipStream_t st, hipEvent_t* ev, int
       (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_scan<false>, kThreads, 0);
     occ = occ < 1 ? 1 : (occ > 8 ? 8 : occ);
     uint32_t grid = (uint32_t)(num_cus * occ);
-    grid = grid / kScanGroups * kScanGroups;
-    if (grid < kScanGroups) grid = kScanGroups;
+    if (grid > a.ntiles) grid = a.ntiles;
     if (a.grep_mode == kGrepLit1)
       hipLaunchKernelGGL(k_scan<true>, dim3(grid), dim3(kThreads), 0, st, a);
     else
       hipLaunchKernelGGL(k_scan<false>, dim3(grid), dim3(kThreads), 0, st, a);
+    KLF_TRY(hipGetLastError());
+    const uint32_t nb = (a.ntiles + kTilesPerScanBlock - 1) / kTilesPerScanBlock;
+    hipLaunchKernelGGL(k_tsum, dim3(nb), dim3(256), 0, st, a);
+    KLF_TRY(hipGetLastError());
+    hipLaunchKernelGGL(k_tbase, dim3(nb), dim3(256), 0, st, a);
+    KLF_TRY(hipGetLastError());
+    uint32_t sg = (a.ntiles + 3) / 4;
+    if (sg > (uint32_t)num_cus * 8) sg = num_cus * 8;
+    hipLaunchKernelGGL(k_scatter, dim3(sg), dim3(256), 0, st, a);
   }
   KLF_TRY(hipGetLastError());
   KLF_TRY(hipEventRecord(ev[2], st));

@@ -23,6 +23,19 @@ constexpr uint32_t kScanGroups = 128;
 constexpr uint32_t kCtrStride = 64;                 // u32 words between group counters
 constexpr uint32_t kCtrScanGroups = 64;             // counters[64 + g * kCtrStride]
 constexpr uint32_t kNumCounters = kCtrScanGroups + kScanGroups * kCtrStride;
+constexpr uint32_t kCtrPool = 4;                    // counters[4]: dense-tile pool allocator
+
+constexpr int kSlots = 528;  // staged line slots per tile (>= 16 KiB / 32-byte kubelet line + 1)
+
+// Per-tile record of the scan (K1a), 32 B.
+struct TileStat {
+  uint32_t events;     // line-end events in the tile
+  uint32_t flags;      // bit0 dense (slots in the pool), bit1 literal hit in the carried-in line
+  uint32_t parsed, since_ok;
+  uint32_t pool_base;  // dense tiles: first pool slot
+  uint32_t carry_off;  // 1 + offset of the furthest literal hit in the carried-in line (0 = none)
+  uint32_t pad[2];
+};
 
 // One segment (= one non-empty stream) of the device batch.
 struct SegDesc {
@@ -81,9 +94,16 @@ struct RunArgs {
   uint32_t grep_mode;
   const uint8_t* lit;  // kGrepLit1 literal (device)
   uint32_t lit_len;
+  uint32_t lit_anchor; // index of the literal's rarest byte (scan anchor)
+  const uint32_t* lit_words;  // the literal as little-endian dwords (zero padded)
   DevPatterns pats;
   // workspace (device)
-  uint64_t* status;     // [ntiles] scan look-back words
+  TileStat* tstat;      // [ntiles]
+  uint32_t* slots;      // [ntiles * kSlots] staged line slots
+  uint32_t* pool;       // [pool_cap] slots of dense tiles
+  uint64_t pool_cap;
+  uint64_t* tile_base;  // [ntiles] global line index of each tile's line 0
+  uint64_t* bsum;       // [ntiles / 4096 + 1] scan block sums
   uint64_t* cstatus;    // [2 * max compaction blocks] compaction look-back words
   uint32_t* counters;   // [kNumCounters]: 1 compact ticket, 2 error flags, 3 compact blocks,
                         // [8, 8+kScanGroups) scan ticket groups
@@ -91,7 +111,6 @@ struct RunArgs {
   uint16_t* meta;       // [cap_lines]
   uint32_t* bits;       // [cap_lines / 32 + 1]
   uint64_t cap_lines;
-  uint32_t* tile_cnt;   // [ntiles * 2] parsed, since_ok
   SegOut* segout;       // [nsegs]
   uint64_t* wpre;       // [nsegs + 1] exclusive prefix of window sizes
   uint8_t* out;         // output bytes (capacity >= total input)
@@ -103,5 +122,8 @@ struct RunArgs {
 // scan, ev[3] after the general matcher, ev[4] after counts+tail+window prefix, ev[5]
 // after compaction.  Returns a hipError_t.
 hipError_t launch_pipeline(const RunArgs& a, hipStream_t stream, hipEvent_t* ev, int num_cus);
+// Diagnostic builds (-DKLF_TIMELINE=1): per-tile scan timeline; hipErrorNotSupported otherwise.
+hipError_t dump_timeline(void* host, size_t bytes);
+hipError_t clear_timeline();
 
 }  // namespace klf

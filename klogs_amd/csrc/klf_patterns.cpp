@@ -639,6 +639,14 @@ bool glushkov_match(const GlushkovTables& g, const uint8_t* s, size_t n) {
   return (d & g.end_accept) != 0;
 }
 
+int log_byte_class(uint8_t c) {
+  if (c >= 0x80 || (c < 0x20 && c != '\t')) return 1;          // control and high bytes
+  if (strchr("!#$%&'*+;<>?@[\\]^_`|~", c) && c) return 2;        // rare punctuation
+  if (c >= 'A' && c <= 'Z') return strchr("ERONWAIFDBUGT", c) ? 4 : 3;  // log-level letters are common
+  if (c >= '0' && c <= '9') return 5;
+  return 6;                                                    // lowercase, space, common punctuation
+}
+
 bool compile_set(const std::vector<std::vector<uint8_t>>& pats, const std::vector<uint32_t>& kinds,
                  CompiledSet& out, std::string& err, int& err_code) {
   out = CompiledSet();
@@ -687,6 +695,11 @@ bool compile_set(const std::vector<std::vector<uint8_t>>& pats, const std::vecto
   if (rxs.empty() && lits.size() == 1 && lits[0].size() <= 256) {
     out.mode = CompiledSet::kLiteral1;
     out.literal = lits[0];
+    int best = 99;
+    for (size_t i = 0; i < out.literal.size(); ++i) {
+      const int cl = log_byte_class(out.literal[i]);
+      if (cl < best) { best = cl; out.literal_anchor = (uint32_t)i; }
+    }
     return true;
   }
   out.mode = CompiledSet::kGeneral;

@@ -43,6 +43,7 @@ struct CompiledSet {
   };
   Mode mode = kNone;
   std::vector<uint8_t> literal;  // kLiteral1
+  uint32_t literal_anchor = 0;   // kLiteral1: index of its rarest byte in log text
 
   // kGeneral: Aho-Corasick over the literals (empty when no literal).
   uint32_t ac_states = 0;
@@ -69,6 +70,9 @@ bool compile_regex(const uint8_t* pat, size_t n, GlushkovTables& out, std::strin
 // Compiles a whole OR'ed pattern set.  kinds[i]: 0 literal, 1 regex.
 bool compile_set(const std::vector<std::vector<uint8_t>>& pats, const std::vector<uint32_t>& kinds,
                  CompiledSet& out, std::string& err, int& err_code);
+
+// Expected-frequency class of a byte in log text (lower = rarer); picks scan anchors.
+int log_byte_class(uint8_t c);
 
 // Host reference simulation of one compiled regex on a content (used by unit tests of
 // the compiler through klf_debug_regex_match; the GPU kernel runs the same recurrence).

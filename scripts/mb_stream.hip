@@ -84,6 +84,15 @@ __global__ __launch_bounds__(256) void v3(const uint4* in, uint32_t* out, uint32
   }
   if (threadIdx.x == 0) atomicAdd(&out[blockIdx.x & 1023], c);
 }
+// ALU calibration: dependent integer ops per lane; reports the effective shader clock
+__global__ __launch_bounds__(256) void alu(uint32_t* out, uint32_t iters) {
+  uint32_t x = threadIdx.x, y = blockIdx.x;
+  for (uint32_t i = 0; i < iters; ++i) {
+#pragma unroll
+    for (int k = 0; k < 16; ++k) { x = x * 1664525u + y; y ^= x >> 7; }
+  }
+  if (x == 0x12345678u && y == 1u) out[0] = x;
+}
 // V4: persistent static, 2 tiles in flight per workgroup (register double buffer)
 __global__ __launch_bounds__(256) void v4(const uint4* in, uint32_t* out, uint32_t ntiles) {
   uint32_t c = 0;
@@ -111,7 +120,8 @@ __global__ __launch_bounds__(256) void v4(const uint4* in, uint32_t* out, uint32
   if ((threadIdx.x & 63) == 0) atomicAdd(&out[blockIdx.x & 1023], c);
 }
 
-int main() {
+int main(int argc, char** argv) {
+  const bool quick = argc > 1;
   const size_t bytes = (size_t)4 << 30;
   const uint32_t ntiles = (uint32_t)(bytes / TILE);
   uint8_t* d;
@@ -132,18 +142,37 @@ int main() {
   auto run = [&](const char* name, auto launch) {
     float best = 1e9;
     for (int r = 0; r < 8; ++r) {
-      hipMemset(out, 0, 4096 * 4);
-      hipMemset(ctr, 0, 1 << 20);
-      hipEventRecord(e0);
+      (void)hipMemset(out, 0, 4096 * 4);
+      (void)hipMemset(ctr, 0, 1 << 20);
+      (void)hipEventRecord(e0);
       launch();
-      hipEventRecord(e1);
-      hipEventSynchronize(e1);
+      (void)hipEventRecord(e1);
+      (void)hipEventSynchronize(e1);
       float ms;
-      hipEventElapsedTime(&ms, e0, e1);
+      (void)hipEventElapsedTime(&ms, e0, e1);
       if (r >= 2 && ms < best) best = ms;
     }
     printf("%-40s %8.3f ms  %7.1f GB/s\n", name, best, bytes / best / 1e6);
   };
+  if (quick) {  // calibration line for scripts/gpu_abl.sh
+    run("calib v1 persistent static x4/CU", [&] { hipLaunchKernelGGL(v1, dim3(cus * 4), dim3(256), 0, 0, in, out, ntiles); });
+    run("calib v4 register double buffer x4/CU", [&] { hipLaunchKernelGGL(v4, dim3(cus * 4), dim3(256), 0, 0, in, out, ntiles); });
+    {
+      const uint32_t iters = 20000;
+      hipLaunchKernelGGL(alu, dim3(cus * 8), dim3(256), 0, 0, out, iters);
+      (void)hipDeviceSynchronize();
+      (void)hipEventRecord(e0);
+      hipLaunchKernelGGL(alu, dim3(cus * 8), dim3(256), 0, 0, out, iters);
+      (void)hipEventRecord(e1);
+      (void)hipEventSynchronize(e1);
+      float ms;
+      (void)hipEventElapsedTime(&ms, e0, e1);
+      // 8 waves/CU over 4 SIMDs = 2 waves per SIMD; each dependent op ~1 issue per 1 cycle
+      // per wave (2 waves interleave): ops per SIMD = 2 * iters * 16 * 3
+      printf("calib alu %.3f ms  ~%.2f G wave-ops/s per SIMD\n", ms, 2.0 * iters * 16 * 3 / (ms * 1e6));
+    }
+    return 0;
+  }
   run("v0 one tile per WG", [&] { hipLaunchKernelGGL(v0, dim3(ntiles), dim3(256), 0, 0, in, out); });
   for (int occ : {4, 8}) {
     char n[96];

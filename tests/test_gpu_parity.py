@@ -75,6 +75,25 @@ def test_multi_stream_and_empty(gpu):
         check_against_c(streams, since, tail, grep)
 
 
+def test_dense_tiles(gpu):
+    """Tiles with more line starts than staged slots (lines < 32 B) take the pool path."""
+    import random as _r
+    rng = _r.Random(7)
+    parts = []
+    for i in range(60000):
+        k = rng.random()
+        if k < 0.5:
+            parts.append(b"\n")
+        elif k < 0.8:
+            parts.append(b"x%d\n" % i)
+        else:
+            parts.append(b"2024-10-22T00:00:%02dZ %s\n" % (i % 60, b"ERR_CONN_RESET" if i % 7 == 0 else b"ok"))
+    d = b"".join(parts)
+    for since, tail, grep in [(None, -1, []), ((synth.T0 + 30, 0), 100, []), (None, 50, [synth.NEEDLE]),
+                              (None, -1, [synth.NEEDLE])]:
+        check_against_c([d, synth.generate(synth.TEXT, 1, 0, 100_000), d[:70001]], since, tail, grep)
+
+
 def _golden():
     import json
     from pathlib import Path
