@@ -355,6 +355,7 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
     a.lit = e->d_lit.as<uint8_t>();
     a.lit_len = (uint32_t)e->cs.literal.size();
     a.lit_anchor = e->cs.literal_anchor;
+    a.lit_anchor_byte = e->cs.literal.empty() ? 0u : e->cs.literal[e->cs.literal_anchor];
     a.lit_words = e->d_lit.as<uint32_t>();
     a.pats = e->dpats;
     a.tstat = e->d_tstat.as<klf::TileStat>();

@@ -391,9 +391,14 @@ __device__ __forceinline__ bool parse_line_at(const uint8_t* lds, const uint8_t*
 #ifndef KLF_SCAN_OCC
 #define KLF_SCAN_OCC 4
 #endif
+// The tile descriptors come in as separate __restrict__ const parameters so that their
+// (wave-uniform) reads compile to scalar loads: a vector load of them would be ordered
+// behind the in-flight prefetch by vmcnt and stall every tile on the next tile's bytes.
 template <bool LIT>
-__global__ __launch_bounds__(kThreads, KLF_SCAN_OCC) void k_scan(RunArgs a) {
+__global__ __launch_bounds__(kThreads, KLF_SCAN_OCC) void k_scan(RunArgs a, const uint32_t* __restrict__ tseg,
+                                                               const SegDesc* __restrict__ segs) {
   __shared__ __attribute__((aligned(16))) uint8_t s_tile[kTile + kHalo];
+  __shared__ __attribute__((aligned(16))) uint32_t s_lit[kMaxFusedLiteral / 4 + 1];  // literal, zero padded
   __shared__ uint32_t s_slot[kSlots];  // line starts (offsets), then the parsed slots
   __shared__ uint32_t s_wsum[4];
   __shared__ uint32_t s_red[4][2];
@@ -403,9 +408,14 @@ __global__ __launch_bounds__(kThreads, KLF_SCAN_OCC) void k_scan(RunArgs a) {
   // One tile ahead in registers: the next tile's 16 KiB (+ halo) is in flight while this
   // tile is parsed (barriers here wait on LDS only, never on these loads).
   static_assert(kTile == kThreads * 16 * 4, "prefetch holds 4 uint4 per thread");
+  if (LIT) {  // the literal lives in LDS for the whole kernel (no vector loads per tile)
+    for (uint32_t i = t; i < kMaxFusedLiteral / 4 + 1; i += kThreads) s_lit[i] = i < (a.lit_len + 3) / 4 ? a.lit_words[i] : 0u;
+    __syncthreads();
+  }
+  const uint8_t* lit = reinterpret_cast<const uint8_t*>(s_lit);
   auto tile_src = [&](uint32_t tl) -> const uint4* {
-    const uint32_t ss = a.tile_seg[tl];
-    const SegDesc d = a.segs[ss];
+    const uint32_t ss = tseg[tl];
+    const SegDesc d = segs[ss];
     return reinterpret_cast<const uint4*>(a.bytes + d.base + (uint64_t)(tl - d.tile0) * kTile);
   };
   uint4 pf0, pf1, pf2, pf3, pfh = make_uint4(0, 0, 0, 0);  // named, not an array: stays in VGPRs
@@ -417,8 +427,8 @@ __global__ __launch_bounds__(kThreads, KLF_SCAN_OCC) void k_scan(RunArgs a) {
   for (uint32_t tile = blockIdx.x; tile < a.ntiles; tile += gridDim.x) {
     KLF_STAMP(tile, 0);
     // descriptors are re-read (scalar, cached) rather than carried: fewer live SGPRs
-    const uint32_t s = a.tile_seg[tile];
-    const SegDesc sd = a.segs[s];
+    const uint32_t s = tseg[tile];
+    const SegDesc sd = segs[s];
     const int64_t rel_lo = (int64_t)(tile - sd.tile0) * kTile;
     const int64_t seg_len = (int64_t)sd.len;
     const int64_t tile_len = seg_len - rel_lo < kTile ? seg_len - rel_lo : kTile;
@@ -449,16 +459,23 @@ __global__ __launch_bounds__(kThreads, KLF_SCAN_OCC) void k_scan(RunArgs a) {
     const uint32_t toff0 = (uint32_t)t * kBytesPerThread;  // my first byte, tile-relative
     uint64_t nl, cand = 0;
     {
-      uint32_t w[16];
+      // The lane's 4 x 16 B are read starting at chunk rot = (t >> 2) & 3: with a plain
+      // order lanes t, t+12, t+20, t+24 of a ds_read_b128 group hit the same banks (4-way
+      // conflict); rotated, every 16-lane group covers all 64 banks once.  The masks are
+      // built in read order and rotated back once.
+      const uint32_t rot = ((uint32_t)t >> 2) & 3u;
       const uint4* l = reinterpret_cast<const uint4*>(s_tile + toff0);
+      uint32_t w[16];
 #pragma unroll
       for (int v = 0; v < 4; ++v) {
-        const uint4 x = l[v];
+        const uint4 x = l[(v + rot) & 3u];
         w[4 * v] = x.x; w[4 * v + 1] = x.y; w[4 * v + 2] = x.z; w[4 * v + 3] = x.w;
       }
-      nl = eq_mask64_words(w, 0x0A0A0A0Au) & vm;
+      const uint32_t rs = 16u * rot;
+      auto unrot = [&](uint64_t m) -> uint64_t { return rs ? (m << rs) | (m >> (64u - rs)) : m; };
+      nl = unrot(eq_mask64_words(w, 0x0A0A0A0Au)) & vm;
       // literal anchor: the literal's rarest byte (chosen on the host), at offset lit_anchor
-      if (LIT) cand = eq_mask64_words(w, a.lit[a.lit_anchor] * 0x01010101u) & vm;
+      if (LIT) cand = unrot(eq_mask64_words(w, a.lit_anchor_byte * 0x01010101u)) & vm;
     }
     const bool has_end = last && nvalid > 0 && rel_lo + toff0 + nvalid == seg_len;
     const int eb = nvalid - 1;
@@ -531,7 +548,7 @@ __global__ __launch_bounds__(kThreads, KLF_SCAN_OCC) void k_scan(RunArgs a) {
       uint64_t hcand = 0;  // halo anchors [kTile, kTile + ka) -> starts in this tile's tail
       if (t == kThreads - 1 && ka > 0 && !last) {
         for (uint32_t j = 0; j < ka; ++j)
-          if (s_tile[kTile + j] == a.lit[ka]) hcand |= 1ull << j;
+          if (s_tile[kTile + j] == a.lit_anchor_byte) hcand |= 1ull << j;
       }
       for (int pass = 0; pass < 2; ++pass) {
         uint64_t cm = pass == 0 ? cand : hcand;
@@ -555,13 +572,13 @@ __global__ __launch_bounds__(kThreads, KLF_SCAN_OCC) void k_scan(RunArgs a) {
                 prev = nx;
                 const uint32_t nb = m - k < 4 ? m - k : 4;
                 const uint32_t msk = nb == 4 ? 0xFFFFFFFFu : ((1u << (8 * nb)) - 1);
-                eq = ((got ^ a.lit_words[k >> 2]) & msk) == 0;
+                eq = ((got ^ s_lit[k >> 2]) & msk) == 0;
               }
             } else {
               for (uint32_t k = 0; k < m && eq; ++k) {
                 const int64_t o = o0 + k;
                 const uint8_t c = o < kTile + kHalo ? s_tile[o] : segp[pos + k];
-                eq = c == a.lit[k];
+                eq = c == lit[k];
               }
             }
           }
@@ -1101,9 +1118,9 @@ hipError_t launch_pipeline(const RunArgs& a, hipStream_t st, hipEvent_t* ev, int
     uint32_t grid = (uint32_t)(num_cus * occ);
     if (grid > a.ntiles) grid = a.ntiles;
     if (a.grep_mode == kGrepLit1)
-      hipLaunchKernelGGL(k_scan<true>, dim3(grid), dim3(kThreads), 0, st, a);
+      hipLaunchKernelGGL(k_scan<true>, dim3(grid), dim3(kThreads), 0, st, a, a.tile_seg, a.segs);
     else
-      hipLaunchKernelGGL(k_scan<false>, dim3(grid), dim3(kThreads), 0, st, a);
+      hipLaunchKernelGGL(k_scan<false>, dim3(grid), dim3(kThreads), 0, st, a, a.tile_seg, a.segs);
     KLF_TRY(hipGetLastError());
     const uint32_t nb = (a.ntiles + kTilesPerScanBlock - 1) / kTilesPerScanBlock;
     hipLaunchKernelGGL(k_tsum, dim3(nb), dim3(256), 0, st, a);

@@ -95,6 +95,7 @@ struct RunArgs {
   const uint8_t* lit;  // kGrepLit1 literal (device)
   uint32_t lit_len;
   uint32_t lit_anchor; // index of the literal's rarest byte (scan anchor)
+  uint32_t lit_anchor_byte;  // that byte
   const uint32_t* lit_words;  // the literal as little-endian dwords (zero padded)
   DevPatterns pats;
   // workspace (device)
