@@ -1,8 +1,9 @@
 // klf_kernels.hip — CDNA4 (gfx950) kernels of the klogs filter path.
 //
 // Pipeline over one device batch (streams laid out as 256-B-aligned segments):
-//   K1 k_scan      newline scan + line index (decoupled look-back over 16 KiB tiles),
-//                  RFC3339Nano parse + since mask per line, fused single-literal grep
+//   K1 k_scan      newline scan + RFC3339Nano parse + since mask per line + fused
+//                  single-literal grep over 4 KiB wave-tiles, staged per tile;
+//                  k_tsum/k_tbase tile line bases; k_scatter -> global line index
 //   K2 k_match     general pattern sets: Aho-Corasick DFA + Glushkov bit-parallel NFA
 //   K3 k_count     per-stream parsed / since_ok / matched counts
 //      k_tail      kubelet tail rule -> per-stream candidate window (one block / stream)
@@ -33,24 +34,6 @@ __device__ uint32_t g_lb_rounds, g_lb_spins;
 
 // ------------------------------------------------------------------ small helpers ---
 
-__device__ __forceinline__ uint32_t zero_bytes(uint32_t x) {
-  // high bit of each byte set iff that byte is 0 (exact, no false positives)
-  return ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x | 0x7F7F7F7Fu);
-}
-__device__ __forceinline__ uint32_t pack4(uint32_t z) {
-  return (((z >> 7) * 0x00204081u) >> 21) & 0xFu;
-}
-// 64-bit mask: bit i set iff byte i of the 64 bytes in w equals the byte in `pat`
-// (pat = byte * 0x01010101).
-__device__ __forceinline__ uint64_t eq_mask64(const uint32_t* w, uint32_t pat) {
-  uint32_t lo = 0, hi = 0;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) lo |= pack4(zero_bytes(w[j] ^ pat)) << (4 * j);
-#pragma unroll
-  for (int j = 0; j < 8; ++j) hi |= pack4(zero_bytes(w[8 + j] ^ pat)) << (4 * j);
-  return ((uint64_t)hi << 32) | lo;
-}
-
 __device__ __forceinline__ uint64_t atomic_load_u64(const uint64_t* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -62,36 +45,6 @@ constexpr uint64_t kFlagA = 1ull << 62;  // aggregate published
 constexpr uint64_t kFlagP = 2ull << 62;  // inclusive prefix published
 constexpr uint64_t kFlagMask = 3ull << 62;
 constexpr uint32_t kSpinLimit = 1u << 24;
-
-// ---- scan summary monoid -----------------------------------------------------------
-// (count of line-end events, IND = a line starts inside the span, P = the line open at
-// the span's end has a parseable prefix).
-// combine(a, b) with a before b.  Packed u32 (thread/block level) and u64 (tiles).
-constexpr uint32_t kInd32 = 1u << 16, kP32 = 1u << 17;
-__device__ __forceinline__ uint32_t comb32(uint32_t a, uint32_t b) {
-  const uint32_t cnt = (a & 0xFFFFu) + (b & 0xFFFFu);
-  const uint32_t pb = (b & kInd32) ? (b & kP32) : (a & kP32);
-  return cnt | ((a | b) & kInd32) | pb;
-}
-constexpr uint64_t kCnt64 = (1ull << 59) - 1;
-constexpr uint64_t kP64 = 1ull << 59, kInd64 = 1ull << 61;
-__device__ __forceinline__ uint64_t comb64(uint64_t a, uint64_t b) {
-  const uint64_t cnt = ((a & kCnt64) + (b & kCnt64)) & kCnt64;
-  const uint64_t pb = (b & kInd64) ? (b & kP64) : (a & kP64);
-  return cnt | ((a | b) & kInd64) | pb;
-}
-__device__ __forceinline__ uint64_t widen(uint32_t x) {
-  return (uint64_t)(x & 0xFFFFu) | ((x & kInd32) ? kInd64 : 0) | ((x & kP32) ? kP64 : 0);
-}
-
-__device__ __forceinline__ uint32_t wave_incl_scan_summary(uint32_t x, int lane) {
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const uint32_t o = __shfl_up(x, d, 64);
-    if (lane >= d) x = comb32(o, x);
-  }
-  return x;
-}
 
 template <class T>
 __device__ __forceinline__ T wave_sum(T x) {
@@ -159,72 +112,8 @@ __device__ uint64_t lookback_wave(uint64_t* st, uint32_t idx, uint64_t agg, uint
   return acc;
 }
 
-// Wave-level decoupled look-back for a SUM chain (the scan's line counts): each lane
-// polls 4 consecutive predecessors, so one round covers 256 tiles.  With ~1500 tiles in
-// flight and a tile starting every ~10 ns, the nearest inclusive prefix trails by
-// ~(round-trip latency / 10 ns) tiles; a 64-wide window needed several dependent round
-// trips per tile, which fed back into a growing lag.  The aggregate must already be
-// published (flag A) unless idx == 0.  Returns the exclusive prefix in every lane.
-__device__ uint64_t lookback_wave_sum(uint64_t* st, uint32_t idx, uint64_t agg, uint32_t* err_flag, int lane) {
-  if (idx == 0) {
-    if (lane == 0) atomic_store_u64(&st[0], agg | kFlagP);
-    return 0;
-  }
-  uint64_t acc = 0;
-  int64_t hi = (int64_t)idx - 1;
-  for (;;) {
-    uint64_t w[4];
-    bool ready[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      w[k] = kFlagP;  // before tile 0: an empty inclusive prefix
-      ready[k] = hi - (4 * lane + k) < 0;
-    }
-    uint32_t spins = 0;
-    for (;;) {
-      bool all = true;
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        if (!ready[k]) {
-          w[k] = atomic_load_u64(&st[hi - (4 * lane + k)]);
-          ready[k] = (w[k] & kFlagMask) != 0;
-        }
-        all &= ready[k];
-      }
-      if (__all(all)) break;
-      __builtin_amdgcn_s_sleep(1);
-      if (++spins > kSpinLimit) {
-        if (lane == 0) atomicOr(err_flag, 2u);
-        return acc;
-      }
-    }
-#if KLF_TIMELINE
-    if (lane == 0 && idx < 300000) { g_timeline[(size_t)idx * 8 + 5] += 1; g_timeline[(size_t)idx * 8 + 6] += spins; }
-#endif
-    // nearest inclusive prefix: smallest distance 4*lane + k with flag P
-    uint32_t d = 0xFFFFFFFFu;
-#pragma unroll
-    for (int k = 3; k >= 0; --k)
-      if ((w[k] & kFlagMask) == kFlagP) d = 4 * lane + k;
-#pragma unroll
-    for (int s = 32; s >= 1; s >>= 1) d = min(d, (uint32_t)__shfl_xor((int)d, s, 64));
-    uint64_t v = 0;
-#pragma unroll
-    for (int k = 0; k < 4; ++k)
-      if ((uint32_t)(4 * lane + k) <= d) v += w[k] & ~kFlagMask;
-    acc += wave_sum(v);
-    if (d != 0xFFFFFFFFu) break;
-    hi -= 256;
-  }
-  if (lane == 0) atomic_store_u64(&st[idx], (acc + agg) | kFlagP);
-  return acc;
-}
-
 struct SumComb {
   __device__ uint64_t operator()(uint64_t a, uint64_t b) const { return (a + b) & ~kFlagMask; }
-};
-struct ScanComb {
-  __device__ uint64_t operator()(uint64_t a, uint64_t b) const { return comb64(a, b); }
 };
 
 __device__ __forceinline__ uint32_t find_seg_by_tile(const SegDesc* segs, uint32_t n, uint32_t tile) {
@@ -260,24 +149,6 @@ struct LineBytes {
     return seg[q];
   }
 };
-struct GlobalBytes {
-  const uint8_t* seg;
-  int64_t p0;
-  int64_t end;
-  __device__ __forceinline__ int operator()(uint32_t i) const {
-    const int64_t q = p0 + (int64_t)i;
-    return q < end ? seg[q] : -1;
-  }
-};
-
-// Cold-path parse (kept out of line so the hot loop's register budget stays at 64).
-__device__ __attribute__((noinline)) bool parse_at_cold(const uint8_t* lds, const uint8_t* seg, int64_t p0,
-                                                       int64_t rel_lo, int64_t seg_len, uint32_t* plen) {
-  TsResult r;
-  LineBytes gb{lds, seg, p0, rel_lo, seg_len};
-  return parse_line_prefix(gb, r, *plen);
-}
-
 __device__ __forceinline__ uint16_t make_meta(bool ok, bool since_ok, uint32_t plen) {
   if (!ok) return 0;
   const uint32_t pl = plen < kPlenEscape ? plen : kPlenEscape;
@@ -285,25 +156,29 @@ __device__ __forceinline__ uint16_t make_meta(bool ok, bool since_ok, uint32_t p
 }
 
 // ============================================================== K1: the scan ==
-// Streaming scan with NO inter-workgroup waiting (MI355X measurements, DESIGN.md §4:
-// a decoupled look-back round costs ~5 us under full-chip streaming, which dominated
-// the single-pass kernel).  Three steps:
-//   K1a k_scan     static tile assignment; per 16 KiB tile: stage in LDS, line-end
-//                  events, parse every line starting in the tile (fast fixed-width path
-//                  for the kubelet prefix), fused literal grep; per-tile results are
-//                  STAGED as one packed u32 per line start in the tile's slot region
-//                  (dense tiles, > kSlots starts, take slots from an overflow pool).
-//   K1b/K1c        device scan of per-tile line counts -> tile line bases, stream line
-//                  ranges.
+// Streaming scan with NO inter-workgroup waiting and NO workgroup barriers.  MI355X
+// measurements: a decoupled look-back round costs ~5 us under full-chip
+// streaming, and workgroup barriers between the phases of a tile left the SIMDs idle
+// while the slowest wave finished.  So the unit of work is a 4 KiB WAVE-TILE owned by one
+// wave from load to record:
+//   K1a k_scan     per wave-tile: register prefetch of the next wave-tile, stage in the
+//                  wave's own LDS region, line-end events, in-wave scan (DPP), parse of
+//                  every line starting in the tile (fast fixed-width path for the
+//                  kubelet prefix), fused literal grep; results STAGED as one packed u32
+//                  slot per line start (dense tiles, > kSlots starts, take slots from a
+//                  pool), plus a 16-B TileStat.
+//   K1b/K1c        device scan of the per-tile line counts -> tile line bases, stream
+//                  line ranges.
 //   K1d k_scatter  staged slots -> global line_off (u64) / meta (u16) / match bitmap.
-// Slot (u32): bits 0..14 line start offset inside the tile (0..16384), bit 15 literal
-// hit, bits 16..31 the line's meta word.
+// Slot (u32): bits 0..14 line start offset inside the tile (0..4095), bit 15 literal hit,
+// bits 16..31 the line's meta word.
 
-// 4-bit mask of the zero bytes of x (exact): bit k set iff byte k of x is 0.
+// 4-bit mask of the bytes of x equal to zero (exact): bit k set iff byte k of x is 0.
 __device__ __forceinline__ uint32_t zmask4(uint32_t x) {
   const uint32_t z = ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x | 0x7F7F7F7Fu);  // 0x80 per zero byte
   return (z * 0x00204081u) >> 28;
 }
+// 64-bit mask over the 64 bytes in w: bit i set iff byte i equals the byte in pat (x4).
 __device__ __forceinline__ uint64_t eq_mask64_words(const uint32_t* w, uint32_t pat) {
   uint32_t lo = 0, hi = 0;
 #pragma unroll
@@ -312,6 +187,32 @@ __device__ __forceinline__ uint64_t eq_mask64_words(const uint32_t* w, uint32_t 
   for (int j = 0; j < 8; ++j) hi |= zmask4(w[8 + j] ^ pat) << (4 * j);
   return ((uint64_t)hi << 32) | lo;
 }
+// Nonzero iff some byte of the 64 bytes in w equals the byte in pat (exact as an any-test:
+// the classic haszero borrow can only add false bits above a true zero byte).
+__device__ __forceinline__ uint32_t any_eq64_words(const uint32_t* w, uint32_t pat) {
+  uint32_t acc = 0;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const uint32_t x = w[j] ^ pat;
+    acc |= (x - 0x01010101u) & ~x;
+  }
+  return acc & 0x80808080u;
+}
+
+template <class T>
+__device__ __forceinline__ T wave_max(T x) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) {
+    const T o = __shfl_xor(x, d, 64);
+    x = o > x ? o : x;
+  }
+  return x;
+}
+
+// A wave's own LDS writes are visible to its later LDS reads (the LDS executes one wave's
+// instructions in order); this keeps the compiler from reordering across the point and
+// waits for the writes to land.  No workgroup barrier is involved.
+__device__ __forceinline__ void wave_lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
 __global__ __launch_bounds__(256) void k_tiles(const SegDesc* segs, uint32_t nsegs, uint32_t ntiles,
                                                uint32_t* tile_seg) {
@@ -361,16 +262,8 @@ __device__ __forceinline__ bool parse_fast_lds(const uint8_t* lds, uint32_t o, T
   return true;
 }
 
-// General RFC3339Nano parse, out of line: non-canonical prefixes are rare, and keeping the
-// byte-at-a-time parser out of the hot loop keeps the loop's register budget.
-__device__ __attribute__((noinline)) bool parse_general_cold(const uint8_t* lds, const uint8_t* segp, int64_t p0,
-                                                            int64_t rel_lo, int64_t seg_len, TsResult* r,
-                                                            uint32_t* plen) {
-  LineBytes gb{lds, segp, p0, rel_lo, seg_len};
-  return parse_line_prefix(gb, *r, *plen);
-}
-
-// Parse of the line starting at stream offset p0: fast path from LDS, else general.
+// Parse of the line starting at stream offset p0: fast path from LDS, else general
+// (LDS where the bytes are staged, global memory past the halo).
 __device__ __forceinline__ bool parse_line_at(const uint8_t* lds, const uint8_t* segp, int64_t p0, int64_t rel_lo,
                                               int64_t seg_len, int64_t ssec, int32_t snsec, bool* since_ok,
                                               uint32_t* plen) {
@@ -397,35 +290,38 @@ __device__ __forceinline__ bool parse_line_at(const uint8_t* lds, const uint8_t*
 template <bool LIT>
 __global__ __launch_bounds__(kThreads, KLF_SCAN_OCC) void k_scan(RunArgs a, const uint32_t* __restrict__ tseg,
                                                                const SegDesc* __restrict__ segs) {
-  __shared__ __attribute__((aligned(16))) uint8_t s_tile[kTile + kHalo];
+  constexpr int kWaves = kThreads / 64;
+  __shared__ __attribute__((aligned(16))) uint8_t s_tile_all[kWaves][kTile + kHalo];
+  __shared__ uint32_t s_slot_all[LIT ? kWaves : 1][LIT ? kSlots : 1];
   __shared__ __attribute__((aligned(16))) uint32_t s_lit[kMaxFusedLiteral / 4 + 1];  // literal, zero padded
-  __shared__ uint32_t s_slot[kSlots];  // line starts (offsets), then the parsed slots
-  __shared__ uint32_t s_wsum[4];
-  __shared__ uint32_t s_red[4][2];
-  __shared__ uint32_t s_pool, s_carry;
-  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  // wv is wave-uniform; readfirstlane tells the compiler so (tile indices stay in SGPRs and
+  // the descriptor reads stay scalar loads)
+  const int t = threadIdx.x, lane = t & 63, wv = __builtin_amdgcn_readfirstlane(t >> 6);
+  uint8_t* s_tile = s_tile_all[wv];
+  uint32_t* s_slot = s_slot_all[LIT ? wv : 0];
   uint32_t* err_flag = a.counters + 2;
-  // One tile ahead in registers: the next tile's 16 KiB (+ halo) is in flight while this
-  // tile is parsed (barriers here wait on LDS only, never on these loads).
-  static_assert(kTile == kThreads * 16 * 4, "prefetch holds 4 uint4 per thread");
-  if (LIT) {  // the literal lives in LDS for the whole kernel (no vector loads per tile)
+  if (LIT) {  // the literal lives in LDS for the whole kernel (the kernel's only block barrier)
     for (uint32_t i = t; i < kMaxFusedLiteral / 4 + 1; i += kThreads) s_lit[i] = i < (a.lit_len + 3) / 4 ? a.lit_words[i] : 0u;
     __syncthreads();
   }
   const uint8_t* lit = reinterpret_cast<const uint8_t*>(s_lit);
+  const uint32_t nwaves = gridDim.x * kWaves;
+  // One wave-tile ahead in registers: the next tile's 4 KiB (+ halo) is in flight while
+  // this one is processed.  Rows of 1 KiB, 16 B per lane: fully coalesced.
+  static_assert(kTile == 64 * 16 * 4, "prefetch holds 4 uint4 per lane");
   auto tile_src = [&](uint32_t tl) -> const uint4* {
     const uint32_t ss = tseg[tl];
     const SegDesc d = segs[ss];
     return reinterpret_cast<const uint4*>(a.bytes + d.base + (uint64_t)(tl - d.tile0) * kTile);
   };
   uint4 pf0, pf1, pf2, pf3, pfh = make_uint4(0, 0, 0, 0);  // named, not an array: stays in VGPRs
-  if (blockIdx.x < a.ntiles) {
-    const uint4* gp = tile_src(blockIdx.x);
-    pf0 = gp[t]; pf1 = gp[kThreads + t]; pf2 = gp[2 * kThreads + t]; pf3 = gp[3 * kThreads + t];
-    if (t < kHalo / 16) pfh = gp[kTile / 16 + t];
+  uint32_t tile = blockIdx.x * kWaves + wv;
+  if (tile < a.ntiles) {
+    const uint4* gp = tile_src(tile);
+    pf0 = gp[lane]; pf1 = gp[64 + lane]; pf2 = gp[128 + lane]; pf3 = gp[192 + lane];
+    if (lane < kHalo / 16) pfh = gp[kTile / 16 + lane];
   }
-  for (uint32_t tile = blockIdx.x; tile < a.ntiles; tile += gridDim.x) {
-    KLF_STAMP(tile, 0);
+  for (; tile < a.ntiles; tile += nwaves) {
     // descriptors are re-read (scalar, cached) rather than carried: fewer live SGPRs
     const uint32_t s = tseg[tile];
     const SegDesc sd = segs[s];
@@ -436,34 +332,32 @@ __global__ __launch_bounds__(kThreads, KLF_SCAN_OCC) void k_scan(RunArgs a, cons
     const bool last = rel_lo + kTile >= seg_len;
     const uint8_t* segp = a.bytes + sd.base;
 
-    // ---- stage this tile in LDS, then start loading the next one ----
+    // ---- stage this tile in the wave's LDS region, then start loading the next one ----
     {
       uint4* l = reinterpret_cast<uint4*>(s_tile);
-      l[t] = pf0; l[kThreads + t] = pf1; l[2 * kThreads + t] = pf2; l[3 * kThreads + t] = pf3;
-      if (t < kHalo / 16) l[kTile / 16 + t] = pfh;
-      const uint32_t nx = tile + gridDim.x;
+      l[lane] = pf0; l[64 + lane] = pf1; l[128 + lane] = pf2; l[192 + lane] = pf3;
+      if (lane < kHalo / 16) l[kTile / 16 + lane] = pfh;
+      const uint32_t nx = tile + nwaves;
       if (nx < a.ntiles) {
         const uint4* gp = tile_src(nx);
-        pf0 = gp[t]; pf1 = gp[kThreads + t]; pf2 = gp[2 * kThreads + t]; pf3 = gp[3 * kThreads + t];
-        if (t < kHalo / 16) pfh = gp[kTile / 16 + t];
+        pf0 = gp[lane]; pf1 = gp[64 + lane]; pf2 = gp[128 + lane]; pf3 = gp[192 + lane];
+        if (lane < kHalo / 16) pfh = gp[kTile / 16 + lane];
       }
     }
-    if (t == 0) s_carry = 0;
-    __syncthreads();
-    KLF_STAMP(tile, 1);
+    wave_lds_sync();
 
     // ---- line-end events of my 64 bytes, literal anchor candidates ----
-    const int nvalid_s = (int)(tile_len - (int64_t)t * kBytesPerThread);
+    const int nvalid_s = (int)(tile_len - (int64_t)lane * kBytesPerThread);
     const int nvalid = nvalid_s <= 0 ? 0 : (nvalid_s >= 64 ? 64 : nvalid_s);
     const uint64_t vm = nvalid >= 64 ? ~0ull : ((1ull << nvalid) - 1);
-    const uint32_t toff0 = (uint32_t)t * kBytesPerThread;  // my first byte, tile-relative
+    const uint32_t toff0 = (uint32_t)lane * kBytesPerThread;  // my first byte, tile-relative
     uint64_t nl, cand = 0;
     {
-      // The lane's 4 x 16 B are read starting at chunk rot = (t >> 2) & 3: with a plain
+      // The lane's 4 x 16 B are read starting at chunk rot = (lane >> 2) & 3: in plain
       // order lanes t, t+12, t+20, t+24 of a ds_read_b128 group hit the same banks (4-way
       // conflict); rotated, every 16-lane group covers all 64 banks once.  The masks are
       // built in read order and rotated back once.
-      const uint32_t rot = ((uint32_t)t >> 2) & 3u;
+      const uint32_t rot = ((uint32_t)lane >> 2) & 3u;
       const uint4* l = reinterpret_cast<const uint4*>(s_tile + toff0);
       uint32_t w[16];
 #pragma unroll
@@ -474,8 +368,12 @@ __global__ __launch_bounds__(kThreads, KLF_SCAN_OCC) void k_scan(RunArgs a, cons
       const uint32_t rs = 16u * rot;
       auto unrot = [&](uint64_t m) -> uint64_t { return rs ? (m << rs) | (m >> (64u - rs)) : m; };
       nl = unrot(eq_mask64_words(w, 0x0A0A0A0Au)) & vm;
-      // literal anchor: the literal's rarest byte (chosen on the host), at offset lit_anchor
-      if (LIT) cand = unrot(eq_mask64_words(w, a.lit_anchor_byte * 0x01010101u)) & vm;
+      // literal anchor (the literal's rarest byte, chosen on the host): a cheap any-test
+      // first, the exact mask only in lanes that see the byte at all
+      if (LIT) {
+        const uint32_t pat = a.lit_anchor_byte * 0x01010101u;
+        if (any_eq64_words(w, pat)) cand = unrot(eq_mask64_words(w, pat)) & vm;
+      }
     }
     const bool has_end = last && nvalid > 0 && rel_lo + toff0 + nvalid == seg_len;
     const int eb = nvalid - 1;
@@ -485,70 +383,65 @@ __global__ __launch_bounds__(kThreads, KLF_SCAN_OCC) void k_scan(RunArgs a, cons
       starts &= ~(1ull << eb);
       a.segout[s].frag = (nl >> eb) & 1 ? 0 : 1;
     }
-    KLF_STAMP(tile, 5);
     const uint32_t cnt = (uint32_t)__popcll(ev);
     const uint32_t incl = wave_incl_scan_add(cnt, lane);
-    if (lane == 63) s_wsum[wv] = incl;
-    __syncthreads();
-    KLF_STAMP(tile, 6);
-    uint32_t wexcl = 0, agg = 0;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      if (k < wv) wexcl += s_wsum[k];
-      agg += s_wsum[k];
-    }
-    const uint32_t texcl = wexcl + incl - cnt;  // events of the tile before my bytes
+    const uint32_t agg = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+    const uint32_t texcl = incl - cnt;  // events of the tile before my bytes
     // Local line k = the line after the tile's k-th event (k = 0: the line open at the
     // tile start).  Lines starting here: k in [k0, k1), slot j = k - k0.
     const uint32_t k0 = first ? 0 : 1;
     const uint32_t k1 = last ? agg : agg + 1;
     const uint32_t nlines = k1 > k0 ? k1 - k0 : 0;
     const bool dense = nlines > (uint32_t)kSlots;
+    uint32_t pool_base = 0;
     if (dense) {
-      if (t == 0) {
-        const uint32_t pb = atomicAdd(&a.counters[kCtrPool], nlines);
-        s_pool = pb;
+      uint32_t pb = 0;
+      if (lane == 0) {
+        pb = atomicAdd(&a.counters[kCtrPool], nlines);
         if ((uint64_t)pb + nlines > a.pool_cap) atomicOr(err_flag, 1u);
       }
-      __syncthreads();
+      pool_base = (uint32_t)__builtin_amdgcn_readlane((int)pb, 0);
     }
-    uint32_t* pool_dst = dense ? a.pool + s_pool : nullptr;
-    const bool pool_ok = !dense || (uint64_t)s_pool + nlines <= a.pool_cap;
-    // ---- parse every line starting in my bytes -> its slot (LDS, or the pool if dense) ----
-    // Each lane parses its own line starts: the starts are already in registers, and the
-    // timestamp bytes are in LDS, so no extra barrier or slot round trip is needed.
+    const bool pool_ok = !dense || (uint64_t)pool_base + nlines <= a.pool_cap;
+    uint32_t* gslot = dense ? a.pool + pool_base : a.slots + (size_t)tile * kSlots;
+
+    // ---- parse every line starting in my bytes -> its slot ----
+    // Slots go to LDS when the literal pass needs them, else straight to their staging
+    // place in global memory (LDS for normal tiles, the pool for dense ones).
     uint32_t n_parsed = 0, n_since = 0;
     auto put = [&](uint32_t j, uint32_t off) {
       bool so;
       uint32_t plen = 0;
       const bool ok = parse_line_at(s_tile, segp, rel_lo + off, rel_lo, seg_len, a.since_sec, a.since_nsec, &so, &plen);
       const uint32_t slot = off | ((uint32_t)make_meta(ok, so, plen) << 16);
-      if (!dense) s_slot[j] = slot;
-      else if (pool_ok) pool_dst[j] = slot;
+      if (LIT && !dense) s_slot[j] = slot;
+      else if (pool_ok) gslot[j] = slot;
       n_parsed += ok;
       n_since += so;
     };
-    if (first && t == 0) put(0, 0);
+    if (first && lane == 0) put(0, 0);
     for (uint64_t m = starts; m;) {
       const int q = __ffsll((unsigned long long)m) - 1;
       m &= m - 1;
       put(texcl + (uint32_t)__popcll(ev & ((2ull << q) - 1)) - k0, toff0 + q + 1);
     }
-    KLF_STAMP(tile, 7);
-    if (dense) __threadfence_block();
-    __syncthreads();
-    KLF_STAMP(tile, 2);
 
     // ---- fused single-literal grep ----
     // Anchor hits are rare (the literal's rarest byte); each names a candidate start
     // p = anchor - lit_anchor.  A tile owns the starts inside it: anchors of this tile
     // whose start lies in the previous tile are left to that tile, which scans its halo.
+    uint32_t carry = 0;  // 1 + furthest literal hit in the line carried in from before the tile
     if (LIT) {
+      if (dense) __threadfence_block();  // pool slots are global: make them visible to the wave
+      wave_lds_sync();
       const uint32_t m = a.lit_len, ka = a.lit_anchor;
       uint64_t hcand = 0;  // halo anchors [kTile, kTile + ka) -> starts in this tile's tail
-      if (t == kThreads - 1 && ka > 0 && !last) {
-        for (uint32_t j = 0; j < ka; ++j)
-          if (s_tile[kTile + j] == a.lit_anchor_byte) hcand |= 1ull << j;
+      if (lane == 63 && ka > 0 && !last) {
+        for (uint32_t j = 0; j < ka; ++j) {
+          const int64_t q = rel_lo + kTile + j;
+          const uint8_t c = j < (uint32_t)kHalo ? s_tile[kTile + j] : (q < seg_len ? segp[q] : 0);
+          if (q < seg_len && c == a.lit_anchor_byte) hcand |= 1ull << j;
+        }
       }
       for (int pass = 0; pass < 2; ++pass) {
         uint64_t cm = pass == 0 ? cand : hcand;
@@ -582,12 +475,11 @@ __global__ __launch_bounds__(kThreads, KLF_SCAN_OCC) void k_scan(RunArgs a, cons
               }
             }
           }
-          if (!eq) continue;
+          if (!eq || !pool_ok) continue;
           // the hit's line: last staged line start at or before pos (binary search)
           const uint32_t off = (uint32_t)(pos - rel_lo);
-          if (!pool_ok) continue;
-          auto slot_at = [&](int i) -> uint32_t { return dense ? pool_dst[i] : s_slot[i]; };
-          int lo = 0, hi = (int)nlines;  // find count of slots with start <= off
+          auto slot_at = [&](int i) -> uint32_t { return dense ? gslot[i] : s_slot[i]; };
+          int lo = 0, hi = (int)nlines;  // count of slots with start <= off
           while (lo < hi) {
             const int mid = (lo + hi) >> 1;
             if ((slot_at(mid) & 0x7FFFu) <= off) lo = mid + 1; else hi = mid;
@@ -597,37 +489,32 @@ __global__ __launch_bounds__(kThreads, KLF_SCAN_OCC) void k_scan(RunArgs a, cons
             const uint32_t mt = v >> 16;
             if ((mt & Meta::kParsed) && off >= (v & 0x7FFFu) + (mt >> 2)) {
               if (!dense) atomicOr(&s_slot[lo - 1], 0x8000u);
-              else atomicOr(&pool_dst[lo - 1], 0x8000u);
+              else atomicOr(&gslot[lo - 1], 0x8000u);
             }
           } else {  // carried in from an earlier tile: k_scatter decides (furthest hit wins)
-            atomicMax(&s_carry, off + 1);
+            carry = carry > off + 1 ? carry : off + 1;
           }
         }
       }
+      carry = wave_max(carry);
+      wave_lds_sync();
+      if (!dense)
+        for (uint32_t j = lane; j < nlines; j += 64) gslot[j] = s_slot[j];
     }
 
-    KLF_STAMP(tile, 3);
-    // ---- per-tile record + staged slots out ----
+    // ---- per-tile record ----
     const uint32_t pp = wave_sum(n_parsed), qq = wave_sum(n_since);
-    if (lane == 0) { s_red[wv][0] = pp; s_red[wv][1] = qq; }
-    __syncthreads();
-    if (!dense) {
-      uint32_t* dst = a.slots + (size_t)tile * kSlots;
-      for (uint32_t j = t; j < nlines; j += kThreads) dst[j] = s_slot[j];
-    }
-    if (t == 0) {
+    if (lane == 0) {
       TileStat ts;
       ts.events = agg;
-      ts.flags = (dense ? 1u : 0u) | (s_carry ? 2u : 0u);
-      ts.carry_off = s_carry;  // furthest literal hit in the carried-in line, + 1
-      ts.parsed = s_red[0][0] + s_red[1][0] + s_red[2][0] + s_red[3][0];
-      ts.since_ok = s_red[0][1] + s_red[1][1] + s_red[2][1] + s_red[3][1];
-      ts.pool_base = dense ? s_pool : 0;
-      ts.pad[0] = ts.pad[1] = 0;
+      ts.pool_base = dense ? pool_base : 0;
+      ts.parsed = (uint16_t)pp;
+      ts.since_ok = (uint16_t)qq;
+      ts.flags = (uint16_t)((dense ? 1u : 0u) | (carry ? 2u : 0u));
+      ts.carry_off = (uint16_t)carry;
       a.tstat[tile] = ts;
     }
-    KLF_STAMP(tile, 4);
-    __syncthreads();  // LDS is reused by the next tile
+    asm volatile("" ::: "memory");  // the next stage overwrites the LDS region read above
   }
 }
 
@@ -684,29 +571,42 @@ __global__ __launch_bounds__(256) void k_tbase(RunArgs a) {
 }
 
 // ---- K1d: scatter staged slots into the global line arrays --------------------------
-// One wave per tile (4 tiles per workgroup iteration), lanes over the tile's lines.
+// One wave per group of kScatterGroup consecutive tiles (~10 lines per 4 KiB tile would
+// leave most lanes of a wave-per-tile idle): lanes 0..G-1 read the group's records into
+// the wave's LDS table, then all lanes walk the group's lines.
+constexpr int kScatterGroup = 16;
+struct ScatterEnt {
+  uint64_t base;     // global line index of the tile's slot 0 (= tile line k0)
+  uint64_t rel_lo;   // tile start, stream-relative
+  uint32_t src;      // index of slot 0 in slots[] (normal) or pool[] (dense, bit 31 set)
+  uint32_t seg;      // stream segment
+  uint32_t pad[2];
+};
+
 __global__ __launch_bounds__(256) void k_scatter(RunArgs a) {
+  __shared__ ScatterEnt s_ent[4][kScatterGroup];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   uint32_t* err_flag = a.counters + 2;
-  for (uint32_t tile = blockIdx.x * 4 + wv; tile < a.ntiles; tile += gridDim.x * 4) {
-    const TileStat ts = a.tstat[tile];
-    const uint32_t s = a.tile_seg[tile];
-    const SegDesc sd = a.segs[s];
-    const int64_t rel_lo = (int64_t)(tile - sd.tile0) * kTile;
-    const bool first = rel_lo == 0, last = rel_lo + kTile >= (int64_t)sd.len;
-    const uint32_t k0 = first ? 0 : 1, k1 = last ? ts.events : ts.events + 1;
-    const uint32_t n = k1 > k0 ? k1 - k0 : 0;
-    const uint64_t base = a.tile_base[tile];
-    const uint32_t* src = (ts.flags & 1u) ? a.pool + ts.pool_base : a.slots + (size_t)tile * kSlots;
-    for (uint32_t j = lane; j < n; j += 64) {
-      const uint32_t sl = src[j];
-      const uint64_t l = base + k0 + j;
-      if (l >= a.cap_lines) { atomicOr(err_flag, 1u); continue; }
-      a.line_off[l + s] = (uint64_t)rel_lo + (sl & 0x7FFFu);
-      a.meta[l] = (uint16_t)(sl >> 16);
-      if (sl & 0x8000u) atomicOr(&a.bits[l >> 5], 1u << (l & 31));
-    }
-    if (lane == 0) {
+  const uint32_t ngroups = (a.ntiles + kScatterGroup - 1) / kScatterGroup;
+  for (uint32_t g = blockIdx.x * 4 + wv; g < ngroups; g += gridDim.x * 4) {
+    const uint32_t tile = g * kScatterGroup + lane;
+    uint32_t n = 0;
+    if (lane < kScatterGroup && tile < a.ntiles) {
+      const TileStat ts = a.tstat[tile];
+      const uint32_t s = a.tile_seg[tile];
+      const SegDesc sd = a.segs[s];
+      const int64_t rel_lo = (int64_t)(tile - sd.tile0) * kTile;
+      const bool first = rel_lo == 0, last = rel_lo + kTile >= (int64_t)sd.len;
+      const uint32_t k0 = first ? 0 : 1, k1 = last ? ts.events : ts.events + 1;
+      n = k1 > k0 ? k1 - k0 : 0;
+      const uint64_t base = a.tile_base[tile];
+      ScatterEnt e;
+      e.base = base + k0;
+      e.rel_lo = (uint64_t)rel_lo;
+      e.src = (ts.flags & 1u) ? (ts.pool_base | 0x80000000u) : 0u;
+      e.seg = s;
+      e.pad[0] = e.pad[1] = 0;
+      s_ent[wv][lane] = e;
       if ((ts.flags & 2u) && base < a.cap_lines) {
         // literal hit inside the line carried in from an earlier tile: that line's start
         // is the last staged start of the nearest earlier tile of the stream that has one
@@ -732,6 +632,34 @@ __global__ __launch_bounds__(256) void k_scatter(RunArgs a) {
         else atomicOr(err_flag, 1u);
       }
     }
+    // inclusive prefix of the group's line counts, then each line finds its tile
+    uint32_t incl = n;
+#pragma unroll
+    for (int d = 1; d < kScatterGroup; d <<= 1) {
+      const uint32_t o = __shfl_up(incl, d, 64);
+      if (lane >= d) incl += o;
+    }
+    uint32_t pre[kScatterGroup];
+#pragma unroll
+    for (int k = 0; k < kScatterGroup; ++k) pre[k] = (uint32_t)__builtin_amdgcn_readlane((int)incl, k);
+    const uint32_t total = pre[kScatterGroup - 1];
+    wave_lds_sync();
+    for (uint32_t l = lane; l < total; l += 64) {
+      uint32_t k = 0;
+#pragma unroll
+      for (int kk = 0; kk < kScatterGroup - 1; ++kk) k += l >= pre[kk] ? 1u : 0u;
+      const uint32_t j = l - (k ? pre[k - 1] : 0u);
+      const ScatterEnt e = s_ent[wv][k];
+      const uint32_t* src = (e.src & 0x80000000u) ? a.pool + (e.src & 0x7FFFFFFFu)
+                                                  : a.slots + (size_t)(g * kScatterGroup + k) * kSlots;
+      const uint32_t sl = src[j];
+      const uint64_t li = e.base + j;
+      if (li >= a.cap_lines) { atomicOr(err_flag, 1u); continue; }
+      a.line_off[li + e.seg] = e.rel_lo + (sl & 0x7FFFu);
+      a.meta[li] = (uint16_t)(sl >> 16);
+      if (sl & 0x8000u) atomicOr(&a.bits[li >> 5], 1u << (li & 31));
+    }
+    asm volatile("" ::: "memory");  // the next group rewrites the wave's LDS table
   }
 }
 
@@ -1127,7 +1055,7 @@ hipError_t launch_pipeline(const RunArgs& a, hipStream_t st, hipEvent_t* ev, int
     KLF_TRY(hipGetLastError());
     hipLaunchKernelGGL(k_tbase, dim3(nb), dim3(256), 0, st, a);
     KLF_TRY(hipGetLastError());
-    uint32_t sg = (a.ntiles + 3) / 4;
+    uint32_t sg = ((a.ntiles + kScatterGroup - 1) / kScatterGroup + 3) / 4;
     if (sg > (uint32_t)num_cus * 8) sg = num_cus * 8;
     hipLaunchKernelGGL(k_scatter, dim3(sg), dim3(256), 0, st, a);
   }

@@ -6,11 +6,12 @@
 
 namespace klf {
 
-// Work decomposition of the scan: a tile = 256 threads x 64 contiguous bytes.
+// Work decomposition of the scan: a tile = one wave x 64 contiguous bytes per lane; a
+// 256-thread workgroup runs 4 independent waves.
 constexpr int kThreads = 256;
 constexpr int kBytesPerThread = 64;
-constexpr int kTile = kThreads * kBytesPerThread;  // 16 KiB
-constexpr int kHalo = 320;                          // LDS bytes past the tile (ts + literal window)
+constexpr int kTile = 64 * kBytesPerThread;  // 4 KiB wave-tile
+constexpr int kHalo = 64;                     // LDS bytes staged past the tile (timestamp window)
 constexpr int kMaxFusedLiteral = 256;
 constexpr uint64_t kSegAlign = 256;                 // segment base alignment in the batch buffer
 constexpr uint64_t kAllocSlack = kTile + kHalo + 1024;
@@ -25,17 +26,17 @@ constexpr uint32_t kCtrScanGroups = 64;             // counters[64 + g * kCtrStr
 constexpr uint32_t kNumCounters = kCtrScanGroups + kScanGroups * kCtrStride;
 constexpr uint32_t kCtrPool = 4;                    // counters[4]: dense-tile pool allocator
 
-constexpr int kSlots = 528;  // staged line slots per tile (>= 16 KiB / 32-byte kubelet line + 1)
+constexpr int kSlots = 132;  // staged line slots per tile (>= 4 KiB / 32-byte kubelet line + 1)
 
-// Per-tile record of the scan (K1a), 32 B.
+// Per-tile record of the scan (K1a), 16 B.
 struct TileStat {
   uint32_t events;     // line-end events in the tile
-  uint32_t flags;      // bit0 dense (slots in the pool), bit1 literal hit in the carried-in line
-  uint32_t parsed, since_ok;
   uint32_t pool_base;  // dense tiles: first pool slot
-  uint32_t carry_off;  // 1 + offset of the furthest literal hit in the carried-in line (0 = none)
-  uint32_t pad[2];
+  uint16_t parsed, since_ok;
+  uint16_t flags;      // bit0 dense (slots in the pool), bit1 literal hit in the carried-in line
+  uint16_t carry_off;  // 1 + offset of the furthest literal hit in the carried-in line (0 = none)
 };
+static_assert(sizeof(TileStat) == 16, "TileStat is one 16-B store");
 
 // One segment (= one non-empty stream) of the device batch.
 struct SegDesc {
