@@ -117,7 +117,8 @@ int klf_run(klf_engine* e, const klf_filter* f, klf_result** out);
 int klf_layout(uint32_t n_streams, const uint64_t* lens, uint64_t* seg_base,
                uint64_t* total_alloc);
 /* Runs over streams already laid out in device memory at d_bytes + seg_base[i]
- * (d_bytes must be a device allocation of >= total_alloc bytes from klf_layout). */
+ * (d_bytes must be a 16-B aligned device allocation of >= total_alloc bytes from klf_layout;
+ * KLF_EINVAL otherwise). */
 int klf_run_device(klf_engine* e, const uint8_t* d_bytes, uint32_t n_streams,
                    const uint64_t* seg_base, const uint64_t* lens, const klf_filter* f,
                    klf_result** out);

@@ -76,15 +76,13 @@ def build_host(force=False, quiet=True):
     LIB.mkdir(parents=True, exist_ok=True)
     so = LIB / "libklogs_host.so"
     exe = LIB / "klogs-filter"
-    deps = [src, CSRC / "klogs_host.hpp", ROOT / "include" / "klogs_host.h", ROOT / "include" / "klf.h",
-            LIB / "libklf.so"]
+    deps = [src, ROOT / "include" / "klogs_host.h", ROOT / "include" / "klf.h", LIB / "libklf.so"]
     deps = [d for d in deps if Path(d).exists()]
     if force or _stale(so, deps):
-        _run(["g++", "-O2", "-std=c++17", "-shared", "-fPIC", src, "-o", so, f"-L{LIB}", "-lklf",
-              f"-Wl,-rpath,$ORIGIN"], quiet)
+        _run(["g++", "-O2", "-std=c++17", "-Wall", "-shared", "-fPIC", src, "-o", so], quiet)
     cli = CSRC / "klogs_filter_main.cpp"
     if cli.exists() and (force or _stale(exe, deps + [cli, so])):
-        _run(["g++", "-O2", "-std=c++17", cli, "-o", exe, f"-L{LIB}", "-lklogs_host", "-lklf",
+        _run(["g++", "-O2", "-std=c++17", "-Wall", cli, "-o", exe, f"-L{LIB}", "-lklogs_host", "-lklf",
               "-Wl,-rpath,$ORIGIN"], quiet)
     return so
 

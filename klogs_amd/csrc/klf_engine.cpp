@@ -64,7 +64,7 @@ struct klf_engine {
   std::vector<SegDesc> last_segs;  // tile_seg cache key
   DevBuf d_tile_seg;
   DevBuf d_batch, d_segs, d_tstat, d_slots, d_pool, d_tile_base, d_bsum, d_cstatus, d_counters, d_line_off,
-      d_meta, d_bits, d_segout, d_wpre, d_out;
+      d_meta, d_bits, d_segout, d_wpre, d_out, d_mpart;
   uint64_t pool_cap = 1 << 20;
   hipEvent_t ev[6] = {};
 };
@@ -222,7 +222,7 @@ extern "C" void klf_close(klf_engine* e) {
   for (DevBuf* b : {&e->d_lit, &e->d_ac_class, &e->d_ac_next, &e->d_ac_accept, &e->d_rx_class, &e->d_rx_b,
                     &e->d_rx_follow, &e->d_rx_vec, &e->d_rx_flags, &e->d_batch, &e->d_segs, &e->d_tstat,
                     &e->d_slots, &e->d_pool, &e->d_tile_base, &e->d_bsum, &e->d_cstatus, &e->d_counters,
-                    &e->d_line_off, &e->d_meta, &e->d_bits, &e->d_segout, &e->d_wpre, &e->d_out, &e->d_tile_seg})
+                    &e->d_line_off, &e->d_meta, &e->d_bits, &e->d_segout, &e->d_wpre, &e->d_out, &e->d_tile_seg, &e->d_mpart})
     b->release();
   for (auto& x : e->ev)
     if (x) (void)hipEventDestroy(x);
@@ -283,6 +283,7 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
   if (!e || !f || !out || (n_streams && (!seg_base || !lens))) return KLF_EINVAL;
   if (f->tail < -1) return set_err(e, KLF_EINVAL, "tail must be >= -1");
   if (f->since.nsec < 0 || f->since.nsec >= 1000000000) return set_err(e, KLF_EINVAL, "since.nsec out of range");
+  if (reinterpret_cast<uintptr_t>(d_bytes) % 16) return set_err(e, KLF_EINVAL, "device bytes must be 16-B aligned");
   *out = nullptr;
   HIPCHK(e, hipSetDevice(e->device), "hipSetDevice");
   auto* r = new (std::nothrow) klf_result();
@@ -328,7 +329,7 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
   HIPCHK(e, e->d_tstat.ensure(ntiles * sizeof(klf::TileStat)), "alloc tstat");
   HIPCHK(e, e->d_slots.ensure(ntiles * klf::kSlots * 4), "alloc slots");
   HIPCHK(e, e->d_tile_base.ensure(ntiles * 8), "alloc tile_base");
-  HIPCHK(e, e->d_bsum.ensure((ntiles / 4096 + 2) * 8), "alloc bsum");
+  HIPCHK(e, e->d_bsum.ensure((ntiles / 4096 + 2) * 3 * 8), "alloc bsum");
   HIPCHK(e, e->d_counters.ensure(klf::kNumCounters * 4), "alloc counters");
   HIPCHK(e, e->d_segout.ensure(nsegs * sizeof(SegOut)), "alloc segout");
   HIPCHK(e, e->d_wpre.ensure((nsegs + 1) * 8), "alloc wpre");
@@ -340,6 +341,7 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
     HIPCHK(e, e->d_meta.ensure(cap * 2 + 16), "alloc meta");
     HIPCHK(e, e->d_bits.ensure((cap / 32 + 1) * 4), "alloc bits");
     HIPCHK(e, e->d_cstatus.ensure(max_cblocks * 2 * 8), "alloc cstatus");
+    HIPCHK(e, e->d_mpart.ensure((cap / klf::kMatchChunk + 2) * 8), "alloc mpart");
     HIPCHK(e, e->d_pool.ensure(e->pool_cap * 4), "alloc pool");
     klf::RunArgs a{};
     a.bytes = d_bytes;
@@ -364,7 +366,8 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
     a.pool_cap = e->pool_cap;
     a.tile_base = e->d_tile_base.as<uint64_t>();
     a.bsum = e->d_bsum.as<uint64_t>();
-    a.cstatus = e->d_cstatus.as<uint64_t>();
+    a.mpart = e->d_mpart.as<uint64_t>();
+    a.csum = e->d_cstatus.as<uint64_t>();
     a.counters = e->d_counters.as<uint32_t>();
     a.line_off = e->d_line_off.as<uint64_t>();
     a.meta = e->d_meta.as<uint16_t>();
@@ -381,7 +384,6 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
     HIPCHK(e, hipMemcpyAsync(counters, e->d_counters.p, sizeof(counters), hipMemcpyDeviceToHost, st), "D2H counters");
     HIPCHK(e, hipStreamSynchronize(st), "sync");
     e->last_segs = segs;
-    if (counters[2] & 2u) { delete r; e->last_segs.clear(); return set_err(e, KLF_EHIP, "look-back spin timeout"); }
     if (counters[2] & 1u) {  // more lines (or dense-tile slots) than estimated: rerun with exact sizes
       cap = std::max<uint64_t>(cap, r->so[nsegs - 1].line_hi + 2);
       e->pool_cap = std::max<uint64_t>(e->pool_cap, (uint64_t)counters[klf::kCtrPool] + 1024);

@@ -5,10 +5,12 @@
 //                  single-literal grep over 4 KiB wave-tiles, staged per tile;
 //                  k_tsum/k_tbase tile line bases; k_scatter -> global line index
 //   K2 k_match     general pattern sets: Aho-Corasick DFA + Glushkov bit-parallel NFA
-//   K3 k_count     per-stream parsed / since_ok / matched counts
+//   K3 k_mcount    per-stream matched counts (chunk partials; parsed / since_ok come
+//                  from k_tbase's prefixes)
 //      k_tail      kubelet tail rule -> per-stream candidate window (one block / stream)
 //      k_wprefix   exclusive prefix of window sizes
-//   K4 k_compact   output offsets (look-back over 1024-line blocks) + content gather copy
+//   K4 k_csum / k_cscan / k_cgather   output offsets (reduce-then-scan over 1024-line
+//                  blocks) + content gather copy
 // Semantics: SPEC.md (kubelet logs.go ReadLogs / tail.go FindTailLineStartIndex /
 // Go time.Parse(RFC3339Nano) / bytes.Contains / regexp.Match).
 #include <hip/hip_runtime.h>
@@ -34,18 +36,6 @@ __device__ uint32_t g_lb_rounds, g_lb_spins;
 
 // ------------------------------------------------------------------ small helpers ---
 
-__device__ __forceinline__ uint64_t atomic_load_u64(const uint64_t* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void atomic_store_u64(uint64_t* p, uint64_t v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-constexpr uint64_t kFlagA = 1ull << 62;  // aggregate published
-constexpr uint64_t kFlagP = 2ull << 62;  // inclusive prefix published
-constexpr uint64_t kFlagMask = 3ull << 62;
-constexpr uint32_t kSpinLimit = 1u << 24;
-
 template <class T>
 __device__ __forceinline__ T wave_sum(T x) {
 #pragma unroll
@@ -61,60 +51,6 @@ __device__ __forceinline__ T wave_incl_scan_add(T x, int lane) {
   }
   return x;
 }
-
-// Decoupled look-back of one tile over a chain of u64 words, run by ONE WAVE: each
-// round reads 64 predecessors at once, waits until all of them have published
-// (aggregate or inclusive), stops at the nearest inclusive prefix and folds the window
-// with an ordered shuffle reduction (earlier tiles sit at higher lanes).  Returns the
-// exclusive prefix (no flag bits) in every lane.  `agg` has no flag bits.  Spins are
-// bounded: a timeout sets counters[2] bit 1 so the host reports an error instead of the
-// GPU hanging.
-template <class Comb>
-__device__ uint64_t lookback_wave(uint64_t* st, uint32_t idx, uint64_t agg, uint64_t ident, Comb comb,
-                                  uint32_t* err_flag, int lane) {
-  if (idx == 0) {
-    if (lane == 0) atomic_store_u64(&st[0], agg | kFlagP);
-    return ident;
-  }
-  if (lane == 0) atomic_store_u64(&st[idx], agg | kFlagA);
-  uint64_t acc = ident;
-  int64_t hi = (int64_t)idx - 1;
-  for (;;) {
-    const int64_t j = hi - lane;
-    uint64_t w = kFlagP | ident;  // before tile 0: acts as an empty inclusive prefix
-    bool ready = j < 0;
-    uint32_t spins = 0;
-    for (;;) {
-      if (!ready) {
-        w = atomic_load_u64(&st[j]);
-        ready = (w & kFlagMask) != 0;
-      }
-      if (__all(ready)) break;
-      __builtin_amdgcn_s_sleep(1);
-      if (++spins > kSpinLimit) {
-        if (lane == 0) atomicOr(err_flag, 2u);
-        return acc;
-      }
-    }
-    const uint64_t pmask = __ballot((w & kFlagMask) == kFlagP);
-    const int plane = pmask ? __ffsll((unsigned long long)pmask) - 1 : 64;
-    uint64_t v = lane <= plane ? (w & ~kFlagMask) : ident;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      const uint64_t o = __shfl_down(v, d, 64);
-      if (lane + d < 64) v = comb(o, v);
-    }
-    acc = comb(__shfl(v, 0, 64), acc);
-    if (plane < 64) break;
-    hi -= 64;
-  }
-  if (lane == 0) atomic_store_u64(&st[idx], comb(acc, agg) | kFlagP);
-  return acc;
-}
-
-struct SumComb {
-  __device__ uint64_t operator()(uint64_t a, uint64_t b) const { return (a + b) & ~kFlagMask; }
-};
 
 __device__ __forceinline__ uint32_t find_seg_by_tile(const SegDesc* segs, uint32_t n, uint32_t tile) {
   uint32_t lo = 0, hi = n;
@@ -519,54 +455,99 @@ __global__ __launch_bounds__(kThreads, KLF_SCAN_OCC) void k_scan(RunArgs a, cons
 }
 
 // ---- K1b/K1c: tile line bases (exclusive scan of TileStat.events) -------------------
+// The same pass scans the per-tile parsed / since_ok counts: a stream's counts are the
+// prefix differences at its first and last tile (no same-address atomics), and zeroes the
+// match-bitmap words whose first line falls in the block's line range (the bitmap is
+// only ever OR-ed into by the kernels after this one).
 constexpr int kTilesPerScanBlock = 4096;  // 256 threads x 16 tiles
 
 __global__ __launch_bounds__(256) void k_tsum(RunArgs a) {
-  __shared__ uint64_t s_w[4];
-  const uint32_t t0 = blockIdx.x * kTilesPerScanBlock + threadIdx.x * 16;
-  uint64_t v = 0;
-  for (int j = 0; j < 16; ++j)
-    if (t0 + j < a.ntiles) v += a.tstat[t0 + j].events;
+  __shared__ uint64_t s_w[3][4];
+  constexpr int R = kTilesPerScanBlock / 256;
+  const uint32_t t0 = blockIdx.x * kTilesPerScanBlock + threadIdx.x;
+  TileStat ts[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {  // all loads in flight at once (coalesced 16-B records)
+    ts[r] = TileStat{};
+    if (t0 + r * 256 < a.ntiles) ts[r] = a.tstat[t0 + r * 256];
+  }
+  uint64_t v = 0, p = 0, q = 0;
+#pragma unroll
+  for (int r = 0; r < R; ++r) { v += ts[r].events; p += ts[r].parsed; q += ts[r].since_ok; }
   v = wave_sum(v);
-  if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = v;
+  p = wave_sum(p);
+  q = wave_sum(q);
+  if ((threadIdx.x & 63) == 0) { s_w[0][threadIdx.x >> 6] = v; s_w[1][threadIdx.x >> 6] = p; s_w[2][threadIdx.x >> 6] = q; }
   __syncthreads();
-  if (threadIdx.x == 0) a.bsum[blockIdx.x] = s_w[0] + s_w[1] + s_w[2] + s_w[3];
+  if (threadIdx.x < 3) {
+    const int k = threadIdx.x;
+    a.bsum[3 * blockIdx.x + k] = s_w[k][0] + s_w[k][1] + s_w[k][2] + s_w[k][3];
+  }
 }
 
+// Rounds of 256 consecutive tiles (one per thread, coalesced), block scan per round.  All
+// rounds' records and tile->stream ids are loaded up front; stream boundaries are where
+// the stream id of the neighbouring tile differs (no dependent descriptor loads).
 __global__ __launch_bounds__(256) void k_tbase(RunArgs a) {
-  __shared__ uint64_t s_w[4];
-  __shared__ uint64_t s_base;
+  constexpr int R = kTilesPerScanBlock / 256;
+  __shared__ uint64_t s_w[2][3][4];
+  __shared__ uint64_t s_base[3];
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const uint32_t t0 = blockIdx.x * kTilesPerScanBlock + t;
+  TileStat ts[R];
+  uint32_t sg[R], sp[R], sn[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const uint32_t tile = t0 + r * 256;
+    ts[r] = TileStat{};
+    sg[r] = sp[r] = sn[r] = 0;
+    if (tile < a.ntiles) {
+      ts[r] = a.tstat[tile];
+      sg[r] = a.tile_seg[tile];
+      sp[r] = tile > 0 ? a.tile_seg[tile - 1] : ~0u;
+      sn[r] = tile + 1 < a.ntiles ? a.tile_seg[tile + 1] : ~0u;
+    }
+  }
   {  // prefix of the preceding blocks' sums
-    uint64_t v = 0;
-    for (uint32_t b = t; b < blockIdx.x; b += 256) v += a.bsum[b];
+    uint64_t v = 0, p = 0, q = 0;
+    for (uint32_t b = t; b < blockIdx.x; b += 256) {
+      v += a.bsum[3 * b];
+      p += a.bsum[3 * b + 1];
+      q += a.bsum[3 * b + 2];
+    }
     v = wave_sum(v);
-    if (lane == 0) s_w[wv] = v;
+    p = wave_sum(p);
+    q = wave_sum(q);
+    if (lane == 0) { s_w[0][0][wv] = v; s_w[0][1][wv] = p; s_w[0][2][wv] = q; }
     __syncthreads();
-    if (t == 0) s_base = s_w[0] + s_w[1] + s_w[2] + s_w[3];
+    if (t < 3) s_base[t] = s_w[0][t][0] + s_w[0][t][1] + s_w[0][t][2] + s_w[0][t][3];
     __syncthreads();
   }
-  const uint32_t t0 = blockIdx.x * kTilesPerScanBlock + t * 16;
-  uint32_t ev[16];
-  uint64_t v = 0;
-  for (int j = 0; j < 16; ++j) {
-    ev[j] = t0 + j < a.ntiles ? a.tstat[t0 + j].events : 0;
-    v += ev[j];
+  const uint64_t blk_lo = s_base[0];
+  uint64_t cv = s_base[0], cp = s_base[1], cq = s_base[2];  // running bases (block-uniform)
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const uint32_t tile = t0 + r * 256;
+    const uint64_t v = ts[r].events, p = ts[r].parsed, q = ts[r].since_ok;
+    const uint64_t iv = wave_incl_scan_add(v, lane), ip = wave_incl_scan_add(p, lane), iq = wave_incl_scan_add(q, lane);
+    const int pb = r & 1;  // double-buffered wave totals: one barrier per round
+    if (lane == 63) { s_w[pb][0][wv] = iv; s_w[pb][1][wv] = ip; s_w[pb][2][wv] = iq; }
+    __syncthreads();
+    uint64_t bv = cv + iv - v, bp = cp + ip - p, bq = cq + iq - q;
+    for (int k = 0; k < wv; ++k) { bv += s_w[pb][0][k]; bp += s_w[pb][1][k]; bq += s_w[pb][2][k]; }
+    cv += s_w[pb][0][0] + s_w[pb][0][1] + s_w[pb][0][2] + s_w[pb][0][3];
+    cp += s_w[pb][1][0] + s_w[pb][1][1] + s_w[pb][1][2] + s_w[pb][1][3];
+    cq += s_w[pb][2][0] + s_w[pb][2][1] + s_w[pb][2][2] + s_w[pb][2][3];
+    if (tile < a.ntiles) {
+      a.tile_base[tile] = bv;
+      const uint32_t s = sg[r];
+      if (sp[r] != s) { a.segout[s].line_lo = bv; a.segout[s].p_lo = bp; a.segout[s].q_lo = bq; }
+      if (sn[r] != s) { a.segout[s].line_hi = bv + v; a.segout[s].p_hi = bp + p; a.segout[s].q_hi = bq + q; }
+    }
   }
-  const uint64_t inc = wave_incl_scan_add(v, lane);
-  if (lane == 63) s_w[wv] = inc;
-  __syncthreads();
-  uint64_t pre = s_base;
-  for (int k = 0; k < wv; ++k) pre += s_w[k];
-  uint64_t b = pre + inc - v;
-  for (int j = 0; j < 16; ++j) {
-    const uint32_t tile = t0 + j;
-    if (tile >= a.ntiles) break;
-    a.tile_base[tile] = b;
-    const uint32_t s = a.tile_seg[tile];
-    if (tile == a.segs[s].tile0) a.segout[s].line_lo = b;
-    if (tile == a.segs[s].tile0 + a.segs[s].ntiles - 1) a.segout[s].line_hi = b + ev[j];
-    b += ev[j];
+  if (a.grep_mode != kGrepNone) {  // bitmap words whose first line is in [blk_lo, blk_hi)
+    const uint64_t w0 = (blk_lo + 31) / 32, w1 = (cv + 31) / 32;
+    for (uint64_t w = w0 + t; w < w1 && w * 32 < a.cap_lines; w += 256) a.bits[w] = 0u;
   }
 }
 
@@ -731,67 +712,53 @@ __global__ __launch_bounds__(256) void k_match(RunArgs a) {
 }
 
 // ============================================================== K3: per-stream counts ==
-// Block-level segmented reduction: one atomic per (block, stream) when the block lies
-// in one stream, per-thread atomics otherwise.
-__device__ void seg_reduce_add(uint32_t seg, uint64_t v, uint64_t* dst_base, size_t stride_words,
-                               uint32_t* s_seg, uint64_t* s_acc) {
-  const int t = threadIdx.x;
-  __syncthreads();
-  if (t == 0) { s_seg[0] = seg; s_seg[1] = 0; }
-  __syncthreads();
-  if (seg != s_seg[0]) atomicOr(&s_seg[1], 1u);
-  __syncthreads();
-  if (s_seg[1] == 0) {
-    const uint64_t ws = wave_sum(v);
-    if ((t & 63) == 0) s_acc[t >> 6] = ws;
-    __syncthreads();
-    if (t == 0) {
-      const uint64_t tot = s_acc[0] + s_acc[1] + s_acc[2] + s_acc[3];
-      if (tot) atomicAdd((unsigned long long*)(dst_base + (size_t)seg * stride_words), (unsigned long long)tot);
-    }
-  } else if (v) {
-    atomicAdd((unsigned long long*)(dst_base + (size_t)seg * stride_words), (unsigned long long)v);
-  }
+// parsed / since_ok come from k_tbase's prefixes.  matched = popcount of the match
+// bitmap per stream: one partial per 8192-line chunk for the stream the chunk starts in
+// (mpart[c], no atomics), the chunk's lines of the next stream as one block atomic, and
+// per-thread atomics only for streams shorter than a chunk.  k_tail adds the partials of
+// the chunks that start inside its stream.
+__device__ __forceinline__ uint32_t word_range_mask(uint64_t w, uint64_t lo, uint64_t hi) {
+  // bits of word w (lines 32w .. 32w+31) inside [lo, hi)
+  const uint64_t l0 = w * 32;
+  uint32_t m = ~0u;
+  if (l0 < lo) m &= lo - l0 >= 32 ? 0u : (~0u << (lo - l0));
+  if (l0 + 32 > hi) m &= hi <= l0 ? 0u : ((1u << (hi - l0)) - 1u);
+  return m;
 }
 
-__global__ __launch_bounds__(256) void k_count(RunArgs a, uint32_t nblk_tiles, uint64_t nwords) {
-  __shared__ uint32_t s_seg[2];
-  __shared__ uint64_t s_acc[4];
+__global__ __launch_bounds__(256) void k_mcount(RunArgs a) {
+  __shared__ uint64_t s_acc[2][4];
   if (a.counters[2]) return;
-  const size_t stride = sizeof(SegOut) / 8;
-  if (blockIdx.x < nblk_tiles) {
-    // parsed / since_ok from the per-tile records: one tile per thread
-    const uint32_t tile = blockIdx.x * 256 + threadIdx.x;
-    const uint32_t tclamp = tile < a.ntiles ? tile : a.ntiles - 1;
-    const uint32_t s = find_seg_by_tile(a.segs, a.nsegs, tclamp);
-    const uint64_t p = tile < a.ntiles ? a.tstat[tile].parsed : 0;
-    const uint64_t q = tile < a.ntiles ? a.tstat[tile].since_ok : 0;
-    seg_reduce_add(s, p, &a.segout[0].parsed, stride, s_seg, s_acc);
-    seg_reduce_add(s, q, &a.segout[0].since_ok, stride, s_seg, s_acc);
-  } else {
-    // matched = popcount of the match bitmap per stream: one 32-line word per thread
-    if (a.grep_mode == kGrepNone) return;
-    const uint64_t L = a.segout[a.nsegs - 1].line_hi;
-    const uint64_t wi = (uint64_t)(blockIdx.x - nblk_tiles) * 256 + threadIdx.x;
-    const uint64_t l0 = wi * 32;
-    const uint64_t lc = l0 < L ? l0 : (L ? L - 1 : 0);
-    uint32_t s = find_seg_by_line(a.segout, a.nsegs, lc);
-    uint64_t v = 0;
-    uint32_t word = (wi < nwords && l0 < L) ? a.bits[wi] : 0;
-    if (word) {
-      // split the word at stream boundaries
-      for (;;) {
-        const uint64_t hi = a.segout[s].line_hi;
-        if (hi >= l0 + 32 || s + 1 >= a.nsegs) { v += __popc(word); break; }
-        const uint32_t nb = (uint32_t)(hi - l0);
-        const uint32_t part = nb >= 32 ? word : (word & ((1u << nb) - 1));
-        if (part) atomicAdd((unsigned long long*)&a.segout[s].matched, (unsigned long long)__popc(part));
-        word &= ~((nb >= 32) ? ~0u : ((1u << nb) - 1));
-        ++s;
-        if (!word) break;
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const uint64_t L = a.segout[a.nsegs - 1].line_hi;
+  const uint64_t nchunks = (L + kMatchChunk - 1) / kMatchChunk;
+  for (uint64_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
+    const uint64_t l0 = c * kMatchChunk;
+    const uint32_t s0 = find_seg_by_line(a.segout, a.nsegs, l0);
+    const uint64_t hi0 = a.segout[s0].line_hi;
+    const uint64_t w = c * (kMatchChunk / 32) + t;
+    uint64_t v0 = 0, v1 = 0;
+    if (w * 32 < L) {
+      const uint32_t word = a.bits[w] & word_range_mask(w, 0, L);
+      v0 = __popc(word & word_range_mask(w, 0, hi0));
+      uint32_t rest = word & ~word_range_mask(w, 0, hi0);
+      for (uint32_t s = s0 + 1; rest && s < a.nsegs; ++s) {
+        const uint32_t part = rest & word_range_mask(w, a.segout[s].line_lo, a.segout[s].line_hi);
+        rest &= ~part;
+        if (s == s0 + 1) v1 += __popc(part);
+        else if (part) atomicAdd((unsigned long long*)&a.segout[s].matched, (unsigned long long)__popc(part));
       }
     }
-    seg_reduce_add(s, v, &a.segout[0].matched, stride, s_seg, s_acc);
+    v0 = wave_sum(v0);
+    v1 = wave_sum(v1);
+    __syncthreads();
+    if (lane == 0) { s_acc[0][wv] = v0; s_acc[1][wv] = v1; }
+    __syncthreads();
+    if (t == 0) {
+      a.mpart[c] = s_acc[0][0] + s_acc[0][1] + s_acc[0][2] + s_acc[0][3];
+      const uint64_t x1 = s_acc[1][0] + s_acc[1][1] + s_acc[1][2] + s_acc[1][3];
+      if (x1) atomicAdd((unsigned long long*)&a.segout[s0 + 1].matched, (unsigned long long)x1);
+    }
   }
 }
 
@@ -812,68 +779,104 @@ __device__ uint32_t block_incl_scan_u32(uint32_t x, uint32_t* s_w, uint32_t* tot
   return inc + pre;
 }
 
+__device__ uint64_t block_sum_u64(uint64_t x, uint64_t* s_w) {
+  const int t = threadIdx.x;
+  x = wave_sum(x);
+  __syncthreads();
+  if ((t & 63) == 0) s_w[t >> 6] = x;
+  __syncthreads();
+  return s_w[0] + s_w[1] + s_w[2] + s_w[3];
+}
+
+constexpr uint64_t kNone = ~0ull;
+
+// The k-th (k >= 1) set bit of the match bitmap counted backwards from hi - 1 within
+// [lo, hi): 256 words (8192 lines) per step, one word per thread (thread 0 = top word).
+__device__ uint64_t select_back_bits(const uint32_t* bits, uint64_t lo, uint64_t hi, uint64_t k, uint32_t* s_w,
+                                     uint64_t* s_res) {
+  const int t = threadIdx.x;
+  __syncthreads();
+  if (t == 0) *s_res = kNone;
+  if (hi <= lo || k == 0) { __syncthreads(); return kNone; }
+  const int64_t wlo = (int64_t)(lo >> 5), whi = (int64_t)((hi - 1) >> 5);
+  uint64_t cum = 0;
+  for (int64_t top = whi; top >= wlo; top -= 256) {
+    const int64_t w = top - t;
+    uint32_t word = 0;
+    if (w >= wlo) word = bits[w] & word_range_mask((uint64_t)w, lo, hi);
+    const uint32_t c = (uint32_t)__popc(word);
+    uint32_t tot;
+    const uint32_t incl = block_incl_scan_u32(c, s_w, &tot);
+    if (cum + tot >= k) {
+      if (c && cum + incl >= k && cum + incl - c < k) {
+        const uint32_t needc = (uint32_t)(k - (cum + incl - c));
+        for (uint32_t i = 1; i < needc; ++i) word &= ~(1u << (31 - __clz(word)));
+        *s_res = (uint64_t)w * 32 + (31 - __clz(word));
+      }
+      break;
+    }
+    cum += tot;
+  }
+  __syncthreads();
+  return *s_res;
+}
+
+// kubelet tail (SPEC.md S4) over G = matching lines (all lines without patterns):
+// start = the `need`-th G line from the end, need = |G| - max(0, T - n) <= n + 1.  The
+// window [start, hi) then holds need G lines; all G lines are parsed when patterns are
+// given (the bitmap only marks parsed lines), so the n-th parsed G line at/after start is
+// the window's second-to-last G line exactly when need = n + 1 (the trailing fragment is
+// then the (n+1)-th and is cut); otherwise every selected line of the window is in.
 __global__ __launch_bounds__(256) void k_tail(RunArgs a) {
   __shared__ uint32_t s_w[4];
-  __shared__ uint64_t s_found;
+  __shared__ uint64_t s_w64[4];
+  __shared__ uint64_t s_res;
   const uint32_t s = blockIdx.x;
   const int t = threadIdx.x;
   if (a.counters[2]) return;
   SegOut& so = a.segout[s];
   const uint64_t lo = so.line_lo, hi = so.line_hi;
+  const bool grep = a.grep_mode != kGrepNone;
+  uint64_t matched = hi - lo;
+  if (grep) {
+    uint64_t v = 0;
+    const uint64_t c0 = (lo + kMatchChunk - 1) / kMatchChunk, c1 = (hi + kMatchChunk - 1) / kMatchChunk;
+    for (uint64_t c = c0 + t; c < c1; c += 256) v += a.mpart[c];
+    matched = block_sum_u64(v, s_w64) + so.matched;
+  }
+  __syncthreads();
+  if (t == 0) {
+    so.parsed = so.p_hi - so.p_lo;
+    so.since_ok = so.q_hi - so.q_lo;
+    so.matched = matched;
+  }
   if (a.tail < 0) {
     if (t == 0) { so.win_lo = lo; so.win_hi = hi; }
     return;
   }
   const uint64_t n = (uint64_t)a.tail;
-  const bool grep = a.grep_mode != kGrepNone;
-  const uint64_t gsize = grep ? so.matched : hi - lo;
+  const uint64_t gsize = matched;
   const uint64_t gfrag = (so.frag && hi > lo && gbit(a, hi - 1)) ? 1 : 0;
   const uint64_t T = gsize - gfrag;
   const uint64_t k = T > n ? T - n : 0;
-  const uint64_t need = gsize - k;  // G lines at / after the start: <= n + 1
-  if (need == 0) {
+  const uint64_t need = gsize - k;
+  if (need == 0 || n == 0) {  // n = 0 emits nothing (ReadLogs stops before the first line)
     if (t == 0) { so.win_lo = hi; so.win_hi = hi; }
     return;
   }
-  // backward: the need-th G line from the end
-  if (t == 0) s_found = lo;
-  uint64_t cum = 0;
-  for (uint64_t end = hi; end > lo;) {
-    const uint64_t cs = end - lo > 256 ? end - 256 : lo;
-    const uint64_t l = cs + t;
-    const uint32_t g = (l < end && gbit(a, l)) ? 1u : 0u;
-    uint32_t tot;
-    const uint32_t pre = block_incl_scan_u32(g, s_w, &tot);
-    if (cum + tot >= need) {
-      const uint64_t needc = need - cum;
-      if (g && (uint64_t)(tot - pre + 1) == needc) s_found = l;
-      break;
-    }
-    cum += tot;
-    end = cs;
-  }
-  __syncthreads();
-  const uint64_t start = s_found;
-  // forward: the n-th parsed G line at / after start bounds the window
-  if (t == 0) s_found = hi;
-  cum = 0;
-  if (n == 0) {
-    if (t == 0) s_found = start;
+  uint64_t start, end = hi;
+  if (grep) {
+    start = select_back_bits(a.bits, lo, hi, need, s_w, &s_res);
+    if (need == n + 1) end = select_back_bits(a.bits, start, hi - 1, 1, s_w, &s_res) + 1;
   } else {
-    for (uint64_t b = start; b < hi; b += 256) {
-      const uint64_t l = b + t;
-      const uint32_t pg = (l < hi && gbit(a, l) && (a.meta[l] & Meta::kParsed)) ? 1u : 0u;
-      uint32_t tot;
-      const uint32_t pre = block_incl_scan_u32(pg, s_w, &tot);
-      if (cum + tot >= n) {
-        if (pg && cum + pre == n) s_found = l + 1;
-        break;
-      }
-      cum += tot;
+    start = hi - need;
+    if (need == n + 1) {  // cut the fragment only if every line of the window is parsed
+      uint32_t bad = 0;
+      for (uint64_t l = start + t; l < hi; l += 256) bad |= (a.meta[l] & Meta::kParsed) ? 0u : 1u;
+      if (__syncthreads_or(bad) == 0) end = hi - 1;
     }
   }
-  __syncthreads();
-  if (t == 0) { so.win_lo = start; so.win_hi = s_found; }
+  if (t == 0) { so.win_lo = start; so.win_hi = end; }
 }
 
 __global__ __launch_bounds__(256) void k_wprefix(RunArgs a) {
@@ -894,109 +897,231 @@ __global__ __launch_bounds__(256) void k_wprefix(RunArgs a) {
     if (s < a.nsegs) a.wpre[s] = carry + pre + inc - v;
     carry += tot;
   }
+  const uint64_t nb0 = (carry + kCompactLines - 1) / kCompactLines;
+  const uint32_t nb = (uint32_t)(nb0 < a.max_cblocks ? nb0 : a.max_cblocks);
   if (t == 0) {
     a.wpre[a.nsegs] = carry;
-    const uint64_t nb = (carry + kCompactLines - 1) / kCompactLines;
-    a.counters[3] = (uint32_t)(nb < a.max_cblocks ? nb : a.max_cblocks);
+    a.counters[3] = nb;
   }
 }
 
+// Zeroes the run's counters and per-stream records (one launch instead of memsets).
+__global__ __launch_bounds__(256) void k_init(RunArgs a) {
+  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+  if (i < kNumCounters) a.counters[i] = 0;
+  const uint32_t nw = a.nsegs * (uint32_t)(sizeof(SegOut) / 8);
+  uint64_t* so = reinterpret_cast<uint64_t*>(a.segout);
+  for (uint32_t k = i; k < nw; k += gridDim.x * 256) so[k] = 0;
+}
+
 // ======================================================= K4: compaction + gather copy ==
-__global__ __launch_bounds__(kThreads) void k_compact(RunArgs a) {
+// Reduce-then-scan over blocks of kCompactLines window lines (no inter-block waiting):
+//   k_csum    per block: selected content bytes and selected lines -> csum[2 * blk]
+//   k_cscan   one block: exclusive scan of the block sums (in place)
+//   k_cgather per block: in-block scan + block base -> output offsets, stream output
+//             ranges, gather copy of the selected contents (prefix stripped)
+// Thread t of a block owns window lines blk * kCompactLines + 4t .. 4t + 3.
+struct WinLines {
+  uint64_t src[4];
+  uint32_t len[4], seg[4];
+  bool first[4], last[4];
+  uint64_t bytes;
+  uint32_t nsel;
+};
+
+__device__ __forceinline__ void window_lines(const RunArgs& a, uint64_t w0, uint64_t W, WinLines& r) {
+  uint32_t s = 0;
+  {
+    const uint64_t wq = w0 < W ? w0 : (W ? W - 1 : 0);
+    uint32_t lo = 0, hi = a.nsegs;
+    while (hi - lo > 1) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (a.wpre[mid] <= wq) lo = mid; else hi = mid;
+    }
+    s = lo;
+  }
+  r.bytes = 0;
+  r.nsel = 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const uint64_t wj = w0 + j;
+    r.len[j] = 0; r.src[j] = 0; r.first[j] = r.last[j] = false; r.seg[j] = s;
+    if (wj >= W) continue;
+    while (wj >= a.wpre[s + 1]) ++s;
+    r.seg[j] = s;
+    r.first[j] = wj == a.wpre[s];
+    r.last[j] = wj + 1 == a.wpre[s + 1];
+    const uint64_t l = a.segout[s].win_lo + (wj - a.wpre[s]);
+    const uint16_t m = a.meta[l];
+    const bool sel = (m & Meta::kParsed) && (m & Meta::kSince) && gbit(a, l);
+    if (sel) {
+      const uint8_t* segp = a.bytes + a.segs[s].base;
+      const uint64_t ls = a.line_off[l + s], le = a.line_off[l + s + 1];
+      const uint32_t plen = line_plen(a, m, segp, ls, le);
+      r.src[j] = a.segs[s].base + ls + plen;
+      r.len[j] = (uint32_t)(le - ls - plen);
+      r.bytes += r.len[j];
+      ++r.nsel;
+    }
+  }
+}
+
+__global__ __launch_bounds__(kThreads) void k_csum(RunArgs a) {
+  __shared__ uint64_t s_wb[4], s_wc[4];
+  if (a.counters[2]) return;
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const uint64_t W = a.wpre[a.nsegs];
+  const uint32_t nblocks = a.counters[3];
+  for (uint32_t blk = blockIdx.x; blk < nblocks; blk += gridDim.x) {
+    WinLines r;
+    window_lines(a, (uint64_t)blk * kCompactLines + (uint64_t)t * 4, W, r);
+    const uint64_t b = wave_sum(r.bytes), c = wave_sum((uint64_t)r.nsel);
+    __syncthreads();
+    if (lane == 0) { s_wb[wv] = b; s_wc[wv] = c; }
+    __syncthreads();
+    if (t == 0) {
+      a.csum[2 * blk] = s_wb[0] + s_wb[1] + s_wb[2] + s_wb[3];
+      a.csum[2 * blk + 1] = s_wc[0] + s_wc[1] + s_wc[2] + s_wc[3];
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void k_cscan(RunArgs a) {
+  __shared__ uint64_t s_wb[4], s_wc[4];
+  if (a.counters[2]) return;
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const uint32_t nb = a.counters[3];
+  const uint32_t per = (nb + 255) / 256;
+  const uint32_t i0 = t * per, i1 = i0 + per < nb ? i0 + per : nb;
+  uint64_t b = 0, c = 0;
+  for (uint32_t i = i0; i < i1; ++i) { b += a.csum[2 * i]; c += a.csum[2 * i + 1]; }
+  const uint64_t ib = wave_incl_scan_add(b, lane), ic = wave_incl_scan_add(c, lane);
+  if (lane == 63) { s_wb[wv] = ib; s_wc[wv] = ic; }
+  __syncthreads();
+  uint64_t pb = ib - b, pc = ic - c;
+  for (int k = 0; k < wv; ++k) { pb += s_wb[k]; pc += s_wc[k]; }
+  for (uint32_t i = i0; i < i1; ++i) {
+    const uint64_t xb = a.csum[2 * i], xc = a.csum[2 * i + 1];
+    a.csum[2 * i] = pb;
+    a.csum[2 * i + 1] = pc;
+    pb += xb;
+    pc += xc;
+  }
+}
+
+// 16 bytes starting at byte offset o (0..15) of the 32-byte window w[0..7].
+__device__ __forceinline__ uint4 extract16(const uint4& lo, const uint4& hi, uint32_t o) {
+  const uint32_t q = o >> 2, r = (o & 3u) * 8u;
+  const uint32_t w[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+  uint32_t x[5];
+#pragma unroll
+  for (int k = 0; k < 5; ++k)  // x[k] = w[q + k] without dynamic register indexing
+    x[k] = q == 0 ? w[k] : q == 1 ? w[k + 1] : q == 2 ? w[k + 2] : w[(k + 3) & 7];
+  uint32_t y[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) y[k] = (uint32_t)((((uint64_t)x[k + 1] << 32) | x[k]) >> r);
+  return make_uint4(y[0], y[1], y[2], y[3]);
+}
+__device__ __forceinline__ uint32_t byte_mask(int b0, int b1, int k) {
+  // bytes [b0, b1) of the chunk that fall in dword k, as a byte mask
+  int lo = b0 - 4 * k, hi = b1 - 4 * k;
+  lo = lo < 0 ? 0 : (lo > 4 ? 4 : lo);
+  hi = hi < 0 ? 0 : (hi > 4 ? 4 : hi);
+  const uint32_t mh = hi >= 4 ? ~0u : ((1u << (8 * hi)) - 1u);
+  const uint32_t ml = lo >= 4 ? ~0u : ((1u << (8 * lo)) - 1u);
+  return mh & ~ml;
+}
+
+// Copies the block's selected contents (LDS tables, output range [ob0, ob1)) with one
+// 16-B output chunk per thread and step: coalesced 16-B stores; each line piece of a chunk
+// is read as an aligned 32-byte window and byte-shifted into place.  Chunks shared with a
+// neighbouring block are written bytewise (only this block's bytes).
+__device__ void block_gather_copy(const uint64_t* s_src, const uint64_t* s_dst, const uint32_t* s_len, uint64_t ob0,
+                                  uint64_t ob1, const uint8_t* __restrict__ src, uint8_t* __restrict__ dst) {
+  if (ob1 <= ob0) return;
+  const uint64_t c0 = ob0 >> 4, c1 = (ob1 + 15) >> 4;
+  int i = 0;  // line of the current position: monotone per thread
+  for (uint64_t c = c0 + threadIdx.x; c < c1; c += blockDim.x) {
+    const uint64_t d0 = c << 4;
+    const uint64_t lo = d0 > ob0 ? d0 : ob0, hi = d0 + 16 < ob1 ? d0 + 16 : ob1;
+    {  // last line with s_dst <= lo, searched in [i, kCompactLines)
+      int l = i, h = kCompactLines;
+      while (h - l > 1) {
+        const int m = (l + h) >> 1;
+        if (s_dst[m] <= lo) l = m; else h = m;
+      }
+      i = l;
+    }
+    uint32_t o[4] = {0, 0, 0, 0};
+    int li = i;
+    for (uint64_t pos = lo; pos < hi;) {
+      while (s_dst[li] + s_len[li] <= pos) ++li;  // zero-length / finished lines
+      const uint64_t pend = s_dst[li] + s_len[li] < hi ? s_dst[li] + s_len[li] : hi;
+      const int64_t ad0 = (int64_t)s_src[li] - (int64_t)s_dst[li] + (int64_t)d0;  // source of chunk byte 0
+      const int b0 = (int)(pos - d0), b1 = (int)(pend - d0);
+      if (ad0 >= 16) {
+        const uint64_t base = (uint64_t)ad0 & ~15ull;
+        const uint4* wp = reinterpret_cast<const uint4*>(src + base);
+        const uint4 v = extract16(wp[0], wp[1], (uint32_t)(ad0 - (int64_t)base));
+        const uint32_t vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const uint32_t m = byte_mask(b0, b1, k);
+          o[k] = (vv[k] & m) | (o[k] & ~m);
+        }
+      } else {
+        for (int b = b0; b < b1; ++b) {
+          const uint32_t byte = src[ad0 + b];
+          o[b >> 2] = (o[b >> 2] & ~(0xFFu << (8 * (b & 3)))) | (byte << (8 * (b & 3)));
+        }
+      }
+      pos = pend;
+    }
+    if (lo == d0 && hi == d0 + 16) {
+      *reinterpret_cast<uint4*>(dst + d0) = make_uint4(o[0], o[1], o[2], o[3]);
+    } else {
+      for (uint64_t pos = lo; pos < hi; ++pos) {
+        const int b = (int)(pos - d0);
+        dst[pos] = (uint8_t)(o[b >> 2] >> (8 * (b & 3)));
+      }
+    }
+  }
+}
+
+__global__ __launch_bounds__(kThreads) void k_cgather(RunArgs a) {
   __shared__ uint64_t s_src[kCompactLines];
   __shared__ uint64_t s_dst[kCompactLines];
   __shared__ uint32_t s_len[kCompactLines];
   __shared__ uint64_t s_wb[4], s_wc[4];
-  __shared__ uint64_t s_exb, s_exc;
-  __shared__ uint32_t s_ticket;
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   if (a.counters[2]) return;
   const uint64_t W = a.wpre[a.nsegs];
   const uint32_t nblocks = a.counters[3];
-  uint64_t* stb = a.cstatus;
-  uint64_t* stc = a.cstatus + a.max_cblocks;
-  for (;;) {
-    if (t == 0) s_ticket = atomicAdd(&a.counters[1], 1u);
-    __syncthreads();
-    const uint32_t blk = s_ticket;
-    if (blk >= nblocks) break;
-    const uint64_t w0 = (uint64_t)blk * kCompactLines + (uint64_t)t * 4;
-    // segment of my first line
-    uint32_t s = 0;
-    {
-      const uint64_t wq = w0 < W ? w0 : (W ? W - 1 : 0);
-      uint32_t lo = 0, hi = a.nsegs;
-      while (hi - lo > 1) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (a.wpre[mid] <= wq) lo = mid; else hi = mid;
-      }
-      s = lo;
-    }
-    uint64_t src[4], blen = 0;
-    uint32_t len[4], seg_of[4];
-    uint32_t nsel = 0;
-    bool is_first[4], is_last[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const uint64_t wj = w0 + j;
-      len[j] = 0; src[j] = 0; is_first[j] = is_last[j] = false; seg_of[j] = s;
-      if (wj >= W) continue;
-      while (wj >= a.wpre[s + 1]) ++s;
-      seg_of[j] = s;
-      is_first[j] = wj == a.wpre[s];
-      is_last[j] = wj + 1 == a.wpre[s + 1];
-      const uint64_t l = a.segout[s].win_lo + (wj - a.wpre[s]);
-      const uint16_t m = a.meta[l];
-      const bool sel = (m & Meta::kParsed) && (m & Meta::kSince) && gbit(a, l);
-      if (sel) {
-        const uint8_t* segp = a.bytes + a.segs[s].base;
-        const uint64_t ls = a.line_off[l + s], le = a.line_off[l + s + 1];
-        const uint32_t plen = line_plen(a, m, segp, ls, le);
-        src[j] = a.segs[s].base + ls + plen;
-        len[j] = (uint32_t)(le - ls - plen);
-        blen += len[j];
-        ++nsel;
-      }
-    }
-    // block scans (bytes, selected lines)
-    const uint64_t ib = wave_incl_scan_add(blen, lane);
-    const uint64_t ic = wave_incl_scan_add((uint64_t)nsel, lane);
+  for (uint32_t blk = blockIdx.x; blk < nblocks; blk += gridDim.x) {
+    WinLines r;
+    window_lines(a, (uint64_t)blk * kCompactLines + (uint64_t)t * 4, W, r);
+    const uint64_t ib = wave_incl_scan_add(r.bytes, lane);
+    const uint64_t ic = wave_incl_scan_add((uint64_t)r.nsel, lane);
+    __syncthreads();  // the previous block's copy is done with the LDS tables
     if (lane == 63) { s_wb[wv] = ib; s_wc[wv] = ic; }
     __syncthreads();
-    uint64_t pb = 0, pc = 0, tb = 0, tc = 0;
-    for (int k = 0; k < 4; ++k) {
-      if (k < wv) { pb += s_wb[k]; pc += s_wc[k]; }
-      tb += s_wb[k]; tc += s_wc[k];
-    }
-    if (wv == 0) {
-      const uint64_t xb = lookback_wave(stb, blk, tb, 0ull, SumComb(), a.counters + 2, lane);
-      const uint64_t xc = lookback_wave(stc, blk, tc, 0ull, SumComb(), a.counters + 2, lane);
-      if (lane == 0) { s_exb = xb; s_exc = xc; }
-    }
-    __syncthreads();
-    uint64_t ob = s_exb + pb + ib - blen;  // my exclusive byte offset
-    uint64_t oc = s_exc + pc + ic - nsel;
+    uint64_t ob = a.csum[2 * blk] + ib - r.bytes, oc = a.csum[2 * blk + 1] + ic - r.nsel;
+    for (int k = 0; k < wv; ++k) { ob += s_wb[k]; oc += s_wc[k]; }
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int i = t * 4 + j;
-      if (is_first[j]) { a.segout[seg_of[j]].out_lo = ob; a.segout[seg_of[j]].sel_lo = oc; }
-      s_src[i] = src[j];
+      if (r.first[j]) { a.segout[r.seg[j]].out_lo = ob; a.segout[r.seg[j]].sel_lo = oc; }
+      s_src[i] = r.src[j];
       s_dst[i] = ob;
-      s_len[i] = len[j];
-      ob += len[j];
-      oc += len[j] ? 1 : 0;
-      if (is_last[j]) { a.segout[seg_of[j]].out_hi = ob; a.segout[seg_of[j]].sel_hi = oc; }
+      s_len[i] = r.len[j];
+      ob += r.len[j];
+      oc += r.len[j] ? 1 : 0;
+      if (r.last[j]) { a.segout[r.seg[j]].out_hi = ob; a.segout[r.seg[j]].sel_hi = oc; }
     }
     __syncthreads();
-    // gather copy: each wave takes lines round-robin, 64 lanes per line
-    for (int i = wv; i < kCompactLines; i += 4) {
-      const uint32_t n = s_len[i];
-      if (!n) continue;
-      const uint8_t* sp = a.bytes + s_src[i];
-      uint8_t* dp = a.out + s_dst[i];
-      for (uint32_t k = lane; k < n; k += 64) dp[k] = sp[k];
-    }
-    __syncthreads();
+    const uint64_t ob0 = a.csum[2 * blk];
+    const uint64_t ob1 = ob0 + s_wb[0] + s_wb[1] + s_wb[2] + s_wb[3];
+    block_gather_copy(s_src, s_dst, s_len, ob0, ob1, a.bytes, a.out);
   }
 }
 
@@ -1025,10 +1150,13 @@ hipError_t launch_pipeline(const RunArgs& a, hipStream_t st, hipEvent_t* ev, int
   hipError_t e;
 #define KLF_TRY(x) do { e = (x); if (e != hipSuccess) return e; } while (0)
   KLF_TRY(hipEventRecord(ev[0], st));
-  KLF_TRY(hipMemsetAsync(a.counters, 0, kNumCounters * sizeof(uint32_t), st));
-  KLF_TRY(hipMemsetAsync(a.segout, 0, (size_t)a.nsegs * sizeof(SegOut), st));
-  KLF_TRY(hipMemsetAsync(a.cstatus, 0, (size_t)a.max_cblocks * 2 * 8, st));
-  if (a.grep_mode != kGrepNone) KLF_TRY(hipMemsetAsync(a.bits, 0, (size_t)(a.cap_lines / 32 + 1) * 4, st));
+  {
+    const uint32_t nw = a.nsegs * (uint32_t)(sizeof(SegOut) / 8);
+    uint32_t g = (nw + 255) / 256;
+    g = g < 1 ? 1 : (g > 1024 ? 1024 : g);
+    hipLaunchKernelGGL(k_init, dim3(g), dim3(256), 0, st, a);
+    KLF_TRY(hipGetLastError());
+  }
   if (a.build_tiles) {
     const uint32_t g = (a.ntiles + 255) / 256;
     hipLaunchKernelGGL(k_tiles, dim3(g < 4096 ? g : 4096), dim3(256), 0, st, a.segs, a.nsegs, a.ntiles,
@@ -1066,17 +1194,22 @@ hipError_t launch_pipeline(const RunArgs& a, hipStream_t st, hipEvent_t* ev, int
     KLF_TRY(hipGetLastError());
   }
   KLF_TRY(hipEventRecord(ev[3], st));
-  const uint32_t nblk_tiles = (a.ntiles + 255) / 256;
-  const uint64_t nwords = a.cap_lines / 32 + 1;
-  const uint32_t nblk_words = a.grep_mode == kGrepNone ? 0 : (uint32_t)((nwords + 255) / 256);
-  hipLaunchKernelGGL(k_count, dim3(nblk_tiles + nblk_words), dim3(256), 0, st, a, nblk_tiles, nwords);
-  KLF_TRY(hipGetLastError());
+  if (a.grep_mode != kGrepNone) {
+    const uint64_t nchunks = a.cap_lines / kMatchChunk + 1;
+    const uint32_t g = (uint32_t)(nchunks < (uint64_t)num_cus * 4 ? nchunks : (uint64_t)num_cus * 4);
+    hipLaunchKernelGGL(k_mcount, dim3(g), dim3(256), 0, st, a);
+    KLF_TRY(hipGetLastError());
+  }
   hipLaunchKernelGGL(k_tail, dim3(a.nsegs), dim3(256), 0, st, a);
   KLF_TRY(hipGetLastError());
   hipLaunchKernelGGL(k_wprefix, dim3(1), dim3(256), 0, st, a);
   KLF_TRY(hipGetLastError());
   KLF_TRY(hipEventRecord(ev[4], st));
-  hipLaunchKernelGGL(k_compact, dim3(num_cus * 4), dim3(kThreads), 0, st, a);
+  hipLaunchKernelGGL(k_csum, dim3(num_cus * 4), dim3(kThreads), 0, st, a);
+  KLF_TRY(hipGetLastError());
+  hipLaunchKernelGGL(k_cscan, dim3(1), dim3(256), 0, st, a);
+  KLF_TRY(hipGetLastError());
+  hipLaunchKernelGGL(k_cgather, dim3(num_cus * 4), dim3(kThreads), 0, st, a);
   KLF_TRY(hipGetLastError());
   KLF_TRY(hipEventRecord(ev[5], st));
 #undef KLF_TRY

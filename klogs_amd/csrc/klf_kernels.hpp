@@ -17,14 +17,9 @@ constexpr uint64_t kSegAlign = 256;                 // segment base alignment in
 constexpr uint64_t kAllocSlack = kTile + kHalo + 1024;
 constexpr uint32_t kPlenEscape = 16383;             // meta plen field saturates here
 constexpr int kCompactLines = 1024;                 // lines per compaction block
-// Scan ticket groups: one counter per group, each on its own 256-B line.  Counters that
-// share a line serialise like a single word (measured on MI355X with
-// scripts/mb_stream.hip: 32 adjacent counters 2.6 TB/s, 128 padded counters 6.2 TB/s).
-constexpr uint32_t kScanGroups = 128;
-constexpr uint32_t kCtrStride = 64;                 // u32 words between group counters
-constexpr uint32_t kCtrScanGroups = 64;             // counters[64 + g * kCtrStride]
-constexpr uint32_t kNumCounters = kCtrScanGroups + kScanGroups * kCtrStride;
+constexpr uint32_t kNumCounters = 64;               // zeroed by k_init each run
 constexpr uint32_t kCtrPool = 4;                    // counters[4]: dense-tile pool allocator
+constexpr uint32_t kMatchChunk = 8192;              // lines per k_mcount partial (256 words)
 
 constexpr int kSlots = 132;  // staged line slots per tile (>= 4 KiB / 32-byte kubelet line + 1)
 
@@ -54,6 +49,8 @@ struct SegOut {
   uint64_t sel_lo, sel_hi;     // selected-line chain values at the window ends
   uint64_t out_lo, out_hi;     // output byte offsets [lo, hi) in the output buffer
   uint64_t frag;               // 1 when the stream ends without '\n'
+  uint64_t p_lo, p_hi;         // parsed-line prefix at the stream's first / past its last tile
+  uint64_t q_lo, q_hi;         // since_ok-line prefix, same
 };
 
 // Line-meta word (u16): bit0 parsed, bit1 since_ok, bits 2..15 content offset (plen),
@@ -105,10 +102,11 @@ struct RunArgs {
   uint32_t* pool;       // [pool_cap] slots of dense tiles
   uint64_t pool_cap;
   uint64_t* tile_base;  // [ntiles] global line index of each tile's line 0
-  uint64_t* bsum;       // [ntiles / 4096 + 1] scan block sums
-  uint64_t* cstatus;    // [2 * max compaction blocks] compaction look-back words
+  uint64_t* bsum;       // [3 * (ntiles / 4096 + 1)] scan block sums (events, parsed, since_ok)
+  uint64_t* mpart;      // [cap_lines / kMatchChunk + 1] matched-line partial per line chunk
+  uint64_t* csum;       // [2 * max compaction blocks] per-block (bytes, lines), then their prefix
   uint32_t* counters;   // [kNumCounters]: 1 compact ticket, 2 error flags, 3 compact blocks,
-                        // [8, 8+kScanGroups) scan ticket groups
+                        // 4 dense-tile pool
   uint64_t* line_off;   // [cap_lines + nsegs]
   uint16_t* meta;       // [cap_lines]
   uint32_t* bits;       // [cap_lines / 32 + 1]
@@ -116,7 +114,7 @@ struct RunArgs {
   SegOut* segout;       // [nsegs]
   uint64_t* wpre;       // [nsegs + 1] exclusive prefix of window sizes
   uint8_t* out;         // output bytes (capacity >= total input)
-  uint32_t max_cblocks; // compaction look-back capacity
+  uint32_t max_cblocks; // compaction block capacity
 };
 
 // Enqueues the whole pipeline on `stream`; `ev` (6 events) brackets the stages for

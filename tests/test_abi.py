@@ -28,6 +28,15 @@ def test_every_declared_symbol_is_exported():
     assert set(names) == set(E.SIGNATURES), set(names) ^ set(E.SIGNATURES)
 
 
+def test_every_host_symbol_is_exported():
+    from klogs_amd import host as H
+    names = _declared(ROOT / "include" / "klogs_host.h")
+    lib = C.CDLL(str(ROOT / "klogs_amd" / "_lib" / "libklogs_host.so"))
+    for n in names:
+        assert hasattr(lib, n), n
+    assert set(names) == set(H.SYMBOLS), set(names) ^ set(H.SYMBOLS)
+
+
 def test_strerror_and_layout():
     assert E.lib().klf_strerror(E.KLF_EPATTERN).decode().startswith("pattern")
     base, total = E.layout([10, 0, 300, 1])

@@ -114,3 +114,20 @@ def test_golden_fixtures(gpu, idx):
     if c["expect_bits"] is not None:
         assert bits.hex() == c["expect_bits"], c["name"]
     assert [cnt["lines"], cnt["parsed"], cnt["since_ok"], cnt["matched"], cnt["selected"]] == c["expect_counts"]
+
+
+@pytest.mark.parametrize("since,tail", [((synth.T0 + synth.SPAN + 1 - 300, 0), 100), (None, -1),
+                                        ((synth.T0 + 1800, 0), -1)])
+def test_c1_64mib(gpu, since, tail):
+    """BASELINE config 1 shape (one 64 MiB stream, --since 5m --tail 100) and the
+    all-lines case that makes the compaction copy the whole stream."""
+    d = synth.generate(synth.TEXT, 3, 0, 64 << 20)
+    check_against_c([d], since, tail, [])
+
+
+def test_many_small_streams_all_selected(gpu):
+    """Many streams, every line selected: output ranges of adjacent streams share 16-B
+    chunks at every boundary (bytewise edge stores)."""
+    streams = [synth.generate(synth.TEXT, 21, i, 1000 + 37 * i) for i in range(300)]
+    check_against_c(streams, None, -1, [])
+    check_against_c(streams, None, 3, [])
