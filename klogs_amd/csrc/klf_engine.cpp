@@ -352,6 +352,14 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
     a.build_tiles = (!same_layout && attempt == 0) ? 1u : 0u;
     a.since_sec = f->since.sec;
     a.since_nsec = f->since.nsec;
+    {
+      const int64_t sec = f->since.sec;
+      const int64_t day = sec >= 0 ? sec / 86400 : -((-sec + 86399) / 86400);
+      a.since_day = (int32_t)std::max<int64_t>(std::min<int64_t>(day, INT32_MAX), INT32_MIN);
+      a.since_sod = (uint32_t)(sec - day * 86400);
+      if (day > INT32_MAX) a.since_sod = 86400;  // later than any fast-path instant
+      if (day < INT32_MIN) a.since_sod = 0;
+    }
     a.tail = f->tail;
     a.grep_mode = (uint32_t)mode;
     a.lit = e->d_lit.as<uint8_t>();

@@ -69,20 +69,15 @@ __device__ __forceinline__ uint32_t find_seg_by_line(const SegOut* so, uint32_t 
   return lo;
 }
 
-// Byte source for the timestamp parser: the tile's LDS image (tile + halo) when the
-// byte is there, global memory otherwise; -1 past the end of the stream.
-struct LineBytes {
-  const uint8_t* lds;   // LDS image; lds[0] = stream byte rel_lo
-  const uint8_t* seg;   // global stream base
-  int64_t p0;           // stream offset of the line start
-  int64_t rel_lo;
+// Byte source for the general timestamp parser (k_fixup): global memory, -1 past the
+// end of the stream.
+struct GlobalBytes {
+  const uint8_t* seg;  // global stream base
+  int64_t p0;          // stream offset of the line start
   int64_t seg_len;
   __device__ __forceinline__ int operator()(uint32_t i) const {
     const int64_t q = p0 + (int64_t)i;
-    if (q >= seg_len) return -1;
-    const int64_t o = q - rel_lo;
-    if (o >= 0 && o < kTile + kHalo) return lds[o];
-    return seg[q];
+    return q < seg_len ? (int)seg[q] : -1;
   }
 };
 __device__ __forceinline__ uint16_t make_meta(bool ok, bool since_ok, uint32_t plen) {
@@ -92,47 +87,43 @@ __device__ __forceinline__ uint16_t make_meta(bool ok, bool since_ok, uint32_t p
 }
 
 // ============================================================== K1: the scan ==
-// Streaming scan with NO inter-workgroup waiting and NO workgroup barriers.  MI355X
-// measurements: a decoupled look-back round costs ~5 us under full-chip
-// streaming, and workgroup barriers between the phases of a tile left the SIMDs idle
-// while the slowest wave finished.  So the unit of work is a 4 KiB WAVE-TILE owned by one
-// wave from load to record:
-//   K1a k_scan     per wave-tile: register prefetch of the next wave-tile, stage in the
-//                  wave's own LDS region, line-end events, in-wave scan (DPP), parse of
-//                  every line starting in the tile (fast fixed-width path for the
-//                  kubelet prefix), fused literal grep; results STAGED as one packed u32
-//                  slot per line start (dense tiles, > kSlots starts, take slots from a
-//                  pool), plus a 16-B TileStat.
-//   K1b/K1c        device scan of the per-tile line counts -> tile line bases, stream
-//                  line ranges.
-//   K1d k_scatter  staged slots -> global line_off (u64) / meta (u16) / match bitmap.
-// Slot (u32): bits 0..14 line start offset inside the tile (0..4095), bit 15 literal hit,
-// bits 16..31 the line's meta word.
+// Streaming scan with no inter-workgroup waiting and no workgroup barriers in the loop.
+// The unit of work is an 8 KiB WAVE-TILE owned by one wave from load to record (static
+// round robin over a persistent grid); the next wave-tile is in flight in registers
+// (32 VGPRs) while this one is processed from the wave's LDS region.
+//   * line ends: per lane 128 contiguous bytes; a SWAR any-test per 16-B chunk (2-3 VALU
+//     per dword), exact byte positions only for chunks that hit (a line ends every few
+//     hundred bytes, so most chunks never take the exact step);
+//   * in-wave scan (DPP) of the per-lane event counts -> local line numbers; the line
+//     starts go to a per-wave LDS list (slot j = j-th line starting in the tile);
+//   * one parse pass over the list, one line per lane: the canonical kubelet prefix
+//     "YYYY-MM-DDTHH:MM:SS.nnnnnnnnnZ " (logs.go timeFormatOut) in SWAR (v_perm digit
+//     packing, u24 multiply-adds, since compared as (day, second of day, ns)); any other
+//     shape is DEFERRED to k_fixup, which runs the general Go time.Parse restatement;
+//   * fused single literal (--grep): rare-byte anchor any-test per chunk, candidates
+//     verified from LDS, the hit's line found by binary search in the list;
+//   * slots (u32: start offset in the tile, defer bit, literal-hit bit, u16 meta) are
+//     written once per tile; tiles with more starts than kSlots use a global pool.
+//   K1b/K1c  device scan of the per-tile line counts -> tile line bases, stream ranges.
+//   K1d      k_scatter: slots -> global line_off (u64) / meta (u16) / match bitmap.
 
-// 4-bit mask of the bytes of x equal to zero (exact): bit k set iff byte k of x is 0.
-__device__ __forceinline__ uint32_t zmask4(uint32_t x) {
-  const uint32_t z = ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x | 0x7F7F7F7Fu);  // 0x80 per zero byte
-  return (z * 0x00204081u) >> 28;
+constexpr uint32_t kSlotOff = 0x3FFFu, kSlotDefer = 0x4000u, kSlotHit = 0x8000u;
+constexpr uint32_t kCtrDefer = 5;  // counters[5]: some line of this run was deferred
+
+// nonzero iff some byte of the 16 bytes equals the byte replicated in c4 (any-test: the
+// haszero borrow can only add false flags above a true zero byte)
+__device__ __forceinline__ uint32_t any_eq16(const uint4& v, uint32_t c4) {
+  auto h = [c4](uint32_t x) { const uint32_t y = x ^ c4; return (y - 0x01010101u) & ~y; };
+  return (h(v.x) | h(v.y) | h(v.z) | h(v.w)) & 0x80808080u;
 }
-// 64-bit mask over the 64 bytes in w: bit i set iff byte i equals the byte in pat (x4).
-__device__ __forceinline__ uint64_t eq_mask64_words(const uint32_t* w, uint32_t pat) {
-  uint32_t lo = 0, hi = 0;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) lo |= zmask4(w[j] ^ pat) << (4 * j);
-#pragma unroll
-  for (int j = 0; j < 8; ++j) hi |= zmask4(w[8 + j] ^ pat) << (4 * j);
-  return ((uint64_t)hi << 32) | lo;
-}
-// Nonzero iff some byte of the 64 bytes in w equals the byte in pat (exact as an any-test:
-// the classic haszero borrow can only add false bits above a true zero byte).
-__device__ __forceinline__ uint32_t any_eq64_words(const uint32_t* w, uint32_t pat) {
-  uint32_t acc = 0;
-#pragma unroll
-  for (int j = 0; j < 16; ++j) {
-    const uint32_t x = w[j] ^ pat;
-    acc |= (x - 0x01010101u) & ~x;
-  }
-  return acc & 0x80808080u;
+// exact: bit i set iff byte i of the 16 bytes equals the byte in c4
+__device__ __forceinline__ uint32_t eq_mask16(const uint4& v, uint32_t c4) {
+  auto z = [c4](uint32_t x) {
+    const uint32_t y = x ^ c4;
+    const uint32_t f = ~(((y & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | y) & 0x80808080u;  // 0x80 per equal byte
+    return (f * 0x00204081u) >> 28;  // flags 7,15,23,31 -> bits 0..3 (no carries)
+  };
+  return z(v.x) | (z(v.y) << 4) | (z(v.z) << 8) | (z(v.w) << 12);
 }
 
 template <class T>
@@ -156,67 +147,84 @@ __global__ __launch_bounds__(256) void k_tiles(const SegDesc* segs, uint32_t nse
     tile_seg[tile] = find_seg_by_tile(segs, nsegs, tile);
 }
 
-// Canonical kubelet prefix "YYYY-MM-DDTHH:MM:SS.nnnnnnnnnZ " (k8s logs.go timeFormatOut):
-// 9 dword LDS reads instead of ~31 dependent byte reads.  Accepts exactly the inputs of
-// this shape the general parser accepts (same value); anything else -> general parser.
-__device__ __forceinline__ bool parse_fast_lds(const uint8_t* lds, uint32_t o, TsResult& r) {
+// Cumulative days before month m (non-leap, low 16 bits) and the month's length (high).
+__constant__ uint32_t c_month[16] = {0,
+                                     0 | (31u << 16),   31 | (28u << 16),  59 | (31u << 16),  90 | (30u << 16),
+                                     120 | (31u << 16), 151 | (30u << 16), 181 | (31u << 16), 212 | (31u << 16),
+                                     243 | (30u << 16), 273 | (31u << 16), 304 | (30u << 16), 334 | (31u << 16),
+                                     0, 0, 0};
+
+// v_mad_u32_u24: a * b + c for a, b < 2^24 (low 32 bits of the product)
+__device__ __forceinline__ uint32_t mad24(uint32_t a, uint32_t b, uint32_t c) { return __umul24(a, b) + c; }
+
+// Two decimal digits per 16-bit half of a dword holding 4 digit values (bytes 0..9):
+// low half = b0 * 10 + b1, high half = b2 * 10 + b3.
+__device__ __forceinline__ uint32_t digit_pairs(uint32_t t) {
+  const uint32_t ev = t & 0x00FF00FFu;                                // b0, b2
+  const uint32_t od = __builtin_amdgcn_perm(0u, t, 0x0C030C01u);      // b1, b3
+  return mad24(ev, 10u, od);
+}
+
+// Canonical kubelet prefix at LDS byte offset o (bytes o .. o + 30 valid): true with
+// since_ok set when the line starts "YYYY-MM-DDTHH:MM:SS.nnnnnnnnnZ " with a valid date,
+// year 1970..2099 (where the Gregorian leap rule is y % 4 == 0).  The value equals Go
+// time.Parse's for exactly these inputs; false sends the line to the general parser.
+__device__ __forceinline__ bool parse_fast(const uint8_t* lds, uint32_t o, const uint32_t* s_month, int32_t sday,
+                                           uint32_t ssod, int32_t snsec, bool& since_ok) {
   const uint32_t* s32 = reinterpret_cast<const uint32_t*>(lds);
-  const uint32_t base = o >> 2, sh = (o & 3) * 8;
+  const uint32_t base = o >> 2, sh = o & 3u;
   uint32_t w[8];
   uint32_t prev = s32[base];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     const uint32_t nx = s32[base + j + 1];
-    w[j] = sh ? (uint32_t)((((uint64_t)nx << 32) | prev) >> sh) : prev;
+    w[j] = __builtin_amdgcn_alignbyte(nx, prev, sh);
     prev = nx;
   }
-#define KLF_B(k) ((w[(k) >> 2] >> (8 * ((k) & 3))) & 0xFFu)
-  if (KLF_B(4) != '-' || KLF_B(7) != '-' || KLF_B(10) != 'T' || KLF_B(13) != ':' || KLF_B(16) != ':' ||
-      KLF_B(19) != '.' || KLF_B(29) != 'Z' || KLF_B(30) != ' ')
-    return false;
-  // digits, folded as they are read (no per-byte array: keeps the register budget)
-  bool ok = true;
-  auto dig = [&](int k) -> uint32_t {
-    const uint32_t v = KLF_B(k) - '0';
-    ok &= v < 10;
-    return v;
-  };
-  const int64_t year = dig(0) * 1000 + dig(1) * 100 + dig(2) * 10 + dig(3);
-  const int month = (int)(dig(5) * 10 + dig(6)), day = (int)(dig(8) * 10 + dig(9));
-  const int hour = (int)(dig(11) * 10 + dig(12)), minute = (int)(dig(14) * 10 + dig(15));
-  const int second = (int)(dig(17) * 10 + dig(18));
-  uint32_t ns = 0;
-#pragma unroll
-  for (int k = 20; k < 29; ++k) ns = ns * 10 + dig(k);
-#undef KLF_B
-  if (!ok) return false;
-  if (month < 1 || month > 12 || hour >= 24 || minute >= 60 || second >= 60) return false;
-  if (day < 1 || day > days_in_month(month, year)) return false;
-  r.sec = days_from_civil(year, month, day) * 86400 + hour * 3600 + minute * 60 + second;
-  r.nsec = (int32_t)ns;
-  r.len = 30;
+  // separators: '-' 4, '-' 7, 'T' 10, ':' 13, ':' 16, '.' 19, 'Z' 29, ' ' 30
+  const uint32_t sep = ((w[1] ^ 0x2D00002Du) & 0xFF0000FFu) | ((w[2] ^ 0x00540000u) & 0x00FF0000u) |
+                       ((w[3] ^ 0x00003A00u) & 0x0000FF00u) | ((w[4] ^ 0x2E00003Au) & 0xFF0000FFu) |
+                       ((w[7] ^ 0x00205A00u) & 0x00FFFF00u);
+  // the 23 digits packed into 6 dwords (one pad '0')
+  const uint32_t p0 = w[0];                                                  // Y Y Y Y
+  const uint32_t p1 = __builtin_amdgcn_perm(w[2], w[1], 0x05040201u);        // M M D D
+  const uint32_t p2 = __builtin_amdgcn_perm(w[3], w[2], 0x07060403u);        // h h m m
+  const uint32_t p3 = __builtin_amdgcn_perm(w[5], w[4], 0x05040201u);        // s s n0 n1
+  const uint32_t p4 = __builtin_amdgcn_perm(w[6], w[5], 0x05040302u);        // n2 n3 n4 n5
+  const uint32_t p5 = __builtin_amdgcn_perm(w[7], w[6], 0x040C0302u) | 0x00300000u;  // n6 n7 0 n8
+  // digit check: high nibble 3 everywhere, low nibble <= 9 (no cross-byte carry once the
+  // high nibbles are 3)
+  const uint32_t t0 = p0 ^ 0x30303030u, t1 = p1 ^ 0x30303030u, t2 = p2 ^ 0x30303030u, t3 = p3 ^ 0x30303030u,
+                 t4 = p4 ^ 0x30303030u, t5 = p5 ^ 0x30303030u;
+  const uint32_t hi = (t0 | t1 | t2 | t3 | t4 | t5) & 0xF0F0F0F0u;
+  const uint32_t lo = ((p0 + 0x06060606u) | (p1 + 0x06060606u) | (p2 + 0x06060606u) | (p3 + 0x06060606u) |
+                       (p4 + 0x06060606u) | (p5 + 0x06060606u)) & 0x40404040u;
+  if ((sep | hi | lo) != 0u) return false;
+  const uint32_t v0 = digit_pairs(t0), v1 = digit_pairs(t1), v2 = digit_pairs(t2), v3 = digit_pairs(t3),
+                 v4 = digit_pairs(t4), v5 = digit_pairs(t5);
+  const uint32_t year = mad24(v0 & 0xFFFFu, 100u, v0 >> 16);
+  const uint32_t month = v1 & 0xFFFFu, day = v1 >> 16, hour = v2 & 0xFFFFu, minute = v2 >> 16;
+  const uint32_t second = v3 & 0xFFFFu;
+  uint32_t ns = mad24(v3 >> 16, 10000000u, 0u);
+  ns = mad24(v4 & 0xFFFFu, 100000u, ns);
+  ns = mad24(v4 >> 16, 1000u, ns);
+  ns = mad24(v5 & 0xFFFFu, 10u, ns) + (v5 >> 16);
+  if (year - 1970u >= 130u || month - 1u >= 12u || hour >= 24u || minute >= 60u || second >= 60u) return false;
+  const uint32_t mt = s_month[month];
+  const uint32_t leap = (year & 3u) == 0u ? 1u : 0u;
+  const uint32_t dim = (mt >> 16) + (month == 2u ? leap : 0u);
+  if (day - 1u >= dim) return false;
+  const int32_t days = (int32_t)(mad24(year - 1970u, 365u, (year - 1969u) >> 2) + (mt & 0xFFFFu) +
+                                 (month > 2u ? leap : 0u) + day - 1u);
+  const uint32_t sod = mad24(hour, 3600u, mad24(minute, 60u, second));
+  const bool before = days < sday || (days == sday && (sod < ssod || (sod == ssod && (int32_t)ns < snsec)));
+  since_ok = !before;
   return true;
 }
 
-// Parse of the line starting at stream offset p0: fast path from LDS, else general
-// (LDS where the bytes are staged, global memory past the halo).
-__device__ __forceinline__ bool parse_line_at(const uint8_t* lds, const uint8_t* segp, int64_t p0, int64_t rel_lo,
-                                              int64_t seg_len, int64_t ssec, int32_t snsec, bool* since_ok,
-                                              uint32_t* plen) {
-  TsResult r;
-  const int64_t o = p0 - rel_lo;
-  bool ok;
-  if (o >= 0 && o + 36 <= kTile + kHalo && p0 + 31 <= seg_len && parse_fast_lds(lds, (uint32_t)o, r)) {
-    ok = true;
-    *plen = 31;
-  } else {
-    LineBytes gb{lds, segp, p0, rel_lo, seg_len};
-    ok = parse_line_prefix(gb, r, *plen);
-  }
-  *since_ok = ok && !time_before(r.sec, r.nsec, ssec, snsec);
-  return ok;
-}
-
+#ifndef KLF_ABL
+#define KLF_ABL 0
+#endif
 #ifndef KLF_SCAN_OCC
 #define KLF_SCAN_OCC 4
 #endif
@@ -227,43 +235,49 @@ template <bool LIT>
 __global__ __launch_bounds__(kThreads, KLF_SCAN_OCC) void k_scan(RunArgs a, const uint32_t* __restrict__ tseg,
                                                                const SegDesc* __restrict__ segs) {
   constexpr int kWaves = kThreads / 64;
+  constexpr int kRows = kTile / 1024;  // 1 KiB rows: 16 B per lane per row
   __shared__ __attribute__((aligned(16))) uint8_t s_tile_all[kWaves][kTile + kHalo];
-  __shared__ uint32_t s_slot_all[LIT ? kWaves : 1][LIT ? kSlots : 1];
+  __shared__ uint32_t s_list_all[kWaves][kSlots];
   __shared__ __attribute__((aligned(16))) uint32_t s_lit[kMaxFusedLiteral / 4 + 1];  // literal, zero padded
+  __shared__ uint32_t s_month[16];
   // wv is wave-uniform; readfirstlane tells the compiler so (tile indices stay in SGPRs and
   // the descriptor reads stay scalar loads)
   const int t = threadIdx.x, lane = t & 63, wv = __builtin_amdgcn_readfirstlane(t >> 6);
   uint8_t* s_tile = s_tile_all[wv];
-  uint32_t* s_slot = s_slot_all[LIT ? wv : 0];
+  uint32_t* s_list = s_list_all[wv];
   uint32_t* err_flag = a.counters + 2;
-  if (LIT) {  // the literal lives in LDS for the whole kernel (the kernel's only block barrier)
-    for (uint32_t i = t; i < kMaxFusedLiteral / 4 + 1; i += kThreads) s_lit[i] = i < (a.lit_len + 3) / 4 ? a.lit_words[i] : 0u;
-    __syncthreads();
-  }
-  const uint8_t* lit = reinterpret_cast<const uint8_t*>(s_lit);
+  for (uint32_t i = t; i < kMaxFusedLiteral / 4 + 1; i += kThreads)
+    s_lit[i] = (LIT && i < (a.lit_len + 3) / 4) ? a.lit_words[i] : 0u;
+  if (t < 16) s_month[t] = c_month[t];
+  __syncthreads();  // the kernel's only block barrier
   const uint32_t nwaves = gridDim.x * kWaves;
-  // One wave-tile ahead in registers: the next tile's 4 KiB (+ halo) is in flight while
-  // this one is processed.  Rows of 1 KiB, 16 B per lane: fully coalesced.
-  static_assert(kTile == 64 * 16 * 4, "prefetch holds 4 uint4 per lane");
   auto tile_src = [&](uint32_t tl) -> const uint4* {
     const uint32_t ss = tseg[tl];
     const SegDesc d = segs[ss];
     return reinterpret_cast<const uint4*>(a.bytes + d.base + (uint64_t)(tl - d.tile0) * kTile);
   };
-  uint4 pf0, pf1, pf2, pf3, pfh = make_uint4(0, 0, 0, 0);  // named, not an array: stays in VGPRs
+  // the prefetch registers are named (an array here was put on the scratch stack)
+  static_assert(kRows == 8, "KLF_ROWS lists the 8 prefetch rows");
+#define KLF_ROWS(X) X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7)
+#define KLF_DECL(r) uint4 pf##r;
+  KLF_ROWS(KLF_DECL)
+#undef KLF_DECL
+#define KLF_LOAD(r) pf##r = gp[r * 64 + lane];
+#define KLF_STORE(r) l[r * 64 + lane] = pf##r;
+  uint4 pfh = make_uint4(0, 0, 0, 0);
   uint32_t tile = blockIdx.x * kWaves + wv;
   if (tile < a.ntiles) {
     const uint4* gp = tile_src(tile);
-    pf0 = gp[lane]; pf1 = gp[64 + lane]; pf2 = gp[128 + lane]; pf3 = gp[192 + lane];
+    KLF_ROWS(KLF_LOAD)
     if (lane < kHalo / 16) pfh = gp[kTile / 16 + lane];
   }
+  bool any_defer = false;
   for (; tile < a.ntiles; tile += nwaves) {
-    // descriptors are re-read (scalar, cached) rather than carried: fewer live SGPRs
     const uint32_t s = tseg[tile];
     const SegDesc sd = segs[s];
     const int64_t rel_lo = (int64_t)(tile - sd.tile0) * kTile;
     const int64_t seg_len = (int64_t)sd.len;
-    const int64_t tile_len = seg_len - rel_lo < kTile ? seg_len - rel_lo : kTile;
+    const int32_t tile_len = (int32_t)(seg_len - rel_lo < kTile ? seg_len - rel_lo : kTile);
     const bool first = rel_lo == 0;
     const bool last = rel_lo + kTile >= seg_len;
     const uint8_t* segp = a.bytes + sd.base;
@@ -271,58 +285,72 @@ __global__ __launch_bounds__(kThreads, KLF_SCAN_OCC) void k_scan(RunArgs a, cons
     // ---- stage this tile in the wave's LDS region, then start loading the next one ----
     {
       uint4* l = reinterpret_cast<uint4*>(s_tile);
-      l[lane] = pf0; l[64 + lane] = pf1; l[128 + lane] = pf2; l[192 + lane] = pf3;
+      KLF_ROWS(KLF_STORE)
       if (lane < kHalo / 16) l[kTile / 16 + lane] = pfh;
       const uint32_t nx = tile + nwaves;
       if (nx < a.ntiles) {
         const uint4* gp = tile_src(nx);
-        pf0 = gp[lane]; pf1 = gp[64 + lane]; pf2 = gp[128 + lane]; pf3 = gp[192 + lane];
+        KLF_ROWS(KLF_LOAD)
         if (lane < kHalo / 16) pfh = gp[kTile / 16 + lane];
       }
     }
     wave_lds_sync();
 
-    // ---- line-end events of my 64 bytes, literal anchor candidates ----
-    const int nvalid_s = (int)(tile_len - (int64_t)lane * kBytesPerThread);
-    const int nvalid = nvalid_s <= 0 ? 0 : (nvalid_s >= 64 ? 64 : nvalid_s);
-    const uint64_t vm = nvalid >= 64 ? ~0ull : ((1ull << nvalid) - 1);
-    const uint32_t toff0 = (uint32_t)lane * kBytesPerThread;  // my first byte, tile-relative
-    uint64_t nl, cand = 0;
+    // ---- any-tests over my 128 bytes: 8 chunks of 16 B, read rotated (chunk (v + lane/2)
+    // mod 8) so that every 16-lane group of a ds_read_b128 covers all 64 banks once ----
+    const uint32_t my0 = (uint32_t)lane * kLaneBytes;
+    const int nvalid_s = tile_len - (int)my0;
+    const int nvalid = nvalid_s <= 0 ? 0 : (nvalid_s >= kLaneBytes ? kLaneBytes : nvalid_s);
+    const uint32_t pat = a.lit_anchor_byte * 0x01010101u;
+    uint32_t nlc = 0, anc = 0;
     {
-      // The lane's 4 x 16 B are read starting at chunk rot = (lane >> 2) & 3: in plain
-      // order lanes t, t+12, t+20, t+24 of a ds_read_b128 group hit the same banks (4-way
-      // conflict); rotated, every 16-lane group covers all 64 banks once.  The masks are
-      // built in read order and rotated back once.
-      const uint32_t rot = ((uint32_t)lane >> 2) & 3u;
-      const uint4* l = reinterpret_cast<const uint4*>(s_tile + toff0);
-      uint32_t w[16];
+      const uint32_t rot = ((uint32_t)lane >> 1) & 7u;
 #pragma unroll
-      for (int v = 0; v < 4; ++v) {
-        const uint4 x = l[(v + rot) & 3u];
-        w[4 * v] = x.x; w[4 * v + 1] = x.y; w[4 * v + 2] = x.z; w[4 * v + 3] = x.w;
+      for (int v = 0; v < 8; ++v) {
+        const uint32_t c = ((uint32_t)v + rot) & 7u;
+        const uint4 x = *reinterpret_cast<const uint4*>(s_tile + my0 + 16u * c);
+        nlc |= any_eq16(x, 0x0A0A0A0Au) ? (1u << c) : 0u;
+        if (LIT && !(KLF_ABL & 2)) anc |= any_eq16(x, pat) ? (1u << c) : 0u;
       }
-      const uint32_t rs = 16u * rot;
-      auto unrot = [&](uint64_t m) -> uint64_t { return rs ? (m << rs) | (m >> (64u - rs)) : m; };
-      nl = unrot(eq_mask64_words(w, 0x0A0A0A0Au)) & vm;
-      // literal anchor (the literal's rarest byte, chosen on the host): a cheap any-test
-      // first, the exact mask only in lanes that see the byte at all
-      if (LIT) {
-        const uint32_t pat = a.lit_anchor_byte * 0x01010101u;
-        if (any_eq64_words(w, pat)) cand = unrot(eq_mask64_words(w, pat)) & vm;
+      if (nvalid < kLaneBytes) {
+        const uint32_t vm = (1u << ((nvalid + 15) >> 4)) - 1u;
+        nlc &= vm;
+        anc &= vm;
       }
     }
-    const bool has_end = last && nvalid > 0 && rel_lo + toff0 + nvalid == seg_len;
-    const int eb = nvalid - 1;
-    uint64_t ev = nl, starts = nl;
-    if (has_end) {
-      ev |= 1ull << eb;
-      starts &= ~(1ull << eb);
-      a.segout[s].frag = (nl >> eb) & 1 ? 0 : 1;
+    auto clip = [&](uint32_t e, uint32_t c) -> uint32_t {  // bytes of chunk c past the tile's end
+      const int nv = nvalid - 16 * (int)c;
+      return nv >= 16 ? e : (nv <= 0 ? 0u : (e & ((1u << nv) - 1u)));
+    };
+    // ---- exact line-end positions in the chunks that hit: a 128-bit event mask ----
+    uint32_t em[4] = {0u, 0u, 0u, 0u};
+    for (uint32_t m = nlc; m; m &= m - 1u) {
+      const uint32_t c = (uint32_t)__builtin_ctz(m);
+      const uint4 x = *reinterpret_cast<const uint4*>(s_tile + my0 + 16u * c);
+      const uint32_t e = clip(eq_mask16(x, 0x0A0A0A0Au), c) << ((c & 1u) * 16u);
+      const uint32_t q = c >> 1;
+      em[0] |= q == 0 ? e : 0u;
+      em[1] |= q == 1 ? e : 0u;
+      em[2] |= q == 2 ? e : 0u;
+      em[3] |= q == 3 ? e : 0u;
     }
-    const uint32_t cnt = (uint32_t)__popcll(ev);
+    // the stream's end is an event too (it closes the last line); it starts no line
+    uint32_t st[4] = {em[0], em[1], em[2], em[3]};
+    if (last && nvalid > 0 && (int)my0 + nvalid == tile_len) {
+      const uint32_t eb = (uint32_t)nvalid - 1u, q = eb >> 5, bit = 1u << (eb & 31u);
+      bool nl_at_end = false;
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if ((uint32_t)k == q) {
+          nl_at_end = (em[k] & bit) != 0u;
+          em[k] |= bit;
+          st[k] &= ~bit;
+        }
+      a.segout[s].frag = nl_at_end ? 0 : 1;
+    }
+    const uint32_t cnt = (uint32_t)(__popc(em[0]) + __popc(em[1]) + __popc(em[2]) + __popc(em[3]));
     const uint32_t incl = wave_incl_scan_add(cnt, lane);
     const uint32_t agg = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
-    const uint32_t texcl = incl - cnt;  // events of the tile before my bytes
     // Local line k = the line after the tile's k-th event (k = 0: the line open at the
     // tile start).  Lines starting here: k in [k0, k1), slot j = k - k0.
     const uint32_t k0 = first ? 0 : 1;
@@ -341,116 +369,201 @@ __global__ __launch_bounds__(kThreads, KLF_SCAN_OCC) void k_scan(RunArgs a, cons
     const bool pool_ok = !dense || (uint64_t)pool_base + nlines <= a.pool_cap;
     uint32_t* gslot = dense ? a.pool + pool_base : a.slots + (size_t)tile * kSlots;
 
-    // ---- parse every line starting in my bytes -> its slot ----
-    // Slots go to LDS when the literal pass needs them, else straight to their staging
-    // place in global memory (LDS for normal tiles, the pool for dense ones).
-    uint32_t n_parsed = 0, n_since = 0;
-    auto put = [&](uint32_t j, uint32_t off) {
-      bool so;
-      uint32_t plen = 0;
-      const bool ok = parse_line_at(s_tile, segp, rel_lo + off, rel_lo, seg_len, a.since_sec, a.since_nsec, &so, &plen);
-      const uint32_t slot = off | ((uint32_t)make_meta(ok, so, plen) << 16);
-      if (LIT && !dense) s_slot[j] = slot;
-      else if (pool_ok) gslot[j] = slot;
-      n_parsed += ok;
-      n_since += so;
-    };
-    if (first && lane == 0) put(0, 0);
-    for (uint64_t m = starts; m;) {
-      const int q = __ffsll((unsigned long long)m) - 1;
-      m &= m - 1;
-      put(texcl + (uint32_t)__popcll(ev & ((2ull << q) - 1)) - k0, toff0 + q + 1);
-    }
-
-    // ---- fused single-literal grep ----
-    // Anchor hits are rare (the literal's rarest byte); each names a candidate start
-    // p = anchor - lit_anchor.  A tile owns the starts inside it: anchors of this tile
-    // whose start lies in the previous tile are left to that tile, which scans its halo.
-    uint32_t carry = 0;  // 1 + furthest literal hit in the line carried in from before the tile
-    if (LIT) {
-      if (dense) __threadfence_block();  // pool slots are global: make them visible to the wave
-      wave_lds_sync();
-      const uint32_t m = a.lit_len, ka = a.lit_anchor;
-      uint64_t hcand = 0;  // halo anchors [kTile, kTile + ka) -> starts in this tile's tail
-      if (lane == 63 && ka > 0 && !last) {
-        for (uint32_t j = 0; j < ka; ++j) {
-          const int64_t q = rel_lo + kTile + j;
-          const uint8_t c = j < (uint32_t)kHalo ? s_tile[kTile + j] : (q < seg_len ? segp[q] : 0);
-          if (q < seg_len && c == a.lit_anchor_byte) hcand |= 1ull << j;
+    // The per-tile work on the line list, instantiated for the LDS list (normal tiles) and
+    // the global pool (dense tiles).
+    uint32_t n_parsed = 0, n_since = 0, n_defer = 0, carry = 0;
+    auto work = [&](uint32_t* list) __attribute__((always_inline)) {
+      // ---- line starts -> list[j] = start offset in the tile ----
+      if (first && lane == 0) list[0] = 0u;
+      {
+        uint32_t kk = incl - cnt;  // events before my bytes
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          for (uint32_t ev = em[q]; ev; ev &= ev - 1u) {
+            const uint32_t b = (uint32_t)__builtin_ctz(ev);
+            ++kk;
+            if ((st[q] >> b) & 1u) list[kk - k0] = my0 + 32u * q + b + 1u;
+          }
         }
       }
-      for (int pass = 0; pass < 2; ++pass) {
-        uint64_t cm = pass == 0 ? cand : hcand;
-        const int64_t abase = pass == 0 ? rel_lo + toff0 : rel_lo + kTile;
-        while (cm) {
-          const int b = __ffsll((unsigned long long)cm) - 1;
-          cm &= cm - 1;
-          const int64_t pos = abase + b - (int64_t)ka;  // candidate literal start
-          if (pos < rel_lo || pos >= rel_lo + tile_len || pos + (int64_t)m > seg_len) continue;
+      if (dense) __threadfence_block();
+      wave_lds_sync();
+      // ---- timestamp + since: one line per lane ----
+      for (uint32_t b0 = 0; b0 < nlines; b0 += 64) {
+        const uint32_t j = b0 + (uint32_t)lane;
+        if (j < nlines) {
+          const uint32_t off = list[j];
+          bool so = false, fast = false;
+#if KLF_ABL & 1
+          fast = true;
+          so = true;
+#else
+          if (rel_lo + (int64_t)off + 31 <= seg_len)
+            fast = parse_fast(s_tile, off, s_month, a.since_day, a.since_sod, a.since_nsec, so);
+#endif
+          list[j] = fast ? (off | ((uint32_t)make_meta(true, so, 31) << 16)) : (off | kSlotDefer);
+          n_parsed += fast ? 1u : 0u;
+          n_since += (fast && so) ? 1u : 0u;
+          n_defer += fast ? 0u : 1u;
+        }
+      }
+      // ---- fused single-literal grep ----
+      // Anchor hits (the literal's rarest byte) name candidate starts p = anchor - ka.  A
+      // tile owns the starts inside it: anchors whose start lies in the previous tile are
+      // left to that tile, which scans its halo.
+      if (LIT) {
+        if (dense) __threadfence_block();
+        wave_lds_sync();
+        const uint32_t m = a.lit_len, ka = a.lit_anchor;
+        auto check = [&](int32_t pos) __attribute__((always_inline)) {
+          if (pos < 0 || pos >= tile_len || rel_lo + pos + (int64_t)m > seg_len) return;
           bool eq = true;
-          {
-            const int64_t o0 = pos - rel_lo;
-            if (o0 + (int64_t)m + 4 <= kTile + kHalo) {  // 4 bytes per LDS read
-              const uint32_t* s32 = reinterpret_cast<const uint32_t*>(s_tile);
-              const uint32_t sh = (uint32_t)(o0 & 3) * 8;
-              uint32_t wi = (uint32_t)(o0 >> 2);
-              uint32_t prev = s32[wi];
-              for (uint32_t k = 0; k < m && eq; k += 4) {
-                const uint32_t nx = s32[++wi];
-                const uint32_t got = sh ? (uint32_t)((((uint64_t)nx << 32) | prev) >> sh) : prev;
-                prev = nx;
-                const uint32_t nb = m - k < 4 ? m - k : 4;
-                const uint32_t msk = nb == 4 ? 0xFFFFFFFFu : ((1u << (8 * nb)) - 1);
-                eq = ((got ^ s_lit[k >> 2]) & msk) == 0;
-              }
-            } else {
-              for (uint32_t k = 0; k < m && eq; ++k) {
-                const int64_t o = o0 + k;
-                const uint8_t c = o < kTile + kHalo ? s_tile[o] : segp[pos + k];
-                eq = c == lit[k];
-              }
+          if ((uint32_t)pos + m + 4 <= (uint32_t)(kTile + kHalo)) {  // 4 bytes per LDS read
+            const uint32_t* s32 = reinterpret_cast<const uint32_t*>(s_tile);
+            const uint32_t sh = (uint32_t)pos & 3u;
+            uint32_t wi = (uint32_t)pos >> 2;
+            uint32_t prev = s32[wi];
+            for (uint32_t k = 0; k < m && eq; k += 4) {
+              const uint32_t nx = s32[++wi];
+              const uint32_t got = __builtin_amdgcn_alignbyte(nx, prev, sh);
+              prev = nx;
+              const uint32_t nb = m - k < 4 ? m - k : 4;
+              const uint32_t msk = nb == 4 ? 0xFFFFFFFFu : ((1u << (8 * nb)) - 1);
+              eq = ((got ^ s_lit[k >> 2]) & msk) == 0;
+            }
+          } else {
+            const uint8_t* lit = reinterpret_cast<const uint8_t*>(s_lit);
+            for (uint32_t k = 0; k < m && eq; ++k) {
+              const uint32_t o = (uint32_t)pos + k;
+              const uint8_t c = o < (uint32_t)(kTile + kHalo) ? s_tile[o] : segp[rel_lo + o];
+              eq = c == lit[k];
             }
           }
-          if (!eq || !pool_ok) continue;
-          // the hit's line: last staged line start at or before pos (binary search)
-          const uint32_t off = (uint32_t)(pos - rel_lo);
-          auto slot_at = [&](int i) -> uint32_t { return dense ? gslot[i] : s_slot[i]; };
-          int lo = 0, hi = (int)nlines;  // count of slots with start <= off
+          if (!eq) return;
+          // the hit's line: last listed start at or before pos
+          int lo = 0, hi = (int)nlines;
           while (lo < hi) {
             const int mid = (lo + hi) >> 1;
-            if ((slot_at(mid) & 0x7FFFu) <= off) lo = mid + 1; else hi = mid;
+            if ((list[mid] & kSlotOff) <= (uint32_t)pos) lo = mid + 1; else hi = mid;
           }
-          if (lo > 0) {  // the line starts in this tile: its slot says where content starts
-            const uint32_t v = slot_at(lo - 1);
+          if (lo > 0) {  // the line starts in this tile: deferred lines are searched by k_fixup
+            const uint32_t v = list[lo - 1];
             const uint32_t mt = v >> 16;
-            if ((mt & Meta::kParsed) && off >= (v & 0x7FFFu) + (mt >> 2)) {
-              if (!dense) atomicOr(&s_slot[lo - 1], 0x8000u);
-              else atomicOr(&gslot[lo - 1], 0x8000u);
-            }
+            if (!(v & kSlotDefer) && (mt & Meta::kParsed) && (uint32_t)pos >= (v & kSlotOff) + (mt >> 2))
+              atomicOr(&list[lo - 1], kSlotHit);
           } else {  // carried in from an earlier tile: k_scatter decides (furthest hit wins)
-            carry = carry > off + 1 ? carry : off + 1;
+            carry = carry > (uint32_t)pos + 1u ? carry : (uint32_t)pos + 1u;
+          }
+        };
+        for (uint32_t cm = anc; cm; cm &= cm - 1u) {
+          const uint32_t c = (uint32_t)__builtin_ctz(cm);
+          const uint4 x = *reinterpret_cast<const uint4*>(s_tile + my0 + 16u * c);
+          for (uint32_t e = clip(eq_mask16(x, pat), c); e; e &= e - 1u)
+            check((int32_t)(my0 + 16u * c + (uint32_t)__builtin_ctz(e)) - (int32_t)ka);
+        }
+        if (lane == 63 && ka > 0 && !last) {  // halo anchors -> starts in this tile's tail
+          for (uint32_t jj = 0; jj < ka; ++jj) {
+            const int64_t q = rel_lo + kTile + jj;
+            if (q >= seg_len) break;
+            const uint8_t c = jj < (uint32_t)kHalo ? s_tile[kTile + jj] : segp[q];
+            if (c == a.lit_anchor_byte) check((int32_t)(kTile + jj) - (int32_t)ka);
           }
         }
+        carry = wave_max(carry);
       }
-      carry = wave_max(carry);
+      if (dense) __threadfence_block();
       wave_lds_sync();
-      if (!dense)
-        for (uint32_t j = lane; j < nlines; j += 64) gslot[j] = s_slot[j];
+    };
+    if (!dense) {
+      work(s_list);
+      for (uint32_t j = lane; j < nlines; j += 64) gslot[j] = s_list[j];
+    } else if (pool_ok) {
+      work(gslot);
     }
 
     // ---- per-tile record ----
-    const uint32_t pp = wave_sum(n_parsed), qq = wave_sum(n_since);
+    const uint32_t pp = wave_sum(n_parsed), qq = wave_sum(n_since), dd = wave_sum(n_defer);
+    any_defer |= dd != 0;
     if (lane == 0) {
       TileStat ts;
       ts.events = agg;
       ts.pool_base = dense ? pool_base : 0;
       ts.parsed = (uint16_t)pp;
       ts.since_ok = (uint16_t)qq;
-      ts.flags = (uint16_t)((dense ? 1u : 0u) | (carry ? 2u : 0u));
+      ts.flags = (uint16_t)((dense ? 1u : 0u) | (carry ? 2u : 0u) | (dd ? 4u : 0u));
       ts.carry_off = (uint16_t)carry;
       a.tstat[tile] = ts;
     }
     asm volatile("" ::: "memory");  // the next stage overwrites the LDS region read above
+  }
+  if (any_defer && lane == 0) a.counters[kCtrDefer] = 1u;
+}
+
+// ---- K1e: general parse of the deferred lines (non-canonical timestamp shapes) ---------
+// One wave per tile that reported deferred lines: Go time.Parse(RFC3339Nano) restated
+// (klf_ts.hpp) from global memory, since, and — with a fused literal — bytes.Contains over
+// the whole content of the line (its hits were not attributed by the scan).  The slot
+// keeps its defer bit (k_scatter then leaves carried hits of the line alone) and the
+// tile's parsed / since_ok counts are corrected before the tile-base scan.
+__device__ bool contains_bytes(const uint8_t* p, int64_t n, const uint8_t* lit, uint32_t m) {
+  if ((int64_t)m > n) return false;
+  for (int64_t i = 0; i + (int64_t)m <= n; ++i) {
+    if (p[i] != lit[0]) continue;
+    uint32_t k = 1;
+    while (k < m && p[i + k] == lit[k]) ++k;
+    if (k == m) return true;
+  }
+  return false;
+}
+
+__global__ __launch_bounds__(256) void k_fixup(RunArgs a) {
+  if (!a.counters[kCtrDefer] || a.counters[2]) return;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  for (uint32_t tile = blockIdx.x * 4 + wv; tile < a.ntiles; tile += gridDim.x * 4) {
+    TileStat ts = a.tstat[tile];
+    if (!(ts.flags & 4u)) continue;
+    const uint32_t s = a.tile_seg[tile];
+    const SegDesc sd = a.segs[s];
+    const int64_t rel_lo = (int64_t)(tile - sd.tile0) * kTile;
+    const int64_t seg_len = (int64_t)sd.len;
+    const bool first = rel_lo == 0, last = rel_lo + kTile >= seg_len;
+    const uint32_t k0 = first ? 0 : 1, k1 = last ? ts.events : ts.events + 1;
+    const uint32_t nlines = k1 > k0 ? k1 - k0 : 0;
+    uint32_t* list = (ts.flags & 1u) ? a.pool + ts.pool_base : a.slots + (size_t)tile * kSlots;
+    const uint8_t* segp = a.bytes + sd.base;
+    uint32_t dp = 0, dq = 0;
+    for (uint32_t j = lane; j < nlines; j += 64) {
+      const uint32_t sl = list[j];
+      if (!(sl & kSlotDefer)) continue;
+      const uint32_t off = sl & kSlotOff;
+      const int64_t p0 = rel_lo + off;
+      TsResult r;
+      uint32_t plen = 0;
+      const bool ok = parse_line_prefix(GlobalBytes{segp, p0, seg_len}, r, plen);
+      const bool so = ok && !time_before(r.sec, r.nsec, a.since_sec, a.since_nsec);
+      uint32_t hit = 0;
+      if (a.grep_mode == kGrepLit1 && ok) {
+        const int64_t cs = p0 + plen;
+        int64_t ce;
+        if (j + 1 < nlines) {
+          ce = rel_lo + (int64_t)(list[j + 1] & kSlotOff) - 1;  // the line's '\n'
+        } else {
+          ce = cs;
+          while (ce < seg_len && segp[ce] != '\n') ++ce;
+        }
+        if (ce > cs && contains_bytes(segp + cs, ce - cs, a.lit, a.lit_len)) hit = kSlotHit;
+      }
+      list[j] = off | kSlotDefer | hit | ((uint32_t)make_meta(ok, so, plen) << 16);
+      dp += ok ? 1u : 0u;
+      dq += so ? 1u : 0u;
+    }
+    dp = wave_sum(dp);
+    dq = wave_sum(dq);
+    if (lane == 0) {
+      ts.parsed = (uint16_t)(ts.parsed + dp);
+      ts.since_ok = (uint16_t)(ts.since_ok + dq);
+      a.tstat[tile] = ts;
+    }
   }
 }
 
@@ -602,7 +715,8 @@ __global__ __launch_bounds__(256) void k_scatter(RunArgs a) {
           const uint32_t* psrc = (pst.flags & 1u) ? a.pool + pst.pool_base : a.slots + (size_t)pt * kSlots;
           const uint32_t v = psrc[pn - 1];
           const uint32_t mt = v >> 16;
-          if (mt & Meta::kParsed) cs = prel + (int64_t)(v & 0x7FFFu) + (mt >> 2);
+          // a deferred line had its whole content searched by k_fixup
+          if ((mt & Meta::kParsed) && !(v & kSlotDefer)) cs = prel + (int64_t)(v & kSlotOff) + (mt >> 2);
           break;
         }
         if (cs >= 0 && rel_lo + (int64_t)ts.carry_off - 1 >= cs) atomicOr(&a.bits[base >> 5], 1u << (base & 31));
@@ -636,9 +750,9 @@ __global__ __launch_bounds__(256) void k_scatter(RunArgs a) {
       const uint32_t sl = src[j];
       const uint64_t li = e.base + j;
       if (li >= a.cap_lines) { atomicOr(err_flag, 1u); continue; }
-      a.line_off[li + e.seg] = e.rel_lo + (sl & 0x7FFFu);
+      a.line_off[li + e.seg] = e.rel_lo + (sl & kSlotOff);
       a.meta[li] = (uint16_t)(sl >> 16);
-      if (sl & 0x8000u) atomicOr(&a.bits[li >> 5], 1u << (li & 31));
+      if (sl & kSlotHit) atomicOr(&a.bits[li >> 5], 1u << (li & 31));
     }
     asm volatile("" ::: "memory");  // the next group rewrites the wave's LDS table
   }
@@ -1177,6 +1291,8 @@ hipError_t launch_pipeline(const RunArgs& a, hipStream_t st, hipEvent_t* ev, int
       hipLaunchKernelGGL(k_scan<true>, dim3(grid), dim3(kThreads), 0, st, a, a.tile_seg, a.segs);
     else
       hipLaunchKernelGGL(k_scan<false>, dim3(grid), dim3(kThreads), 0, st, a, a.tile_seg, a.segs);
+    KLF_TRY(hipGetLastError());
+    hipLaunchKernelGGL(k_fixup, dim3(num_cus * 2), dim3(256), 0, st, a);
     KLF_TRY(hipGetLastError());
     const uint32_t nb = (a.ntiles + kTilesPerScanBlock - 1) / kTilesPerScanBlock;
     hipLaunchKernelGGL(k_tsum, dim3(nb), dim3(256), 0, st, a);

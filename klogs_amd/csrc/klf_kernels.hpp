@@ -6,11 +6,11 @@
 
 namespace klf {
 
-// Work decomposition of the scan: a tile = one wave x 64 contiguous bytes per lane; a
+// Work decomposition of the scan: a tile = one wave x 128 contiguous bytes per lane; a
 // 256-thread workgroup runs 4 independent waves.
 constexpr int kThreads = 256;
-constexpr int kBytesPerThread = 64;
-constexpr int kTile = 64 * kBytesPerThread;  // 4 KiB wave-tile
+constexpr int kLaneBytes = 128;
+constexpr int kTile = 64 * kLaneBytes;        // 8 KiB wave-tile
 constexpr int kHalo = 64;                     // LDS bytes staged past the tile (timestamp window)
 constexpr int kMaxFusedLiteral = 256;
 constexpr uint64_t kSegAlign = 256;                 // segment base alignment in the batch buffer
@@ -21,14 +21,15 @@ constexpr uint32_t kNumCounters = 64;               // zeroed by k_init each run
 constexpr uint32_t kCtrPool = 4;                    // counters[4]: dense-tile pool allocator
 constexpr uint32_t kMatchChunk = 8192;              // lines per k_mcount partial (256 words)
 
-constexpr int kSlots = 132;  // staged line slots per tile (>= 4 KiB / 32-byte kubelet line + 1)
+constexpr int kSlots = kTile / 32 + 2;  // staged line slots per tile (>= 8 KiB / 32-byte kubelet line + 1)
 
 // Per-tile record of the scan (K1a), 16 B.
 struct TileStat {
   uint32_t events;     // line-end events in the tile
   uint32_t pool_base;  // dense tiles: first pool slot
   uint16_t parsed, since_ok;
-  uint16_t flags;      // bit0 dense (slots in the pool), bit1 literal hit in the carried-in line
+  uint16_t flags;      // bit0 dense (slots in the pool), bit1 literal hit in the carried-in line,
+                       // bit2 some line deferred to k_fixup
   uint16_t carry_off;  // 1 + offset of the furthest literal hit in the carried-in line (0 = none)
 };
 static_assert(sizeof(TileStat) == 16, "TileStat is one 16-B store");
@@ -88,6 +89,8 @@ struct RunArgs {
   // filter
   int64_t since_sec;
   int32_t since_nsec;
+  int32_t since_day;    // floor(since_sec / 86400)
+  uint32_t since_sod;   // since_sec - since_day * 86400
   int64_t tail;
   uint32_t grep_mode;
   const uint8_t* lit;  // kGrepLit1 literal (device)

@@ -41,7 +41,7 @@ def test_strerror_and_layout():
     assert E.lib().klf_strerror(E.KLF_EPATTERN).decode().startswith("pattern")
     base, total = E.layout([10, 0, 300, 1])
     assert list(base) == [0, 256, 256, 768]
-    assert total >= 1024 + 4096 + 64  # scan read-ahead: one 4 KiB wave-tile + halo past the end
+    assert total >= 1024 + 8192 + 64  # scan read-ahead: one 8 KiB wave-tile + halo past the end
 
 
 @pytest.mark.parametrize("s,want", [(b"2024-10-22T00:00:00.123Z", (1729555200, 123000000)),
