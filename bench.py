@@ -37,6 +37,17 @@ SINCE_S = 300  # --since 5m
 TAIL = 100
 
 
+def pmc_traffic():
+    """Per-launch HBM bytes of k_scan<literal> from the newest committed rocprofv3 --pmc
+    summary (profiles/<round>/traffic.json, written by scripts/pmc_traffic.py from
+    FETCH_SIZE / WRITE_SIZE passes over this same command), or None."""
+    files = sorted(ROOT.glob("profiles/r*/traffic.json"))
+    if not files:
+        return None, None
+    t = json.loads(files[-1].read_text())
+    return int(t["traffic_bytes"]), str(files[-1].relative_to(ROOT))
+
+
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
@@ -95,13 +106,14 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    scan_ms, total_ms = [], []
+    scan_ms, k1_ms, total_ms = [], [], []
     t0 = time.perf_counter()
     last = None
     for i in range(args.steps):
         r = step()
         tm = r.timing()
-        scan_ms.append(tm[0])
+        scan_ms.append(tm[6])  # the k_scan kernel alone
+        k1_ms.append(tm[0])    # K1 stage: k_scan + k_fixup + tile-base scan + scatter
         total_ms.append(tm[4])
         if i + 1 < args.steps:
             r.free()
@@ -119,11 +131,14 @@ def main():
     tot = last.totals()
     lines = tot["lines"]
     out_bytes = tot["out_bytes"]
-    # algorithmic bytes of the scan kernel per launch: input read once,
-    # the u64 line-offset index (L + 1 per stream) and the match bitmap written once
-    scan_alg = n + 8 * (lines + 1) + 4 * (lines // 32 + 1)
-    step_alg = scan_alg + out_bytes
+    # algorithmic bytes.  k_scan, the dominant kernel, reads every input
+    # byte once; its staged per-line slots are intermediate (not counted).  The K1 stage
+    # adds the u64 line-offset index (L + 1 per stream) and the match bitmap, written once.
+    scan_alg = n
+    k1_alg = n + 8 * (lines + 1) + 4 * (lines // 32 + 1)
+    step_alg = k1_alg + out_bytes
     scan_avg_s = float(np.mean(scan_ms)) / 1e3
+    k1_avg_s = float(np.mean(k1_ms)) / 1e3
     dev_avg_s = float(np.mean(total_ms)) / 1e3
     achieved = scan_alg / scan_avg_s / 1e9
 
@@ -155,6 +170,7 @@ def main():
                          f"(memchr line split, Go time.Parse restated, memmem grep, kubelet tail+since) "
                          f"on 1 host core, {cpu_t:.1f} s"}
 
+    traffic, traffic_src = pmc_traffic()
     value = world * n * args.steps / dt / 1e9
     res = {
         "metric": METRIC,
@@ -176,10 +192,13 @@ def main():
                    "parallelism": f"streams sharded, 1 stream per GPU x {world}"},
         "roofline": {"bound": "hbm", "kernel": "k_scan<literal>", "achieved": round(achieved, 1),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                     "traffic": None, "alg_bytes_per_launch": scan_alg,
+                     "traffic": traffic, "traffic_source": traffic_src, "alg_bytes_per_launch": scan_alg,
                      "avg_launch_ms": round(scan_avg_s * 1e3, 4)},
         "cpu_baseline": cpu,
         "extra": {"device_ms_per_step": round(dev_avg_s * 1e3, 4),
+                  "k1_stage": {"kernels": "k_scan+k_fixup+k_tsum+k_tbase+k_scatter", "alg_bytes": k1_alg,
+                               "avg_ms": round(k1_avg_s * 1e3, 4),
+                               "achieved_GBps": round(k1_alg / k1_avg_s / 1e9, 1)},
                   "step_alg_frac_of_peak": round(step_alg / dev_avg_s / 1e9 / HBM_PEAK_GBS, 4),
                   "stage_ms_last": [round(x, 4) for x in last.timing()],
                   "selected_lines": tot["selected"], "matched_lines": tot["matched"], "out_bytes": out_bytes,

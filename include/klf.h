@@ -140,7 +140,8 @@ int klf_result_device_out(klf_result* r, uint32_t stream_id, const uint8_t** d_o
 /* Per-stage device time of the run in ms, HIP events on the launch stream:
  * [0] scan kernel (newline + line index + timestamp + since + fused literal grep),
  * [1] general pattern matcher, [2] counts + tail + window prefix, [3] compaction,
- * [4] total device time, [5] workspace memsets.  n = number of entries written. */
+ * [4] total device time, [5] workspace memsets, [6] the k_scan kernel alone (part of
+ * [0]).  n = number of entries written. */
 int klf_result_timing(const klf_result* r, double* ms, uint32_t cap, uint32_t* n);
 /* Totals across streams. */
 int klf_result_totals(const klf_result* r, klf_counts* totals);

@@ -66,7 +66,7 @@ struct klf_engine {
   DevBuf d_batch, d_segs, d_tstat, d_slots, d_pool, d_tile_base, d_bsum, d_cstatus, d_counters, d_line_off,
       d_meta, d_bits, d_segout, d_wpre, d_out, d_mpart;
   uint64_t pool_cap = 1 << 20;
-  hipEvent_t ev[6] = {};
+  hipEvent_t ev[7] = {};
 };
 
 struct klf_result {
@@ -78,7 +78,7 @@ struct klf_result {
   std::vector<uint64_t> seg_base;    // per segment (device byte offset)
   bool has_bits = false;
   uint64_t total_lines = 0, total_out = 0;
-  double ms[6] = {0, 0, 0, 0, 0, 0};
+  double ms[7] = {0, 0, 0, 0, 0, 0, 0};
   // lazily filled host copies
   bool have_out = false, have_lines = false, have_bits = false;
   std::vector<uint8_t> out;
@@ -414,6 +414,7 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
     if (hipEventElapsedTime(&ms, e->ev[k + 1], e->ev[k + 2]) == hipSuccess) r->ms[k] = ms;
   if (hipEventElapsedTime(&ms, e->ev[0], e->ev[5]) == hipSuccess) r->ms[4] = ms;
   if (hipEventElapsedTime(&ms, e->ev[0], e->ev[1]) == hipSuccess) r->ms[5] = ms;
+  if (hipEventElapsedTime(&ms, e->ev[1], e->ev[6]) == hipSuccess) r->ms[6] = ms;
   r->total_lines = r->so[nsegs - 1].line_hi;
   for (auto& s : r->so) r->total_out = std::max(r->total_out, s.out_hi);
   *out = r;
@@ -554,7 +555,7 @@ extern "C" int klf_result_device_out(klf_result* r, uint32_t id, const uint8_t**
 
 extern "C" int klf_result_timing(const klf_result* r, double* ms, uint32_t cap, uint32_t* n) {
   if (!r || (cap && !ms)) return KLF_EINVAL;
-  const uint32_t k = std::min<uint32_t>(cap, 6);
+  const uint32_t k = std::min<uint32_t>(cap, 7);
   for (uint32_t i = 0; i < k; ++i) ms[i] = r->ms[i];
   if (n) *n = k;
   return KLF_OK;

@@ -1292,6 +1292,7 @@ hipError_t launch_pipeline(const RunArgs& a, hipStream_t st, hipEvent_t* ev, int
     else
       hipLaunchKernelGGL(k_scan<false>, dim3(grid), dim3(kThreads), 0, st, a, a.tile_seg, a.segs);
     KLF_TRY(hipGetLastError());
+    KLF_TRY(hipEventRecord(ev[6], st));  // k_scan alone (the roofline kernel)
     hipLaunchKernelGGL(k_fixup, dim3(num_cus * 2), dim3(256), 0, st, a);
     KLF_TRY(hipGetLastError());
     const uint32_t nb = (a.ntiles + kTilesPerScanBlock - 1) / kTilesPerScanBlock;

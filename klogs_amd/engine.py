@@ -224,9 +224,9 @@ class Result:
         return p.value or 0, off.value, n.value
 
     def timing(self) -> List[float]:
-        ms = (C.c_double * 6)()
+        ms = (C.c_double * 7)()
         k = C.c_uint32()
-        _check(_lib.klf_result_timing(self._p, ms, 6, C.byref(k)))
+        _check(_lib.klf_result_timing(self._p, ms, 7, C.byref(k)))
         return list(ms[: k.value])
 
     def totals(self) -> dict:
