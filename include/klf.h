@@ -157,6 +157,12 @@ int klf_parse_rfc3339nano(const uint8_t* s, size_t n, klf_time* out);
 int klf_debug_compile(const klf_pattern* pats, uint32_t n, uint32_t* mode, char* err, size_t err_cap);
 /* Runs the compiled tables (the exact recurrences the GPU matcher runs) on one content. */
 int klf_debug_match(const klf_pattern* pats, uint32_t n, const uint8_t* content, size_t len, int* match);
+/* The prefiltered path of general sets on one content, as the scan runs it: q-gram
+ * samples at positions = phase (mod stride), bitmap + bucket verification, literal hits
+ * final, regex factor hits -> Glushkov NFA.  info (nullable) = {prefilter on, q, stride,
+ * needles}; when the prefilter is off *match is the full matcher's answer. */
+int klf_debug_prefilter(const klf_pattern* pats, uint32_t n, const uint8_t* content, size_t len,
+                        uint32_t phase, int* match, uint32_t* info);
 
 #ifdef __cplusplus
 }

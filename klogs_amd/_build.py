@@ -65,7 +65,7 @@ def build_synth(force=False, quiet=True) -> Path:
     out = LIB / "libklf_synth.so"
     src = CSRC / "klf_synth.c"
     if force or _stale(out, [src]):
-        _run(["gcc", "-O2", "-shared", "-fPIC", "-pthread", src, "-o", out], quiet)
+        _run(["gcc", "-O2", "-shared", "-fPIC", "-pthread", src, "-o", out, "-lm"], quiet)
     return out
 
 

@@ -643,6 +643,30 @@ extern "C" int klf_debug_match(const klf_pattern* pats, uint32_t n, const uint8_
   return KLF_OK;
 }
 
+extern "C" int klf_debug_prefilter(const klf_pattern* pats, uint32_t n, const uint8_t* content, size_t len,
+                                   uint32_t phase, int* match, uint32_t* info) {
+  if ((n && !pats) || (len && !content) || !match) return KLF_EINVAL;
+  std::vector<std::vector<uint8_t>> ps;
+  std::vector<uint32_t> kinds;
+  for (uint32_t i = 0; i < n; ++i) {
+    ps.emplace_back(pats[i].bytes, pats[i].bytes + pats[i].len);
+    kinds.push_back(pats[i].kind);
+  }
+  klf::CompiledSet cs;
+  std::string err;
+  int code = KLF_OK;
+  if (!klf::compile_set(ps, kinds, cs, err, code)) return code;
+  if (info) {
+    info[0] = cs.qf_on ? 1u : 0u;
+    info[1] = cs.qf_q;
+    info[2] = cs.qf_stride;
+    info[3] = (uint32_t)cs.qf_nlen.size();
+  }
+  if (cs.mode != klf::CompiledSet::kGeneral || !cs.qf_on) return klf_debug_match(pats, n, content, len, match);
+  *match = klf::prefilter_match(cs, content, len, phase) ? 1 : 0;
+  return KLF_OK;
+}
+
 extern "C" int klf_debug_compile(const klf_pattern* pats, uint32_t n, uint32_t* mode, char* err, size_t err_cap) {
   if ((n && !pats) || !mode) return KLF_EINVAL;
   std::vector<std::vector<uint8_t>> ps;

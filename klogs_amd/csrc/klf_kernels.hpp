@@ -23,6 +23,16 @@ constexpr uint32_t kMatchChunk = 8192;              // lines per k_mcount partia
 
 constexpr int kSlots = kTile / 32 + 2;  // staged line slots per tile (>= 8 KiB / 32-byte kubelet line + 1)
 
+// q-gram prefilter of general pattern sets (klf_patterns.hpp CompiledSet::qf_*)
+constexpr int kQfBits = 17;                          // bitmap: 2^17 bits = 16 KiB of LDS
+constexpr uint32_t kQfWords = 1u << (kQfBits - 5);
+constexpr int kQfBucketBits = 12;                    // verification buckets: top hash bits
+constexpr uint32_t kQfMinNeedle = 3;                 // shorter literal / factor: no prefilter
+constexpr uint32_t kQfMaxFactor = 32;                // regex factors are cut to this length
+constexpr uint32_t kCtrQueue = 6;                    // counters[6]: NFA candidate queue length
+constexpr uint32_t kCtrQOver = 7;                    // counters[7]: queue overflow -> k_match
+__host__ __device__ inline uint32_t qf_hash(uint32_t g) { return (g * 0x9E3779B1u) >> (32 - kQfBits); }
+
 // Per-tile record of the scan (K1a), 16 B.
 struct TileStat {
   uint32_t events;     // line-end events in the tile
@@ -76,6 +86,15 @@ struct DevPatterns {  // device copies of CompiledSet tables (kGrepGeneral)
   const uint64_t* rx_end = nullptr;
   const uint32_t* rx_flags = nullptr;
   uint32_t rx_count = 0, rx_classes = 0;
+  // q-gram prefilter (qf_on): bitmap, buckets, needles
+  uint32_t qf_on = 0, qf_stride = 1, qf_fold = 0, qf_mask = ~0u;
+  const uint32_t* qf_bitmap = nullptr;
+  const uint32_t* qf_head = nullptr;
+  const uint32_t* qf_ent = nullptr;
+  const uint32_t* qf_noff = nullptr;
+  const uint32_t* qf_nlen = nullptr;
+  const uint32_t* qf_nmeta = nullptr;
+  const uint32_t* qf_nbytes = nullptr;
 };
 
 struct RunArgs {
@@ -118,6 +137,8 @@ struct RunArgs {
   uint64_t* wpre;       // [nsegs + 1] exclusive prefix of window sizes
   uint8_t* out;         // output bytes (capacity >= total input)
   uint32_t max_cblocks; // compaction block capacity
+  uint64_t* cand;       // [cand_cap] NFA candidates: batch byte offset | regex << 40
+  uint32_t cand_cap;
 };
 
 // Enqueues the whole pipeline on `stream`; `ev` (6 events) brackets the stages for

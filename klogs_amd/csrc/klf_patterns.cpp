@@ -9,6 +9,7 @@
 #include <queue>
 
 #include "../../include/klf.h"
+#include "klf_kernels.hpp"
 
 namespace klf {
 namespace {
@@ -574,7 +575,143 @@ uint64_t closure(uint64_t entered, uint64_t holds, const std::vector<uint64_t>& 
   return entered;
 }
 
+// ---- required factors (prefilter) ------------------------------------------------------
+// Per node: `exact` when the node matches exactly one string (a byte set of one byte or
+// one ASCII case pair counts as one byte; zero-width assertions are ""), and `req`, an
+// OR-set of strings one of which every match contains.  Case pairs make the factor loose
+// (stored OR 0x20).  The same analysis as RE2's prefilter, restricted to what the q-gram
+// scan can use: the best set maximises its shortest alternative.
+struct FInfo {
+  bool has_exact = false;
+  std::string exact;
+  bool exact_loose = false;
+  std::vector<std::string> req;
+  bool req_loose = false;
+};
+
+size_t req_score(const std::vector<std::string>& r) {
+  if (r.empty()) return 0;
+  size_t m = SIZE_MAX;
+  for (auto& s : r) m = std::min(m, s.size());
+  return m;
+}
+
+void consider(FInfo& f, const std::vector<std::string>& r, bool loose) {
+  const size_t a = req_score(r), b = req_score(f.req);
+  if (a > b || (a == b && a > 0 && r.size() < f.req.size())) {
+    f.req = r;
+    f.req_loose = loose;
+  }
+}
+
+std::vector<std::string> req_or_exact(const FInfo& f, bool& loose) {
+  if (f.has_exact) { loose = f.exact_loose; return {f.exact}; }
+  loose = f.req_loose;
+  return f.req;
+}
+
+FInfo factor_of(const std::vector<RNode>& pool, int x) {
+  const RNode& n = pool[x];
+  FInfo f;
+  switch (n.k) {
+    case RNode::kEmpty: case RNode::kBot: case RNode::kEot:
+      f.has_exact = true;
+      return f;
+    case RNode::kSet: {
+      const size_t c = n.set.count();
+      int b0 = -1, b1 = -1;
+      for (int b = 0; b < 256 && c <= 2; ++b)
+        if (n.set.test(b)) { if (b0 < 0) b0 = b; else b1 = b; }
+      if (c == 1) {
+        f.has_exact = true;
+        f.exact.assign(1, (char)b0);
+      } else if (c == 2 && b0 >= 'A' && b0 <= 'Z' && b1 == b0 + 32) {
+        f.has_exact = true;
+        f.exact.assign(1, (char)b1);
+        f.exact_loose = true;
+      }
+      return f;
+    }
+    case RNode::kCat: {
+      std::string run;
+      bool run_loose = false, all = true;
+      for (int k : n.kids) {
+        const FInfo kf = factor_of(pool, k);
+        consider(f, kf.req, kf.req_loose);
+        if (kf.has_exact) {
+          run += kf.exact;
+          run_loose |= kf.exact_loose;
+        } else {
+          if (!run.empty()) consider(f, {run}, run_loose);
+          run.clear();
+          run_loose = false;
+          all = false;
+        }
+      }
+      if (!run.empty()) consider(f, {run}, run_loose);
+      if (all) { f.has_exact = true; f.exact = run; f.exact_loose = run_loose; }
+      return f;
+    }
+    case RNode::kAlt: {
+      std::vector<std::string> u;
+      bool loose = false;
+      for (int k : n.kids) {
+        bool l = false;
+        const std::vector<std::string> r = req_or_exact(factor_of(pool, k), l);
+        if (req_score(r) == 0) return f;  // some branch needs no byte at all
+        loose |= l;
+        for (auto& s : r)
+          if (std::find(u.begin(), u.end(), s) == u.end()) u.push_back(s);
+      }
+      if (u.size() <= 16) { f.req = u; f.req_loose = loose; }
+      return f;
+    }
+    case RNode::kPlus: {
+      f.req = req_or_exact(factor_of(pool, n.kids[0]), f.req_loose);
+      return f;
+    }
+    case RNode::kRepeat: {
+      if (n.lo == 0) return f;
+      const FInfo kf = factor_of(pool, n.kids[0]);
+      if (kf.has_exact) {
+        std::string rep;
+        for (int r = 0; r < n.lo && rep.size() <= kQfMaxFactor; ++r) rep += kf.exact;
+        if (n.hi == n.lo) { f.has_exact = true; f.exact = rep; f.exact_loose = kf.exact_loose; }
+        else { f.req = {rep}; f.req_loose = kf.exact_loose; }
+        if (rep.empty()) f.req.clear();
+      } else {
+        f.req = kf.req;
+        f.req_loose = kf.req_loose;
+      }
+      return f;
+    }
+    default:  // kStar, kQuest: a match may skip the node
+      return f;
+  }
+}
+
 }  // namespace
+
+bool regex_factors(const uint8_t* pat, size_t n, std::vector<std::string>& alts, bool& loose) {
+  alts.clear();
+  loose = false;
+  Parser ps(pat, n);
+  const int root = ps.parse();
+  if (root < 0) return false;
+  alts = req_or_exact(factor_of(ps.pool, root), loose);
+  if (req_score(alts) == 0) { alts.clear(); return false; }
+  for (auto& s : alts) {
+    if (s.size() > kQfMaxFactor) s.resize(kQfMaxFactor);  // a substring of a factor is one too
+    if (loose)
+      for (auto& c : s) c = (char)((uint8_t)c | 0x20);
+  }
+  std::sort(alts.begin(), alts.end());
+  alts.erase(std::unique(alts.begin(), alts.end()), alts.end());
+  return true;
+}
+
+void build_prefilter(const std::vector<std::vector<uint8_t>>& lits, const std::vector<std::vector<std::string>>& rx_fac,
+                     const std::vector<bool>& rx_loose, CompiledSet& out);
 
 bool compile_regex(const uint8_t* pat, size_t n, GlushkovTables& out, std::string& err,
                    int& err_code) {
@@ -661,6 +798,8 @@ bool compile_set(const std::vector<std::vector<uint8_t>>& pats, const std::vecto
   }
   std::vector<std::vector<uint8_t>> lits;
   std::vector<GlushkovTables> rxs;
+  std::vector<std::vector<std::string>> rx_fac;  // required factors per regex (prefilter)
+  std::vector<bool> rx_loose;
   bool always = false;
   for (size_t k = 0; k < pats.size(); ++k) {
     if (kinds[k] == KLF_PAT_LITERAL) {
@@ -676,6 +815,11 @@ bool compile_set(const std::vector<std::vector<uint8_t>>& pats, const std::vecto
       }
       if (g.accept_at_start && g.accept_empty) { always = true; continue; }
       rxs.push_back(std::move(g));
+      std::vector<std::string> alts;
+      bool loose = false;
+      regex_factors(pats[k].data(), pats[k].size(), alts, loose);
+      rx_fac.push_back(alts);
+      rx_loose.push_back(loose);
     } else {
       err = "unknown pattern kind";
       err_code = KLF_EINVAL;
@@ -798,7 +942,120 @@ bool compile_set(const std::vector<std::vector<uint8_t>>& pats, const std::vecto
       out.rx_flags.push_back((rxs[r].accept_at_start ? 1u : 0u) | (rxs[r].accept_empty ? 2u : 0u));
     }
   }
+  build_prefilter(lits, rx_fac, rx_loose, out);
   return true;
+}
+
+// q-gram prefilter tables (CompiledSet::qf_*).  Off (k_match decides every line) when a
+// literal or some regex's best factor is shorter than kQfMinNeedle, or a regex can match
+// without any factor (e.g. `\d+`): those need a look at every line anyway.
+void build_prefilter(const std::vector<std::vector<uint8_t>>& lits, const std::vector<std::vector<std::string>>& rx_fac,
+                     const std::vector<bool>& rx_loose, CompiledSet& out) {
+  struct Needle {
+    std::string s;
+    uint32_t meta;
+  };
+  std::vector<Needle> nd;
+  for (auto& l : lits) nd.push_back({std::string(l.begin(), l.end()), 0u});
+  for (size_t r = 0; r < rx_fac.size(); ++r) {
+    if (rx_fac[r].empty()) { out.qf_why = "regex " + std::to_string(r) + " has no required literal factor"; return; }
+    for (auto& s : rx_fac[r]) nd.push_back({s, 0x80000000u | (rx_loose[r] ? 0x40000000u : 0u) | (uint32_t)r});
+  }
+  if (nd.empty()) { out.qf_why = "no needles"; return; }
+  if (nd.size() > (1u << 24)) { out.qf_why = "too many needles"; return; }
+  size_t minlen = SIZE_MAX;
+  bool loose = false;
+  for (auto& n : nd) {
+    minlen = std::min(minlen, n.s.size());
+    loose |= (n.meta & 0x40000000u) != 0;
+  }
+  if (minlen < kQfMinNeedle) { out.qf_why = "a needle is shorter than 3 bytes"; return; }
+  const uint32_t q = (uint32_t)std::min<size_t>(4, minlen);
+  const uint32_t span = (uint32_t)std::min<size_t>(4, minlen - q + 1);  // sampling gap allowed
+  const uint32_t S = span >= 4 ? 4 : (span >= 2 ? 2 : 1);
+  out.qf_q = q;
+  out.qf_stride = S;
+  out.qf_fold = loose ? 0x20202020u : 0u;
+  out.qf_mask = q == 4 ? ~0u : ((1u << (8 * q)) - 1u);
+  out.qf_bitmap.assign(kQfWords, 0u);
+  std::vector<std::vector<uint32_t>> buckets(1u << kQfBucketBits);
+  for (uint32_t i = 0; i < nd.size(); ++i) {
+    const std::string& s = nd[i].s;
+    for (uint32_t k = 0; k < S; ++k) {
+      uint32_t g = 0;
+      for (uint32_t b = 0; b < q; ++b) g |= (uint32_t)(uint8_t)s[k + b] << (8 * b);
+      const uint32_t h = qf_hash((g | out.qf_fold) & out.qf_mask);
+      out.qf_bitmap[h >> 5] |= 1u << (h & 31);
+      buckets[h >> (kQfBits - kQfBucketBits)].push_back(i << 2 | k);
+    }
+  }
+  out.qf_head.assign((1u << kQfBucketBits) + 1, 0u);
+  for (uint32_t b = 0; b < buckets.size(); ++b) {
+    out.qf_head[b] = (uint32_t)out.qf_ent.size();
+    out.qf_ent.insert(out.qf_ent.end(), buckets[b].begin(), buckets[b].end());
+  }
+  out.qf_head[buckets.size()] = (uint32_t)out.qf_ent.size();
+  for (auto& n : nd) {
+    out.qf_noff.push_back((uint32_t)out.qf_nbytes.size());
+    out.qf_nlen.push_back((uint32_t)n.s.size());
+    out.qf_nmeta.push_back(n.meta);
+    for (size_t b = 0; b < n.s.size(); b += 4) {
+      uint32_t w = 0;
+      for (size_t j = 0; j < 4 && b + j < n.s.size(); ++j) w |= (uint32_t)(uint8_t)n.s[b + j] << (8 * j);
+      out.qf_nbytes.push_back(w);
+    }
+  }
+  out.qf_on = true;
+}
+
+namespace {
+// needle `i` at s[x ..): exact, or OR 0x20 per byte when loose
+bool needle_at(const CompiledSet& cs, uint32_t i, const uint8_t* s, size_t n, int64_t x) {
+  const uint32_t m = cs.qf_nlen[i];
+  if (x < 0 || (uint64_t)x + m > n) return false;
+  const uint8_t* nb = reinterpret_cast<const uint8_t*>(cs.qf_nbytes.data() + cs.qf_noff[i]);
+  const uint8_t lm = (cs.qf_nmeta[i] & 0x40000000u) ? 0x20 : 0;
+  for (uint32_t k = 0; k < m; ++k)
+    if ((uint8_t)(s[x + k] | lm) != nb[k]) return false;
+  return true;
+}
+}  // namespace
+
+bool prefilter_match(const CompiledSet& cs, const uint8_t* s, size_t n, uint32_t phase) {
+  // Any window of S consecutive positions holds a sample, and every needle is at least
+  // q + S - 1 long, so each occurrence spans a sample with its gram inside the needle.
+  std::vector<uint8_t> cand(cs.rx_count, 0);
+  const uint32_t S = cs.qf_stride;
+  for (size_t p = phase % S; p < n; p += S) {
+    uint32_t g = 0;
+    for (uint32_t b = 0; b < 4; ++b) g |= (uint32_t)(p + b < n ? s[p + b] : 0) << (8 * b);
+    const uint32_t h = qf_hash((g | cs.qf_fold) & cs.qf_mask);
+    if (!((cs.qf_bitmap[h >> 5] >> (h & 31)) & 1u)) continue;
+    const uint32_t b = h >> (kQfBits - kQfBucketBits);
+    for (uint32_t e = cs.qf_head[b]; e < cs.qf_head[b + 1]; ++e) {
+      const uint32_t i = cs.qf_ent[e] >> 2;
+      const int64_t x = (int64_t)p - (int64_t)(cs.qf_ent[e] & 3u);
+      if (!needle_at(cs, i, s, n, x)) continue;
+      if (!(cs.qf_nmeta[i] & 0x80000000u)) return true;  // literal: final
+      cand[cs.qf_nmeta[i] & 0xFFFFFFu] = 1;
+    }
+  }
+  for (uint32_t r = 0; r < cs.rx_count; ++r) {
+    if (!cand[r]) continue;
+    const uint32_t fl = cs.rx_flags[r];
+    if (n == 0) { if (fl & 2u) return true; continue; }
+    if (fl & 1u) return true;
+    uint64_t d = cs.rx_init0[r];
+    for (size_t i = 0; i < n; ++i) {
+      const uint64_t c = d & cs.rx_b[(size_t)r * cs.rx_classes + cs.rx_class[s[i]]];
+      if (c & cs.rx_last[r]) return true;
+      uint64_t nd = cs.rx_first[r];
+      for (uint64_t m = c; m; m &= m - 1) nd |= cs.rx_follow[(size_t)r * 64 + __builtin_ctzll(m)];
+      d = nd;
+    }
+    if (d & cs.rx_end[r]) return true;
+  }
+  return false;
 }
 
 }  // namespace klf

@@ -60,7 +60,36 @@ struct CompiledSet {
   std::vector<uint64_t> rx_follow;    // [rx_count * 64]
   std::vector<uint64_t> rx_first, rx_last, rx_init0, rx_end;  // [rx_count]
   std::vector<uint32_t> rx_flags;     // bit0 accept_at_start, bit1 accept_empty
+
+  // kGeneral: q-gram prefilter fused into the scan (qf_on).  Needles = the literals
+  // (final: a verified hit is a match) and one required factor set per regex (a verified
+  // hit makes the line a candidate the Glushkov NFA then decides).  Sampled positions
+  // p = 0 mod qf_stride of every 8 KiB tile probe a hashed bitmap of the needles' q-grams
+  // at offsets 0..stride-1; bitmap hits are verified against the needles of the bucket.
+  bool qf_on = false;
+  uint32_t qf_q = 4;         // gram length (bytes)
+  uint32_t qf_stride = 1;    // 1, 2 or 4
+  uint32_t qf_fold = 0;      // 0x20202020 when some needle compares case-insensitively
+  uint32_t qf_mask = ~0u;    // gram bytes (q < 4: low q bytes)
+  std::vector<uint32_t> qf_bitmap;   // [1 << (kQfBits - 5)]
+  std::vector<uint32_t> qf_head;     // [(1 << kQfBucketBits) + 1] bucket -> first entry
+  std::vector<uint32_t> qf_ent;      // needle << 2 | offset of the gram in the needle
+  std::vector<uint32_t> qf_noff;     // [needles] dword offset of the needle's bytes
+  std::vector<uint32_t> qf_nlen;     // [needles]
+  std::vector<uint32_t> qf_nmeta;    // [needles] bit31 regex factor, bit30 loose compare,
+                                     // low 24 bits regex index
+  std::vector<uint32_t> qf_nbytes;   // needle bytes, each padded to whole dwords
+  std::string qf_why;                // why the prefilter is off (diagnostics)
 };
+
+// Required literal factors of one regex (Go syntax, SPEC.md S5): every match contains
+// one of `alts`; `loose` when some byte is an ASCII case pair ((?i)), then every byte is
+// stored OR 0x20 and compared that way.  False when the regex has no factor.
+bool regex_factors(const uint8_t* pat, size_t n, std::vector<std::string>& alts, bool& loose);
+
+// Host emulation of the prefiltered matcher on one content (tests): sampled positions
+// p = phase mod stride, bitmap probe, bucket verification, NFA on factor hits.
+bool prefilter_match(const CompiledSet& cs, const uint8_t* s, size_t n, uint32_t phase);
 
 // Parses one Go-syntax regex (SPEC.md S5) and builds its Glushkov tables.
 // Returns false with `err` set for syntax outside the subset or > 64 positions.

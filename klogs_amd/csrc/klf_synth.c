@@ -17,14 +17,19 @@
  * Timestamps of TEXT/JSON are monotonic: t0 + i * step, step = span / estimated lines,
  * fixed-width "YYYY-MM-DDTHH:MM:SS.nnnnnnnnnZ ".
  */
+#include <math.h>
 #include <pthread.h>
 #include <stdint.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
 #define KS_TEXT 0
 #define KS_JSON 1
 #define KS_ADVERSARIAL 2
+#define KS_MIXED 3    /* C4: mixed-length word lines, 16 B..8 KiB (lognormal), literal hits   */
+#define KS_LONGJSON 4 /* C5: long JSON lines, 1..32 KiB (log-uniform), regex events + misses */
+#define KS_C4_LITS 1024
 
 static inline uint64_t mix(uint64_t x) {
   x += 0x9E3779B97F4A7C15ull;
@@ -93,9 +98,54 @@ static inline uint64_t line_key(const gen_cfg* g, uint64_t i) {
   return mix(mix(g->seed ^ (0x5851F42D4C957F2Dull * (g->stream + 1ull))) + i);
 }
 
+/* ---- C4 literal vocabulary / C5 regex set ----------------------------------------- */
+static const char* const kLitPrefix[8] = {"ERR_", "E", "TX-", "REQ", "ORA-", "HTTP_", "SIG", "KEY"};
+
+/* Literal i of the C4 vocabulary: 6..24 bytes of [A-Z0-9_-] (log text is lower case). */
+uint32_t ks_c4_literal(uint32_t i, uint8_t* out) {
+  static const char al[] = "ABCDEFGHIJKLMNOPQRSTUVWXYZ0123456789";
+  uint64_t r = mix(0xC4C4C4C4ull ^ ((uint64_t)i * 0x9E3779B97F4A7C15ull));
+  const uint32_t len = 6 + (uint32_t)(r % 19);
+  const char* pre = kLitPrefix[(r >> 8) & 7];
+  uint32_t o = 0;
+  for (; pre[o] && o < len; ++o) out[o] = (uint8_t)pre[o];
+  while (o < len) { r = mix(r); out[o++] = (uint8_t)al[r % 36]; }
+  return len;
+}
+
+/* C5: 8 families x 8 variants (regex index = family * 8 + variant): the regex, a snippet
+ * it matches, and a near miss that holds the regex's required factor but no match. */
+static const char* const kC5[8][3] = {
+    {"(?i)panic: \\w+ error in mod%u", "PANIC: runtime error in mod%u", "retry error in mod%u"},
+    {"user%u_id=u\\d{4,6} (login|logout)", "user%u_id=u12345 logout", "user%u_id=u12 login"},
+    {"status=5\\d\\d path=/api/v%u/\\w+", "status=503 path=/api/v%u/orders", "status=200 path=/api/v%u/orders"},
+    {"tx-[0-9a-f]{8}-commit%u", "tx-0a1b2c3d-commit%u", "tx-0a1b-commit%u"},
+    {"(?i)oom(killed|_score_adj) for pid%u=\\d+", "OOMKilled for pid%u=42", "oomfoo for pid%u=42"},
+    {"shard%u deadline exceeded after \\d+\\.\\d+s", "shard%u deadline exceeded after 1.25s",
+     "shard%u deadline exceeded after xs"},
+    {"GET /v%u/items/\\d+ (4\\d\\d|5\\d\\d)", "GET /v%u/items/77 404", "GET /v%u/items/77 200"},
+    {"(?i)conn(ection)? reset by peer%u", "Connection reset by peer%u", "pipe reset by peer%u"},
+};
+
+/* which: 0 regex, 1 matching snippet, 2 near miss.  Returns the length (no NUL). */
+uint32_t ks_c5_pattern(uint32_t r, int which, char* out, uint32_t cap) {
+  const int n = snprintf(out, cap, kC5[(r >> 3) & 7][which % 3], r & 7u);
+  return n < 0 ? 0 : (uint32_t)n;
+}
+
 /* content length (without prefix and '\n') */
 static uint32_t content_len(const gen_cfg* g, uint64_t k) {
   if (g->kind == KS_TEXT) return kLogn[k & 255];
+  if (g->kind == KS_MIXED) {  /* lognormal-ish: median 180 B, clamped to 16 B .. 8 KiB */
+    const uint64_t m = mix(k ^ 0x4D49ull);
+    const double u = ((m & 0xFFFF) + ((m >> 16) & 0xFFFF) + ((m >> 32) & 0xFFFF) + ((m >> 48) & 0xFFFF)) / 65536.0;
+    const double z = (u - 2.0) * 1.7320508075688772;
+    double l = 180.0 * exp(1.1 * z);
+    l = l < 16 ? 16 : (l > 8192 ? 8192 : l);
+    return (uint32_t)l;
+  }
+  if (g->kind == KS_LONGJSON) /* log-uniform 1 KiB .. 32 KiB */
+    return (uint32_t)(1024.0 * exp2(5.0 * (double)(mix(k ^ 0x10C6ull) >> 11) / 9007199254740992.0));
   return 200 + (uint32_t)((k >> 8) % 400); /* JSON */
 }
 
@@ -120,6 +170,13 @@ static void write_line(const gen_cfg* g, uint64_t i, uint64_t k, uint8_t* p, uin
   uint8_t* c = p + 31;
   if (g->kind == KS_TEXT) {
     fill_words(c, clen, k);
+  } else if (g->kind == KS_MIXED) {
+    fill_words(c, clen, k);
+    if (((k >> 32) % 1000) < g->needle_permille) {
+      uint8_t lit[32];
+      const uint32_t ll = ks_c4_literal((uint32_t)((k >> 42) % KS_C4_LITS), lit);
+      if (ll + 2 <= clen) memcpy(c + 1 + (uint32_t)((k >> 20) % (clen - ll - 1)), lit, ll);
+    }
   } else {
     /* {"ts":"<24>","level":"<L>","msg":"<...>","trace":"<32 hex>"} */
     static const char hex[] = "0123456789abcdef";
@@ -139,7 +196,19 @@ static void write_line(const gen_cfg* g, uint64_t i, uint64_t k, uint8_t* p, uin
     const uint32_t tail_len = 11 + 32 + 2; /* ","trace":" + 32 hex + "} */
     const uint32_t msg_len = clen - o - tail_len;
     fill_words(c + o, msg_len, k ^ 0xABCDEFull);
-    if (g->needle_len && g->needle_len + 2 <= msg_len && ((k >> 32) % 1000) < g->needle_permille) {
+    if (g->kind == KS_LONGJSON) {  /* regex events (permille) and near misses (2 x permille) */
+      const uint32_t ev = (uint32_t)((k >> 32) % 1000);
+      if (ev < 3 * g->needle_permille) {
+        char snip[96];
+        const uint32_t sl = ks_c5_pattern((uint32_t)((k >> 42) % 64), ev < g->needle_permille ? 1 : 2, snip, sizeof snip);
+        if (sl + 4 <= msg_len) {
+          const uint32_t at = 1 + (uint32_t)((k >> 50) % (msg_len - sl - 2));
+          c[o + at - 1] = ' ';
+          memcpy(c + o + at, snip, sl);
+          c[o + at + sl] = ' ';
+        }
+      }
+    } else if (g->needle_len && g->needle_len + 2 <= msg_len && ((k >> 32) % 1000) < g->needle_permille) {
       const uint32_t at = (uint32_t)((k >> 42) % (msg_len - g->needle_len - 1)) + 1;
       memcpy(c + o + at, g->needle, g->needle_len);
     }
@@ -262,7 +331,7 @@ uint64_t ks_generate(uint32_t kind, uint64_t seed, uint32_t stream, uint64_t tar
     if (drop_final_nl && s.n && (!buf || s.n <= cap) && (!buf || buf[s.n - 1] == '\n')) s.n -= 1;
     return s.n;
   }
-  const uint64_t avg = kind == KS_TEXT ? 154 : 432;
+  const uint64_t avg = kind == KS_TEXT ? 154 : kind == KS_MIXED ? 350 : kind == KS_LONGJSON ? 9500 : 432;
   const uint64_t est = target / avg + 1;
   g.step_ns = (span_sec * 1000000000ll) / (int64_t)est;
   /* pass 1: line lengths until the target is reached */

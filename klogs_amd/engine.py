@@ -89,6 +89,8 @@ SIGNATURES = {
                                     C.c_size_t]),
     "klf_debug_match": (C.c_int, [C.POINTER(_Pattern), C.c_uint32, C.c_void_p, C.c_size_t,
                                   C.POINTER(C.c_int)]),
+    "klf_debug_prefilter": (C.c_int, [C.POINTER(_Pattern), C.c_uint32, C.c_void_p, C.c_size_t, C.c_uint32,
+                                      C.POINTER(C.c_int), C.POINTER(C.c_uint32)]),
 }
 
 
@@ -178,6 +180,16 @@ def debug_match(content: bytes, grep=(), match=()) -> bool:
     buf = C.create_string_buffer(content, len(content) or 1)
     _check(_lib.klf_debug_match(arr, n, buf, len(content), C.byref(m)))
     return bool(m.value)
+
+
+def debug_prefilter(content: bytes, grep=(), match=(), phase: int = 0):
+    """(match, {on, q, stride, needles}) of the prefiltered general matcher on the host."""
+    arr, n, keep = _patterns(grep, match)
+    m = C.c_int()
+    info = (C.c_uint32 * 4)()
+    buf = C.create_string_buffer(content, len(content) or 1)
+    _check(_lib.klf_debug_prefilter(arr, n, buf, len(content), phase, C.byref(m), info))
+    return bool(m.value), dict(on=bool(info[0]), q=info[1], stride=info[2], needles=info[3])
 
 
 @dataclass

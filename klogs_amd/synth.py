@@ -7,7 +7,7 @@ from pathlib import Path
 
 import numpy as np
 
-TEXT, JSON, ADVERSARIAL = 0, 1, 2
+TEXT, JSON, ADVERSARIAL, MIXED, LONGJSON = 0, 1, 2, 3, 4
 T0 = 1729555200  # 2024-10-22T00:00:00Z (the reference snapshot date)
 SPAN = 3600      # each stream spans 60 minutes
 NEEDLE = b"ERR_CONN_RESET"
@@ -16,6 +16,36 @@ _lib = C.CDLL(str(Path(__file__).resolve().parent / "_lib" / "libklf_synth.so"))
 _lib.ks_generate.restype = C.c_uint64
 _lib.ks_generate.argtypes = [C.c_uint32, C.c_uint64, C.c_uint32, C.c_uint64, C.c_int64, C.c_int64,
                              C.c_char_p, C.c_uint32, C.c_uint32, C.c_int, C.c_void_p, C.c_uint64, C.c_int]
+
+
+_lib.ks_c4_literal.restype = C.c_uint32
+_lib.ks_c4_literal.argtypes = [C.c_uint32, C.c_char_p]
+_lib.ks_c5_pattern.restype = C.c_uint32
+_lib.ks_c5_pattern.argtypes = [C.c_uint32, C.c_int, C.c_char_p, C.c_uint32]
+
+
+def c4_literals(n: int = 1024):
+    """The C4 --grep set: the first n distinct literals of the generator's vocabulary
+    (MIXED streams embed literals 0..1023)."""
+    out, seen, i = [], set(), 0
+    buf = C.create_string_buffer(32)
+    while len(out) < n:
+        b = buf.raw[:_lib.ks_c4_literal(i, buf)]
+        if b not in seen:
+            seen.add(b)
+            out.append(b)
+        i += 1
+    return out
+
+
+def c5_pattern(r: int, which: int) -> bytes:
+    buf = C.create_string_buffer(128)
+    return buf.raw[:_lib.ks_c5_pattern(r, which, buf, 128)]
+
+
+def c5_regexes():
+    """The C5 --match set: 64 RE2-subset regexes (8 families x 8 variants)."""
+    return [c5_pattern(r, 0) for r in range(64)]
 
 
 def _threads():

@@ -1,0 +1,120 @@
+"""The q-gram prefilter of general pattern sets (klf_patterns.cpp build_prefilter /
+regex_factors) on the host: the prefiltered decision (samples at every phase of the
+stride, bitmap, bucket verification, literal hits final, regex factor hits -> Glushkov
+NFA) must equal the full matcher's and Python re / bytes.Contains on every content."""
+import random
+
+import pytest
+
+import klf_oracle as po
+from klogs_amd import engine as E
+from klogs_amd import synth
+
+ALPH = b"abcdeERO0123456789_-= .:\"{}tiumo"
+
+
+def _text(rng, n):
+    return bytes(rng.choice(ALPH) for _ in range(n))
+
+
+def _want(s, grep, match):
+    return any(g in s for g in grep) or any(po.Pattern("regex", m).matches(s) for m in match)
+
+
+def _check(grep, match, contents):
+    info = None
+    for s in contents:
+        want = _want(s, grep, match)
+        assert E.debug_match(s, grep=grep, match=match) == want, s
+        for ph in range(4):
+            got, info = E.debug_prefilter(s, grep=grep, match=match, phase=ph)
+            assert got == want, (s, ph, info)
+    return info
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_literal_sets(seed):
+    rng = random.Random(seed)
+    lits = [_text(rng, rng.randint(3, 12)) for _ in range(rng.randint(2, 60))]
+    contents = []
+    for _ in range(200):
+        s = _text(rng, rng.randint(0, 60))
+        if rng.random() < 0.3:
+            lit = rng.choice(lits)
+            k = rng.randint(0, len(s))
+            s = s[:k] + lit + s[k:]
+        contents.append(s)
+    info = _check(lits, [], contents)
+    assert info["on"] and info["needles"] == len(set(lits))
+
+
+RX_SETS = [
+    [rb"timeout after \d+ms", rb"(?i)panic: [a-z]+", rb"status=(500|502|503)"],
+    [rb"user_id=u\d{4,6}", rb"(?i)OOM(killed|_score)", rb"tx-[0-9a-f]{4}-done"],
+    [rb"abc(de|fg)*hij", rb"^start.*end$", rb"x{3}y+"],
+    [rb"(?i)error: (disk|net)\w* full", rb"\Qa.b*c\E", rb"abc.def"],
+]
+
+
+@pytest.mark.parametrize("idx", range(len(RX_SETS)))
+def test_regex_sets(idx):
+    rng = random.Random(100 + idx)
+    match = RX_SETS[idx]
+    inserts = [b"timeout after 123ms", b"timeout after ms", b"PANIC: xyz", b"panic: 1", b"status=502",
+               b"user_id=u12345", b"user_id=u12", b"oomKILLED", b"tx-0a9f-done", b"abcdefghij", b"abchij",
+               b"start mid end", b"xxxyy", b"ERROR: disk0 full", b"a.b*c", b"abcXdef", b"Error: Network full"]
+    contents = []
+    for _ in range(300):
+        s = _text(rng, rng.randint(0, 40))
+        if rng.random() < 0.5:
+            k = rng.randint(0, len(s))
+            s = s[:k] + rng.choice(inserts) + s[k:]
+        contents.append(s)
+    info = _check([], match, contents + inserts)
+    assert info["on"], info
+
+
+def test_mixed_literals_and_regexes_prefiltered():
+    rng = random.Random(7)
+    grep = [b"ERR_CONN_RESET", b"segfault"]
+    match = [rb"user=\w+ took \d{3,}ms", rb"(?i)deadline exceeded"]
+    extra = [b"user=bob took 1234ms", b"user=bob took 12ms", b"DEADLINE Exceeded", b"ERR_CONN_RESET", b"segfault"]
+    contents = [_text(rng, rng.randint(0, 50)) + (rng.choice(extra) if rng.random() < 0.5 else b"")
+                for _ in range(300)]
+    info = _check(grep, match, contents)
+    assert info["on"] and info["stride"] >= 2
+
+
+@pytest.mark.parametrize("grep,match,why", [
+    ([b"ab", b"xyz"], [], "short literal"),
+    ([], [rb"\d+"], "regex without a factor"),
+    ([], [rb"a.b"], "1-byte factors"),
+])
+def test_prefilter_off_falls_back(grep, match, why):
+    _, info = E.debug_prefilter(b"x", grep=grep, match=match)
+    assert not info["on"], why
+    rng = random.Random(1)
+    _check(grep, match, [_text(rng, rng.randint(0, 20)) for _ in range(100)])
+
+
+@pytest.mark.parametrize("grep,match,q,stride", [
+    ([b"abcdefg", b"0123456789"], [], 4, 4),
+    ([b"abcdef", b"0123456789"], [], 4, 2),
+    ([b"abcd", b"0123456789"], [], 4, 1),
+    ([b"abc", b"0123456789"], [], 3, 1),
+    ([], [rb"(?i)timeout"], 4, 4),
+])
+def test_gram_and_stride_choice(grep, match, q, stride):
+    _, info = E.debug_prefilter(b"", grep=grep, match=match)
+    assert info["on"] and (info["q"], info["stride"]) == (q, stride), info
+
+
+def test_c4_c5_sets_are_prefiltered():
+    lits = synth.c4_literals(1024)
+    assert len(lits) == 1024 and min(map(len, lits)) >= 6 and max(map(len, lits)) <= 24
+    _, info = E.debug_prefilter(b"", grep=lits)
+    assert info["on"] and info["stride"] >= 2, info
+    rx = synth.c5_regexes()
+    assert len(rx) == 64
+    _, info = E.debug_prefilter(b"", match=rx)
+    assert info["on"], info
