@@ -59,6 +59,8 @@ struct klf_engine {
   std::vector<std::vector<uint8_t>> staged;
   // device pattern tables
   DevBuf d_lit, d_ac_class, d_ac_next, d_ac_accept, d_rx_class, d_rx_b, d_rx_follow, d_rx_vec, d_rx_flags;
+  DevBuf d_qf_bitmap, d_qf_head, d_qf_ent, d_qf_noff, d_qf_nlen, d_qf_nmeta, d_qf_nbytes, d_cand;
+  uint32_t cand_cap = 1u << 22;  // NFA candidate queue (32 MiB); overflow -> k_match
   klf::DevPatterns dpats;
   // workspace
   std::vector<SegDesc> last_segs;  // tile_seg cache key
@@ -210,7 +212,32 @@ extern "C" int klf_open(const klf_config* cfg, klf_engine** out) {
       P.rx_count = cs.rx_count;
       P.rx_classes = cs.rx_classes;
     }
+    if (cs.qf_on) {
+      if ((h = upload(e->d_qf_bitmap, cs.qf_bitmap, st)) != hipSuccess ||
+          (h = upload(e->d_qf_head, cs.qf_head, st)) != hipSuccess ||
+          (h = upload(e->d_qf_ent, cs.qf_ent, st)) != hipSuccess ||
+          (h = upload(e->d_qf_noff, cs.qf_noff, st)) != hipSuccess ||
+          (h = upload(e->d_qf_nlen, cs.qf_nlen, st)) != hipSuccess ||
+          (h = upload(e->d_qf_nmeta, cs.qf_nmeta, st)) != hipSuccess ||
+          (h = upload(e->d_qf_nbytes, cs.qf_nbytes, st)) != hipSuccess) {
+        *out = e;
+        return hip_err(e, h, "upload prefilter tables");
+      }
+      P.qf_on = 1;
+      P.qf_stride = cs.qf_stride;
+      P.qf_fold = cs.qf_fold;
+      P.qf_mask = cs.qf_mask;
+      P.qf_bitmap = e->d_qf_bitmap.as<uint32_t>();
+      P.qf_head = e->d_qf_head.as<uint32_t>();
+      P.qf_ent = e->d_qf_ent.as<uint32_t>();
+      P.qf_noff = e->d_qf_noff.as<uint32_t>();
+      P.qf_nlen = e->d_qf_nlen.as<uint32_t>();
+      P.qf_nmeta = e->d_qf_nmeta.as<uint32_t>();
+      P.qf_nbytes = e->d_qf_nbytes.as<uint32_t>();
+    }
   }
+  if (const char* cc = getenv("KLF_CAND_CAP"))  // tests: force the queue-overflow fallback
+    e->cand_cap = (uint32_t)std::max(1L, std::min(atol(cc), 1L << 28));
   if (cfg->staging_hint) e->staged.reserve(16);
   *out = e;
   return KLF_OK;
@@ -220,7 +247,8 @@ extern "C" void klf_close(klf_engine* e) {
   if (!e) return;
   if (e->stream) (void)hipStreamSynchronize(e->stream);
   for (DevBuf* b : {&e->d_lit, &e->d_ac_class, &e->d_ac_next, &e->d_ac_accept, &e->d_rx_class, &e->d_rx_b,
-                    &e->d_rx_follow, &e->d_rx_vec, &e->d_rx_flags, &e->d_batch, &e->d_segs, &e->d_tstat,
+                    &e->d_rx_follow, &e->d_rx_vec, &e->d_rx_flags, &e->d_qf_bitmap, &e->d_qf_head,
+                    &e->d_qf_ent, &e->d_qf_noff, &e->d_qf_nlen, &e->d_qf_nmeta, &e->d_qf_nbytes, &e->d_cand, &e->d_batch, &e->d_segs, &e->d_tstat,
                     &e->d_slots, &e->d_pool, &e->d_tile_base, &e->d_bsum, &e->d_cstatus, &e->d_counters,
                     &e->d_line_off, &e->d_meta, &e->d_bits, &e->d_segout, &e->d_wpre, &e->d_out, &e->d_tile_seg, &e->d_mpart})
     b->release();
@@ -334,6 +362,8 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
   HIPCHK(e, e->d_segout.ensure(nsegs * sizeof(SegOut)), "alloc segout");
   HIPCHK(e, e->d_wpre.ensure((nsegs + 1) * 8), "alloc wpre");
   HIPCHK(e, e->d_out.ensure(total_bytes + 64), "alloc out");
+  const bool need_cand = mode == klf::CompiledSet::kGeneral && e->cs.qf_on && e->cs.rx_count;
+  if (need_cand) HIPCHK(e, e->d_cand.ensure((size_t)e->cand_cap * 8), "alloc cand");
 
   for (int attempt = 0; attempt < 2; ++attempt) {
     const uint64_t max_cblocks = cap / klf::kCompactLines + 2;
@@ -385,6 +415,8 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
     a.wpre = e->d_wpre.as<uint64_t>();
     a.out = e->d_out.as<uint8_t>();
     a.max_cblocks = (uint32_t)max_cblocks;
+    a.cand = need_cand ? e->d_cand.as<uint64_t>() : nullptr;
+    a.cand_cap = need_cand ? e->cand_cap : 0;
     HIPCHK(e, klf::launch_pipeline(a, st, e->ev, e->num_cus), "launch");
     r->so.resize(nsegs);
     uint32_t counters[8];

@@ -228,18 +228,25 @@ __device__ __forceinline__ bool parse_fast(const uint8_t* lds, uint32_t o, const
 #ifndef KLF_SCAN_OCC
 #define KLF_SCAN_OCC 4
 #endif
+// Scan variants: no patterns, the fused single literal, general sets through the fused
+// q-gram prefilter (QS = sampling stride).
+constexpr int kScanPlain = 0, kScanLit = 1, kScanGen = 2;
+
 // The tile descriptors come in as separate __restrict__ const parameters so that their
 // (wave-uniform) reads compile to scalar loads: a vector load of them would be ordered
 // behind the in-flight prefetch by vmcnt and stall every tile on the next tile's bytes.
-template <bool LIT>
-__global__ __launch_bounds__(kThreads, KLF_SCAN_OCC) void k_scan(RunArgs a, const uint32_t* __restrict__ tseg,
+template <int MODE, int QS>
+__global__ __launch_bounds__(kThreads, MODE == kScanGen ? 3 : KLF_SCAN_OCC) void k_scan(RunArgs a, const uint32_t* __restrict__ tseg,
                                                                const SegDesc* __restrict__ segs) {
+  constexpr bool LIT = MODE == kScanLit;
+  constexpr bool GEN = MODE == kScanGen;
   constexpr int kWaves = kThreads / 64;
   constexpr int kRows = kTile / 1024;  // 1 KiB rows: 16 B per lane per row
   __shared__ __attribute__((aligned(16))) uint8_t s_tile_all[kWaves][kTile + kHalo];
   __shared__ uint32_t s_list_all[kWaves][kSlots];
   __shared__ __attribute__((aligned(16))) uint32_t s_lit[kMaxFusedLiteral / 4 + 1];  // literal, zero padded
   __shared__ uint32_t s_month[16];
+  __shared__ uint32_t s_qf[GEN ? kQfWords : 1];  // q-gram bitmap of the needles
   // wv is wave-uniform; readfirstlane tells the compiler so (tile indices stay in SGPRs and
   // the descriptor reads stay scalar loads)
   const int t = threadIdx.x, lane = t & 63, wv = __builtin_amdgcn_readfirstlane(t >> 6);
@@ -249,6 +256,8 @@ __global__ __launch_bounds__(kThreads, KLF_SCAN_OCC) void k_scan(RunArgs a, cons
   for (uint32_t i = t; i < kMaxFusedLiteral / 4 + 1; i += kThreads)
     s_lit[i] = (LIT && i < (a.lit_len + 3) / 4) ? a.lit_words[i] : 0u;
   if (t < 16) s_month[t] = c_month[t];
+  if (GEN)
+    for (uint32_t i = t; i < kQfWords; i += kThreads) s_qf[i] = a.pats.qf_bitmap[i];
   __syncthreads();  // the kernel's only block barrier
   const uint32_t nwaves = gridDim.x * kWaves;
   auto tile_src = [&](uint32_t tl) -> const uint4* {
@@ -407,6 +416,27 @@ __global__ __launch_bounds__(kThreads, KLF_SCAN_OCC) void k_scan(RunArgs a, cons
           n_defer += fast ? 0u : 1u;
         }
       }
+      // number of listed line starts at or before tile offset pos
+      auto starts_upto = [&](int32_t pos) __attribute__((always_inline)) -> int {
+        int lo = 0, hi = (int)nlines;
+        while (lo < hi) {
+          const int mid = (lo + hi) >> 1;
+          if ((list[mid] & kSlotOff) <= (uint32_t)pos) lo = mid + 1; else hi = mid;
+        }
+        return lo;
+      };
+      // a final (literal) hit starting at tile offset pos -> its line's hit bit
+      auto attribute = [&](int32_t pos) __attribute__((always_inline)) {
+        const int lo = starts_upto(pos);
+        if (lo > 0) {  // the line starts in this tile: deferred lines are searched by k_fixup
+          const uint32_t v = list[lo - 1];
+          const uint32_t mt = v >> 16;
+          if (!(v & kSlotDefer) && (mt & Meta::kParsed) && (uint32_t)pos >= (v & kSlotOff) + (mt >> 2))
+            atomicOr(&list[lo - 1], kSlotHit);
+        } else {  // carried in from an earlier tile: k_scatter decides (furthest hit wins)
+          carry = carry > (uint32_t)pos + 1u ? carry : (uint32_t)pos + 1u;
+        }
+      };
       // ---- fused single-literal grep ----
       // Anchor hits (the literal's rarest byte) name candidate starts p = anchor - ka.  A
       // tile owns the starts inside it: anchors whose start lies in the previous tile are
@@ -440,20 +470,7 @@ __global__ __launch_bounds__(kThreads, KLF_SCAN_OCC) void k_scan(RunArgs a, cons
             }
           }
           if (!eq) return;
-          // the hit's line: last listed start at or before pos
-          int lo = 0, hi = (int)nlines;
-          while (lo < hi) {
-            const int mid = (lo + hi) >> 1;
-            if ((list[mid] & kSlotOff) <= (uint32_t)pos) lo = mid + 1; else hi = mid;
-          }
-          if (lo > 0) {  // the line starts in this tile: deferred lines are searched by k_fixup
-            const uint32_t v = list[lo - 1];
-            const uint32_t mt = v >> 16;
-            if (!(v & kSlotDefer) && (mt & Meta::kParsed) && (uint32_t)pos >= (v & kSlotOff) + (mt >> 2))
-              atomicOr(&list[lo - 1], kSlotHit);
-          } else {  // carried in from an earlier tile: k_scatter decides (furthest hit wins)
-            carry = carry > (uint32_t)pos + 1u ? carry : (uint32_t)pos + 1u;
-          }
+          attribute(pos);
         };
         for (uint32_t cm = anc; cm; cm &= cm - 1u) {
           const uint32_t c = (uint32_t)__builtin_ctz(cm);
@@ -468,6 +485,112 @@ __global__ __launch_bounds__(kThreads, KLF_SCAN_OCC) void k_scan(RunArgs a, cons
             const uint8_t c = jj < (uint32_t)kHalo ? s_tile[kTile + jj] : segp[q];
             if (c == a.lit_anchor_byte) check((int32_t)(kTile + jj) - (int32_t)ka);
           }
+        }
+        carry = wave_max(carry);
+      }
+      // ---- general sets: fused q-gram prefilter ----
+      // Samples p = 0 mod QS of the tile (every needle is >= q + QS - 1 bytes, so each
+      // occurrence spans one with its gram inside the needle) probe the LDS bitmap;
+      // bitmap hits are verified against the needles of the hash bucket.  A verified
+      // literal is a match (attributed like the fused literal); a verified regex factor
+      // queues (batch offset, regex) for k_nfa.  As with the literal, a tile owns the
+      // occurrences that start in it: the sample at p = kTile (halo) serves its tail.
+      if (GEN) {
+        if (dense) __threadfence_block();
+        wave_lds_sync();
+        const DevPatterns& P = a.pats;
+        const uint32_t fold = P.qf_fold, qmask = P.qf_mask;
+        const uint32_t* s32 = reinterpret_cast<const uint32_t*>(s_tile);
+        uint32_t last_key = ~0u;  // (line, regex) this lane queued last: no duplicate work
+        auto verify = [&](uint32_t h, int32_t p) __attribute__((always_inline)) {
+          const uint32_t b = h >> (kQfBits - kQfBucketBits);
+          const uint32_t e1 = P.qf_head[b + 1];
+          for (uint32_t e = P.qf_head[b]; e < e1; ++e) {
+            const uint32_t ent = P.qf_ent[e];
+            const uint32_t nd = ent >> 2;
+            const int32_t x = p - (int32_t)(ent & 3u);
+            if (x < 0 || x >= tile_len) continue;
+            const uint32_t m = P.qf_nlen[nd];
+            if (rel_lo + (int64_t)x + (int64_t)m > seg_len) continue;
+            const uint32_t meta = P.qf_nmeta[nd];
+            const uint32_t lm = (meta & 0x40000000u) ? 0x20202020u : 0u;
+            const uint32_t* nw = P.qf_nbytes + P.qf_noff[nd];
+            bool eq = true;
+            if ((uint32_t)x + m + 4 <= (uint32_t)(kTile + kHalo)) {
+              const uint32_t sh = (uint32_t)x & 3u;
+              uint32_t wi = (uint32_t)x >> 2;
+              uint32_t prev = s32[wi];
+              for (uint32_t k = 0; k < m && eq; k += 4) {
+                const uint32_t nx = s32[++wi];
+                const uint32_t got = __builtin_amdgcn_alignbyte(nx, prev, sh) | lm;
+                prev = nx;
+                const uint32_t nb = m - k < 4 ? m - k : 4;
+                const uint32_t msk = nb == 4 ? 0xFFFFFFFFu : ((1u << (8 * nb)) - 1);
+                eq = ((got ^ nw[k >> 2]) & msk) == 0;
+              }
+            } else {
+              const uint8_t* nb8 = reinterpret_cast<const uint8_t*>(nw);
+              for (uint32_t k = 0; k < m && eq; ++k) {
+                const uint32_t o = (uint32_t)x + k;
+                const uint8_t cc = o < (uint32_t)(kTile + kHalo) ? s_tile[o] : segp[rel_lo + o];
+                eq = (uint8_t)(cc | (uint8_t)lm) == nb8[k];
+              }
+            }
+            if (!eq) continue;
+            if (!(meta & 0x80000000u)) {
+              attribute(x);
+              continue;
+            }
+            const uint32_t r = meta & 0xFFFFFFu;
+            const uint32_t key = (uint32_t)starts_upto(x) * (uint32_t)kMaxRegexSet + r;
+            if (key == last_key) continue;
+            last_key = key;
+            const uint32_t qi = atomicAdd(&a.counters[kCtrQueue], 1u);
+            if (qi < a.cand_cap) a.cand[qi] = (sd.base + (uint64_t)rel_lo + (uint64_t)x) | ((uint64_t)r << 40);
+            else atomicOr(&a.counters[kCtrQOver], 1u);
+          }
+        };
+        auto probe = [&](uint32_t g) __attribute__((always_inline)) -> uint32_t {
+          const uint32_t h = qf_hash((g | fold) & qmask);
+          return (s_qf[h >> 5] >> (h & 31)) & 1u;
+        };
+        // bitmap probes of my samples -> a 128-bit hit mask (bit = byte offset in my range)
+        uint32_t hq0 = 0, hq1 = 0, hq2 = 0, hq3 = 0;
+        const uint32_t rot = ((uint32_t)lane >> 1) & 7u;
+#pragma unroll
+        for (int v = 0; v < 8; ++v) {
+          const uint32_t c = ((uint32_t)v + rot) & 7u;
+          const uint32_t o0 = my0 + 16u * c;
+          const uint4 x = *reinterpret_cast<const uint4*>(s_tile + o0);
+          const uint32_t w4 = QS < 4 ? s32[(o0 >> 2) + 4] : 0u;
+          const uint32_t w[5] = {x.x, x.y, x.z, x.w, w4};
+          uint32_t hm = 0;
+#pragma unroll
+          for (int d = 0; d < 4; ++d)
+#pragma unroll
+            for (int o = 0; o < 4; o += QS) {
+              const uint32_t g = o == 0 ? w[d] : __builtin_amdgcn_alignbyte(w[d + 1], w[d], o);
+              hm |= probe(g) << (4 * d + o);
+            }
+          hm = clip(hm, c) << ((c & 1u) * 16u);
+          const uint32_t q = c >> 1;
+          hq0 |= q == 0 ? hm : 0u;
+          hq1 |= q == 1 ? hm : 0u;
+          hq2 |= q == 2 ? hm : 0u;
+          hq3 |= q == 3 ? hm : 0u;
+        }
+        const uint32_t hq[4] = {hq0, hq1, hq2, hq3};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          for (uint32_t m = hq[q]; m; m &= m - 1u) {
+            const uint32_t p = my0 + 32u * q + (uint32_t)__builtin_ctz(m);
+            const uint32_t g = __builtin_amdgcn_alignbyte(s32[(p >> 2) + 1], s32[p >> 2], p & 3u);
+            verify(qf_hash((g | fold) & qmask), (int32_t)p);
+          }
+        }
+        if (QS > 1 && lane == 63 && !last) {
+          const uint32_t g = s32[kTile >> 2];
+          if (probe(g)) verify(qf_hash((g | fold) & qmask), kTile);
         }
         carry = wave_max(carry);
       }
@@ -516,6 +639,16 @@ __device__ bool contains_bytes(const uint8_t* p, int64_t n, const uint8_t* lit, 
   return false;
 }
 
+__device__ bool ac_match(const DevPatterns& P, const uint8_t* p, int64_t n);
+__device__ bool rx_match(const DevPatterns& P, uint32_t r, const uint8_t* p, int64_t n);
+// the whole general set on one (non-empty) content: AC over the literals, every regex
+__device__ bool general_match(const DevPatterns& P, const uint8_t* p, int64_t n) {
+  if (P.ac_states && ac_match(P, p, n)) return true;
+  for (uint32_t r = 0; r < P.rx_count; ++r)
+    if (rx_match(P, r, p, n)) return true;
+  return false;
+}
+
 __global__ __launch_bounds__(256) void k_fixup(RunArgs a) {
   if (!a.counters[kCtrDefer] || a.counters[2]) return;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -542,7 +675,8 @@ __global__ __launch_bounds__(256) void k_fixup(RunArgs a) {
       const bool ok = parse_line_prefix(GlobalBytes{segp, p0, seg_len}, r, plen);
       const bool so = ok && !time_before(r.sec, r.nsec, a.since_sec, a.since_nsec);
       uint32_t hit = 0;
-      if (a.grep_mode == kGrepLit1 && ok) {
+      const bool gen = a.grep_mode == kGrepGeneral && a.pats.qf_on;  // the scan attributed none
+      if ((a.grep_mode == kGrepLit1 || gen) && ok) {
         const int64_t cs = p0 + plen;
         int64_t ce;
         if (j + 1 < nlines) {
@@ -551,7 +685,8 @@ __global__ __launch_bounds__(256) void k_fixup(RunArgs a) {
           ce = cs;
           while (ce < seg_len && segp[ce] != '\n') ++ce;
         }
-        if (ce > cs && contains_bytes(segp + cs, ce - cs, a.lit, a.lit_len)) hit = kSlotHit;
+        if (ce > cs && !gen && contains_bytes(segp + cs, ce - cs, a.lit, a.lit_len)) hit = kSlotHit;
+        if (ce > cs && gen && general_match(a.pats, segp + cs, ce - cs)) hit = kSlotHit;
       }
       list[j] = off | kSlotDefer | hit | ((uint32_t)make_meta(ok, so, plen) << 16);
       dp += ok ? 1u : 0u;
@@ -801,8 +936,45 @@ __device__ __forceinline__ uint32_t line_plen(const RunArgs& a, uint16_t meta, c
   return plen;
 }
 
+// K2b: the prefiltered regex stage.  One lane per queued (batch offset, regex) candidate:
+// the offset's stream and line (binary searches over the segment table and the line
+// index), then the Glushkov NFA of that regex over the line's content.  Lines already
+// matched are skipped.
+__global__ __launch_bounds__(256) void k_nfa(RunArgs a) {
+  if (a.counters[2] || a.counters[kCtrQOver]) return;  // overflow: k_match decides every line
+  const uint32_t nq = a.counters[kCtrQueue] < a.cand_cap ? a.counters[kCtrQueue] : a.cand_cap;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nq; i += gridDim.x * blockDim.x) {
+    const uint64_t e = a.cand[i];
+    const uint64_t pos = e & ((1ull << 40) - 1);
+    const uint32_t r = (uint32_t)(e >> 40);
+    uint32_t lo = 0, hi = a.nsegs;
+    while (hi - lo > 1) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (a.segs[mid].base <= pos) lo = mid; else hi = mid;
+    }
+    const uint32_t s = lo;
+    const uint64_t rel = pos - a.segs[s].base;
+    uint64_t l0 = a.segout[s].line_lo, l1 = a.segout[s].line_hi;
+    while (l1 - l0 > 1) {
+      const uint64_t mid = (l0 + l1) >> 1;
+      if (a.line_off[mid + s] <= rel) l0 = mid; else l1 = mid;
+    }
+    const uint64_t l = l0;
+    if ((a.bits[l >> 5] >> (l & 31)) & 1u) continue;
+    const uint16_t m = a.meta[l];
+    if (!(m & Meta::kParsed)) continue;
+    const uint8_t* segp = a.bytes + a.segs[s].base;
+    const uint64_t ls = a.line_off[l + s], le = a.line_off[l + s + 1];
+    const uint32_t plen = line_plen(a, m, segp, ls, le);
+    uint64_t cs = ls + plen, ce = le;
+    if (ce > cs && segp[ce - 1] == '\n') --ce;
+    if (ce > cs && rx_match(a.pats, r, segp + cs, (int64_t)(ce - cs))) atomicOr(&a.bits[l >> 5], 1u << (l & 31));
+  }
+}
+
 __global__ __launch_bounds__(256) void k_match(RunArgs a) {
   if (a.counters[2]) return;
+  if (a.grep_mode == kGrepGeneral && a.pats.qf_on && !a.counters[kCtrQOver]) return;  // prefiltered
   const uint64_t L = a.segout[a.nsegs - 1].line_hi;
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   for (uint64_t l = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; l < L; l += stride) {
@@ -1260,6 +1432,17 @@ hipError_t clear_timeline() {
 #endif
 }
 
+template <int MODE, int QS>
+hipError_t launch_scan(const RunArgs& a, hipStream_t st, int num_cus) {
+  int occ = 0;
+  (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_scan<MODE, QS>, kThreads, 0);
+  occ = occ < 1 ? 1 : (occ > 8 ? 8 : occ);
+  uint32_t grid = (uint32_t)(num_cus * occ);
+  if (grid > a.ntiles) grid = a.ntiles;
+  hipLaunchKernelGGL((k_scan<MODE, QS>), dim3(grid), dim3(kThreads), 0, st, a, a.tile_seg, a.segs);
+  return hipGetLastError();
+}
+
 hipError_t launch_pipeline(const RunArgs& a, hipStream_t st, hipEvent_t* ev, int num_cus) {
   hipError_t e;
 #define KLF_TRY(x) do { e = (x); if (e != hipSuccess) return e; } while (0)
@@ -1279,19 +1462,16 @@ hipError_t launch_pipeline(const RunArgs& a, hipStream_t st, hipEvent_t* ev, int
   }
   KLF_TRY(hipEventRecord(ev[1], st));
   {
-    int occ = 0;
     if (a.grep_mode == kGrepLit1)
-      (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_scan<true>, kThreads, 0);
+      KLF_TRY((launch_scan<kScanLit, 1>(a, st, num_cus)));
+    else if (a.grep_mode == kGrepGeneral && a.pats.qf_on && a.pats.qf_stride == 4)
+      KLF_TRY((launch_scan<kScanGen, 4>(a, st, num_cus)));
+    else if (a.grep_mode == kGrepGeneral && a.pats.qf_on && a.pats.qf_stride == 2)
+      KLF_TRY((launch_scan<kScanGen, 2>(a, st, num_cus)));
+    else if (a.grep_mode == kGrepGeneral && a.pats.qf_on)
+      KLF_TRY((launch_scan<kScanGen, 1>(a, st, num_cus)));
     else
-      (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_scan<false>, kThreads, 0);
-    occ = occ < 1 ? 1 : (occ > 8 ? 8 : occ);
-    uint32_t grid = (uint32_t)(num_cus * occ);
-    if (grid > a.ntiles) grid = a.ntiles;
-    if (a.grep_mode == kGrepLit1)
-      hipLaunchKernelGGL(k_scan<true>, dim3(grid), dim3(kThreads), 0, st, a, a.tile_seg, a.segs);
-    else
-      hipLaunchKernelGGL(k_scan<false>, dim3(grid), dim3(kThreads), 0, st, a, a.tile_seg, a.segs);
-    KLF_TRY(hipGetLastError());
+      KLF_TRY((launch_scan<kScanPlain, 1>(a, st, num_cus)));
     KLF_TRY(hipEventRecord(ev[6], st));  // k_scan alone (the roofline kernel)
     hipLaunchKernelGGL(k_fixup, dim3(num_cus * 2), dim3(256), 0, st, a);
     KLF_TRY(hipGetLastError());
@@ -1306,6 +1486,10 @@ hipError_t launch_pipeline(const RunArgs& a, hipStream_t st, hipEvent_t* ev, int
   }
   KLF_TRY(hipGetLastError());
   KLF_TRY(hipEventRecord(ev[2], st));
+  if (a.grep_mode == kGrepGeneral && a.pats.qf_on && a.pats.rx_count) {
+    hipLaunchKernelGGL(k_nfa, dim3(num_cus * 4), dim3(256), 0, st, a);
+    KLF_TRY(hipGetLastError());
+  }
   if (a.grep_mode == kGrepGeneral || a.grep_mode == kGrepAll) {
     hipLaunchKernelGGL(k_match, dim3(num_cus * 8), dim3(256), 0, st, a);
     KLF_TRY(hipGetLastError());

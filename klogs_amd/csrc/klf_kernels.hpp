@@ -29,7 +29,8 @@ constexpr uint32_t kQfWords = 1u << (kQfBits - 5);
 constexpr int kQfBucketBits = 12;                    // verification buckets: top hash bits
 constexpr uint32_t kQfMinNeedle = 3;                 // shorter literal / factor: no prefilter
 constexpr uint32_t kQfMaxFactor = 32;                // regex factors are cut to this length
-constexpr uint32_t kCtrQueue = 6;                    // counters[6]: NFA candidate queue length
+constexpr uint32_t kMaxRegexSet = 1024;              // = klf_patterns.hpp kMaxRegexes
+constexpr uint32_t kCtrQueue = 6;                   // counters[6]: NFA candidate queue length
 constexpr uint32_t kCtrQOver = 7;                    // counters[7]: queue overflow -> k_match
 __host__ __device__ inline uint32_t qf_hash(uint32_t g) { return (g * 0x9E3779B1u) >> (32 - kQfBits); }
 

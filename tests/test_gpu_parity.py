@@ -131,3 +131,77 @@ def test_many_small_streams_all_selected(gpu):
     streams = [synth.generate(synth.TEXT, 21, i, 1000 + 37 * i) for i in range(300)]
     check_against_c(streams, None, -1, [])
     check_against_c(streams, None, 3, [])
+
+
+# ---- general pattern sets: fused q-gram prefilter + Glushkov NFA on candidates -----------
+def check_against_py(streams, since, tail, grep=(), match=()):
+    got = run_engine(streams, since=since, tail=tail, grep=grep, match=match)
+    pats = po.compile_patterns(grep, match)
+    for i, s in enumerate(streams):
+        ref = po.filter_stream(s, since or GZ, tail, pats)
+        g_out, g_lo, g_bits, g_c = got[i]
+        assert g_out == ref.out, f"stream {i}: out differs ({len(g_out)} vs {len(ref.out)})"
+        assert g_lo.tolist() == ref.line_off, f"stream {i}: line offsets differ"
+        assert g_bits == ref.match_bits, f"stream {i}: match bits differ"
+        assert [g_c[k] for k in ("lines", "parsed", "since_ok", "matched", "selected")] == \
+            [ref.n_lines, ref.n_parsed, ref.n_since, ref.n_matched, ref.n_selected], (i, g_c)
+
+
+@pytest.mark.parametrize("since,tail", [(None, -1), ((synth.T0 + 1800, 0), 50)])
+def test_c4_literal_set_mixed_lines(gpu, since, tail):
+    """BASELINE config 4 shape at test size: 1,024 literals over mixed-length lines."""
+    lits = synth.c4_literals(1024)
+    assert E.debug_prefilter(b"", grep=lits)[1]["on"]
+    d = synth.generate(synth.MIXED, 4, 0, 3_000_000, permille=5)
+    check_against_c([d, synth.generate(synth.MIXED, 4, 1, 700_000, permille=50)], since, tail, lits)
+
+
+@pytest.mark.parametrize("since,tail", [(None, -1), ((synth.T0 + 1800, 0), 20)])
+def test_c5_regex_set_long_json(gpu, since, tail):
+    """BASELINE config 5 shape at test size: 64 regexes over 1-32 KiB JSON lines (events
+    and near misses that hold the factor but not the match)."""
+    rx = synth.c5_regexes()
+    assert E.debug_prefilter(b"", match=rx)[1]["on"]
+    streams = [synth.generate(synth.LONGJSON, 5, i, 2_000_000, permille=20) for i in range(3)]
+    check_against_py(streams, since, tail, match=rx)
+
+
+GEN_SETS = [
+    ([synth.NEEDLE, b"volume", b"x" * 80], [rb"(?i)took \d+ms", rb"status=(200|5\d\d)"]),
+    ([b"pod", b"ready"], []),
+    ([], [rb"(?i)ERR_CONN_\w+", rb"user= ?\w+ took"]),
+    ([b"ab"], [rb"\d+"]),  # prefilter off: k_match decides every line
+]
+
+
+@pytest.mark.parametrize("idx", range(len(GEN_SETS)))
+@pytest.mark.parametrize("seed", range(2))
+def test_general_sets_adversarial(gpu, idx, seed):
+    grep, match = GEN_SETS[idx]
+    d = synth.generate(synth.ADVERSARIAL, 50 + seed, 0, 3000, drop_final_nl=bool(seed), permille=40)
+    t = synth.generate(synth.TEXT, 60 + seed, 0, 400_000)
+    # long literal across tile boundaries
+    t = t.replace(b"volume", b"volume" + b"x" * 80, 50)
+    for since, tail in [(None, -1), ((synth.T0 + 1800, 0), 7), (None, 0)]:
+        check_against_py([d, t, b"", b"2024-10-22T00:00:00Z pod ready\n"], since, tail, grep, match)
+
+
+def test_general_set_dense_tiles(gpu):
+    rng = random.Random(3)
+    parts = []
+    for i in range(40000):
+        k = rng.random()
+        if k < 0.4:
+            parts.append(b"\n")
+        else:
+            parts.append(b"2024-10-22T00:00:%02dZ %s\n" % (i % 60, rng.choice([b"ok", b"took 12ms", b"pod x", b"q"])))
+    d = b"".join(parts)
+    check_against_py([d], None, -1, [b"pod x"], [rb"took \d+ms"])
+    check_against_py([d], None, 100, [b"pod x"], [rb"took \d+ms"])
+
+
+def test_candidate_queue_overflow_falls_back(gpu, monkeypatch):
+    """More NFA candidates than the queue holds: k_match decides every line (exact)."""
+    monkeypatch.setenv("KLF_CAND_CAP", "16")
+    d = synth.generate(synth.LONGJSON, 9, 0, 1_500_000, permille=100)
+    check_against_py([d], None, -1, match=synth.c5_regexes()[:16])
