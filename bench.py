@@ -8,6 +8,13 @@ over the device-resident batch plus the per-stream count gather across ranks.  W
 scaling: every rank owns its own stream (streams shard across GPUs; no data-path
 collective).  value = total input bytes of all ranks / max-over-ranks wall time.
 
+At N = 1 the same line also carries BASELINE configs 4 and 5 under "extra.configs" (the
+general matcher: the scan with the fused q-gram prefilter, then the per-candidate NFA):
+  C4: 32 GiB of mixed-length lines (8 streams), 1,024 --grep literals, --since 5m --tail 100
+  C5: 32 GiB of 1-32 KiB JSON lines, 8 pods with 1-2 init containers (-i stream table),
+      64 --match regexes, --since 5m --tail 100
+each measured the same way (device-resident, HIP events on the launch stream).
+
 Launch: python bench.py [--gpus 1 --steps K --warmup W]; for N > 1 the driver runs
 `python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...`.
 """
@@ -60,6 +67,8 @@ def main():
     ap.add_argument("--bytes", type=int, default=STREAM_BYTES, help="stream bytes per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-verify", action="store_true")
+    ap.add_argument("--extra-configs", default="c4,c5", help="N=1 only: comma list of c4,c5 ('' = none)")
+    ap.add_argument("--extra-bytes", type=int, default=32 << 30, help="total bytes of each extra config")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -207,10 +216,95 @@ def main():
     }
     last.free()
     eng.close()
+    del dev, host
+    torch.cuda.empty_cache()
+    if world == 1 and args.extra_configs:
+        res["extra"]["configs"] = {}
+        for name in [x for x in args.extra_configs.split(",") if x]:
+            res["extra"]["configs"][name] = run_extra(name, args, local, now)
+            torch.cuda.empty_cache()
     if rank == 0:
         print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def extra_streams(name: str, total: int):
+    """(stream sizes, generator kind, patterns, description) of BASELINE configs 4 / 5."""
+    if name == "c4":
+        n = 8
+        return [total // n] * n, synth.MIXED, dict(grep=synth.c4_literals(1024)), 5, \
+            "C4: 8 streams of mixed-length lines (16 B-8 KiB, lognormal), 1,024 --grep literals (6-24 B, " \
+            "0.5% of lines hold one), --since 5m --tail 100"
+    if name == "c5":
+        from klogs_amd import host as H
+        pods = [(f"synthetic-{p}", [f"init-{k}" for k in range(1 + p % 2)], ["app", "sidecar"]) for p in range(8)]
+        table = H.stream_table(pods, init=True)  # getPodLogs order with -i (cmd/root.go:240-262)
+        w = [1 if is_init else 4 for _, _, is_init in table]
+        sizes = [total * x // sum(w) for x in w]
+        return sizes, synth.LONGJSON, dict(match=synth.c5_regexes()), 5, \
+            f"C5: {len(table)} streams (8 pods x 1-2 init containers + 2 containers, -i), 1-32 KiB JSON " \
+            "lines, 64 --match regexes (0.5% of lines match one, 1% hold a factor but no match), " \
+            "--since 5m --tail 100"
+    raise ValueError(name)
+
+
+def run_extra(name: str, args, local: int, now: int) -> dict:
+    sizes, kind, pats, permille, desc = extra_streams(name, args.extra_bytes)
+    t = time.time()
+    lens = [synth.size(kind, 42, i, sz, permille=permille) for i, sz in enumerate(sizes)]
+    seg_base, total = E.layout(lens)
+    dev = torch.empty(total, dtype=torch.uint8, device=f"cuda:{local}")
+    for i, (sz, n) in enumerate(zip(sizes, lens)):  # one stream at a time through host memory
+        h = np.empty(n + 1, dtype=np.uint8)
+        synth.generate_into(h, kind, 42, i, sz, permille=permille)
+        dev[int(seg_base[i]):int(seg_base[i]) + n].copy_(torch.from_numpy(h[:n]))
+        del h
+    torch.cuda.synchronize()
+    log(f"[{name}] generated + uploaded {sum(lens)} B in {time.time() - t:.1f}s")
+    since = (now - SINCE_S, 0)
+    stream = torch.cuda.current_stream()
+    eng = E.Engine(local, hip_stream=stream.cuda_stream, **pats)
+    ptr = dev.data_ptr()
+    for _ in range(args.warmup):
+        eng.run_device(ptr, seg_base, lens, since=since, tail=TAIL).free()
+    torch.cuda.synchronize()
+    scan_ms, match_ms, total_ms = [], [], []
+    t0 = time.perf_counter()
+    last = None
+    for i in range(args.steps):
+        r = eng.run_device(ptr, seg_base, lens, since=since, tail=TAIL)
+        tm = r.timing()
+        scan_ms.append(tm[6])
+        match_ms.append(tm[1])
+        total_ms.append(tm[4])
+        if i + 1 < args.steps:
+            r.free()
+        else:
+            last = r
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    tot = last.totals()
+    n = sum(lens)
+    scan_s = float(np.mean(scan_ms)) / 1e3
+    dev_s = float(np.mean(total_ms)) / 1e3
+    step_alg = n + 8 * (tot["lines"] + len(lens)) + 4 * (tot["lines"] // 32 + 1) + tot["out_bytes"]
+    out = {
+        "workload": desc, "streams": len(lens), "bytes": n, "lines": tot["lines"],
+        "value_GBps": round(n * args.steps / dt / 1e9, 1), "ms_per_step": round(dt / args.steps * 1e3, 3),
+        "device_ms_per_step": round(dev_s * 1e3, 3),
+        "roofline": {"bound": "hbm", "kernel": "k_scan<general, q-gram prefilter>",
+                     "achieved": round(n / scan_s / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(n / scan_s / 1e9 / HBM_PEAK_GBS, 4), "avg_launch_ms": round(scan_s * 1e3, 4)},
+        "matcher_ms": round(float(np.mean(match_ms)), 4),
+        "step_alg_frac_of_peak": round(step_alg / dev_s / 1e9 / HBM_PEAK_GBS, 4),
+        "matched_lines": tot["matched"], "selected_lines": tot["selected"], "out_bytes": tot["out_bytes"],
+        "stage_ms_last": [round(x, 4) for x in last.timing()],
+    }
+    last.free()
+    eng.close()
+    del dev
+    return out
 
 
 if __name__ == "__main__":

@@ -59,7 +59,7 @@ struct klf_engine {
   std::vector<std::vector<uint8_t>> staged;
   // device pattern tables
   DevBuf d_lit, d_ac_class, d_ac_next, d_ac_accept, d_rx_class, d_rx_b, d_rx_follow, d_rx_vec, d_rx_flags;
-  DevBuf d_qf_bitmap, d_qf_head, d_qf_ent, d_qf_noff, d_qf_nlen, d_qf_nmeta, d_qf_nbytes, d_cand;
+  DevBuf d_qf_bitmap, d_qf_head, d_qf_ent, d_qf_nbytes, d_cand, d_rx_vec4;
   uint32_t cand_cap = 1u << 22;  // NFA candidate queue (32 MiB); overflow -> k_match
   klf::DevPatterns dpats;
   // workspace
@@ -209,16 +209,19 @@ extern "C" int klf_open(const klf_config* cfg, klf_engine** out) {
       P.rx_init0 = v + 2 * cs.rx_count;
       P.rx_end = v + 3 * cs.rx_count;
       P.rx_flags = e->d_rx_flags.as<uint32_t>();
+      std::vector<uint64_t> vec4;  // [rx][4] interleaved for k_nfa
+      for (uint32_t r = 0; r < cs.rx_count; ++r)
+        for (const auto* v : {&cs.rx_first, &cs.rx_last, &cs.rx_init0, &cs.rx_end}) vec4.push_back((*v)[r]);
+      if ((h = upload(e->d_rx_vec4, vec4, st)) != hipSuccess) { *out = e; return hip_err(e, h, "upload regex vec"); }
+      P.rx_vec = e->d_rx_vec4.as<uint64_t>();
       P.rx_count = cs.rx_count;
       P.rx_classes = cs.rx_classes;
+      P.rx_maxpos = std::max<uint32_t>(1, cs.rx_maxpos);
     }
     if (cs.qf_on) {
       if ((h = upload(e->d_qf_bitmap, cs.qf_bitmap, st)) != hipSuccess ||
           (h = upload(e->d_qf_head, cs.qf_head, st)) != hipSuccess ||
           (h = upload(e->d_qf_ent, cs.qf_ent, st)) != hipSuccess ||
-          (h = upload(e->d_qf_noff, cs.qf_noff, st)) != hipSuccess ||
-          (h = upload(e->d_qf_nlen, cs.qf_nlen, st)) != hipSuccess ||
-          (h = upload(e->d_qf_nmeta, cs.qf_nmeta, st)) != hipSuccess ||
           (h = upload(e->d_qf_nbytes, cs.qf_nbytes, st)) != hipSuccess) {
         *out = e;
         return hip_err(e, h, "upload prefilter tables");
@@ -229,10 +232,7 @@ extern "C" int klf_open(const klf_config* cfg, klf_engine** out) {
       P.qf_mask = cs.qf_mask;
       P.qf_bitmap = e->d_qf_bitmap.as<uint32_t>();
       P.qf_head = e->d_qf_head.as<uint32_t>();
-      P.qf_ent = e->d_qf_ent.as<uint32_t>();
-      P.qf_noff = e->d_qf_noff.as<uint32_t>();
-      P.qf_nlen = e->d_qf_nlen.as<uint32_t>();
-      P.qf_nmeta = e->d_qf_nmeta.as<uint32_t>();
+      P.qf_ent = e->d_qf_ent.as<uint4>();
       P.qf_nbytes = e->d_qf_nbytes.as<uint32_t>();
     }
   }
@@ -248,7 +248,7 @@ extern "C" void klf_close(klf_engine* e) {
   if (e->stream) (void)hipStreamSynchronize(e->stream);
   for (DevBuf* b : {&e->d_lit, &e->d_ac_class, &e->d_ac_next, &e->d_ac_accept, &e->d_rx_class, &e->d_rx_b,
                     &e->d_rx_follow, &e->d_rx_vec, &e->d_rx_flags, &e->d_qf_bitmap, &e->d_qf_head,
-                    &e->d_qf_ent, &e->d_qf_noff, &e->d_qf_nlen, &e->d_qf_nmeta, &e->d_qf_nbytes, &e->d_cand, &e->d_batch, &e->d_segs, &e->d_tstat,
+                    &e->d_qf_ent, &e->d_qf_nbytes, &e->d_rx_vec4, &e->d_cand, &e->d_batch, &e->d_segs, &e->d_tstat,
                     &e->d_slots, &e->d_pool, &e->d_tile_base, &e->d_bsum, &e->d_cstatus, &e->d_counters,
                     &e->d_line_off, &e->d_meta, &e->d_bits, &e->d_segout, &e->d_wpre, &e->d_out, &e->d_tile_seg, &e->d_mpart})
     b->release();
@@ -692,7 +692,7 @@ extern "C" int klf_debug_prefilter(const klf_pattern* pats, uint32_t n, const ui
     info[0] = cs.qf_on ? 1u : 0u;
     info[1] = cs.qf_q;
     info[2] = cs.qf_stride;
-    info[3] = (uint32_t)cs.qf_nlen.size();
+    info[3] = cs.qf_needles;
   }
   if (cs.mode != klf::CompiledSet::kGeneral || !cs.qf_on) return klf_debug_match(pats, n, content, len, match);
   *match = klf::prefilter_match(cs, content, len, phase) ? 1 : 0;

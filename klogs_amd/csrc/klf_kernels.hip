@@ -418,7 +418,7 @@ __global__ __launch_bounds__(kThreads, MODE == kScanGen ? 3 : KLF_SCAN_OCC) void
       }
       // number of listed line starts at or before tile offset pos
       auto starts_upto = [&](int32_t pos) __attribute__((always_inline)) -> int {
-        int lo = 0, hi = (int)nlines;
+        int lo = 0, hi = pos < 0 ? 0 : (int)nlines;  // pos < 0: in the carried-in line
         while (lo < hi) {
           const int mid = (lo + hi) >> 1;
           if ((list[mid] & kSlotOff) <= (uint32_t)pos) lo = mid + 1; else hi = mid;
@@ -434,7 +434,8 @@ __global__ __launch_bounds__(kThreads, MODE == kScanGen ? 3 : KLF_SCAN_OCC) void
           if (!(v & kSlotDefer) && (mt & Meta::kParsed) && (uint32_t)pos >= (v & kSlotOff) + (mt >> 2))
             atomicOr(&list[lo - 1], kSlotHit);
         } else {  // carried in from an earlier tile: k_scatter decides (furthest hit wins)
-          carry = carry > (uint32_t)pos + 1u ? carry : (uint32_t)pos + 1u;
+          const uint32_t c1 = (uint32_t)(pos + 1 + (int32_t)kCarryBias);  // pos >= -kCarryBias
+          carry = carry > c1 ? carry : c1;
         }
       };
       // ---- fused single-literal grep ----
@@ -489,12 +490,13 @@ __global__ __launch_bounds__(kThreads, MODE == kScanGen ? 3 : KLF_SCAN_OCC) void
         carry = wave_max(carry);
       }
       // ---- general sets: fused q-gram prefilter ----
-      // Samples p = 0 mod QS of the tile (every needle is >= q + QS - 1 bytes, so each
-      // occurrence spans one with its gram inside the needle) probe the LDS bitmap;
-      // bitmap hits are verified against the needles of the hash bucket.  A verified
-      // literal is a match (attributed like the fused literal); a verified regex factor
-      // queues (batch offset, regex) for k_nfa.  As with the literal, a tile owns the
-      // occurrences that start in it: the sample at p = kTile (halo) serves its tail.
+      // Samples p = 0 mod QS of the tile (each needle's chosen window is q + QS - 1 long,
+      // so every occurrence spans exactly one sample whose gram lies in the window) probe
+      // the LDS bitmap (two bits per gram); bitmap hits are verified against the 16-B
+      // entries of the hash bucket (first needle dword pre-checked from the entry).  A tile
+      // owns its samples; the occurrence may start before the tile (its line is then the
+      // carried-in one).  A verified literal is a match (attributed like the fused
+      // literal); a verified regex factor queues (batch offset, regex) for k_nfa.
       if (GEN) {
         if (dense) __threadfence_block();
         wave_lds_sync();
@@ -502,63 +504,55 @@ __global__ __launch_bounds__(kThreads, MODE == kScanGen ? 3 : KLF_SCAN_OCC) void
         const uint32_t fold = P.qf_fold, qmask = P.qf_mask;
         const uint32_t* s32 = reinterpret_cast<const uint32_t*>(s_tile);
         uint32_t last_key = ~0u;  // (line, regex) this lane queued last: no duplicate work
-        auto verify = [&](uint32_t h, int32_t p) __attribute__((always_inline)) {
-          const uint32_t b = h >> (kQfBits - kQfBucketBits);
+        // byte at tile offset o (may be negative or past the halo): LDS or global
+        auto tbyte = [&](int32_t o) __attribute__((always_inline)) -> uint32_t {
+          return (o >= 0 && o < kTile + kHalo) ? (uint32_t)s_tile[o] : (uint32_t)segp[rel_lo + o];
+        };
+        // 4 bytes at tile offset o (o >= 0 and o + 8 <= kTile + kHalo: LDS)
+        auto tword = [&](int32_t o) __attribute__((always_inline)) -> uint32_t {
+          if (o >= 0 && o + 8 <= kTile + kHalo)
+            return __builtin_amdgcn_alignbyte(s32[(o >> 2) + 1], s32[o >> 2], (uint32_t)o & 3u);
+          return tbyte(o) | tbyte(o + 1) << 8 | tbyte(o + 2) << 16 | tbyte(o + 3) << 24;
+        };
+        auto verify = [&](uint32_t b, int32_t p) __attribute__((always_inline)) {
           const uint32_t e1 = P.qf_head[b + 1];
           for (uint32_t e = P.qf_head[b]; e < e1; ++e) {
-            const uint32_t ent = P.qf_ent[e];
-            const uint32_t nd = ent >> 2;
-            const int32_t x = p - (int32_t)(ent & 3u);
-            if (x < 0 || x >= tile_len) continue;
-            const uint32_t m = P.qf_nlen[nd];
-            if (rel_lo + (int64_t)x + (int64_t)m > seg_len) continue;
-            const uint32_t meta = P.qf_nmeta[nd];
-            const uint32_t lm = (meta & 0x40000000u) ? 0x20202020u : 0u;
-            const uint32_t* nw = P.qf_nbytes + P.qf_noff[nd];
+            const uint4 E = P.qf_ent[e];
+            const uint32_t m = E.y & 0xFFFFu;
+            const int32_t x = p - (int32_t)((E.y >> 16) & 0xFFu);
+            if (rel_lo + (int64_t)x < 0 || rel_lo + (int64_t)x + (int64_t)m > seg_len) continue;
+            const uint32_t lm = (E.y & kQfLoose) ? 0x20202020u : 0u;
+            const uint32_t m0 = m >= 4 ? 0xFFFFFFFFu : ((1u << (8 * m)) - 1u);
+            if (((tword(x) | lm) ^ E.w) & m0) continue;  // pre-check: the first 4 bytes
             bool eq = true;
-            if ((uint32_t)x + m + 4 <= (uint32_t)(kTile + kHalo)) {
-              const uint32_t sh = (uint32_t)x & 3u;
-              uint32_t wi = (uint32_t)x >> 2;
-              uint32_t prev = s32[wi];
-              for (uint32_t k = 0; k < m && eq; k += 4) {
-                const uint32_t nx = s32[++wi];
-                const uint32_t got = __builtin_amdgcn_alignbyte(nx, prev, sh) | lm;
-                prev = nx;
-                const uint32_t nb = m - k < 4 ? m - k : 4;
-                const uint32_t msk = nb == 4 ? 0xFFFFFFFFu : ((1u << (8 * nb)) - 1);
-                eq = ((got ^ nw[k >> 2]) & msk) == 0;
-              }
-            } else {
-              const uint8_t* nb8 = reinterpret_cast<const uint8_t*>(nw);
-              for (uint32_t k = 0; k < m && eq; ++k) {
-                const uint32_t o = (uint32_t)x + k;
-                const uint8_t cc = o < (uint32_t)(kTile + kHalo) ? s_tile[o] : segp[rel_lo + o];
-                eq = (uint8_t)(cc | (uint8_t)lm) == nb8[k];
-              }
+            for (uint32_t k = 4; k < m && eq; k += 4) {
+              const uint32_t nb = m - k < 4 ? m - k : 4;
+              const uint32_t msk = nb == 4 ? 0xFFFFFFFFu : ((1u << (8 * nb)) - 1);
+              eq = (((tword(x + (int32_t)k) | lm) ^ P.qf_nbytes[E.x + (k >> 2)]) & msk) == 0;
             }
             if (!eq) continue;
-            if (!(meta & 0x80000000u)) {
+            if (!(E.y & kQfRegex)) {
               attribute(x);
               continue;
             }
-            const uint32_t r = meta & 0xFFFFFFu;
-            const uint32_t key = (uint32_t)starts_upto(x) * (uint32_t)kMaxRegexSet + r;
+            const uint32_t key = (uint32_t)starts_upto(x) * kMaxRegexSet + E.z;
             if (key == last_key) continue;
             last_key = key;
             const uint32_t qi = atomicAdd(&a.counters[kCtrQueue], 1u);
-            if (qi < a.cand_cap) a.cand[qi] = (sd.base + (uint64_t)rel_lo + (uint64_t)x) | ((uint64_t)r << 40);
+            if (qi < a.cand_cap) a.cand[qi] = (sd.base + (uint64_t)(rel_lo + x)) | ((uint64_t)E.z << 40);
             else atomicOr(&a.counters[kCtrQOver], 1u);
           }
         };
         auto probe = [&](uint32_t g) __attribute__((always_inline)) -> uint32_t {
-          const uint32_t h = qf_hash((g | fold) & qmask);
-          return (s_qf[h >> 5] >> (h & 31)) & 1u;
+          const uint32_t gf = (g | fold) & qmask;
+          const uint32_t h1 = qf_hash(gf), h2 = qf_hash2(gf);
+          return (s_qf[h1 >> 5] >> (h1 & 31)) & (s_qf[h2 >> 5] >> (h2 & 31)) & 1u;
         };
         // bitmap probes of my samples -> a 128-bit hit mask (bit = byte offset in my range)
         uint32_t hq0 = 0, hq1 = 0, hq2 = 0, hq3 = 0;
         const uint32_t rot = ((uint32_t)lane >> 1) & 7u;
 #pragma unroll
-        for (int v = 0; v < 8; ++v) {
+        for (int v = 0; v < ((KLF_ABL & 4) ? 0 : 8); ++v) {
           const uint32_t c = ((uint32_t)v + rot) & 7u;
           const uint32_t o0 = my0 + 16u * c;
           const uint4 x = *reinterpret_cast<const uint4*>(s_tile + o0);
@@ -579,18 +573,18 @@ __global__ __launch_bounds__(kThreads, MODE == kScanGen ? 3 : KLF_SCAN_OCC) void
           hq2 |= q == 2 ? hm : 0u;
           hq3 |= q == 3 ? hm : 0u;
         }
+#if KLF_ABL & 8
+        any_defer |= (hq0 | hq1 | hq2 | hq3) == 0xFFFFFFFFu;  // timing build: probes only
+        hq0 = hq1 = hq2 = hq3 = 0;
+#endif
         const uint32_t hq[4] = {hq0, hq1, hq2, hq3};
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           for (uint32_t m = hq[q]; m; m &= m - 1u) {
             const uint32_t p = my0 + 32u * q + (uint32_t)__builtin_ctz(m);
-            const uint32_t g = __builtin_amdgcn_alignbyte(s32[(p >> 2) + 1], s32[p >> 2], p & 3u);
-            verify(qf_hash((g | fold) & qmask), (int32_t)p);
+            const uint32_t g = (__builtin_amdgcn_alignbyte(s32[(p >> 2) + 1], s32[p >> 2], p & 3u) | fold) & qmask;
+            verify(qf_hash(g) >> (kQfBits - kQfBucketBits), (int32_t)p);
           }
-        }
-        if (QS > 1 && lane == 63 && !last) {
-          const uint32_t g = s32[kTile >> 2];
-          if (probe(g)) verify(qf_hash((g | fold) & qmask), kTile);
         }
         carry = wave_max(carry);
       }
@@ -854,7 +848,8 @@ __global__ __launch_bounds__(256) void k_scatter(RunArgs a) {
           if ((mt & Meta::kParsed) && !(v & kSlotDefer)) cs = prel + (int64_t)(v & kSlotOff) + (mt >> 2);
           break;
         }
-        if (cs >= 0 && rel_lo + (int64_t)ts.carry_off - 1 >= cs) atomicOr(&a.bits[base >> 5], 1u << (base & 31));
+        if (cs >= 0 && rel_lo + (int64_t)ts.carry_off - 1 - (int64_t)kCarryBias >= cs)
+          atomicOr(&a.bits[base >> 5], 1u << (base & 31));
       }
       if (last) {
         const uint64_t lend = base + ts.events;
@@ -939,11 +934,119 @@ __device__ __forceinline__ uint32_t line_plen(const RunArgs& a, uint16_t meta, c
 // K2b: the prefiltered regex stage.  One lane per queued (batch offset, regex) candidate:
 // the offset's stream and line (binary searches over the segment table and the line
 // index), then the Glushkov NFA of that regex over the line's content.  Lines already
-// matched are skipped.
+// matched are skipped.  LDS: the regex tables (byte classes, B[regex][class],
+// follow[regex][position < maxpos], first/last/init0/end) are staged once per block;
+// content is read 16 B at a time and the 16 class / B lookups of a block are issued
+// before the state recurrence walks it (only the follow lookups depend on the state).
+struct NfaTables {
+  const uint8_t* cls;
+  const uint64_t* b;      // [rx][classes]
+  const uint64_t* fol;    // [rx][fstride]
+  const uint64_t* vec;    // [rx][4]: first, last, init0, end
+  uint32_t classes, fstride;
+};
+
+// Runs regex r over p[0, n) from entered set d.  inject: unanchored search (first is
+// entered at every boundary); without it only the given set is followed and the run
+// stops as soon as it dies out.  Sets hit on a match; returns the entered set at the end.
+__device__ __forceinline__ uint64_t nfa_chunk(const NfaTables& T, uint32_t r, const uint8_t* p, uint64_t n,
+                                              uint64_t d, bool inject, bool& hit) {
+  const uint64_t* V = T.vec + 4 * (size_t)r;
+  const uint64_t first = inject ? V[0] : 0ull, lastm = V[1];
+  const uint64_t* B = T.b + (size_t)r * T.classes;
+  const uint64_t* F = T.fol + (size_t)r * T.fstride;
+  const uintptr_t a0 = reinterpret_cast<uintptr_t>(p);
+  const uint4* q = reinterpret_cast<const uint4*>(a0 & ~(uintptr_t)15);
+  uint32_t skip = (uint32_t)(a0 & 15);  // bytes of the first block before p
+  uint64_t left = n;
+  while (left) {
+    if (!inject && d == 0) return 0;
+    const uint4 v = *q++;
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    uint64_t bm[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) bm[j] = B[T.cls[(w[j >> 2] >> (8 * (j & 3))) & 0xFFu]];
+    const uint32_t j0 = skip;
+    const uint32_t j1 = (uint64_t)(16 - skip) < left ? 16u : skip + (uint32_t)left;
+    left -= j1 - j0;
+    skip = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < 16; ++j) {
+      if (j < j0 || j >= j1) continue;
+      const uint64_t c = d & bm[j];
+      if (c & lastm) { hit = true; return 0; }
+      uint64_t nd = first;
+      for (uint64_t m = c; m; m &= m - 1) nd |= F[__ffsll((unsigned long long)m) - 1];
+      d = nd;
+    }
+  }
+  return d;
+}
+
+// One wave decides regex r on content p[0, n): the content is cut into <= 64 chunks
+// (16-B multiples), every lane runs its chunk from the fresh state (init0 for chunk 0,
+// `first` otherwise; every reachable state contains `first`).  The transition is a union
+// homomorphism (delta(A u B) = delta(A) u delta'(B), delta' without the injection of
+// `first`), so the partial matches crossing chunk boundaries are then followed by extra
+// runs of delta' from the boundary states, rounds until no extra state survives a chunk.
+__device__ bool nfa_wave(const NfaTables& T, uint32_t r, const uint8_t* p, uint64_t n, int lane) {
+  const uint64_t* V = T.vec + 4 * (size_t)r;
+  const uint64_t first = V[0];
+  uint64_t L = (n + 63) / 64;
+  L = (L + 15) & ~15ull;
+  const uint32_t nc = (uint32_t)((n + L - 1) / L);
+  const bool mine = (uint32_t)lane < nc;
+  const uint64_t lo = mine ? (uint64_t)lane * L : 0, hi = mine ? (lo + L < n ? lo + L : n) : 0;
+  bool hit = false;
+  uint64_t e = 0;
+  if (mine) e = nfa_chunk(T, r, p + lo, hi - lo, lane == 0 ? V[2] : first, true, hit);
+  if (__any(hit)) return true;
+  uint64_t fin = (uint32_t)lane == nc - 1 ? e : 0;  // entered set after the last byte
+  uint64_t x = __shfl_up(e & ~first, 1, 64);
+  if (lane == 0 || !mine) x = 0;
+  for (int round = 0; round < 64 && __any(x != 0); ++round) {
+    uint64_t y = 0;
+    if (x) y = nfa_chunk(T, r, p + lo, hi - lo, x, false, hit);
+    if (__any(hit)) return true;
+    if ((uint32_t)lane == nc - 1) fin |= y;
+    x = __shfl_up(y, 1, 64);
+    if (lane == 0 || !mine) x = 0;
+  }
+  const uint64_t f = __shfl(fin, (int)nc - 1, 64);
+  return (f & V[3]) != 0;
+}
+
+template <bool LDS>
 __global__ __launch_bounds__(256) void k_nfa(RunArgs a) {
+  extern __shared__ uint64_t s_nfa[];
   if (a.counters[2] || a.counters[kCtrQOver]) return;  // overflow: k_match decides every line
   const uint32_t nq = a.counters[kCtrQueue] < a.cand_cap ? a.counters[kCtrQueue] : a.cand_cap;
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nq; i += gridDim.x * blockDim.x) {
+  if (nq == 0 || blockIdx.x * (blockDim.x / 64) >= nq) return;  // one wave per candidate
+  const DevPatterns& P = a.pats;
+  const uint32_t R = P.rx_count, C = P.rx_classes, FS = LDS ? P.rx_maxpos : 64;
+  NfaTables T;
+  if (LDS) {
+    uint64_t* sb = s_nfa;                      // [R][C]
+    uint64_t* sf = sb + (size_t)R * C;          // [R][FS]
+    uint64_t* sv = sf + (size_t)R * FS;         // [R][4]
+    uint8_t* sc = reinterpret_cast<uint8_t*>(sv + 4 * (size_t)R);
+    for (uint32_t i = threadIdx.x; i < R * C; i += blockDim.x) sb[i] = P.rx_b[i];
+    for (uint32_t i = threadIdx.x; i < R * FS; i += blockDim.x) sf[i] = P.rx_follow[(size_t)(i / FS) * 64 + i % FS];
+    for (uint32_t i = threadIdx.x; i < R; i += blockDim.x) {
+      sv[4 * i] = P.rx_first[i];
+      sv[4 * i + 1] = P.rx_last[i];
+      sv[4 * i + 2] = P.rx_init0[i];
+      sv[4 * i + 3] = P.rx_end[i];
+    }
+    for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) sc[i] = P.rx_class[i];
+    __syncthreads();
+    T = NfaTables{sc, sb, sf, sv, C, FS};
+  } else {
+    T = NfaTables{P.rx_class, P.rx_b, P.rx_follow, P.rx_vec, C, 64};
+  }
+  const int lane = threadIdx.x & 63;
+  const uint32_t nw = gridDim.x * (blockDim.x / 64);
+  for (uint32_t i = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6); i < nq; i += nw) {
     const uint64_t e = a.cand[i];
     const uint64_t pos = e & ((1ull << 40) - 1);
     const uint32_t r = (uint32_t)(e >> 40);
@@ -968,7 +1071,9 @@ __global__ __launch_bounds__(256) void k_nfa(RunArgs a) {
     const uint32_t plen = line_plen(a, m, segp, ls, le);
     uint64_t cs = ls + plen, ce = le;
     if (ce > cs && segp[ce - 1] == '\n') --ce;
-    if (ce > cs && rx_match(a.pats, r, segp + cs, (int64_t)(ce - cs))) atomicOr(&a.bits[l >> 5], 1u << (l & 31));
+    if (ce <= cs) continue;  // factor-bearing regexes never match empty content
+    const bool hit = (P.rx_flags[r] & 1u) || nfa_wave(T, r, segp + cs, ce - cs, lane);
+    if (hit && lane == 0) atomicOr(&a.bits[l >> 5], 1u << (l & 31));
   }
 }
 
@@ -1432,6 +1537,10 @@ hipError_t clear_timeline() {
 #endif
 }
 
+size_t nfa_lds_bytes(const DevPatterns& P) {
+  return 8ull * P.rx_count * (P.rx_classes + P.rx_maxpos + 4) + 256;
+}
+
 template <int MODE, int QS>
 hipError_t launch_scan(const RunArgs& a, hipStream_t st, int num_cus) {
   int occ = 0;
@@ -1487,7 +1596,11 @@ hipError_t launch_pipeline(const RunArgs& a, hipStream_t st, hipEvent_t* ev, int
   KLF_TRY(hipGetLastError());
   KLF_TRY(hipEventRecord(ev[2], st));
   if (a.grep_mode == kGrepGeneral && a.pats.qf_on && a.pats.rx_count) {
-    hipLaunchKernelGGL(k_nfa, dim3(num_cus * 4), dim3(256), 0, st, a);
+    const size_t lds = nfa_lds_bytes(a.pats);
+    if (lds <= kNfaMaxLds)
+      hipLaunchKernelGGL(k_nfa<true>, dim3(num_cus * 4), dim3(256), lds, st, a);
+    else
+      hipLaunchKernelGGL(k_nfa<false>, dim3(num_cus * 4), dim3(256), 0, st, a);
     KLF_TRY(hipGetLastError());
   }
   if (a.grep_mode == kGrepGeneral || a.grep_mode == kGrepAll) {

@@ -32,7 +32,12 @@ constexpr uint32_t kQfMaxFactor = 32;                // regex factors are cut to
 constexpr uint32_t kMaxRegexSet = 1024;              // = klf_patterns.hpp kMaxRegexes
 constexpr uint32_t kCtrQueue = 6;                   // counters[6]: NFA candidate queue length
 constexpr uint32_t kCtrQOver = 7;                    // counters[7]: queue overflow -> k_match
+constexpr uint32_t kQfRegex = 1u << 24;              // entry flags: regex factor (else literal)
+constexpr uint32_t kQfLoose = 1u << 25;              //   compare OR 0x20 per byte
+constexpr size_t kNfaMaxLds = 64 * 1024;            // k_nfa stages its tables in LDS up to this
+constexpr uint32_t kCarryBias = 256;                 // TileStat.carry_off = hit offset + 1 + bias
 __host__ __device__ inline uint32_t qf_hash(uint32_t g) { return (g * 0x9E3779B1u) >> (32 - kQfBits); }
+__host__ __device__ inline uint32_t qf_hash2(uint32_t g) { return (g * 0x85EBCA77u) >> (32 - kQfBits); }
 
 // Per-tile record of the scan (K1a), 16 B.
 struct TileStat {
@@ -41,7 +46,8 @@ struct TileStat {
   uint16_t parsed, since_ok;
   uint16_t flags;      // bit0 dense (slots in the pool), bit1 literal hit in the carried-in line,
                        // bit2 some line deferred to k_fixup
-  uint16_t carry_off;  // 1 + offset of the furthest literal hit in the carried-in line (0 = none)
+  uint16_t carry_off;  // 1 + kCarryBias + tile offset (>= -kCarryBias) of the furthest final hit in
+                       // the carried-in line (0 = none)
 };
 static_assert(sizeof(TileStat) == 16, "TileStat is one 16-B store");
 
@@ -85,16 +91,14 @@ struct DevPatterns {  // device copies of CompiledSet tables (kGrepGeneral)
   const uint64_t* rx_last = nullptr;
   const uint64_t* rx_init0 = nullptr;
   const uint64_t* rx_end = nullptr;
+  const uint64_t* rx_vec = nullptr;   // [rx_count][4]: first, last, init0, end
   const uint32_t* rx_flags = nullptr;
-  uint32_t rx_count = 0, rx_classes = 0;
+  uint32_t rx_count = 0, rx_classes = 0, rx_maxpos = 64;
   // q-gram prefilter (qf_on): bitmap, buckets, needles
   uint32_t qf_on = 0, qf_stride = 1, qf_fold = 0, qf_mask = ~0u;
   const uint32_t* qf_bitmap = nullptr;
   const uint32_t* qf_head = nullptr;
-  const uint32_t* qf_ent = nullptr;
-  const uint32_t* qf_noff = nullptr;
-  const uint32_t* qf_nlen = nullptr;
-  const uint32_t* qf_nmeta = nullptr;
+  const uint4* qf_ent = nullptr;
   const uint32_t* qf_nbytes = nullptr;
 };
 

@@ -817,7 +817,13 @@ bool compile_set(const std::vector<std::vector<uint8_t>>& pats, const std::vecto
       rxs.push_back(std::move(g));
       std::vector<std::string> alts;
       bool loose = false;
-      regex_factors(pats[k].data(), pats[k].size(), alts, loose);
+      if (regex_factors(pats[k].data(), pats[k].size(), alts, loose)) {
+        // content never holds '\n': such alternatives cannot occur; none left = no match ever
+        alts.erase(std::remove_if(alts.begin(), alts.end(),
+                                  [](const std::string& f) { return f.find('\n') != std::string::npos; }),
+                   alts.end());
+        if (alts.empty()) { rxs.pop_back(); continue; }
+      }
       rx_fac.push_back(alts);
       rx_loose.push_back(loose);
     } else {
@@ -935,6 +941,7 @@ bool compile_set(const std::vector<std::vector<uint8_t>>& pats, const std::vecto
     out.rx_follow.assign((size_t)rxs.size() * 64, 0);
     for (size_t r = 0; r < rxs.size(); ++r) {
       for (int p = 0; p < rxs[r].npos; ++p) out.rx_follow[r * 64 + p] = rxs[r].follow[p];
+      out.rx_maxpos = std::max<uint32_t>(out.rx_maxpos, (uint32_t)rxs[r].npos);
       out.rx_first.push_back(rxs[r].first);
       out.rx_last.push_back(rxs[r].last);
       out.rx_init0.push_back(rxs[r].init0);
@@ -949,17 +956,23 @@ bool compile_set(const std::vector<std::vector<uint8_t>>& pats, const std::vecto
 // q-gram prefilter tables (CompiledSet::qf_*).  Off (k_match decides every line) when a
 // literal or some regex's best factor is shorter than kQfMinNeedle, or a regex can match
 // without any factor (e.g. `\d+`): those need a look at every line anyway.
+//
+// Each needle is sampled through a window of q + S - 1 of its bytes (any substring of a
+// literal / factor occurs wherever the needle does): the window whose S grams are the
+// least common in log text and among the needles already placed, so that grams like
+// "user" or a prefix shared by many literals do not flood the verification buckets.
+// Every gram sets two bits of the bitmap (Bloom, k = 2).
 void build_prefilter(const std::vector<std::vector<uint8_t>>& lits, const std::vector<std::vector<std::string>>& rx_fac,
                      const std::vector<bool>& rx_loose, CompiledSet& out) {
   struct Needle {
     std::string s;
-    uint32_t meta;
+    uint32_t flags, rx;
   };
   std::vector<Needle> nd;
-  for (auto& l : lits) nd.push_back({std::string(l.begin(), l.end()), 0u});
+  for (auto& l : lits) nd.push_back({std::string(l.begin(), l.end()), 0u, 0u});
   for (size_t r = 0; r < rx_fac.size(); ++r) {
     if (rx_fac[r].empty()) { out.qf_why = "regex " + std::to_string(r) + " has no required literal factor"; return; }
-    for (auto& s : rx_fac[r]) nd.push_back({s, 0x80000000u | (rx_loose[r] ? 0x40000000u : 0u) | (uint32_t)r});
+    for (auto& f : rx_fac[r]) nd.push_back({f, kQfRegex | (rx_loose[r] ? kQfLoose : 0u), (uint32_t)r});
   }
   if (nd.empty()) { out.qf_why = "no needles"; return; }
   if (nd.size() > (1u << 24)) { out.qf_why = "too many needles"; return; }
@@ -967,7 +980,7 @@ void build_prefilter(const std::vector<std::vector<uint8_t>>& lits, const std::v
   bool loose = false;
   for (auto& n : nd) {
     minlen = std::min(minlen, n.s.size());
-    loose |= (n.meta & 0x40000000u) != 0;
+    loose |= (n.flags & kQfLoose) != 0;
   }
   if (minlen < kQfMinNeedle) { out.qf_why = "a needle is shorter than 3 bytes"; return; }
   const uint32_t q = (uint32_t)std::min<size_t>(4, minlen);
@@ -978,66 +991,96 @@ void build_prefilter(const std::vector<std::vector<uint8_t>>& lits, const std::v
   out.qf_fold = loose ? 0x20202020u : 0u;
   out.qf_mask = q == 4 ? ~0u : ((1u << (8 * q)) - 1u);
   out.qf_bitmap.assign(kQfWords, 0u);
+  auto gram_at = [&](const std::string& s, uint32_t k) {
+    uint32_t g = 0;
+    for (uint32_t b = 0; b < q; ++b) g |= (uint32_t)(uint8_t)s[k + b] << (8 * b);
+    return (g | out.qf_fold) & out.qf_mask;
+  };
+  auto common = [&](uint8_t c) -> int {  // rough frequency rank of a byte in log text
+    if (loose && c >= 'A' && c <= 'Z') c |= 0x20;
+    if ((c >= 'a' && c <= 'z') || c == ' ') return 4;
+    if (c == '"' || c == ':' || c == ',' || c == '=' || c == '.' || c == '/' || c == '{' || c == '}' ||
+        (c >= '0' && c <= '9'))
+      return 2;
+    return 1;  // upper case, '_', '-', other punctuation, control and high bytes
+  };
+  std::map<uint32_t, int> used;  // gram -> needles sampling it so far
   std::vector<std::vector<uint32_t>> buckets(1u << kQfBucketBits);
   for (uint32_t i = 0; i < nd.size(); ++i) {
     const std::string& s = nd[i].s;
-    for (uint32_t k = 0; k < S; ++k) {
-      uint32_t g = 0;
-      for (uint32_t b = 0; b < q; ++b) g |= (uint32_t)(uint8_t)s[k + b] << (8 * b);
-      const uint32_t h = qf_hash((g | out.qf_fold) & out.qf_mask);
-      out.qf_bitmap[h >> 5] |= 1u << (h & 31);
-      buckets[h >> (kQfBits - kQfBucketBits)].push_back(i << 2 | k);
+    const uint32_t amax = (uint32_t)std::min<size_t>(s.size() - (q + S - 1), 255 - (S - 1));
+    uint32_t best_a = 0;
+    int best = INT32_MAX;
+    for (uint32_t a = 0; a <= amax; ++a) {
+      int sc = 0;
+      for (uint32_t j = 0; j < S; ++j) {
+        int c = 0;
+        for (uint32_t b = 0; b < q; ++b) c += common((uint8_t)s[a + j + b]);
+        auto it = used.find(gram_at(s, a + j));
+        sc = std::max(sc, c + 6 * (it == used.end() ? 0 : it->second));
+      }
+      if (sc < best) { best = sc; best_a = a; }
+    }
+    for (uint32_t j = 0; j < S; ++j) {
+      const uint32_t k = best_a + j, g = gram_at(s, k);
+      used[g]++;
+      const uint32_t h1 = qf_hash(g), h2 = qf_hash2(g);
+      out.qf_bitmap[h1 >> 5] |= 1u << (h1 & 31);
+      out.qf_bitmap[h2 >> 5] |= 1u << (h2 & 31);
+      buckets[h1 >> (kQfBits - kQfBucketBits)].push_back(i << 8 | k);
     }
   }
-  out.qf_head.assign((1u << kQfBucketBits) + 1, 0u);
-  for (uint32_t b = 0; b < buckets.size(); ++b) {
-    out.qf_head[b] = (uint32_t)out.qf_ent.size();
-    out.qf_ent.insert(out.qf_ent.end(), buckets[b].begin(), buckets[b].end());
-  }
-  out.qf_head[buckets.size()] = (uint32_t)out.qf_ent.size();
+  // needle bytes (loose needles are already stored OR 0x20), then 16-B entries per bucket
+  std::vector<uint32_t> noff;
   for (auto& n : nd) {
-    out.qf_noff.push_back((uint32_t)out.qf_nbytes.size());
-    out.qf_nlen.push_back((uint32_t)n.s.size());
-    out.qf_nmeta.push_back(n.meta);
+    noff.push_back((uint32_t)out.qf_nbytes.size());
     for (size_t b = 0; b < n.s.size(); b += 4) {
       uint32_t w = 0;
       for (size_t j = 0; j < 4 && b + j < n.s.size(); ++j) w |= (uint32_t)(uint8_t)n.s[b + j] << (8 * j);
       out.qf_nbytes.push_back(w);
     }
   }
+  out.qf_head.assign((1u << kQfBucketBits) + 1, 0u);
+  for (uint32_t b = 0; b < buckets.size(); ++b) {
+    out.qf_head[b] = (uint32_t)(out.qf_ent.size() / 4);
+    for (uint32_t v : buckets[b]) {
+      const Needle& n = nd[v >> 8];
+      out.qf_ent.push_back(noff[v >> 8]);
+      out.qf_ent.push_back((uint32_t)n.s.size() | (v & 0xFFu) << 16 | n.flags);
+      out.qf_ent.push_back(n.rx);
+      out.qf_ent.push_back(out.qf_nbytes[noff[v >> 8]]);  // first dword: the pre-check
+    }
+  }
+  out.qf_head[buckets.size()] = (uint32_t)(out.qf_ent.size() / 4);
+  out.qf_needles = (uint32_t)nd.size();
   out.qf_on = true;
 }
 
-namespace {
-// needle `i` at s[x ..): exact, or OR 0x20 per byte when loose
-bool needle_at(const CompiledSet& cs, uint32_t i, const uint8_t* s, size_t n, int64_t x) {
-  const uint32_t m = cs.qf_nlen[i];
-  if (x < 0 || (uint64_t)x + m > n) return false;
-  const uint8_t* nb = reinterpret_cast<const uint8_t*>(cs.qf_nbytes.data() + cs.qf_noff[i]);
-  const uint8_t lm = (cs.qf_nmeta[i] & 0x40000000u) ? 0x20 : 0;
-  for (uint32_t k = 0; k < m; ++k)
-    if ((uint8_t)(s[x + k] | lm) != nb[k]) return false;
-  return true;
-}
-}  // namespace
-
 bool prefilter_match(const CompiledSet& cs, const uint8_t* s, size_t n, uint32_t phase) {
-  // Any window of S consecutive positions holds a sample, and every needle is at least
-  // q + S - 1 long, so each occurrence spans a sample with its gram inside the needle.
+  // Any window of S consecutive positions holds a sample, and every needle's chosen
+  // window is q + S - 1 long, so each occurrence spans one sample with its gram inside
+  // the window (the scan's tiles own their samples; the occurrence may start before).
   std::vector<uint8_t> cand(cs.rx_count, 0);
   const uint32_t S = cs.qf_stride;
   for (size_t p = phase % S; p < n; p += S) {
     uint32_t g = 0;
     for (uint32_t b = 0; b < 4; ++b) g |= (uint32_t)(p + b < n ? s[p + b] : 0) << (8 * b);
-    const uint32_t h = qf_hash((g | cs.qf_fold) & cs.qf_mask);
-    if (!((cs.qf_bitmap[h >> 5] >> (h & 31)) & 1u)) continue;
-    const uint32_t b = h >> (kQfBits - kQfBucketBits);
+    g = (g | cs.qf_fold) & cs.qf_mask;
+    const uint32_t h1 = qf_hash(g), h2 = qf_hash2(g);
+    if (!((cs.qf_bitmap[h1 >> 5] >> (h1 & 31)) & (cs.qf_bitmap[h2 >> 5] >> (h2 & 31)) & 1u)) continue;
+    const uint32_t b = h1 >> (kQfBits - kQfBucketBits);
     for (uint32_t e = cs.qf_head[b]; e < cs.qf_head[b + 1]; ++e) {
-      const uint32_t i = cs.qf_ent[e] >> 2;
-      const int64_t x = (int64_t)p - (int64_t)(cs.qf_ent[e] & 3u);
-      if (!needle_at(cs, i, s, n, x)) continue;
-      if (!(cs.qf_nmeta[i] & 0x80000000u)) return true;  // literal: final
-      cand[cs.qf_nmeta[i] & 0xFFFFFFu] = 1;
+      const uint32_t* E = cs.qf_ent.data() + 4 * (size_t)e;
+      const uint32_t m = E[1] & 0xFFFFu, k = (E[1] >> 16) & 0xFFu;
+      const int64_t x = (int64_t)p - (int64_t)k;
+      if (x < 0 || (uint64_t)x + m > n) continue;
+      const uint8_t* nb = reinterpret_cast<const uint8_t*>(cs.qf_nbytes.data() + E[0]);
+      const uint8_t lm = (E[1] & kQfLoose) ? 0x20 : 0;
+      bool eq = true;
+      for (uint32_t j = 0; j < m && eq; ++j) eq = (uint8_t)(s[x + j] | lm) == nb[j];
+      if (!eq) continue;
+      if (!(E[1] & kQfRegex)) return true;  // literal: final
+      cand[E[2]] = 1;
     }
   }
   for (uint32_t r = 0; r < cs.rx_count; ++r) {

@@ -60,6 +60,7 @@ struct CompiledSet {
   std::vector<uint64_t> rx_follow;    // [rx_count * 64]
   std::vector<uint64_t> rx_first, rx_last, rx_init0, rx_end;  // [rx_count]
   std::vector<uint32_t> rx_flags;     // bit0 accept_at_start, bit1 accept_empty
+  uint32_t rx_maxpos = 0;             // most Glushkov positions of any regex
 
   // kGeneral: q-gram prefilter fused into the scan (qf_on).  Needles = the literals
   // (final: a verified hit is a match) and one required factor set per regex (a verified
@@ -71,14 +72,12 @@ struct CompiledSet {
   uint32_t qf_stride = 1;    // 1, 2 or 4
   uint32_t qf_fold = 0;      // 0x20202020 when some needle compares case-insensitively
   uint32_t qf_mask = ~0u;    // gram bytes (q < 4: low q bytes)
-  std::vector<uint32_t> qf_bitmap;   // [1 << (kQfBits - 5)]
-  std::vector<uint32_t> qf_head;     // [(1 << kQfBucketBits) + 1] bucket -> first entry
-  std::vector<uint32_t> qf_ent;      // needle << 2 | offset of the gram in the needle
-  std::vector<uint32_t> qf_noff;     // [needles] dword offset of the needle's bytes
-  std::vector<uint32_t> qf_nlen;     // [needles]
-  std::vector<uint32_t> qf_nmeta;    // [needles] bit31 regex factor, bit30 loose compare,
-                                     // low 24 bits regex index
+  std::vector<uint32_t> qf_bitmap;   // [kQfWords]: 2 bits (qf_hash, qf_hash2) per gram
+  std::vector<uint32_t> qf_head;     // [(1 << kQfBucketBits) + 1] bucket (top bits of qf_hash) -> entry
+  std::vector<uint32_t> qf_ent;      // 16-B entries {needle dword offset, len | k << 16 | flags,
+                                     //  regex, first needle dword}; k = offset of the gram
   std::vector<uint32_t> qf_nbytes;   // needle bytes, each padded to whole dwords
+  uint32_t qf_needles = 0;
   std::string qf_why;                // why the prefilter is off (diagnostics)
 };
 

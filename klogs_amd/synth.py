@@ -30,7 +30,8 @@ def c4_literals(n: int = 1024):
     out, seen, i = [], set(), 0
     buf = C.create_string_buffer(32)
     while len(out) < n:
-        b = buf.raw[:_lib.ks_c4_literal(i, buf)]
+        m = _lib.ks_c4_literal(i, buf)  # call first: buf.raw[:f(buf)] would read the stale buffer
+        b = buf.raw[:m]
         if b not in seen:
             seen.add(b)
             out.append(b)
@@ -40,7 +41,8 @@ def c4_literals(n: int = 1024):
 
 def c5_pattern(r: int, which: int) -> bytes:
     buf = C.create_string_buffer(128)
-    return buf.raw[:_lib.ks_c5_pattern(r, which, buf, 128)]
+    m = _lib.ks_c5_pattern(r, which, buf, 128)
+    return buf.raw[:m]
 
 
 def c5_regexes():

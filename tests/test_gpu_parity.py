@@ -171,6 +171,7 @@ GEN_SETS = [
     ([b"pod", b"ready"], []),
     ([], [rb"(?i)ERR_CONN_\w+", rb"user= ?\w+ took"]),
     ([b"ab"], [rb"\d+"]),  # prefilter off: k_match decides every line
+    ([b"READY_X"], [rb"a\nb", rb"took \d+ms"]),  # a factor holding "\n" never occurs in content
 ]
 
 
