@@ -59,8 +59,9 @@ struct klf_engine {
   std::vector<std::vector<uint8_t>> staged;
   // device pattern tables
   DevBuf d_lit, d_ac_class, d_ac_next, d_ac_accept, d_rx_class, d_rx_b, d_rx_follow, d_rx_vec, d_rx_flags;
-  DevBuf d_qf_bitmap, d_qf_head, d_qf_ent, d_qf_nbytes, d_cand, d_rx_vec4;
+  DevBuf d_qf_bitmap, d_qf_head, d_qf_ent, d_qf_nbytes, d_cand, d_rx_vec4, d_qhits, d_hslots;
   uint32_t cand_cap = 1u << 22;  // NFA candidate queue (32 MiB); overflow -> k_match
+  uint64_t hits_cap_max = 1u << 26;  // prefilter hit list (512 MiB at most); overflow -> k_match
   klf::DevPatterns dpats;
   // workspace
   std::vector<SegDesc> last_segs;  // tile_seg cache key
@@ -238,6 +239,8 @@ extern "C" int klf_open(const klf_config* cfg, klf_engine** out) {
   }
   if (const char* cc = getenv("KLF_CAND_CAP"))  // tests: force the queue-overflow fallback
     e->cand_cap = (uint32_t)std::max(1L, std::min(atol(cc), 1L << 28));
+  if (const char* hc = getenv("KLF_HITS_CAP"))  // tests: force the hit-list overflow fallback
+    e->hits_cap_max = (uint64_t)std::max(1L, std::min(atol(hc), 1L << 28));
   if (cfg->staging_hint) e->staged.reserve(16);
   *out = e;
   return KLF_OK;
@@ -248,7 +251,7 @@ extern "C" void klf_close(klf_engine* e) {
   if (e->stream) (void)hipStreamSynchronize(e->stream);
   for (DevBuf* b : {&e->d_lit, &e->d_ac_class, &e->d_ac_next, &e->d_ac_accept, &e->d_rx_class, &e->d_rx_b,
                     &e->d_rx_follow, &e->d_rx_vec, &e->d_rx_flags, &e->d_qf_bitmap, &e->d_qf_head,
-                    &e->d_qf_ent, &e->d_qf_nbytes, &e->d_rx_vec4, &e->d_cand, &e->d_batch, &e->d_segs, &e->d_tstat,
+                    &e->d_qf_ent, &e->d_qf_nbytes, &e->d_rx_vec4, &e->d_qhits, &e->d_hslots, &e->d_cand, &e->d_batch, &e->d_segs, &e->d_tstat,
                     &e->d_slots, &e->d_pool, &e->d_tile_base, &e->d_bsum, &e->d_cstatus, &e->d_counters,
                     &e->d_line_off, &e->d_meta, &e->d_bits, &e->d_segout, &e->d_wpre, &e->d_out, &e->d_tile_seg, &e->d_mpart})
     b->release();
@@ -364,13 +367,22 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
   HIPCHK(e, e->d_out.ensure(total_bytes + 64), "alloc out");
   const bool need_cand = mode == klf::CompiledSet::kGeneral && e->cs.qf_on && e->cs.rx_count;
   if (need_cand) HIPCHK(e, e->d_cand.ensure((size_t)e->cand_cap * 8), "alloc cand");
+  const bool need_hits = mode == klf::CompiledSet::kGeneral && e->cs.qf_on;
+  // bitmap hits: < 1 per 8 KiB tile on log text, kHitSlots per tile recorded in place;
+  // spills beyond 1 per 1 KiB of input -> k_match decides
+  const uint32_t qhits_cap = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(total_bytes / 1024, 1u << 16),
+                                                          e->hits_cap_max);
+  if (need_hits) {
+    HIPCHK(e, e->d_qhits.ensure((size_t)qhits_cap * 8), "alloc qhits");
+    HIPCHK(e, e->d_hslots.ensure((size_t)ntiles * klf::kHitSlots * 2), "alloc hslots");
+  }
 
   for (int attempt = 0; attempt < 2; ++attempt) {
     const uint64_t max_cblocks = cap / klf::kCompactLines + 2;
     HIPCHK(e, e->d_line_off.ensure((cap + nsegs + 1) * 8), "alloc line_off");
     HIPCHK(e, e->d_meta.ensure(cap * 2 + 16), "alloc meta");
     HIPCHK(e, e->d_bits.ensure((cap / 32 + 1) * 4), "alloc bits");
-    HIPCHK(e, e->d_cstatus.ensure(max_cblocks * 2 * 8), "alloc cstatus");
+    HIPCHK(e, e->d_cstatus.ensure((max_cblocks + 1) * 3 * 8), "alloc cstatus");
     HIPCHK(e, e->d_mpart.ensure((cap / klf::kMatchChunk + 2) * 8), "alloc mpart");
     HIPCHK(e, e->d_pool.ensure(e->pool_cap * 4), "alloc pool");
     klf::RunArgs a{};
@@ -417,13 +429,20 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
     a.max_cblocks = (uint32_t)max_cblocks;
     a.cand = need_cand ? e->d_cand.as<uint64_t>() : nullptr;
     a.cand_cap = need_cand ? e->cand_cap : 0;
+    a.qhits = need_hits ? e->d_qhits.as<uint64_t>() : nullptr;
+    a.hslots = need_hits ? e->d_hslots.as<uint16_t>() : nullptr;
+    a.qhits_cap = need_hits ? qhits_cap : 0;
     HIPCHK(e, klf::launch_pipeline(a, st, e->ev, e->num_cus), "launch");
     r->so.resize(nsegs);
-    uint32_t counters[8];
+    uint32_t counters[16];
     HIPCHK(e, hipMemcpyAsync(r->so.data(), e->d_segout.p, nsegs * sizeof(SegOut), hipMemcpyDeviceToHost, st), "D2H segout");
     HIPCHK(e, hipMemcpyAsync(counters, e->d_counters.p, sizeof(counters), hipMemcpyDeviceToHost, st), "D2H counters");
     HIPCHK(e, hipStreamSynchronize(st), "sync");
     e->last_segs = segs;
+    if (getenv("KLF_DIAG"))
+      fprintf(stderr, "[klf] hits=%u spilled=%u hits_over=%u nfa_queue=%u queue_over=%u deferred=%u\n",
+              counters[klf::kCtrVerified], counters[klf::kCtrHits], counters[klf::kCtrHitsOver],
+              counters[klf::kCtrQueue], counters[klf::kCtrQOver], counters[5]);
     if (counters[2] & 1u) {  // more lines (or dense-tile slots) than estimated: rerun with exact sizes
       cap = std::max<uint64_t>(cap, r->so[nsegs - 1].line_hi + 2);
       e->pool_cap = std::max<uint64_t>(e->pool_cap, (uint64_t)counters[klf::kCtrPool] + 1024);

@@ -489,105 +489,6 @@ __global__ __launch_bounds__(kThreads, MODE == kScanGen ? 3 : KLF_SCAN_OCC) void
         }
         carry = wave_max(carry);
       }
-      // ---- general sets: fused q-gram prefilter ----
-      // Samples p = 0 mod QS of the tile (each needle's chosen window is q + QS - 1 long,
-      // so every occurrence spans exactly one sample whose gram lies in the window) probe
-      // the LDS bitmap (two bits per gram); bitmap hits are verified against the 16-B
-      // entries of the hash bucket (first needle dword pre-checked from the entry).  A tile
-      // owns its samples; the occurrence may start before the tile (its line is then the
-      // carried-in one).  A verified literal is a match (attributed like the fused
-      // literal); a verified regex factor queues (batch offset, regex) for k_nfa.
-      if (GEN) {
-        if (dense) __threadfence_block();
-        wave_lds_sync();
-        const DevPatterns& P = a.pats;
-        const uint32_t fold = P.qf_fold, qmask = P.qf_mask;
-        const uint32_t* s32 = reinterpret_cast<const uint32_t*>(s_tile);
-        uint32_t last_key = ~0u;  // (line, regex) this lane queued last: no duplicate work
-        // byte at tile offset o (may be negative or past the halo): LDS or global
-        auto tbyte = [&](int32_t o) __attribute__((always_inline)) -> uint32_t {
-          return (o >= 0 && o < kTile + kHalo) ? (uint32_t)s_tile[o] : (uint32_t)segp[rel_lo + o];
-        };
-        // 4 bytes at tile offset o (o >= 0 and o + 8 <= kTile + kHalo: LDS)
-        auto tword = [&](int32_t o) __attribute__((always_inline)) -> uint32_t {
-          if (o >= 0 && o + 8 <= kTile + kHalo)
-            return __builtin_amdgcn_alignbyte(s32[(o >> 2) + 1], s32[o >> 2], (uint32_t)o & 3u);
-          return tbyte(o) | tbyte(o + 1) << 8 | tbyte(o + 2) << 16 | tbyte(o + 3) << 24;
-        };
-        auto verify = [&](uint32_t b, int32_t p) __attribute__((always_inline)) {
-          const uint32_t e1 = P.qf_head[b + 1];
-          for (uint32_t e = P.qf_head[b]; e < e1; ++e) {
-            const uint4 E = P.qf_ent[e];
-            const uint32_t m = E.y & 0xFFFFu;
-            const int32_t x = p - (int32_t)((E.y >> 16) & 0xFFu);
-            if (rel_lo + (int64_t)x < 0 || rel_lo + (int64_t)x + (int64_t)m > seg_len) continue;
-            const uint32_t lm = (E.y & kQfLoose) ? 0x20202020u : 0u;
-            const uint32_t m0 = m >= 4 ? 0xFFFFFFFFu : ((1u << (8 * m)) - 1u);
-            if (((tword(x) | lm) ^ E.w) & m0) continue;  // pre-check: the first 4 bytes
-            bool eq = true;
-            for (uint32_t k = 4; k < m && eq; k += 4) {
-              const uint32_t nb = m - k < 4 ? m - k : 4;
-              const uint32_t msk = nb == 4 ? 0xFFFFFFFFu : ((1u << (8 * nb)) - 1);
-              eq = (((tword(x + (int32_t)k) | lm) ^ P.qf_nbytes[E.x + (k >> 2)]) & msk) == 0;
-            }
-            if (!eq) continue;
-            if (!(E.y & kQfRegex)) {
-              attribute(x);
-              continue;
-            }
-            const uint32_t key = (uint32_t)starts_upto(x) * kMaxRegexSet + E.z;
-            if (key == last_key) continue;
-            last_key = key;
-            const uint32_t qi = atomicAdd(&a.counters[kCtrQueue], 1u);
-            if (qi < a.cand_cap) a.cand[qi] = (sd.base + (uint64_t)(rel_lo + x)) | ((uint64_t)E.z << 40);
-            else atomicOr(&a.counters[kCtrQOver], 1u);
-          }
-        };
-        auto probe = [&](uint32_t g) __attribute__((always_inline)) -> uint32_t {
-          const uint32_t gf = (g | fold) & qmask;
-          const uint32_t h1 = qf_hash(gf), h2 = qf_hash2(gf);
-          return (s_qf[h1 >> 5] >> (h1 & 31)) & (s_qf[h2 >> 5] >> (h2 & 31)) & 1u;
-        };
-        // bitmap probes of my samples -> a 128-bit hit mask (bit = byte offset in my range)
-        uint32_t hq0 = 0, hq1 = 0, hq2 = 0, hq3 = 0;
-        const uint32_t rot = ((uint32_t)lane >> 1) & 7u;
-#pragma unroll
-        for (int v = 0; v < ((KLF_ABL & 4) ? 0 : 8); ++v) {
-          const uint32_t c = ((uint32_t)v + rot) & 7u;
-          const uint32_t o0 = my0 + 16u * c;
-          const uint4 x = *reinterpret_cast<const uint4*>(s_tile + o0);
-          const uint32_t w4 = QS < 4 ? s32[(o0 >> 2) + 4] : 0u;
-          const uint32_t w[5] = {x.x, x.y, x.z, x.w, w4};
-          uint32_t hm = 0;
-#pragma unroll
-          for (int d = 0; d < 4; ++d)
-#pragma unroll
-            for (int o = 0; o < 4; o += QS) {
-              const uint32_t g = o == 0 ? w[d] : __builtin_amdgcn_alignbyte(w[d + 1], w[d], o);
-              hm |= probe(g) << (4 * d + o);
-            }
-          hm = clip(hm, c) << ((c & 1u) * 16u);
-          const uint32_t q = c >> 1;
-          hq0 |= q == 0 ? hm : 0u;
-          hq1 |= q == 1 ? hm : 0u;
-          hq2 |= q == 2 ? hm : 0u;
-          hq3 |= q == 3 ? hm : 0u;
-        }
-#if KLF_ABL & 8
-        any_defer |= (hq0 | hq1 | hq2 | hq3) == 0xFFFFFFFFu;  // timing build: probes only
-        hq0 = hq1 = hq2 = hq3 = 0;
-#endif
-        const uint32_t hq[4] = {hq0, hq1, hq2, hq3};
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          for (uint32_t m = hq[q]; m; m &= m - 1u) {
-            const uint32_t p = my0 + 32u * q + (uint32_t)__builtin_ctz(m);
-            const uint32_t g = (__builtin_amdgcn_alignbyte(s32[(p >> 2) + 1], s32[p >> 2], p & 3u) | fold) & qmask;
-            verify(qf_hash(g) >> (kQfBits - kQfBucketBits), (int32_t)p);
-          }
-        }
-        carry = wave_max(carry);
-      }
       if (dense) __threadfence_block();
       wave_lds_sync();
     };
@@ -596,6 +497,81 @@ __global__ __launch_bounds__(kThreads, MODE == kScanGen ? 3 : KLF_SCAN_OCC) void
       for (uint32_t j = lane; j < nlines; j += 64) gslot[j] = s_list[j];
     } else if (pool_ok) {
       work(gslot);
+    }
+
+    uint32_t tile_hits = 0;
+    // ---- general sets: fused q-gram prefilter ----
+    // Samples p = 0 mod QS of the tile (each needle's chosen window is q + QS - 1 long, so
+    // every occurrence spans exactly one sample whose gram lies in the window) probe the
+    // LDS bitmap (one word, two bits per gram).  The few bitmap hits are appended to a global list
+    // (one atomic per wave and tile) and verified by k_verify once the line index exists:
+    // the scan keeps no verification code, and the latency-bound bucket walks run with
+    // the whole GPU's parallelism.
+    if (GEN) {
+      const uint32_t fold = a.pats.qf_fold, qmask = a.pats.qf_mask;
+      const uint32_t* s32 = reinterpret_cast<const uint32_t*>(s_tile);
+      auto probe = [&](uint32_t g) __attribute__((always_inline)) -> uint32_t {
+        const uint32_t gf = (g | fold) & qmask;
+        const uint32_t h1 = qf_h1(gf), bits = qf_bits(h1, qf_h2(gf));
+        return (s_qf[qf_word(h1)] & bits) == bits ? 1u : 0u;
+      };
+      // bitmap probes of my samples -> a 128-bit hit mask (bit = byte offset in my range)
+      uint32_t hq0 = 0, hq1 = 0, hq2 = 0, hq3 = 0;
+      const uint32_t rot = ((uint32_t)lane >> 1) & 7u;
+#pragma unroll
+      for (int v = 0; v < ((KLF_ABL & 4) ? 0 : 8); ++v) {
+        const uint32_t c = ((uint32_t)v + rot) & 7u;
+        const uint32_t o0 = my0 + 16u * c;
+        const uint4 x = *reinterpret_cast<const uint4*>(s_tile + o0);
+        const uint32_t w4 = QS < 4 ? s32[(o0 >> 2) + 4] : 0u;
+        const uint32_t w[5] = {x.x, x.y, x.z, x.w, w4};
+        uint32_t hm = 0;
+#pragma unroll
+        for (int d = 0; d < 4; ++d)
+#pragma unroll
+          for (int o = 0; o < 4; o += QS) {
+            const uint32_t g = o == 0 ? w[d] : __builtin_amdgcn_alignbyte(w[d + 1], w[d], o);
+            hm |= probe(g) << (4 * d + o);
+          }
+        hm = clip(hm, c) << ((c & 1u) * 16u);
+        const uint32_t q = c >> 1;
+        hq0 |= q == 0 ? hm : 0u;
+        hq1 |= q == 1 ? hm : 0u;
+        hq2 |= q == 2 ? hm : 0u;
+        hq3 |= q == 3 ? hm : 0u;
+      }
+#if KLF_ABL & 8
+      any_defer |= (hq0 | hq1 | hq2 | hq3) == 0xFFFFFFFFu;  // timing build: probes only
+      hq0 = hq1 = hq2 = hq3 = 0;
+#endif
+      const uint32_t nh = (uint32_t)(__popc(hq0) + __popc(hq1) + __popc(hq2) + __popc(hq3));
+      if (__any(nh != 0)) {
+        // tile-owned slots (u16 tile offsets, no atomics); only a tile with more than
+        // kHitSlots hits spills the rest to the global list
+        const uint32_t ih = wave_incl_scan_add(nh, lane);
+        const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)ih, 63);
+        uint32_t ob = 0;
+        if (tot > kHitSlots) {
+          if (lane == 63) ob = atomicAdd(&a.counters[kCtrHits], tot - kHitSlots);
+          ob = (uint32_t)__builtin_amdgcn_readlane((int)ob, 63);
+        }
+        uint16_t* hs = a.hslots + (size_t)tile * kHitSlots;
+        uint32_t k = ih - nh;
+        const uint32_t hq[4] = {hq0, hq1, hq2, hq3};
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          for (uint32_t m = hq[q]; m; m &= m - 1u, ++k) {
+            const uint32_t off = my0 + 32u * q + (uint32_t)__builtin_ctz(m);
+            if (k < kHitSlots) {
+              hs[k] = (uint16_t)off;
+            } else if ((uint64_t)ob + (k - kHitSlots) < a.qhits_cap) {
+              a.qhits[ob + (k - kHitSlots)] = sd.base + (uint64_t)rel_lo + off;
+            } else {
+              atomicOr(&a.counters[kCtrHitsOver], 1u);
+            }
+          }
+        tile_hits = tot < kHitSlots ? tot : kHitSlots;
+      }
     }
 
     // ---- per-tile record ----
@@ -608,7 +584,7 @@ __global__ __launch_bounds__(kThreads, MODE == kScanGen ? 3 : KLF_SCAN_OCC) void
       ts.parsed = (uint16_t)pp;
       ts.since_ok = (uint16_t)qq;
       ts.flags = (uint16_t)((dense ? 1u : 0u) | (carry ? 2u : 0u) | (dd ? 4u : 0u));
-      ts.carry_off = (uint16_t)carry;
+      ts.carry_off = (uint16_t)(GEN ? tile_hits : carry);  // GEN: hit slots used
       a.tstat[tile] = ts;
     }
     asm volatile("" ::: "memory");  // the next stage overwrites the LDS region read above
@@ -931,6 +907,90 @@ __device__ __forceinline__ uint32_t line_plen(const RunArgs& a, uint16_t meta, c
   return plen;
 }
 
+// K2a: verification of the prefilter's bitmap hits.  One lane per hit: the sample's gram
+// (global bytes), the 16-B entries of its bucket, the needle compare (first dword from the
+// entry), then the line of the occurrence start (segment + line-index binary searches).
+// A literal starting inside a parsed line's content is a match; a regex factor queues
+// (line, regex) for k_nfa.  The occurrence may start before the sample's tile.
+__device__ __forceinline__ uint32_t gword(const uint8_t* p) {  // 4 bytes at any alignment
+  const uintptr_t a0 = reinterpret_cast<uintptr_t>(p);
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(a0 & ~(uintptr_t)3);
+  return __builtin_amdgcn_alignbyte(w[1], w[0], (uint32_t)(a0 & 3));
+}
+
+// one bitmap hit at batch offset pos (the sample) in segment s
+__device__ void verify_hit(const RunArgs& a, uint32_t s, uint64_t pos) {
+  const DevPatterns& P = a.pats;
+  const SegDesc sd = a.segs[s];
+  const uint8_t* segp = a.bytes + sd.base;
+  const int64_t rp = (int64_t)(pos - sd.base);
+  const uint32_t g = (gword(segp + rp) | P.qf_fold) & P.qf_mask;
+  const uint32_t b = qf_word(qf_h1(g));
+  const uint32_t e1 = P.qf_head[b + 1];
+  for (uint32_t e = P.qf_head[b]; e < e1; ++e) {
+    const uint4 E = P.qf_ent[e];
+    const uint32_t m = E.y & 0xFFFFu;
+    const int64_t x = rp - (int64_t)((E.y >> 16) & 0xFFu);
+    if (x < 0 || x + (int64_t)m > (int64_t)sd.len) continue;
+    const uint32_t lm = (E.y & kQfLoose) ? 0x20202020u : 0u;
+    bool eq = true;
+    for (uint32_t k = 0; k < m && eq; k += 4) {
+      const uint32_t nb = m - k < 4 ? m - k : 4;
+      const uint32_t msk = nb == 4 ? 0xFFFFFFFFu : ((1u << (8 * nb)) - 1);
+      const uint32_t want = k == 0 ? E.w : P.qf_nbytes[E.x + (k >> 2)];
+      eq = (((gword(segp + x + k) | lm) ^ want) & msk) == 0;
+    }
+    if (!eq) continue;
+    uint64_t l0 = a.segout[s].line_lo, l1 = a.segout[s].line_hi;
+    while (l1 - l0 > 1) {
+      const uint64_t mid = (l0 + l1) >> 1;
+      if (a.line_off[mid + s] <= (uint64_t)x) l0 = mid; else l1 = mid;
+    }
+    const uint64_t l = l0;
+    const uint16_t mt = a.meta[l];
+    if (!(mt & Meta::kParsed)) continue;
+    if (!(E.y & kQfRegex)) {  // literal: a match when it starts inside the content
+      const uint64_t ls = a.line_off[l + s];
+      const uint32_t plen = line_plen(a, mt, segp, ls, a.line_off[l + s + 1]);
+      if ((uint64_t)x >= ls + plen) atomicOr(&a.bits[l >> 5], 1u << (l & 31));
+      continue;
+    }
+    if ((a.bits[l >> 5] >> (l & 31)) & 1u) continue;
+    const uint32_t qi = atomicAdd(&a.counters[kCtrQueue], 1u);
+    if (qi < a.cand_cap) a.cand[qi] = l | ((uint64_t)E.z << 40);
+    else atomicOr(&a.counters[kCtrQOver], 1u);
+  }
+}
+
+// Thread per tile over the tile-owned hit slots, then the spilled hits.
+__global__ __launch_bounds__(256) void k_verify(RunArgs a) {
+  if (a.counters[2] || a.counters[kCtrHitsOver]) return;
+  const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x, stride = gridDim.x * blockDim.x;
+  uint32_t walked = 0;
+  for (uint32_t tile = gid; tile < a.ntiles; tile += stride) {
+    const uint32_t n = a.tstat[tile].carry_off;
+    walked += n;
+    if (!n) continue;
+    const uint32_t s = a.tile_seg[tile];
+    const SegDesc sd = a.segs[s];
+    const uint64_t t0 = sd.base + (uint64_t)(tile - sd.tile0) * kTile;
+    const uint16_t* hs = a.hslots + (size_t)tile * kHitSlots;
+    for (uint32_t j = 0; j < n; ++j) verify_hit(a, s, t0 + hs[j]);
+  }
+  const uint32_t nh = a.counters[kCtrHits] < a.qhits_cap ? a.counters[kCtrHits] : a.qhits_cap;
+  for (uint32_t i = gid; i < nh; i += stride) {
+    const uint64_t pos = a.qhits[i];
+    uint32_t lo = 0, hi = a.nsegs;
+    while (hi - lo > 1) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (a.segs[mid].base <= pos) lo = mid; else hi = mid;
+    }
+    verify_hit(a, lo, pos);
+  }
+  walked = wave_sum(walked);
+  if ((threadIdx.x & 63) == 0 && walked) atomicAdd(&a.counters[kCtrVerified], walked);
+}
+
 // K2b: the prefiltered regex stage.  One lane per queued (batch offset, regex) candidate:
 // the offset's stream and line (binary searches over the segment table and the line
 // index), then the Glushkov NFA of that regex over the line's content.  Lines already
@@ -1019,7 +1079,7 @@ __device__ bool nfa_wave(const NfaTables& T, uint32_t r, const uint8_t* p, uint6
 template <bool LDS>
 __global__ __launch_bounds__(256) void k_nfa(RunArgs a) {
   extern __shared__ uint64_t s_nfa[];
-  if (a.counters[2] || a.counters[kCtrQOver]) return;  // overflow: k_match decides every line
+  if (a.counters[2] || a.counters[kCtrQOver] || a.counters[kCtrHitsOver]) return;  // k_match decides
   const uint32_t nq = a.counters[kCtrQueue] < a.cand_cap ? a.counters[kCtrQueue] : a.cand_cap;
   if (nq == 0 || blockIdx.x * (blockDim.x / 64) >= nq) return;  // one wave per candidate
   const DevPatterns& P = a.pats;
@@ -1048,21 +1108,9 @@ __global__ __launch_bounds__(256) void k_nfa(RunArgs a) {
   const uint32_t nw = gridDim.x * (blockDim.x / 64);
   for (uint32_t i = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6); i < nq; i += nw) {
     const uint64_t e = a.cand[i];
-    const uint64_t pos = e & ((1ull << 40) - 1);
+    const uint64_t l = e & ((1ull << 40) - 1);
     const uint32_t r = (uint32_t)(e >> 40);
-    uint32_t lo = 0, hi = a.nsegs;
-    while (hi - lo > 1) {
-      const uint32_t mid = (lo + hi) >> 1;
-      if (a.segs[mid].base <= pos) lo = mid; else hi = mid;
-    }
-    const uint32_t s = lo;
-    const uint64_t rel = pos - a.segs[s].base;
-    uint64_t l0 = a.segout[s].line_lo, l1 = a.segout[s].line_hi;
-    while (l1 - l0 > 1) {
-      const uint64_t mid = (l0 + l1) >> 1;
-      if (a.line_off[mid + s] <= rel) l0 = mid; else l1 = mid;
-    }
-    const uint64_t l = l0;
+    const uint32_t s = find_seg_by_line(a.segout, a.nsegs, l);
     if ((a.bits[l >> 5] >> (l & 31)) & 1u) continue;
     const uint16_t m = a.meta[l];
     if (!(m & Meta::kParsed)) continue;
@@ -1079,7 +1127,8 @@ __global__ __launch_bounds__(256) void k_nfa(RunArgs a) {
 
 __global__ __launch_bounds__(256) void k_match(RunArgs a) {
   if (a.counters[2]) return;
-  if (a.grep_mode == kGrepGeneral && a.pats.qf_on && !a.counters[kCtrQOver]) return;  // prefiltered
+  if (a.grep_mode == kGrepGeneral && a.pats.qf_on && !a.counters[kCtrQOver] && !a.counters[kCtrHitsOver])
+    return;  // prefiltered
   const uint64_t L = a.segout[a.nsegs - 1].line_hi;
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   for (uint64_t l = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; l < L; l += stride) {
@@ -1307,7 +1356,7 @@ __global__ __launch_bounds__(256) void k_init(RunArgs a) {
 
 // ======================================================= K4: compaction + gather copy ==
 // Reduce-then-scan over blocks of kCompactLines window lines (no inter-block waiting):
-//   k_csum    per block: selected content bytes and selected lines -> csum[2 * blk]
+//   k_csum    per block: selected content bytes and selected lines -> csum[3 * blk]
 //   k_cscan   one block: exclusive scan of the block sums (in place)
 //   k_cgather per block: in-block scan + block base -> output offsets, stream output
 //             ranges, gather copy of the selected contents (prefix stripped)
@@ -1371,32 +1420,43 @@ __global__ __launch_bounds__(kThreads) void k_csum(RunArgs a) {
     if (lane == 0) { s_wb[wv] = b; s_wc[wv] = c; }
     __syncthreads();
     if (t == 0) {
-      a.csum[2 * blk] = s_wb[0] + s_wb[1] + s_wb[2] + s_wb[3];
-      a.csum[2 * blk + 1] = s_wc[0] + s_wc[1] + s_wc[2] + s_wc[3];
+      a.csum[3 * blk] = s_wb[0] + s_wb[1] + s_wb[2] + s_wb[3];
+      a.csum[3 * blk + 1] = s_wc[0] + s_wc[1] + s_wc[2] + s_wc[3];
     }
   }
 }
 
+// Exclusive prefixes of the block sums (bytes, lines) and of the copy chunks per block
+// (ceil(bytes / kCopyChunk), at least 1): long selected lines spread their copy over many
+// workgroups instead of the one that owns their 1024-line block.
 __global__ __launch_bounds__(256) void k_cscan(RunArgs a) {
-  __shared__ uint64_t s_wb[4], s_wc[4];
+  __shared__ uint64_t s_wb[4], s_wc[4], s_wk[4];
   if (a.counters[2]) return;
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const uint32_t nb = a.counters[3];
   const uint32_t per = (nb + 255) / 256;
   const uint32_t i0 = t * per, i1 = i0 + per < nb ? i0 + per : nb;
-  uint64_t b = 0, c = 0;
-  for (uint32_t i = i0; i < i1; ++i) { b += a.csum[2 * i]; c += a.csum[2 * i + 1]; }
-  const uint64_t ib = wave_incl_scan_add(b, lane), ic = wave_incl_scan_add(c, lane);
-  if (lane == 63) { s_wb[wv] = ib; s_wc[wv] = ic; }
+  auto chunks = [](uint64_t bytes) -> uint64_t { return bytes ? (bytes + kCopyChunk - 1) / kCopyChunk : 1; };
+  uint64_t b = 0, c = 0, k = 0;
+  for (uint32_t i = i0; i < i1; ++i) { b += a.csum[3 * i]; c += a.csum[3 * i + 1]; k += chunks(a.csum[3 * i]); }
+  const uint64_t ib = wave_incl_scan_add(b, lane), ic = wave_incl_scan_add(c, lane), ik = wave_incl_scan_add(k, lane);
+  if (lane == 63) { s_wb[wv] = ib; s_wc[wv] = ic; s_wk[wv] = ik; }
   __syncthreads();
-  uint64_t pb = ib - b, pc = ic - c;
-  for (int k = 0; k < wv; ++k) { pb += s_wb[k]; pc += s_wc[k]; }
+  uint64_t pb = ib - b, pc = ic - c, pk = ik - k;
+  for (int w = 0; w < wv; ++w) { pb += s_wb[w]; pc += s_wc[w]; pk += s_wk[w]; }
   for (uint32_t i = i0; i < i1; ++i) {
-    const uint64_t xb = a.csum[2 * i], xc = a.csum[2 * i + 1];
-    a.csum[2 * i] = pb;
-    a.csum[2 * i + 1] = pc;
+    const uint64_t xb = a.csum[3 * i], xc = a.csum[3 * i + 1];
+    a.csum[3 * i] = pb;
+    a.csum[3 * i + 1] = pc;
+    a.csum[3 * i + 2] = pk;
     pb += xb;
     pc += xc;
+    pk += chunks(xb);
+  }
+  if (t == 255) {
+    a.csum[3 * nb] = pb;  // total output bytes
+    a.csum[3 * nb + 2] = pk;
+    a.counters[kCtrCopyChunks] = (uint32_t)pk;
   }
 }
 
@@ -1487,32 +1547,40 @@ __global__ __launch_bounds__(kThreads) void k_cgather(RunArgs a) {
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   if (a.counters[2]) return;
   const uint64_t W = a.wpre[a.nsegs];
-  const uint32_t nblocks = a.counters[3];
-  for (uint32_t blk = blockIdx.x; blk < nblocks; blk += gridDim.x) {
+  const uint32_t nblocks = a.counters[3], nchunks = a.counters[kCtrCopyChunks];
+  for (uint32_t w = blockIdx.x; w < nchunks; w += gridDim.x) {
+    uint32_t lo = 0, hi = nblocks;  // the compaction block of copy chunk w
+    while (hi - lo > 1) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (a.csum[3 * mid + 2] <= w) lo = mid; else hi = mid;
+    }
+    const uint32_t blk = lo, sub = w - (uint32_t)a.csum[3 * blk + 2];
     WinLines r;
     window_lines(a, (uint64_t)blk * kCompactLines + (uint64_t)t * 4, W, r);
     const uint64_t ib = wave_incl_scan_add(r.bytes, lane);
     const uint64_t ic = wave_incl_scan_add((uint64_t)r.nsel, lane);
-    __syncthreads();  // the previous block's copy is done with the LDS tables
+    __syncthreads();  // the previous chunk's copy is done with the LDS tables
     if (lane == 63) { s_wb[wv] = ib; s_wc[wv] = ic; }
     __syncthreads();
-    uint64_t ob = a.csum[2 * blk] + ib - r.bytes, oc = a.csum[2 * blk + 1] + ic - r.nsel;
+    uint64_t ob = a.csum[3 * blk] + ib - r.bytes, oc = a.csum[3 * blk + 1] + ic - r.nsel;
     for (int k = 0; k < wv; ++k) { ob += s_wb[k]; oc += s_wc[k]; }
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int i = t * 4 + j;
-      if (r.first[j]) { a.segout[r.seg[j]].out_lo = ob; a.segout[r.seg[j]].sel_lo = oc; }
+      if (sub == 0 && r.first[j]) { a.segout[r.seg[j]].out_lo = ob; a.segout[r.seg[j]].sel_lo = oc; }
       s_src[i] = r.src[j];
       s_dst[i] = ob;
       s_len[i] = r.len[j];
       ob += r.len[j];
       oc += r.len[j] ? 1 : 0;
-      if (r.last[j]) { a.segout[r.seg[j]].out_hi = ob; a.segout[r.seg[j]].sel_hi = oc; }
+      if (sub == 0 && r.last[j]) { a.segout[r.seg[j]].out_hi = ob; a.segout[r.seg[j]].sel_hi = oc; }
     }
     __syncthreads();
-    const uint64_t ob0 = a.csum[2 * blk];
+    const uint64_t ob0 = a.csum[3 * blk];
     const uint64_t ob1 = ob0 + s_wb[0] + s_wb[1] + s_wb[2] + s_wb[3];
-    block_gather_copy(s_src, s_dst, s_len, ob0, ob1, a.bytes, a.out);
+    const uint64_t c0 = ob0 + (uint64_t)sub * kCopyChunk;
+    const uint64_t c1 = c0 + kCopyChunk < ob1 ? c0 + kCopyChunk : ob1;
+    block_gather_copy(s_src, s_dst, s_len, c0, c1, a.bytes, a.out);
   }
 }
 
@@ -1595,6 +1663,10 @@ hipError_t launch_pipeline(const RunArgs& a, hipStream_t st, hipEvent_t* ev, int
   }
   KLF_TRY(hipGetLastError());
   KLF_TRY(hipEventRecord(ev[2], st));
+  if (a.grep_mode == kGrepGeneral && a.pats.qf_on) {
+    hipLaunchKernelGGL(k_verify, dim3(num_cus * 8), dim3(256), 0, st, a);
+    KLF_TRY(hipGetLastError());
+  }
   if (a.grep_mode == kGrepGeneral && a.pats.qf_on && a.pats.rx_count) {
     const size_t lds = nfa_lds_bytes(a.pats);
     if (lds <= kNfaMaxLds)
@@ -1623,7 +1695,7 @@ hipError_t launch_pipeline(const RunArgs& a, hipStream_t st, hipEvent_t* ev, int
   KLF_TRY(hipGetLastError());
   hipLaunchKernelGGL(k_cscan, dim3(1), dim3(256), 0, st, a);
   KLF_TRY(hipGetLastError());
-  hipLaunchKernelGGL(k_cgather, dim3(num_cus * 4), dim3(kThreads), 0, st, a);
+  hipLaunchKernelGGL(k_cgather, dim3(num_cus * 8), dim3(kThreads), 0, st, a);
   KLF_TRY(hipGetLastError());
   KLF_TRY(hipEventRecord(ev[5], st));
 #undef KLF_TRY

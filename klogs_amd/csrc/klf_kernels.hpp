@@ -24,20 +24,36 @@ constexpr uint32_t kMatchChunk = 8192;              // lines per k_mcount partia
 constexpr int kSlots = kTile / 32 + 2;  // staged line slots per tile (>= 8 KiB / 32-byte kubelet line + 1)
 
 // q-gram prefilter of general pattern sets (klf_patterns.hpp CompiledSet::qf_*)
-constexpr int kQfBits = 17;                          // bitmap: 2^17 bits = 16 KiB of LDS
-constexpr uint32_t kQfWords = 1u << (kQfBits - 5);
-constexpr int kQfBucketBits = 12;                    // verification buckets: top hash bits
+constexpr int kQfBucketBits = 12;                    // bitmap words = verification buckets
+constexpr uint32_t kQfWords = 1u << kQfBucketBits;   // bitmap: 4096 words = 16 KiB of LDS
 constexpr uint32_t kQfMinNeedle = 3;                 // shorter literal / factor: no prefilter
 constexpr uint32_t kQfMaxFactor = 32;                // regex factors are cut to this length
 constexpr uint32_t kMaxRegexSet = 1024;              // = klf_patterns.hpp kMaxRegexes
 constexpr uint32_t kCtrQueue = 6;                   // counters[6]: NFA candidate queue length
 constexpr uint32_t kCtrQOver = 7;                    // counters[7]: queue overflow -> k_match
+constexpr uint32_t kHitSlots = 32;                   // prefilter hits a tile records itself
+constexpr uint32_t kCtrHits = 8;                     // counters[8]: spilled prefilter hits
+constexpr uint32_t kCtrHitsOver = 9;                 // counters[9]: hit list overflow -> k_match
+constexpr uint32_t kCtrCopyChunks = 11;              // counters[11]: output copy chunks (k_cgather)
+constexpr uint64_t kCopyChunk = 64 * 1024;           // output bytes per k_cgather work item
+constexpr uint32_t kCtrVerified = 10;                // counters[10]: hits k_verify walked (diagnostics)
 constexpr uint32_t kQfRegex = 1u << 24;              // entry flags: regex factor (else literal)
 constexpr uint32_t kQfLoose = 1u << 25;              //   compare OR 0x20 per byte
 constexpr size_t kNfaMaxLds = 64 * 1024;            // k_nfa stages its tables in LDS up to this
 constexpr uint32_t kCarryBias = 256;                 // TileStat.carry_off = hit offset + 1 + bias
-__host__ __device__ inline uint32_t qf_hash(uint32_t g) { return (g * 0x9E3779B1u) >> (32 - kQfBits); }
-__host__ __device__ inline uint32_t qf_hash2(uint32_t g) { return (g * 0x85EBCA77u) >> (32 - kQfBits); }
+// Blocked Bloom filter, one 32-bit bitmap word per probe.  The gram is folded to 24 bits
+// (byte 3 xor-ed into bits 11..18) so that both hashes are full-rate 24-bit multiplies:
+// word = top 12 bits of the low product (also the verification bucket), two bits inside
+// the word from the low and the high product.
+__host__ __device__ inline uint32_t qf_fold24(uint32_t g) { return (g ^ (g >> 13)) & 0xFFFFFFu; }
+__host__ __device__ inline uint32_t qf_h1(uint32_t g) { return qf_fold24(g) * 0x9E3779u; }
+__host__ __device__ inline uint32_t qf_h2(uint32_t g) {
+  return (uint32_t)(((uint64_t)qf_fold24(g) * 0xC2B2AEu) >> 32);  // v_mul_hi_u32_u24
+}
+__host__ __device__ inline uint32_t qf_word(uint32_t h1) { return h1 >> (32 - kQfBucketBits); }
+__host__ __device__ inline uint32_t qf_bits(uint32_t h1, uint32_t h2) {
+  return (1u << ((h1 >> 15) & 31u)) | (1u << (h2 & 31u));
+}
 
 // Per-tile record of the scan (K1a), 16 B.
 struct TileStat {
@@ -46,8 +62,8 @@ struct TileStat {
   uint16_t parsed, since_ok;
   uint16_t flags;      // bit0 dense (slots in the pool), bit1 literal hit in the carried-in line,
                        // bit2 some line deferred to k_fixup
-  uint16_t carry_off;  // 1 + kCarryBias + tile offset (>= -kCarryBias) of the furthest final hit in
-                       // the carried-in line (0 = none)
+  uint16_t carry_off;  // literal: 1 + kCarryBias + tile offset of the furthest hit in the
+                       // carried-in line (0 = none); general sets: hit slots used
 };
 static_assert(sizeof(TileStat) == 16, "TileStat is one 16-B store");
 
@@ -131,7 +147,8 @@ struct RunArgs {
   uint64_t* tile_base;  // [ntiles] global line index of each tile's line 0
   uint64_t* bsum;       // [3 * (ntiles / 4096 + 1)] scan block sums (events, parsed, since_ok)
   uint64_t* mpart;      // [cap_lines / kMatchChunk + 1] matched-line partial per line chunk
-  uint64_t* csum;       // [2 * max compaction blocks] per-block (bytes, lines), then their prefix
+  uint64_t* csum;       // [3 * (max compaction blocks + 1)] per-block (bytes, lines), then their
+                        // prefixes and the prefix of copy chunks
   uint32_t* counters;   // [kNumCounters]: 1 compact ticket, 2 error flags, 3 compact blocks,
                         // 4 dense-tile pool
   uint64_t* line_off;   // [cap_lines + nsegs]
@@ -142,8 +159,11 @@ struct RunArgs {
   uint64_t* wpre;       // [nsegs + 1] exclusive prefix of window sizes
   uint8_t* out;         // output bytes (capacity >= total input)
   uint32_t max_cblocks; // compaction block capacity
-  uint64_t* cand;       // [cand_cap] NFA candidates: batch byte offset | regex << 40
+  uint64_t* cand;       // [cand_cap] NFA candidates: global line index | regex << 40
   uint32_t cand_cap;
+  uint16_t* hslots;     // [ntiles * kHitSlots] prefilter hits (tile offsets of the samples)
+  uint64_t* qhits;      // [qhits_cap] spilled hits (batch byte offsets of the samples)
+  uint32_t qhits_cap;
 };
 
 // Enqueues the whole pipeline on `stream`; `ev` (6 events) brackets the stages for

@@ -961,7 +961,7 @@ bool compile_set(const std::vector<std::vector<uint8_t>>& pats, const std::vecto
 // literal / factor occurs wherever the needle does): the window whose S grams are the
 // least common in log text and among the needles already placed, so that grams like
 // "user" or a prefix shared by many literals do not flood the verification buckets.
-// Every gram sets two bits of the bitmap (Bloom, k = 2).
+// Every gram sets two bits of one bitmap word (blocked Bloom, k = 2).
 void build_prefilter(const std::vector<std::vector<uint8_t>>& lits, const std::vector<std::vector<std::string>>& rx_fac,
                      const std::vector<bool>& rx_loose, CompiledSet& out) {
   struct Needle {
@@ -983,9 +983,11 @@ void build_prefilter(const std::vector<std::vector<uint8_t>>& lits, const std::v
     loose |= (n.flags & kQfLoose) != 0;
   }
   if (minlen < kQfMinNeedle) { out.qf_why = "a needle is shorter than 3 bytes"; return; }
-  const uint32_t q = (uint32_t)std::min<size_t>(4, minlen);
-  const uint32_t span = (uint32_t)std::min<size_t>(4, minlen - q + 1);  // sampling gap allowed
-  const uint32_t S = span >= 4 ? 4 : (span >= 2 ? 2 : 1);
+  // the widest sampling stride that keeps grams of >= 3 bytes (the probes are LDS-bound),
+  // then the longest gram that stride allows
+  const size_t sw = std::min<size_t>(4, minlen - 2);
+  const uint32_t S = sw >= 4 ? 4 : (sw >= 2 ? 2 : 1);
+  const uint32_t q = (uint32_t)std::min<size_t>(4, minlen - S + 1);
   out.qf_q = q;
   out.qf_stride = S;
   out.qf_fold = loose ? 0x20202020u : 0u;
@@ -1024,10 +1026,9 @@ void build_prefilter(const std::vector<std::vector<uint8_t>>& lits, const std::v
     for (uint32_t j = 0; j < S; ++j) {
       const uint32_t k = best_a + j, g = gram_at(s, k);
       used[g]++;
-      const uint32_t h1 = qf_hash(g), h2 = qf_hash2(g);
-      out.qf_bitmap[h1 >> 5] |= 1u << (h1 & 31);
-      out.qf_bitmap[h2 >> 5] |= 1u << (h2 & 31);
-      buckets[h1 >> (kQfBits - kQfBucketBits)].push_back(i << 8 | k);
+      const uint32_t h1 = qf_h1(g);
+      out.qf_bitmap[qf_word(h1)] |= qf_bits(h1, qf_h2(g));
+      buckets[qf_word(h1)].push_back(i << 8 | k);
     }
   }
   // needle bytes (loose needles are already stored OR 0x20), then 16-B entries per bucket
@@ -1066,9 +1067,9 @@ bool prefilter_match(const CompiledSet& cs, const uint8_t* s, size_t n, uint32_t
     uint32_t g = 0;
     for (uint32_t b = 0; b < 4; ++b) g |= (uint32_t)(p + b < n ? s[p + b] : 0) << (8 * b);
     g = (g | cs.qf_fold) & cs.qf_mask;
-    const uint32_t h1 = qf_hash(g), h2 = qf_hash2(g);
-    if (!((cs.qf_bitmap[h1 >> 5] >> (h1 & 31)) & (cs.qf_bitmap[h2 >> 5] >> (h2 & 31)) & 1u)) continue;
-    const uint32_t b = h1 >> (kQfBits - kQfBucketBits);
+    const uint32_t h1 = qf_h1(g), bits = qf_bits(h1, qf_h2(g));
+    if ((cs.qf_bitmap[qf_word(h1)] & bits) != bits) continue;
+    const uint32_t b = qf_word(h1);
     for (uint32_t e = cs.qf_head[b]; e < cs.qf_head[b + 1]; ++e) {
       const uint32_t* E = cs.qf_ent.data() + 4 * (size_t)e;
       const uint32_t m = E[1] & 0xFFFFu, k = (E[1] >> 16) & 0xFFu;

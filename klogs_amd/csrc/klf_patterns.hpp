@@ -72,8 +72,8 @@ struct CompiledSet {
   uint32_t qf_stride = 1;    // 1, 2 or 4
   uint32_t qf_fold = 0;      // 0x20202020 when some needle compares case-insensitively
   uint32_t qf_mask = ~0u;    // gram bytes (q < 4: low q bytes)
-  std::vector<uint32_t> qf_bitmap;   // [kQfWords]: 2 bits (qf_hash, qf_hash2) per gram
-  std::vector<uint32_t> qf_head;     // [(1 << kQfBucketBits) + 1] bucket (top bits of qf_hash) -> entry
+  std::vector<uint32_t> qf_bitmap;   // [kQfWords]: 2 bits of word qf_word(qf_h1) per gram
+  std::vector<uint32_t> qf_head;     // [kQfWords + 1] bucket (= bitmap word) -> first entry
   std::vector<uint32_t> qf_ent;      // 16-B entries {needle dword offset, len | k << 16 | flags,
                                      //  regex, first needle dword}; k = offset of the gram
   std::vector<uint32_t> qf_nbytes;   // needle bytes, each padded to whole dwords

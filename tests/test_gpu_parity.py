@@ -206,3 +206,18 @@ def test_candidate_queue_overflow_falls_back(gpu, monkeypatch):
     monkeypatch.setenv("KLF_CAND_CAP", "16")
     d = synth.generate(synth.LONGJSON, 9, 0, 1_500_000, permille=100)
     check_against_py([d], None, -1, match=synth.c5_regexes()[:16])
+
+
+def test_hit_list_overflow_falls_back(gpu, monkeypatch):
+    """More prefilter bitmap hits than the list holds: k_match decides every line."""
+    monkeypatch.setenv("KLF_HITS_CAP", "16")
+    d = synth.generate(synth.TEXT, 8, 0, 1_000_000)  # "pod" / "took": tens of hits per tile -> spills
+    check_against_c([d], None, 10, [b"pod", b"ready"])
+    check_against_py([d], None, -1, grep=[b"ERR_"], match=[rb"(?i)took \d+ms"])
+
+
+@pytest.mark.parametrize("since,tail", [(None, -1), (None, 100), ((synth.T0 + 3000, 0), -1)])
+def test_long_lines_copy_chunks(gpu, since, tail):
+    """Selected output of 1-32 KiB lines: one compaction block spans many 64 KiB copy chunks."""
+    streams = [synth.generate(synth.LONGJSON, 12, i, 3_000_000 + 777 * i, permille=5) for i in range(3)]
+    check_against_c(streams, since, tail, [])

@@ -99,8 +99,9 @@ def test_prefilter_off_falls_back(grep, match, why):
 
 @pytest.mark.parametrize("grep,match,q,stride", [
     ([b"abcdefg", b"0123456789"], [], 4, 4),
-    ([b"abcdef", b"0123456789"], [], 4, 2),
-    ([b"abcd", b"0123456789"], [], 4, 1),
+    ([b"abcdef", b"0123456789"], [], 3, 4),
+    ([b"abcde", b"0123456789"], [], 4, 2),
+    ([b"abcd", b"0123456789"], [], 3, 2),
     ([b"abc", b"0123456789"], [], 3, 1),
     ([], [rb"(?i)timeout"], 4, 4),
 ])
