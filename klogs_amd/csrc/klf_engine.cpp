@@ -59,7 +59,7 @@ struct klf_engine {
   std::vector<std::vector<uint8_t>> staged;
   // device pattern tables
   DevBuf d_lit, d_ac_class, d_ac_next, d_ac_accept, d_rx_class, d_rx_b, d_rx_follow, d_rx_vec, d_rx_flags;
-  DevBuf d_qf_bitmap, d_qf_head, d_qf_ent, d_qf_nbytes, d_cand, d_rx_vec4, d_qhits, d_hslots;
+  DevBuf d_qf_bitmap, d_qf_head, d_qf_ent, d_qf_nbytes, d_cand, d_rx_vec4, d_qhits, d_hslots, d_hist;
   uint32_t cand_cap = 1u << 22;  // NFA candidate queue (32 MiB); overflow -> k_match
   uint64_t hits_cap_max = 1u << 26;  // prefilter hit list (512 MiB at most); overflow -> k_match
   klf::DevPatterns dpats;
@@ -251,7 +251,7 @@ extern "C" void klf_close(klf_engine* e) {
   if (e->stream) (void)hipStreamSynchronize(e->stream);
   for (DevBuf* b : {&e->d_lit, &e->d_ac_class, &e->d_ac_next, &e->d_ac_accept, &e->d_rx_class, &e->d_rx_b,
                     &e->d_rx_follow, &e->d_rx_vec, &e->d_rx_flags, &e->d_qf_bitmap, &e->d_qf_head,
-                    &e->d_qf_ent, &e->d_qf_nbytes, &e->d_rx_vec4, &e->d_qhits, &e->d_hslots, &e->d_cand, &e->d_batch, &e->d_segs, &e->d_tstat,
+                    &e->d_qf_ent, &e->d_qf_nbytes, &e->d_rx_vec4, &e->d_qhits, &e->d_hslots, &e->d_hist, &e->d_cand, &e->d_batch, &e->d_segs, &e->d_tstat,
                     &e->d_slots, &e->d_pool, &e->d_tile_base, &e->d_bsum, &e->d_cstatus, &e->d_counters,
                     &e->d_line_off, &e->d_meta, &e->d_bits, &e->d_segout, &e->d_wpre, &e->d_out, &e->d_tile_seg, &e->d_mpart})
     b->release();
@@ -356,6 +356,32 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
            "H2D segs");
     HIPCHK(e, hipStreamSynchronize(st), "sync segs");
     HIPCHK(e, e->d_tile_seg.ensure(ntiles * 4), "alloc tile_seg");
+  }
+  if (mode == klf::CompiledSet::kGeneral && e->cs.qf_on && !e->cs.qf_tuned) {
+    // first batch: place the needles' sampling windows on the data's own gram statistics
+    e->cs.qf_tuned = true;
+    const char* tune = getenv("KLF_QF_TUNE");
+    if (!tune || strcmp(tune, "0") != 0) {
+      std::vector<uint32_t> hist(klf::kQfHistBins);
+      HIPCHK(e, e->d_hist.ensure(klf::kQfHistBins * 4), "alloc hist");
+      HIPCHK(e, klf::launch_gramhist(d_bytes, e->d_segs.as<SegDesc>(), nsegs, 1u << 20, e->cs.qf_fold, e->cs.qf_mask,
+                                     e->d_hist.as<uint32_t>(), st), "gram histogram");
+      HIPCHK(e, hipMemcpyAsync(hist.data(), e->d_hist.p, hist.size() * 4, hipMemcpyDeviceToHost, st), "D2H hist");
+      HIPCHK(e, hipStreamSynchronize(st), "sync hist");
+      if (getenv("KLF_DIAG")) {
+        uint64_t tot = 0, nz = 0, mx = 0;
+        for (uint32_t v : hist) { tot += v; nz += v != 0; mx = std::max<uint64_t>(mx, v); }
+        fprintf(stderr, "[klf] gram histogram: %llu grams, %llu bins used, max bin %llu\n", (unsigned long long)tot,
+                (unsigned long long)nz, (unsigned long long)mx);
+      }
+      klf::place_needles(e->cs, &hist);
+      HIPCHK(e, upload(e->d_qf_bitmap, e->cs.qf_bitmap, st), "upload bitmap");
+      HIPCHK(e, upload(e->d_qf_head, e->cs.qf_head, st), "upload buckets");
+      HIPCHK(e, upload(e->d_qf_ent, e->cs.qf_ent, st), "upload entries");
+      e->dpats.qf_bitmap = e->d_qf_bitmap.as<uint32_t>();
+      e->dpats.qf_head = e->d_qf_head.as<uint32_t>();
+      e->dpats.qf_ent = e->d_qf_ent.as<uint4>();
+    }
   }
   HIPCHK(e, e->d_tstat.ensure(ntiles * sizeof(klf::TileStat)), "alloc tstat");
   HIPCHK(e, e->d_slots.ensure(ntiles * klf::kSlots * 4), "alloc slots");

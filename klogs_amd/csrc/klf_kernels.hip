@@ -918,41 +918,66 @@ __device__ __forceinline__ uint32_t gword(const uint8_t* p) {  // 4 bytes at any
   return __builtin_amdgcn_alignbyte(w[1], w[0], (uint32_t)(a0 & 3));
 }
 
-// one bitmap hit at batch offset pos (the sample) in segment s
-__device__ void verify_hit(const RunArgs& a, uint32_t s, uint64_t pos) {
+// One bitmap hit: the sample at tile offset p of `tile` (stream s).  The occurrence start
+// x = p - k may lie before the tile: an occurrence holds no '\n', so it is then in the
+// tile's carried-in line.  Inside the tile, its line comes from the tile's own staged
+// line starts (slots, meta in the high half) instead of a search of the whole index.
+__device__ void verify_hit(const RunArgs& a, uint32_t tile, uint32_t s, int32_t p) {
+#if KLF_ABL & 16
+  if (p == 0x7FFF) atomicOr(&a.counters[13], s);  // timing build: no verification work
+  return;
+#endif
   const DevPatterns& P = a.pats;
   const SegDesc sd = a.segs[s];
   const uint8_t* segp = a.bytes + sd.base;
-  const int64_t rp = (int64_t)(pos - sd.base);
-  const uint32_t g = (gword(segp + rp) | P.qf_fold) & P.qf_mask;
+  const int64_t rel_lo = (int64_t)(tile - sd.tile0) * kTile;
+  const uint32_t g = (gword(segp + rel_lo + p) | P.qf_fold) & P.qf_mask;
   const uint32_t b = qf_word(qf_h1(g));
   const uint32_t e1 = P.qf_head[b + 1];
   for (uint32_t e = P.qf_head[b]; e < e1; ++e) {
     const uint4 E = P.qf_ent[e];
     const uint32_t m = E.y & 0xFFFFu;
-    const int64_t x = rp - (int64_t)((E.y >> 16) & 0xFFu);
-    if (x < 0 || x + (int64_t)m > (int64_t)sd.len) continue;
+    const int32_t x = p - (int32_t)((E.y >> 16) & 0xFFu);
+    if (rel_lo + x < 0 || rel_lo + x + (int64_t)m > (int64_t)sd.len) continue;
     const uint32_t lm = (E.y & kQfLoose) ? 0x20202020u : 0u;
     bool eq = true;
     for (uint32_t k = 0; k < m && eq; k += 4) {
       const uint32_t nb = m - k < 4 ? m - k : 4;
       const uint32_t msk = nb == 4 ? 0xFFFFFFFFu : ((1u << (8 * nb)) - 1);
       const uint32_t want = k == 0 ? E.w : P.qf_nbytes[E.x + (k >> 2)];
-      eq = (((gword(segp + x + k) | lm) ^ want) & msk) == 0;
+      eq = (((gword(segp + rel_lo + x + k) | lm) ^ want) & msk) == 0;
     }
     if (!eq) continue;
-    uint64_t l0 = a.segout[s].line_lo, l1 = a.segout[s].line_hi;
-    while (l1 - l0 > 1) {
-      const uint64_t mid = (l0 + l1) >> 1;
-      if (a.line_off[mid + s] <= (uint64_t)x) l0 = mid; else l1 = mid;
+#if KLF_ABL & 32
+    atomicOr(&a.counters[13], x);  // timing build: bucket walk only
+    continue;
+#endif
+    // the occurrence's line: global index, start (stream offset), meta
+    const TileStat ts = a.tstat[tile];
+    const bool first = rel_lo == 0, last = rel_lo + kTile >= (int64_t)sd.len;
+    const uint32_t k0 = first ? 0 : 1, k1 = last ? ts.events : ts.events + 1;
+    const uint32_t nl = k1 > k0 ? k1 - k0 : 0;
+    const uint32_t* list = (ts.flags & 1u) ? a.pool + ts.pool_base : a.slots + (size_t)tile * kSlots;
+    int lo = 0, hi = x < 0 ? 0 : (int)nl;  // starts <= x
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if ((int32_t)(list[mid] & kSlotOff) <= x) lo = mid + 1; else hi = mid;
     }
-    const uint64_t l = l0;
-    const uint16_t mt = a.meta[l];
+    const uint64_t l = a.tile_base[tile] + (lo > 0 ? k0 + (uint32_t)lo - 1 : 0);
+    uint16_t mt;
+    uint64_t ls;
+    if (lo > 0) {
+      const uint32_t v = list[lo - 1];
+      mt = (uint16_t)(v >> 16);
+      ls = (uint64_t)rel_lo + (v & kSlotOff);
+    } else {
+      mt = a.meta[l];
+      ls = a.line_off[l + s];
+    }
     if (!(mt & Meta::kParsed)) continue;
     if (!(E.y & kQfRegex)) {  // literal: a match when it starts inside the content
-      const uint64_t ls = a.line_off[l + s];
-      const uint32_t plen = line_plen(a, mt, segp, ls, a.line_off[l + s + 1]);
-      if ((uint64_t)x >= ls + plen) atomicOr(&a.bits[l >> 5], 1u << (l & 31));
+      const uint32_t plen = (mt >> 2) == kPlenEscape ? line_plen(a, mt, segp, ls, a.line_off[l + s + 1]) : mt >> 2;
+      if ((uint64_t)(rel_lo + x) >= ls + plen) atomicOr(&a.bits[l >> 5], 1u << (l & 31));
       continue;
     }
     if ((a.bits[l >> 5] >> (l & 31)) & 1u) continue;
@@ -962,30 +987,48 @@ __device__ void verify_hit(const RunArgs& a, uint32_t s, uint64_t pos) {
   }
 }
 
-// Thread per tile over the tile-owned hit slots, then the spilled hits.
+// A wave per 64 consecutive tiles: the tiles' hit counts are prefix-summed across the
+// lanes, then every lane verifies one hit per round (the hit's tile found by a binary
+// search over the lanes' prefixes), so a tile with many hits spreads over the wave
+// instead of one thread walking them in series.  The spilled hits follow, one per lane.
 __global__ __launch_bounds__(256) void k_verify(RunArgs a) {
   if (a.counters[2] || a.counters[kCtrHitsOver]) return;
-  const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x, stride = gridDim.x * blockDim.x;
+  const int lane = threadIdx.x & 63;
+  const uint32_t nwaves = gridDim.x * (blockDim.x / 64);
   uint32_t walked = 0;
-  for (uint32_t tile = gid; tile < a.ntiles; tile += stride) {
-    const uint32_t n = a.tstat[tile].carry_off;
+  for (uint32_t t0 = (blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6)) * 64; t0 < a.ntiles; t0 += nwaves * 64) {
+    const uint32_t tile = t0 + (uint32_t)lane;
+    const uint32_t n = tile < a.ntiles ? a.tstat[tile].carry_off : 0u;
+    const uint32_t incl = wave_incl_scan_add(n, lane);
+    const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
     walked += n;
-    if (!n) continue;
-    const uint32_t s = a.tile_seg[tile];
-    const SegDesc sd = a.segs[s];
-    const uint64_t t0 = sd.base + (uint64_t)(tile - sd.tile0) * kTile;
-    const uint16_t* hs = a.hslots + (size_t)tile * kHitSlots;
-    for (uint32_t j = 0; j < n; ++j) verify_hit(a, s, t0 + hs[j]);
+    for (uint32_t h0 = 0; h0 < tot; h0 += 64) {
+      const uint32_t h = h0 + (uint32_t)lane;
+      // owning lane: the first lane whose inclusive prefix exceeds h
+      int lo = 0;
+#pragma unroll
+      for (int step = 32; step >= 1; step >>= 1) {
+        const uint32_t v = (uint32_t)__shfl((int)incl, lo + step - 1, 64);
+        if (v <= h) lo += step;
+      }
+      const uint32_t ex = (uint32_t)__shfl((int)(incl - n), lo, 64);
+      if (h < tot) {
+        const uint32_t tl = t0 + (uint32_t)lo;
+        verify_hit(a, tl, a.tile_seg[tl], a.hslots[(size_t)tl * kHitSlots + (h - ex)]);
+      }
+    }
   }
   const uint32_t nh = a.counters[kCtrHits] < a.qhits_cap ? a.counters[kCtrHits] : a.qhits_cap;
-  for (uint32_t i = gid; i < nh; i += stride) {
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nh; i += gridDim.x * blockDim.x) {
     const uint64_t pos = a.qhits[i];
     uint32_t lo = 0, hi = a.nsegs;
     while (hi - lo > 1) {
       const uint32_t mid = (lo + hi) >> 1;
       if (a.segs[mid].base <= pos) lo = mid; else hi = mid;
     }
-    verify_hit(a, lo, pos);
+    const uint64_t rel = pos - a.segs[lo].base;
+    const uint32_t tile = a.segs[lo].tile0 + (uint32_t)(rel / kTile);
+    verify_hit(a, tile, lo, (int32_t)(rel % kTile));
   }
   walked = wave_sum(walked);
   if ((threadIdx.x & 63) == 0 && walked) atomicAdd(&a.counters[kCtrVerified], walked);
@@ -1584,6 +1627,28 @@ __global__ __launch_bounds__(kThreads) void k_cgather(RunArgs a) {
   }
 }
 
+// Gram statistics for the prefilter's window choice: every byte position of a sample of
+// the batch into a count-min sketch (two rows, global atomics; one-off, first batch).
+__global__ __launch_bounds__(256) void k_gramhist(const uint8_t* bytes, const SegDesc* segs, uint32_t nsegs,
+                                                  uint64_t sample, uint32_t fold, uint32_t qmask, uint32_t* hist) {
+  const uint32_t nseg = nsegs < 16 ? nsegs : 16;
+  const uint32_t step = nsegs / nseg;
+  const uint64_t per = sample / 4;  // dwords per segment sample
+  for (uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; w < per * nseg; w += (uint64_t)gridDim.x * blockDim.x) {
+    const SegDesc sd = segs[(uint32_t)(w / per) * step];
+    const uint64_t o = (w % per) * 4;
+    if (o + 8 > sd.len) continue;
+    const uint32_t* p = reinterpret_cast<const uint32_t*>(bytes + sd.base + o);
+    const uint32_t w0 = p[0], w1 = p[1];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t g = ((k ? __builtin_amdgcn_alignbyte(w1, w0, k) : w0) | fold) & qmask;
+      atomicAdd(&hist[qf_hist_bin0(g)], 1u);
+      atomicAdd(&hist[qf_hist_bin1(g)], 1u);
+    }
+  }
+}
+
 }  // namespace
 
 hipError_t dump_timeline(void* host, size_t bytes) {
@@ -1603,6 +1668,14 @@ hipError_t clear_timeline() {
 #else
   return hipSuccess;
 #endif
+}
+
+hipError_t launch_gramhist(const uint8_t* bytes, const SegDesc* segs, uint32_t nsegs, uint64_t sample, uint32_t fold,
+                           uint32_t qmask, uint32_t* hist, hipStream_t st) {
+  hipError_t e = hipMemsetAsync(hist, 0, kQfHistBins * 4, st);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_gramhist, dim3(1024), dim3(256), 0, st, bytes, segs, nsegs, sample, fold, qmask, hist);
+  return hipGetLastError();
 }
 
 size_t nfa_lds_bytes(const DevPatterns& P) {

@@ -43,16 +43,23 @@ constexpr size_t kNfaMaxLds = 64 * 1024;            // k_nfa stages its tables i
 constexpr uint32_t kCarryBias = 256;                 // TileStat.carry_off = hit offset + 1 + bias
 // Blocked Bloom filter, one 32-bit bitmap word per probe.  The gram is folded to 24 bits
 // (byte 3 xor-ed into bits 11..18) so that both hashes are full-rate 24-bit multiplies:
-// word = top 12 bits of the low product (also the verification bucket), two bits inside
+// word = top 12 bits of the low product (also the verification bucket), three bits inside
 // the word from the low and the high product.
 __host__ __device__ inline uint32_t qf_fold24(uint32_t g) { return (g ^ (g >> 13)) & 0xFFFFFFu; }
 __host__ __device__ inline uint32_t qf_h1(uint32_t g) { return qf_fold24(g) * 0x9E3779u; }
 __host__ __device__ inline uint32_t qf_h2(uint32_t g) {
   return (uint32_t)(((uint64_t)qf_fold24(g) * 0xC2B2AEu) >> 32);  // v_mul_hi_u32_u24
 }
+// Gram statistics of the window choice: a count-min sketch, 2 rows of 2^16 bins
+constexpr int kQfHistBits = 16;
+constexpr uint32_t kQfHistBins = 2u << kQfHistBits;
+__host__ __device__ inline uint32_t qf_hist_bin0(uint32_t g) { return qf_h1(g) >> (32 - kQfHistBits); }
+__host__ __device__ inline uint32_t qf_hist_bin1(uint32_t g) {
+  return (1u << kQfHistBits) + ((g * 0x85EBCA77u) >> (32 - kQfHistBits));
+}
 __host__ __device__ inline uint32_t qf_word(uint32_t h1) { return h1 >> (32 - kQfBucketBits); }
 __host__ __device__ inline uint32_t qf_bits(uint32_t h1, uint32_t h2) {
-  return (1u << ((h1 >> 15) & 31u)) | (1u << (h2 & 31u));
+  return (1u << ((h1 >> 15) & 31u)) | (1u << (h2 & 31u)) | (1u << ((h2 >> 5) & 31u));
 }
 
 // Per-tile record of the scan (K1a), 16 B.
@@ -171,6 +178,10 @@ struct RunArgs {
 // scan, ev[3] after the general matcher, ev[4] after counts+tail+window prefix, ev[5]
 // after compaction.  Returns a hipError_t.
 hipError_t launch_pipeline(const RunArgs& a, hipStream_t stream, hipEvent_t* ev, int num_cus);
+// Gram sketch (kQfHistBins u32 bins, zeroed here) of the first `sample` bytes of each
+// of up to 16 segments, every position, grams folded / masked like the prefilter's.
+hipError_t launch_gramhist(const uint8_t* bytes, const SegDesc* segs, uint32_t nsegs, uint64_t sample, uint32_t fold,
+                           uint32_t qmask, uint32_t* hist, hipStream_t stream);
 // Diagnostic builds (-DKLF_TIMELINE=1): per-tile scan timeline; hipErrorNotSupported otherwise.
 hipError_t dump_timeline(void* host, size_t bytes);
 hipError_t clear_timeline();

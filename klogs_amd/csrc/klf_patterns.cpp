@@ -958,10 +958,7 @@ bool compile_set(const std::vector<std::vector<uint8_t>>& pats, const std::vecto
 // without any factor (e.g. `\d+`): those need a look at every line anyway.
 //
 // Each needle is sampled through a window of q + S - 1 of its bytes (any substring of a
-// literal / factor occurs wherever the needle does): the window whose S grams are the
-// least common in log text and among the needles already placed, so that grams like
-// "user" or a prefix shared by many literals do not flood the verification buckets.
-// Every gram sets two bits of one bitmap word (blocked Bloom, k = 2).
+// literal / factor occurs wherever the needle does); place_needles picks the windows.
 void build_prefilter(const std::vector<std::vector<uint8_t>>& lits, const std::vector<std::vector<std::string>>& rx_fac,
                      const std::vector<bool>& rx_loose, CompiledSet& out) {
   struct Needle {
@@ -992,7 +989,31 @@ void build_prefilter(const std::vector<std::vector<uint8_t>>& lits, const std::v
   out.qf_stride = S;
   out.qf_fold = loose ? 0x20202020u : 0u;
   out.qf_mask = q == 4 ? ~0u : ((1u << (8 * q)) - 1u);
+  out.qf_needle.clear();
+  out.qf_nflags.clear();
+  out.qf_nrx.clear();
+  for (auto& n : nd) {
+    out.qf_needle.push_back(n.s);
+    out.qf_nflags.push_back(n.flags);
+    out.qf_nrx.push_back(n.rx);
+  }
+  out.qf_needles = (uint32_t)nd.size();
+  out.qf_on = true;
+  place_needles(out, nullptr);
+}
+
+// Window choice + tables.  Each needle is sampled through q + S - 1 of its bytes: the
+// window whose S grams are the least frequent -- in the gram histogram of the data when
+// one is given (k_gramhist count-min sketch over a sample of the first batch), else by
+// a byte-class estimate -- with a small penalty for grams other needles already sample
+// (bucket length).  Every gram sets three bits of one bitmap word (blocked Bloom, k = 3).
+void place_needles(CompiledSet& out, const std::vector<uint32_t>* hist) {
+  const uint32_t q = out.qf_q, S = out.qf_stride;
+  const bool loose = out.qf_fold != 0;
   out.qf_bitmap.assign(kQfWords, 0u);
+  out.qf_head.clear();
+  out.qf_ent.clear();
+  out.qf_nbytes.clear();
   auto gram_at = [&](const std::string& s, uint32_t k) {
     uint32_t g = 0;
     for (uint32_t b = 0; b < q; ++b) g |= (uint32_t)(uint8_t)s[k + b] << (8 * b);
@@ -1000,26 +1021,32 @@ void build_prefilter(const std::vector<std::vector<uint8_t>>& lits, const std::v
   };
   auto common = [&](uint8_t c) -> int {  // rough frequency rank of a byte in log text
     if (loose && c >= 'A' && c <= 'Z') c |= 0x20;
-    if ((c >= 'a' && c <= 'z') || c == ' ') return 4;
-    if (c == '"' || c == ':' || c == ',' || c == '=' || c == '.' || c == '/' || c == '{' || c == '}' ||
-        (c >= '0' && c <= '9'))
-      return 2;
-    return 1;  // upper case, '_', '-', other punctuation, control and high bytes
+    if ((c >= 'a' && c <= 'z') || c == ' ' || (c >= '0' && c <= '9')) return 4;  // words, numbers, timestamps
+    if (strchr("\":,=./{}-TZ", c) && c) return 3;                                  // JSON / timestamp punctuation
+    return 1;  // upper case, '_', other punctuation, control and high bytes
   };
   std::map<uint32_t, int> used;  // gram -> needles sampling it so far
-  std::vector<std::vector<uint32_t>> buckets(1u << kQfBucketBits);
-  for (uint32_t i = 0; i < nd.size(); ++i) {
-    const std::string& s = nd[i].s;
+  std::vector<std::vector<uint32_t>> buckets(kQfWords);
+  const size_t n = out.qf_needle.size();
+  for (uint32_t i = 0; i < n; ++i) {
+    const std::string& s = out.qf_needle[i];
     const uint32_t amax = (uint32_t)std::min<size_t>(s.size() - (q + S - 1), 255 - (S - 1));
     uint32_t best_a = 0;
-    int best = INT32_MAX;
+    uint64_t best = UINT64_MAX;
     for (uint32_t a = 0; a <= amax; ++a) {
-      int sc = 0;
+      uint64_t sc = 0;
       for (uint32_t j = 0; j < S; ++j) {
-        int c = 0;
-        for (uint32_t b = 0; b < q; ++b) c += common((uint8_t)s[a + j + b]);
-        auto it = used.find(gram_at(s, a + j));
-        sc = std::max(sc, c + 6 * (it == used.end() ? 0 : it->second));
+        const uint32_t g = gram_at(s, a + j);
+        auto it = used.find(g);
+        const uint64_t u = it == used.end() ? 0 : (uint64_t)it->second;
+        uint64_t c;
+        if (hist) {
+          c = ((uint64_t)std::min((*hist)[qf_hist_bin0(g)], (*hist)[qf_hist_bin1(g)]) << 8) + 2 * u;
+        } else {
+          c = 2 * u;
+          for (uint32_t b = 0; b < q; ++b) c += common((uint8_t)s[a + j + b]);
+        }
+        sc = std::max(sc, c);
       }
       if (sc < best) { best = sc; best_a = a; }
     }
@@ -1033,28 +1060,26 @@ void build_prefilter(const std::vector<std::vector<uint8_t>>& lits, const std::v
   }
   // needle bytes (loose needles are already stored OR 0x20), then 16-B entries per bucket
   std::vector<uint32_t> noff;
-  for (auto& n : nd) {
+  for (auto& ns : out.qf_needle) {
     noff.push_back((uint32_t)out.qf_nbytes.size());
-    for (size_t b = 0; b < n.s.size(); b += 4) {
+    for (size_t b = 0; b < ns.size(); b += 4) {
       uint32_t w = 0;
-      for (size_t j = 0; j < 4 && b + j < n.s.size(); ++j) w |= (uint32_t)(uint8_t)n.s[b + j] << (8 * j);
+      for (size_t j = 0; j < 4 && b + j < ns.size(); ++j) w |= (uint32_t)(uint8_t)ns[b + j] << (8 * j);
       out.qf_nbytes.push_back(w);
     }
   }
-  out.qf_head.assign((1u << kQfBucketBits) + 1, 0u);
+  out.qf_head.assign(kQfWords + 1, 0u);
   for (uint32_t b = 0; b < buckets.size(); ++b) {
     out.qf_head[b] = (uint32_t)(out.qf_ent.size() / 4);
     for (uint32_t v : buckets[b]) {
-      const Needle& n = nd[v >> 8];
-      out.qf_ent.push_back(noff[v >> 8]);
-      out.qf_ent.push_back((uint32_t)n.s.size() | (v & 0xFFu) << 16 | n.flags);
-      out.qf_ent.push_back(n.rx);
-      out.qf_ent.push_back(out.qf_nbytes[noff[v >> 8]]);  // first dword: the pre-check
+      const uint32_t i = v >> 8;
+      out.qf_ent.push_back(noff[i]);
+      out.qf_ent.push_back((uint32_t)out.qf_needle[i].size() | (v & 0xFFu) << 16 | out.qf_nflags[i]);
+      out.qf_ent.push_back(out.qf_nrx[i]);
+      out.qf_ent.push_back(out.qf_nbytes[noff[i]]);  // first dword: the pre-check
     }
   }
   out.qf_head[buckets.size()] = (uint32_t)(out.qf_ent.size() / 4);
-  out.qf_needles = (uint32_t)nd.size();
-  out.qf_on = true;
 }
 
 bool prefilter_match(const CompiledSet& cs, const uint8_t* s, size_t n, uint32_t phase) {

@@ -78,6 +78,9 @@ struct CompiledSet {
                                      //  regex, first needle dword}; k = offset of the gram
   std::vector<uint32_t> qf_nbytes;   // needle bytes, each padded to whole dwords
   uint32_t qf_needles = 0;
+  std::vector<std::string> qf_needle;  // literal / factor bytes (loose: OR 0x20)
+  std::vector<uint32_t> qf_nflags, qf_nrx;
+  bool qf_tuned = false;               // windows placed from the data's gram histogram
   std::string qf_why;                // why the prefilter is off (diagnostics)
 };
 
@@ -85,6 +88,11 @@ struct CompiledSet {
 // one of `alts`; `loose` when some byte is an ASCII case pair ((?i)), then every byte is
 // stored OR 0x20 and compared that way.  False when the regex has no factor.
 bool regex_factors(const uint8_t* pat, size_t n, std::vector<std::string>& alts, bool& loose);
+
+// (Re)places every needle's sampling window and rebuilds the bitmap and buckets; hist =
+// gram count-min sketch of a data sample (kQfHistBins bins) or null for the byte-class
+// estimate.
+void place_needles(CompiledSet& cs, const std::vector<uint32_t>* hist);
 
 // Host emulation of the prefiltered matcher on one content (tests): sampled positions
 // p = phase mod stride, bitmap probe, bucket verification, NFA on factor hits.
