@@ -35,7 +35,7 @@ ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
 from klogs_amd import engine as E  # noqa: E402  (binds to torch's HIP runtime)
-from klogs_amd import synth  # noqa: E402
+from klogs_amd import shard, synth  # noqa: E402
 
 METRIC = "filtered log GB/s (whole node) at 1/2/4/8 MI355X; % of HBM peak"
 HBM_PEAK_GBS = 8000.0  # MI355X spec, /opt/skills/guides/MI355X_MICROARCH.md
@@ -79,6 +79,7 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     # ---- synthetic input: stream `rank` of the C2 family, generated on the host ----
+    assert shard.local_streams([args.bytes] * world, world, rank) == [rank]  # LPT: equal streams 1:1
     t = time.time()
     n = synth.size(synth.JSON, 42, rank, args.bytes, permille=10)
     host = np.empty(n + 1, dtype=np.uint8)
@@ -101,12 +102,8 @@ def main():
 
     def step():
         r = eng.run_device(ptr, seg_base, [n], since=since, tail=TAIL)
-        c = r.totals()
-        rec = torch.tensor([rank, c["lines"], c["matched"], c["selected"], c["out_bytes"]],
-                           dtype=torch.int64, device=f"cuda:{local}")
-        if world > 1:  # per-stream count records -> every rank (RCCL over xGMI)
-            gathered = torch.empty(world * rec.numel(), dtype=torch.int64, device=rec.device)
-            dist.all_gather_into_tensor(gathered, rec)
+        if world > 1:  # per-stream count records -> every rank (one all-gather, RCCL over xGMI)
+            shard.gather_counts({rank: r.totals()}, [n] * world, world, device=f"cuda:{local}")
         return r
 
     for _ in range(args.warmup):

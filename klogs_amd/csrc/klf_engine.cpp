@@ -59,7 +59,7 @@ struct klf_engine {
   std::vector<std::vector<uint8_t>> staged;
   // device pattern tables
   DevBuf d_lit, d_ac_class, d_ac_next, d_ac_accept, d_rx_class, d_rx_b, d_rx_follow, d_rx_vec, d_rx_flags;
-  DevBuf d_qf_bitmap, d_qf_head, d_qf_ent, d_qf_nbytes, d_cand, d_rx_vec4, d_qhits, d_hslots, d_hist;
+  DevBuf d_qf_bitmap, d_qf_head, d_qf_ent, d_qf_nbytes, d_cand, d_rx_vec4, d_qhits, d_hslots, d_hist, d_hflat;
   uint32_t cand_cap = 1u << 22;  // NFA candidate queue (32 MiB); overflow -> k_match
   uint64_t hits_cap_max = 1u << 26;  // prefilter hit list (512 MiB at most); overflow -> k_match
   klf::DevPatterns dpats;
@@ -251,7 +251,7 @@ extern "C" void klf_close(klf_engine* e) {
   if (e->stream) (void)hipStreamSynchronize(e->stream);
   for (DevBuf* b : {&e->d_lit, &e->d_ac_class, &e->d_ac_next, &e->d_ac_accept, &e->d_rx_class, &e->d_rx_b,
                     &e->d_rx_follow, &e->d_rx_vec, &e->d_rx_flags, &e->d_qf_bitmap, &e->d_qf_head,
-                    &e->d_qf_ent, &e->d_qf_nbytes, &e->d_rx_vec4, &e->d_qhits, &e->d_hslots, &e->d_hist, &e->d_cand, &e->d_batch, &e->d_segs, &e->d_tstat,
+                    &e->d_qf_ent, &e->d_qf_nbytes, &e->d_rx_vec4, &e->d_qhits, &e->d_hslots, &e->d_hist, &e->d_hflat, &e->d_cand, &e->d_batch, &e->d_segs, &e->d_tstat,
                     &e->d_slots, &e->d_pool, &e->d_tile_base, &e->d_bsum, &e->d_cstatus, &e->d_counters,
                     &e->d_line_off, &e->d_meta, &e->d_bits, &e->d_segout, &e->d_wpre, &e->d_out, &e->d_tile_seg, &e->d_mpart})
     b->release();
@@ -386,7 +386,7 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
   HIPCHK(e, e->d_tstat.ensure(ntiles * sizeof(klf::TileStat)), "alloc tstat");
   HIPCHK(e, e->d_slots.ensure(ntiles * klf::kSlots * 4), "alloc slots");
   HIPCHK(e, e->d_tile_base.ensure(ntiles * 8), "alloc tile_base");
-  HIPCHK(e, e->d_bsum.ensure((ntiles / 4096 + 2) * 3 * 8), "alloc bsum");
+  HIPCHK(e, e->d_bsum.ensure((ntiles / 4096 + 2) * 4 * 8), "alloc bsum");
   HIPCHK(e, e->d_counters.ensure(klf::kNumCounters * 4), "alloc counters");
   HIPCHK(e, e->d_segout.ensure(nsegs * sizeof(SegOut)), "alloc segout");
   HIPCHK(e, e->d_wpre.ensure((nsegs + 1) * 8), "alloc wpre");
@@ -398,9 +398,13 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
   // spills beyond 1 per 1 KiB of input -> k_match decides
   const uint32_t qhits_cap = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(total_bytes / 1024, 1u << 16),
                                                           e->hits_cap_max);
+  // flattened hit slots: up to 1 per 512 B of input (~16 per tile); more -> k_match decides
+  const uint64_t hflat_cap = std::min<uint64_t>(std::max<uint64_t>(total_bytes / 512, 1u << 20),
+                                                (uint64_t)ntiles * klf::kHitSlots);
   if (need_hits) {
     HIPCHK(e, e->d_qhits.ensure((size_t)qhits_cap * 8), "alloc qhits");
     HIPCHK(e, e->d_hslots.ensure((size_t)ntiles * klf::kHitSlots * 2), "alloc hslots");
+    HIPCHK(e, e->d_hflat.ensure((size_t)hflat_cap * 4), "alloc hflat");
   }
 
   for (int attempt = 0; attempt < 2; ++attempt) {
@@ -457,6 +461,8 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
     a.cand_cap = need_cand ? e->cand_cap : 0;
     a.qhits = need_hits ? e->d_qhits.as<uint64_t>() : nullptr;
     a.hslots = need_hits ? e->d_hslots.as<uint16_t>() : nullptr;
+    a.hflat = need_hits ? e->d_hflat.as<uint32_t>() : nullptr;
+    a.hflat_cap = need_hits ? hflat_cap : 0;
     a.qhits_cap = need_hits ? qhits_cap : 0;
     HIPCHK(e, klf::launch_pipeline(a, st, e->ev, e->num_cus), "launch");
     r->so.resize(nsegs);

@@ -110,11 +110,18 @@ __device__ __forceinline__ uint16_t make_meta(bool ok, bool since_ok, uint32_t p
 constexpr uint32_t kSlotOff = 0x3FFFu, kSlotDefer = 0x4000u, kSlotHit = 0x8000u;
 constexpr uint32_t kCtrDefer = 5;  // counters[5]: some line of this run was deferred
 
-// nonzero iff some byte of the 16 bytes equals the byte replicated in c4 (any-test: the
-// haszero borrow can only add false flags above a true zero byte)
+// Any-test: nonzero when some byte of the 16 equals the byte replicated in c4.  One
+// v_xad_u32 per dword ((x ^ c4) - 0x01..01: bit 7 of an equal byte is set) and 3-input
+// ORs; it also flags bytes with (x ^ c) >= 0x81 (non-ASCII text) and bytes above a true
+// match (borrow) -- false flags only send the chunk to the exact test.
+__device__ __forceinline__ uint32_t xad(uint32_t x, uint32_t c, uint32_t d) {  // (x ^ c) + d
+  uint32_t r;
+  asm("v_xad_u32 %0, %1, %2, %3" : "=v"(r) : "v"(x), "s"(c), "v"(d));
+  return r;
+}
 __device__ __forceinline__ uint32_t any_eq16(const uint4& v, uint32_t c4) {
-  auto h = [c4](uint32_t x) { const uint32_t y = x ^ c4; return (y - 0x01010101u) & ~y; };
-  return (h(v.x) | h(v.y) | h(v.z) | h(v.w)) & 0x80808080u;
+  const uint32_t m = 0xFEFEFEFFu;  // -0x01010101
+  return (xad(v.x, c4, m) | xad(v.y, c4, m) | xad(v.z, c4, m) | xad(v.w, c4, m)) & 0x80808080u;
 }
 // exact: bit i set iff byte i of the 16 bytes equals the byte in c4
 __device__ __forceinline__ uint32_t eq_mask16(const uint4& v, uint32_t c4) {
@@ -679,8 +686,13 @@ __global__ __launch_bounds__(256) void k_fixup(RunArgs a) {
 // only ever OR-ed into by the kernels after this one).
 constexpr int kTilesPerScanBlock = 4096;  // 256 threads x 16 tiles
 
+// TileStat.carry_off is the tile's hit-slot count with the q-gram prefilter (GEN scan)
+__device__ __forceinline__ uint32_t tile_hits(const RunArgs& a, const TileStat& ts) {
+  return (a.grep_mode == kGrepGeneral && a.pats.qf_on) ? ts.carry_off : 0u;
+}
+
 __global__ __launch_bounds__(256) void k_tsum(RunArgs a) {
-  __shared__ uint64_t s_w[3][4];
+  __shared__ uint64_t s_w[4][4];
   constexpr int R = kTilesPerScanBlock / 256;
   const uint32_t t0 = blockIdx.x * kTilesPerScanBlock + threadIdx.x;
   TileStat ts[R];
@@ -689,27 +701,32 @@ __global__ __launch_bounds__(256) void k_tsum(RunArgs a) {
     ts[r] = TileStat{};
     if (t0 + r * 256 < a.ntiles) ts[r] = a.tstat[t0 + r * 256];
   }
-  uint64_t v = 0, p = 0, q = 0;
+  uint64_t v = 0, p = 0, q = 0, h = 0;
 #pragma unroll
-  for (int r = 0; r < R; ++r) { v += ts[r].events; p += ts[r].parsed; q += ts[r].since_ok; }
+  for (int r = 0; r < R; ++r) { v += ts[r].events; p += ts[r].parsed; q += ts[r].since_ok; h += tile_hits(a, ts[r]); }
   v = wave_sum(v);
   p = wave_sum(p);
   q = wave_sum(q);
-  if ((threadIdx.x & 63) == 0) { s_w[0][threadIdx.x >> 6] = v; s_w[1][threadIdx.x >> 6] = p; s_w[2][threadIdx.x >> 6] = q; }
+  h = wave_sum(h);
+  if ((threadIdx.x & 63) == 0) {
+    s_w[0][threadIdx.x >> 6] = v; s_w[1][threadIdx.x >> 6] = p; s_w[2][threadIdx.x >> 6] = q; s_w[3][threadIdx.x >> 6] = h;
+  }
   __syncthreads();
-  if (threadIdx.x < 3) {
+  if (threadIdx.x < 4) {
     const int k = threadIdx.x;
-    a.bsum[3 * blockIdx.x + k] = s_w[k][0] + s_w[k][1] + s_w[k][2] + s_w[k][3];
+    a.bsum[4 * blockIdx.x + k] = s_w[k][0] + s_w[k][1] + s_w[k][2] + s_w[k][3];
   }
 }
 
 // Rounds of 256 consecutive tiles (one per thread, coalesced), block scan per round.  All
 // rounds' records and tile->stream ids are loaded up front; stream boundaries are where
-// the stream id of the neighbouring tile differs (no dependent descriptor loads).
+// the stream id of the neighbouring tile differs (no dependent descriptor loads).  With
+// the q-gram prefilter the same scan flattens the tiles' hit slots into one list for
+// k_verify (hit slot ids tile * kHitSlots + j).
 __global__ __launch_bounds__(256) void k_tbase(RunArgs a) {
   constexpr int R = kTilesPerScanBlock / 256;
-  __shared__ uint64_t s_w[2][3][4];
-  __shared__ uint64_t s_base[3];
+  __shared__ uint64_t s_w[2][4][4];
+  __shared__ uint64_t s_base[4];
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const uint32_t t0 = blockIdx.x * kTilesPerScanBlock + t;
   TileStat ts[R];
@@ -727,41 +744,51 @@ __global__ __launch_bounds__(256) void k_tbase(RunArgs a) {
     }
   }
   {  // prefix of the preceding blocks' sums
-    uint64_t v = 0, p = 0, q = 0;
+    uint64_t v = 0, p = 0, q = 0, h = 0;
     for (uint32_t b = t; b < blockIdx.x; b += 256) {
-      v += a.bsum[3 * b];
-      p += a.bsum[3 * b + 1];
-      q += a.bsum[3 * b + 2];
+      v += a.bsum[4 * b];
+      p += a.bsum[4 * b + 1];
+      q += a.bsum[4 * b + 2];
+      h += a.bsum[4 * b + 3];
     }
     v = wave_sum(v);
     p = wave_sum(p);
     q = wave_sum(q);
-    if (lane == 0) { s_w[0][0][wv] = v; s_w[0][1][wv] = p; s_w[0][2][wv] = q; }
+    h = wave_sum(h);
+    if (lane == 0) { s_w[0][0][wv] = v; s_w[0][1][wv] = p; s_w[0][2][wv] = q; s_w[0][3][wv] = h; }
     __syncthreads();
-    if (t < 3) s_base[t] = s_w[0][t][0] + s_w[0][t][1] + s_w[0][t][2] + s_w[0][t][3];
+    if (t < 4) s_base[t] = s_w[0][t][0] + s_w[0][t][1] + s_w[0][t][2] + s_w[0][t][3];
     __syncthreads();
   }
   const uint64_t blk_lo = s_base[0];
-  uint64_t cv = s_base[0], cp = s_base[1], cq = s_base[2];  // running bases (block-uniform)
+  uint64_t cv = s_base[0], cp = s_base[1], cq = s_base[2], ch = s_base[3];  // running bases (block-uniform)
 #pragma unroll
   for (int r = 0; r < R; ++r) {
     const uint32_t tile = t0 + r * 256;
-    const uint64_t v = ts[r].events, p = ts[r].parsed, q = ts[r].since_ok;
-    const uint64_t iv = wave_incl_scan_add(v, lane), ip = wave_incl_scan_add(p, lane), iq = wave_incl_scan_add(q, lane);
+    const uint64_t v = ts[r].events, p = ts[r].parsed, q = ts[r].since_ok, h = tile_hits(a, ts[r]);
+    const uint64_t iv = wave_incl_scan_add(v, lane), ip = wave_incl_scan_add(p, lane), iq = wave_incl_scan_add(q, lane),
+                   ih = wave_incl_scan_add(h, lane);
     const int pb = r & 1;  // double-buffered wave totals: one barrier per round
-    if (lane == 63) { s_w[pb][0][wv] = iv; s_w[pb][1][wv] = ip; s_w[pb][2][wv] = iq; }
+    if (lane == 63) { s_w[pb][0][wv] = iv; s_w[pb][1][wv] = ip; s_w[pb][2][wv] = iq; s_w[pb][3][wv] = ih; }
     __syncthreads();
-    uint64_t bv = cv + iv - v, bp = cp + ip - p, bq = cq + iq - q;
-    for (int k = 0; k < wv; ++k) { bv += s_w[pb][0][k]; bp += s_w[pb][1][k]; bq += s_w[pb][2][k]; }
+    uint64_t bv = cv + iv - v, bp = cp + ip - p, bq = cq + iq - q, bh = ch + ih - h;
+    for (int k = 0; k < wv; ++k) { bv += s_w[pb][0][k]; bp += s_w[pb][1][k]; bq += s_w[pb][2][k]; bh += s_w[pb][3][k]; }
     cv += s_w[pb][0][0] + s_w[pb][0][1] + s_w[pb][0][2] + s_w[pb][0][3];
     cp += s_w[pb][1][0] + s_w[pb][1][1] + s_w[pb][1][2] + s_w[pb][1][3];
     cq += s_w[pb][2][0] + s_w[pb][2][1] + s_w[pb][2][2] + s_w[pb][2][3];
+    ch += s_w[pb][3][0] + s_w[pb][3][1] + s_w[pb][3][2] + s_w[pb][3][3];
     if (tile < a.ntiles) {
       a.tile_base[tile] = bv;
       const uint32_t s = sg[r];
       if (sp[r] != s) { a.segout[s].line_lo = bv; a.segout[s].p_lo = bp; a.segout[s].q_lo = bq; }
       if (sn[r] != s) { a.segout[s].line_hi = bv + v; a.segout[s].p_hi = bp + p; a.segout[s].q_hi = bq + q; }
+      for (uint32_t j = 0; j < (uint32_t)h; ++j)
+        if (bh + j < a.hflat_cap) a.hflat[bh + j] = tile * kHitSlots + j;
     }
+  }
+  if (t == 0 && blockIdx.x == gridDim.x - 1 && a.hflat) {  // the last block knows the total
+    a.counters[kCtrFlatHits] = (uint32_t)(ch < 0xFFFFFFFFull ? ch : 0xFFFFFFFFull);
+    if (ch > a.hflat_cap) atomicOr(&a.counters[kCtrHitsOver], 1u);
   }
   if (a.grep_mode != kGrepNone) {  // bitmap words whose first line is in [blk_lo, blk_hi)
     const uint64_t w0 = (blk_lo + 31) / 32, w1 = (cv + 31) / 32;
@@ -987,39 +1014,18 @@ __device__ void verify_hit(const RunArgs& a, uint32_t tile, uint32_t s, int32_t 
   }
 }
 
-// A wave per 64 consecutive tiles: the tiles' hit counts are prefix-summed across the
-// lanes, then every lane verifies one hit per round (the hit's tile found by a binary
-// search over the lanes' prefixes), so a tile with many hits spreads over the wave
-// instead of one thread walking them in series.  The spilled hits follow, one per lane.
+// Thread per hit: the flattened tile hit slots (k_tbase), then the spilled hits.
 __global__ __launch_bounds__(256) void k_verify(RunArgs a) {
   if (a.counters[2] || a.counters[kCtrHitsOver]) return;
-  const int lane = threadIdx.x & 63;
-  const uint32_t nwaves = gridDim.x * (blockDim.x / 64);
-  uint32_t walked = 0;
-  for (uint32_t t0 = (blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6)) * 64; t0 < a.ntiles; t0 += nwaves * 64) {
-    const uint32_t tile = t0 + (uint32_t)lane;
-    const uint32_t n = tile < a.ntiles ? a.tstat[tile].carry_off : 0u;
-    const uint32_t incl = wave_incl_scan_add(n, lane);
-    const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
-    walked += n;
-    for (uint32_t h0 = 0; h0 < tot; h0 += 64) {
-      const uint32_t h = h0 + (uint32_t)lane;
-      // owning lane: the first lane whose inclusive prefix exceeds h
-      int lo = 0;
-#pragma unroll
-      for (int step = 32; step >= 1; step >>= 1) {
-        const uint32_t v = (uint32_t)__shfl((int)incl, lo + step - 1, 64);
-        if (v <= h) lo += step;
-      }
-      const uint32_t ex = (uint32_t)__shfl((int)(incl - n), lo, 64);
-      if (h < tot) {
-        const uint32_t tl = t0 + (uint32_t)lo;
-        verify_hit(a, tl, a.tile_seg[tl], a.hslots[(size_t)tl * kHitSlots + (h - ex)]);
-      }
-    }
+  const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x, stride = gridDim.x * blockDim.x;
+  const uint32_t nf = a.counters[kCtrFlatHits];
+  for (uint32_t i = gid; i < nf; i += stride) {
+    const uint32_t slot = a.hflat[i];
+    const uint32_t tile = slot / kHitSlots;
+    verify_hit(a, tile, a.tile_seg[tile], a.hslots[slot]);
   }
   const uint32_t nh = a.counters[kCtrHits] < a.qhits_cap ? a.counters[kCtrHits] : a.qhits_cap;
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nh; i += gridDim.x * blockDim.x) {
+  for (uint32_t i = gid; i < nh; i += stride) {
     const uint64_t pos = a.qhits[i];
     uint32_t lo = 0, hi = a.nsegs;
     while (hi - lo > 1) {
@@ -1030,8 +1036,7 @@ __global__ __launch_bounds__(256) void k_verify(RunArgs a) {
     const uint32_t tile = a.segs[lo].tile0 + (uint32_t)(rel / kTile);
     verify_hit(a, tile, lo, (int32_t)(rel % kTile));
   }
-  walked = wave_sum(walked);
-  if ((threadIdx.x & 63) == 0 && walked) atomicAdd(&a.counters[kCtrVerified], walked);
+  if (gid == 0) a.counters[kCtrVerified] = nf + nh;
 }
 
 // K2b: the prefiltered regex stage.  One lane per queued (batch offset, regex) candidate:

@@ -34,6 +34,7 @@ constexpr uint32_t kCtrQOver = 7;                    // counters[7]: queue overf
 constexpr uint32_t kHitSlots = 32;                   // prefilter hits a tile records itself
 constexpr uint32_t kCtrHits = 8;                     // counters[8]: spilled prefilter hits
 constexpr uint32_t kCtrHitsOver = 9;                 // counters[9]: hit list overflow -> k_match
+constexpr uint32_t kCtrFlatHits = 12;                // counters[12]: hit slots flattened by k_tbase
 constexpr uint32_t kCtrCopyChunks = 11;              // counters[11]: output copy chunks (k_cgather)
 constexpr uint64_t kCopyChunk = 64 * 1024;           // output bytes per k_cgather work item
 constexpr uint32_t kCtrVerified = 10;                // counters[10]: hits k_verify walked (diagnostics)
@@ -152,7 +153,7 @@ struct RunArgs {
   uint32_t* pool;       // [pool_cap] slots of dense tiles
   uint64_t pool_cap;
   uint64_t* tile_base;  // [ntiles] global line index of each tile's line 0
-  uint64_t* bsum;       // [3 * (ntiles / 4096 + 1)] scan block sums (events, parsed, since_ok)
+  uint64_t* bsum;       // [4 * (ntiles / 4096 + 1)] scan block sums (events, parsed, since_ok, hits)
   uint64_t* mpart;      // [cap_lines / kMatchChunk + 1] matched-line partial per line chunk
   uint64_t* csum;       // [3 * (max compaction blocks + 1)] per-block (bytes, lines), then their
                         // prefixes and the prefix of copy chunks
@@ -169,6 +170,8 @@ struct RunArgs {
   uint64_t* cand;       // [cand_cap] NFA candidates: global line index | regex << 40
   uint32_t cand_cap;
   uint16_t* hslots;     // [ntiles * kHitSlots] prefilter hits (tile offsets of the samples)
+  uint32_t* hflat;      // [hflat_cap] hit slot ids (tile * kHitSlots + j), flattened by k_tbase
+  uint64_t hflat_cap;
   uint64_t* qhits;      // [qhits_cap] spilled hits (batch byte offsets of the samples)
   uint32_t qhits_cap;
 };
