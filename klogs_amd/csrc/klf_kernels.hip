@@ -52,6 +52,43 @@ __device__ __forceinline__ T wave_incl_scan_add(T x, int lane) {
   return x;
 }
 
+// 32-bit wave scans / reductions on DPP (row_shr within 16-lane rows, then the row totals
+// through v_readlane): no LDS round trips (the generic __shfl versions above lower to
+// ds_bpermute, ~100 cycles each, six in a chain).  Exact-type overloads: every u32 call
+// site picks these.
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp0(uint32_t x) {  // lanes with no source read 0
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, 0xF, 0xF, true);
+}
+__device__ __forceinline__ uint32_t wave_incl_scan_add(uint32_t x, int lane) {
+  x += dpp0<0x111>(x);  // row_shr:1
+  x += dpp0<0x112>(x);  // row_shr:2
+  x += dpp0<0x114>(x);  // row_shr:4
+  x += dpp0<0x118>(x);  // row_shr:8
+  const uint32_t r0 = (uint32_t)__builtin_amdgcn_readlane((int)x, 15);
+  const uint32_t r1 = r0 + (uint32_t)__builtin_amdgcn_readlane((int)x, 31);
+  const uint32_t r2 = r1 + (uint32_t)__builtin_amdgcn_readlane((int)x, 47);
+  const int row = lane >> 4;
+  return x + (row == 0 ? 0u : row == 1 ? r0 : row == 2 ? r1 : r2);
+}
+__device__ __forceinline__ uint32_t wave_sum(uint32_t x) {
+  x += dpp0<0x111>(x);
+  x += dpp0<0x112>(x);
+  x += dpp0<0x114>(x);
+  x += dpp0<0x118>(x);
+  return (uint32_t)__builtin_amdgcn_readlane((int)x, 15) + (uint32_t)__builtin_amdgcn_readlane((int)x, 31) +
+         (uint32_t)__builtin_amdgcn_readlane((int)x, 47) + (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
+}
+__device__ __forceinline__ uint32_t wave_max(uint32_t x) {
+  auto mx = [](uint32_t a, uint32_t b) { return a > b ? a : b; };
+  x = mx(x, dpp0<0x111>(x));
+  x = mx(x, dpp0<0x112>(x));
+  x = mx(x, dpp0<0x114>(x));
+  x = mx(x, dpp0<0x118>(x));
+  return mx(mx((uint32_t)__builtin_amdgcn_readlane((int)x, 15), (uint32_t)__builtin_amdgcn_readlane((int)x, 31)),
+            mx((uint32_t)__builtin_amdgcn_readlane((int)x, 47), (uint32_t)__builtin_amdgcn_readlane((int)x, 63)));
+}
+
 __device__ __forceinline__ uint32_t find_seg_by_tile(const SegDesc* segs, uint32_t n, uint32_t tile) {
   uint32_t lo = 0, hi = n;
   while (hi - lo > 1) {
