@@ -92,9 +92,13 @@ int klf_reset(klf_engine* e);
 typedef struct klf_filter {
   klf_time since;   /* lines with ts.Before(since) are dropped (S3)                    */
   int64_t tail;     /* -1 = all, else >= 0 (S4)                                        */
-  uint32_t flags;   /* reserved, 0                                                     */
+  uint32_t flags;   /* KLF_FILTER_* bits, 0 = none                                     */
   uint32_t _reserved;
 } klf_filter;
+
+/* klf_filter.flags: record the inner stage boundaries (klf_result_timing [0]-[3]).
+ * Each boundary costs a few microseconds of idle GPU; off, only [4]-[6] are measured. */
+#define KLF_FILTER_STAGE_TIMES 1u
 
 typedef struct klf_counts {
   uint64_t lines;      /* all lines (a trailing fragment counts)                       */
@@ -138,10 +142,10 @@ int klf_result_match_bits(klf_result* r, uint32_t stream_id, const uint8_t** bit
 int klf_result_device_out(klf_result* r, uint32_t stream_id, const uint8_t** d_out,
                           uint64_t* off, uint64_t* len);
 /* Per-stage device time of the run in ms, HIP events on the launch stream:
- * [0] scan kernel (newline + line index + timestamp + since + fused literal grep),
- * [1] general pattern matcher, [2] counts + tail + window prefix, [3] compaction,
- * [4] total device time, [5] workspace memsets, [6] the k_scan kernel alone (part of
- * [0]).  n = number of entries written. */
+ * [0] scan stage (newline + line index + timestamp + since + fused grep prefilter),
+ * [1] pattern verification / matchers, [2] counts + tail + window prefix, [3] compaction
+ * (these four only with KLF_FILTER_STAGE_TIMES, else 0), [4] total device time,
+ * [5] workspace memsets, [6] the k_scan kernel alone (part of [0]).  n = entries written. */
 int klf_result_timing(const klf_result* r, double* ms, uint32_t cap, uint32_t* n);
 /* Totals across streams. */
 int klf_result_totals(const klf_result* r, klf_counts* totals);

@@ -457,6 +457,7 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
     a.wpre = e->d_wpre.as<uint64_t>();
     a.out = e->d_out.as<uint8_t>();
     a.max_cblocks = (uint32_t)max_cblocks;
+    a.stage_times = (f->flags & KLF_FILTER_STAGE_TIMES) ? 1u : 0u;
     a.cand = need_cand ? e->d_cand.as<uint64_t>() : nullptr;
     a.cand_cap = need_cand ? e->cand_cap : 0;
     a.qhits = need_hits ? e->d_qhits.as<uint64_t>() : nullptr;
@@ -493,8 +494,9 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
     }
   }
   float ms;
-  for (int k = 0; k < 4; ++k)  // scan, match, tail stage, compaction
-    if (hipEventElapsedTime(&ms, e->ev[k + 1], e->ev[k + 2]) == hipSuccess) r->ms[k] = ms;
+  if (f->flags & KLF_FILTER_STAGE_TIMES)
+    for (int k = 0; k < 4; ++k)  // scan stage, match, tail stage, compaction
+      if (hipEventElapsedTime(&ms, e->ev[k + 1], e->ev[k + 2]) == hipSuccess) r->ms[k] = ms;
   if (hipEventElapsedTime(&ms, e->ev[0], e->ev[5]) == hipSuccess) r->ms[4] = ms;
   if (hipEventElapsedTime(&ms, e->ev[0], e->ev[1]) == hipSuccess) r->ms[5] = ms;
   if (hipEventElapsedTime(&ms, e->ev[1], e->ev[6]) == hipSuccess) r->ms[6] = ms;

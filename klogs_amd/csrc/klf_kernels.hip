@@ -1726,9 +1726,11 @@ size_t nfa_lds_bytes(const DevPatterns& P) {
 
 template <int MODE, int QS>
 hipError_t launch_scan(const RunArgs& a, hipStream_t st, int num_cus) {
-  int occ = 0;
-  (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_scan<MODE, QS>, kThreads, 0);
-  occ = occ < 1 ? 1 : (occ > 8 ? 8 : occ);
+  static int occ = 0;  // queried once per variant: the host query delays the launch
+  if (occ == 0) {
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_scan<MODE, QS>, kThreads, 0);
+    occ = occ < 1 ? 1 : (occ > 8 ? 8 : occ);
+  }
   uint32_t grid = (uint32_t)(num_cus * occ);
   if (grid > a.ntiles) grid = a.ntiles;
   hipLaunchKernelGGL((k_scan<MODE, QS>), dim3(grid), dim3(kThreads), 0, st, a, a.tile_seg, a.segs);
@@ -1777,7 +1779,7 @@ hipError_t launch_pipeline(const RunArgs& a, hipStream_t st, hipEvent_t* ev, int
     hipLaunchKernelGGL(k_scatter, dim3(sg), dim3(256), 0, st, a);
   }
   KLF_TRY(hipGetLastError());
-  KLF_TRY(hipEventRecord(ev[2], st));
+  if (a.stage_times) KLF_TRY(hipEventRecord(ev[2], st));  // ~5 us of idle GPU each
   if (a.grep_mode == kGrepGeneral && a.pats.qf_on) {
     hipLaunchKernelGGL(k_verify, dim3(num_cus * 8), dim3(256), 0, st, a);
     KLF_TRY(hipGetLastError());
@@ -1794,7 +1796,7 @@ hipError_t launch_pipeline(const RunArgs& a, hipStream_t st, hipEvent_t* ev, int
     hipLaunchKernelGGL(k_match, dim3(num_cus * 8), dim3(256), 0, st, a);
     KLF_TRY(hipGetLastError());
   }
-  KLF_TRY(hipEventRecord(ev[3], st));
+  if (a.stage_times) KLF_TRY(hipEventRecord(ev[3], st));  // ~5 us of idle GPU each
   if (a.grep_mode != kGrepNone) {
     const uint64_t nchunks = a.cap_lines / kMatchChunk + 1;
     const uint32_t g = (uint32_t)(nchunks < (uint64_t)num_cus * 4 ? nchunks : (uint64_t)num_cus * 4);
@@ -1805,7 +1807,7 @@ hipError_t launch_pipeline(const RunArgs& a, hipStream_t st, hipEvent_t* ev, int
   KLF_TRY(hipGetLastError());
   hipLaunchKernelGGL(k_wprefix, dim3(1), dim3(256), 0, st, a);
   KLF_TRY(hipGetLastError());
-  KLF_TRY(hipEventRecord(ev[4], st));
+  if (a.stage_times) KLF_TRY(hipEventRecord(ev[4], st));  // ~5 us of idle GPU each
   hipLaunchKernelGGL(k_csum, dim3(num_cus * 4), dim3(kThreads), 0, st, a);
   KLF_TRY(hipGetLastError());
   hipLaunchKernelGGL(k_cscan, dim3(1), dim3(256), 0, st, a);

@@ -36,7 +36,7 @@ constexpr uint32_t kCtrHits = 8;                     // counters[8]: spilled pre
 constexpr uint32_t kCtrHitsOver = 9;                 // counters[9]: hit list overflow -> k_match
 constexpr uint32_t kCtrFlatHits = 12;                // counters[12]: hit slots flattened by k_tbase
 constexpr uint32_t kCtrCopyChunks = 11;              // counters[11]: output copy chunks (k_cgather)
-constexpr uint64_t kCopyChunk = 64 * 1024;           // output bytes per k_cgather work item
+constexpr uint64_t kCopyChunk = 16 * 1024;           // output bytes per k_cgather work item
 constexpr uint32_t kCtrVerified = 10;                // counters[10]: hits k_verify walked (diagnostics)
 constexpr uint32_t kQfRegex = 1u << 24;              // entry flags: regex factor (else literal)
 constexpr uint32_t kQfLoose = 1u << 25;              //   compare OR 0x20 per byte
@@ -167,6 +167,7 @@ struct RunArgs {
   uint64_t* wpre;       // [nsegs + 1] exclusive prefix of window sizes
   uint8_t* out;         // output bytes (capacity >= total input)
   uint32_t max_cblocks; // compaction block capacity
+  uint32_t stage_times; // record the inner stage events (ev[2..4])
   uint64_t* cand;       // [cand_cap] NFA candidates: global line index | regex << 40
   uint32_t cand_cap;
   uint16_t* hslots;     // [ntiles * kHitSlots] prefilter hits (tile offsets of the samples)

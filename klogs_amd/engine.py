@@ -142,11 +142,15 @@ def _patterns(grep: Sequence[bytes], match: Sequence[bytes]):
     return arr, len(items), keep
 
 
-def _filter(since: Optional[Tuple[int, int]], tail: int) -> _Filter:
+KLF_FILTER_STAGE_TIMES = 1
+
+
+def _filter(since: Optional[Tuple[int, int]], tail: int, stage_times: bool = False) -> _Filter:
     f = _Filter()
     s = GO_ZERO_TIME if since is None else since
     f.since.sec, f.since.nsec = int(s[0]), int(s[1])
     f.tail = int(tail)
+    f.flags = KLF_FILTER_STAGE_TIMES if stage_times else 0
     return f
 
 
@@ -291,18 +295,18 @@ class Engine:
     def reset(self):
         _check(_lib.klf_reset(self._h), self._h)
 
-    def run(self, since=None, tail: int = -1, n_streams: Optional[int] = None) -> Result:
-        f = _filter(since, tail)
+    def run(self, since=None, tail: int = -1, n_streams: Optional[int] = None, stage_times: bool = False) -> Result:
+        f = _filter(since, tail, stage_times)
         r = C.c_void_p()
         _check(_lib.klf_run(self._h, C.byref(f), C.byref(r)), self._h)
         return Result(r.value or 0, n_streams if n_streams is not None else 0, self)
 
     def run_device(self, d_ptr: int, seg_base: Sequence[int], lens: Sequence[int], since=None,
-                   tail: int = -1) -> Result:
+                   tail: int = -1, stage_times: bool = False) -> Result:
         n = len(lens)
         B = (C.c_uint64 * max(1, n))(*[int(x) for x in seg_base])
         L = (C.c_uint64 * max(1, n))(*[int(x) for x in lens])
-        f = _filter(since, tail)
+        f = _filter(since, tail, stage_times)
         r = C.c_void_p()
         _check(_lib.klf_run_device(self._h, C.c_void_p(d_ptr), n, B, L, C.byref(f), C.byref(r)), self._h)
         return Result(r.value or 0, n, self)

@@ -19,7 +19,7 @@ for name, kind, pats in (("c4", synth.MIXED, dict(grep=synth.c4_literals(1024)))
         eng = E.Engine(0, **kw)
         ts = []
         for i in range(10):
-            r = eng.run_device(dev.data_ptr(), base, lens, since=(synth.T0 + 3301, 0), tail=100)
+            r = eng.run_device(dev.data_ptr(), base, lens, since=(synth.T0 + 3301, 0), tail=100, stage_times=True)
             ts.append(r.timing()); tot = r.totals(); r.free()
         ts = np.array(ts[2:])
         res[f"{name}_{tag}"] = {"scan_ms": round(float(np.median(ts[:, 6])), 3), "match_ms": round(float(np.median(ts[:, 1])), 3),
