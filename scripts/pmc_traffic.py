@@ -11,7 +11,7 @@ import csv
 import json
 import sys
 
-KERNEL = "k_scan<true>"
+KERNEL = "k_scan<1, 1>"  # the literal variant: BASELINE config 2 (C2)
 
 
 def per_launch(path, counter):
