@@ -287,7 +287,7 @@ __global__ __launch_bounds__(kThreads, MODE == kScanGen ? 3 : KLF_SCAN_OCC) void
   constexpr int kWaves = kThreads / 64;
   constexpr int kRows = kTile / 1024;  // 1 KiB rows: 16 B per lane per row
   __shared__ __attribute__((aligned(16))) uint8_t s_tile_all[kWaves][kTile + kHalo];
-  __shared__ uint32_t s_list_all[kWaves][kSlots];
+  __shared__ __attribute__((aligned(16))) uint32_t s_list_all[kWaves][kSlotStride];
   __shared__ __attribute__((aligned(16))) uint32_t s_lit[kMaxFusedLiteral / 4 + 1];  // literal, zero padded
   __shared__ uint32_t s_month[16];
   __shared__ uint32_t s_qf[GEN ? kQfWords : 1];  // q-gram bitmap of the needles
@@ -304,11 +304,7 @@ __global__ __launch_bounds__(kThreads, MODE == kScanGen ? 3 : KLF_SCAN_OCC) void
     for (uint32_t i = t; i < kQfWords; i += kThreads) s_qf[i] = a.pats.qf_bitmap[i];
   __syncthreads();  // the kernel's only block barrier
   const uint32_t nwaves = gridDim.x * kWaves;
-  auto tile_src = [&](uint32_t tl) -> const uint4* {
-    const uint32_t ss = tseg[tl];
-    const SegDesc d = segs[ss];
-    return reinterpret_cast<const uint4*>(a.bytes + d.base + (uint64_t)(tl - d.tile0) * kTile);
-  };
+
   // the prefetch registers are named (an array here was put on the scratch stack)
   static_assert(kRows == 8, "KLF_ROWS lists the 8 prefetch rows");
 #define KLF_ROWS(X) X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7)
@@ -319,15 +315,23 @@ __global__ __launch_bounds__(kThreads, MODE == kScanGen ? 3 : KLF_SCAN_OCC) void
 #define KLF_STORE(r) l[r * 64 + lane] = pf##r;
   uint4 pfh = make_uint4(0, 0, 0, 0);
   uint32_t tile = blockIdx.x * kWaves + wv;
+  // The segment of the prefetched tile travels with it (scalar registers): a stride of
+  // nwaves tiles stays inside one stream for all but the last tiles of a long stream, so
+  // the dependent descriptor loads (tseg -> segs, scalar-cache misses at this stride) leave
+  // the path that issues the next prefetch.
+  uint32_t pf_s = 0;
+  SegDesc pf_sd{};
   if (tile < a.ntiles) {
-    const uint4* gp = tile_src(tile);
+    pf_s = tseg[tile];
+    pf_sd = segs[pf_s];
+    const uint4* gp = reinterpret_cast<const uint4*>(a.bytes + pf_sd.base + (uint64_t)(tile - pf_sd.tile0) * kTile);
     KLF_ROWS(KLF_LOAD)
     if (lane < kHalo / 16) pfh = gp[kTile / 16 + lane];
   }
   bool any_defer = false;
   for (; tile < a.ntiles; tile += nwaves) {
-    const uint32_t s = tseg[tile];
-    const SegDesc sd = segs[s];
+    const uint32_t s = pf_s;
+    const SegDesc sd = pf_sd;
     const int64_t rel_lo = (int64_t)(tile - sd.tile0) * kTile;
     const int64_t seg_len = (int64_t)sd.len;
     const int32_t tile_len = (int32_t)(seg_len - rel_lo < kTile ? seg_len - rel_lo : kTile);
@@ -342,7 +346,11 @@ __global__ __launch_bounds__(kThreads, MODE == kScanGen ? 3 : KLF_SCAN_OCC) void
       if (lane < kHalo / 16) l[kTile / 16 + lane] = pfh;
       const uint32_t nx = tile + nwaves;
       if (nx < a.ntiles) {
-        const uint4* gp = tile_src(nx);
+        if (nx - sd.tile0 >= sd.ntiles) {
+          pf_s = tseg[nx];
+          pf_sd = segs[pf_s];
+        }
+        const uint4* gp = reinterpret_cast<const uint4*>(a.bytes + pf_sd.base + (uint64_t)(nx - pf_sd.tile0) * kTile);
         KLF_ROWS(KLF_LOAD)
         if (lane < kHalo / 16) pfh = gp[kTile / 16 + lane];
       }
@@ -358,12 +366,15 @@ __global__ __launch_bounds__(kThreads, MODE == kScanGen ? 3 : KLF_SCAN_OCC) void
     uint32_t nlc = 0, anc = 0;
     {
       const uint32_t rot = ((uint32_t)lane >> 1) & 7u;
+      // all eight reads in flight before the first test (one LDS round trip, not eight)
+      uint4 xs[8];
+#pragma unroll
+      for (int v = 0; v < 8; ++v) xs[v] = *reinterpret_cast<const uint4*>(s_tile + my0 + 16u * (((uint32_t)v + rot) & 7u));
 #pragma unroll
       for (int v = 0; v < 8; ++v) {
         const uint32_t c = ((uint32_t)v + rot) & 7u;
-        const uint4 x = *reinterpret_cast<const uint4*>(s_tile + my0 + 16u * c);
-        nlc |= any_eq16(x, 0x0A0A0A0Au) ? (1u << c) : 0u;
-        if (LIT && !(KLF_ABL & 2)) anc |= any_eq16(x, pat) ? (1u << c) : 0u;
+        nlc |= any_eq16(xs[v], 0x0A0A0A0Au) ? (1u << c) : 0u;
+        if (LIT && !(KLF_ABL & 2)) anc |= any_eq16(xs[v], pat) ? (1u << c) : 0u;
       }
       if (nvalid < kLaneBytes) {
         const uint32_t vm = (1u << ((nvalid + 15) >> 4)) - 1u;
@@ -371,6 +382,18 @@ __global__ __launch_bounds__(kThreads, MODE == kScanGen ? 3 : KLF_SCAN_OCC) void
         anc &= vm;
       }
     }
+#if KLF_ABL & 64  // timing build: staging + any-test only
+    {
+      const uint32_t ev = wave_sum((uint32_t)__popc(nlc | anc));
+      if (lane == 0) {
+        TileStat ts{};
+        ts.events = ev;
+        a.tstat[tile] = ts;
+      }
+      asm volatile("" ::: "memory");
+      continue;
+    }
+#endif
     auto clip = [&](uint32_t e, uint32_t c) -> uint32_t {  // bytes of chunk c past the tile's end
       const int nv = nvalid - 16 * (int)c;
       return nv >= 16 ? e : (nv <= 0 ? 0u : (e & ((1u << nv) - 1u)));
@@ -420,7 +443,7 @@ __global__ __launch_bounds__(kThreads, MODE == kScanGen ? 3 : KLF_SCAN_OCC) void
       pool_base = (uint32_t)__builtin_amdgcn_readlane((int)pb, 0);
     }
     const bool pool_ok = !dense || (uint64_t)pool_base + nlines <= a.pool_cap;
-    uint32_t* gslot = dense ? a.pool + pool_base : a.slots + (size_t)tile * kSlots;
+    uint32_t* gslot = dense ? a.pool + pool_base : a.slots + (size_t)tile * kSlotStride;
 
     // The per-tile work on the line list, instantiated for the LDS list (normal tiles) and
     // the global pool (dense tiles).
@@ -536,9 +559,14 @@ __global__ __launch_bounds__(kThreads, MODE == kScanGen ? 3 : KLF_SCAN_OCC) void
       if (dense) __threadfence_block();
       wave_lds_sync();
     };
-    if (!dense) {
+    if (KLF_ABL & 128) {  // timing build: no line list / parse / literal
+    } else if (!dense) {
       work(s_list);
-      for (uint32_t j = lane; j < nlines; j += 64) gslot[j] = s_list[j];
+      if (KLF_ABL & 4096) {  // timing build: half the slot bytes (u16 slots)
+        for (uint32_t j = lane; j < nlines; j += 64) reinterpret_cast<uint16_t*>(gslot)[j] = (uint16_t)s_list[j];
+      } else if (!(KLF_ABL & 512)) {
+        for (uint32_t j = lane; j < nlines; j += 64) gslot[j] = s_list[j];
+      }
     } else if (pool_ok) {
       work(gslot);
     }
@@ -676,7 +704,7 @@ __global__ __launch_bounds__(256) void k_fixup(RunArgs a) {
     const bool first = rel_lo == 0, last = rel_lo + kTile >= seg_len;
     const uint32_t k0 = first ? 0 : 1, k1 = last ? ts.events : ts.events + 1;
     const uint32_t nlines = k1 > k0 ? k1 - k0 : 0;
-    uint32_t* list = (ts.flags & 1u) ? a.pool + ts.pool_base : a.slots + (size_t)tile * kSlots;
+    uint32_t* list = (ts.flags & 1u) ? a.pool + ts.pool_base : a.slots + (size_t)tile * kSlotStride;
     const uint8_t* segp = a.bytes + sd.base;
     uint32_t dp = 0, dq = 0;
     for (uint32_t j = lane; j < nlines; j += 64) {
@@ -711,7 +739,7 @@ __global__ __launch_bounds__(256) void k_fixup(RunArgs a) {
     if (lane == 0) {
       ts.parsed = (uint16_t)(ts.parsed + dp);
       ts.since_ok = (uint16_t)(ts.since_ok + dq);
-      a.tstat[tile] = ts;
+      if (!(KLF_ABL & 256)) a.tstat[tile] = ts;
     }
   }
 }
@@ -721,17 +749,18 @@ __global__ __launch_bounds__(256) void k_fixup(RunArgs a) {
 // prefix differences at its first and last tile (no same-address atomics), and zeroes the
 // match-bitmap words whose first line falls in the block's line range (the bitmap is
 // only ever OR-ed into by the kernels after this one).
-constexpr int kTilesPerScanBlock = 4096;  // 256 threads x 16 tiles
+// Tiles per block: 256 threads x R.  R = 4 up to kScanSmallTiles tiles (enough blocks to
+// fill the chip; each block sums the preceding blocks' totals itself), R = 16 above.
 
 // TileStat.carry_off is the tile's hit-slot count with the q-gram prefilter (GEN scan)
 __device__ __forceinline__ uint32_t tile_hits(const RunArgs& a, const TileStat& ts) {
   return (a.grep_mode == kGrepGeneral && a.pats.qf_on) ? ts.carry_off : 0u;
 }
 
+template <int R>
 __global__ __launch_bounds__(256) void k_tsum(RunArgs a) {
   __shared__ uint64_t s_w[4][4];
-  constexpr int R = kTilesPerScanBlock / 256;
-  const uint32_t t0 = blockIdx.x * kTilesPerScanBlock + threadIdx.x;
+  const uint32_t t0 = blockIdx.x * (256 * R) + threadIdx.x;
   TileStat ts[R];
 #pragma unroll
   for (int r = 0; r < R; ++r) {  // all loads in flight at once (coalesced 16-B records)
@@ -760,12 +789,12 @@ __global__ __launch_bounds__(256) void k_tsum(RunArgs a) {
 // the stream id of the neighbouring tile differs (no dependent descriptor loads).  With
 // the q-gram prefilter the same scan flattens the tiles' hit slots into one list for
 // k_verify (hit slot ids tile * kHitSlots + j).
+template <int R>
 __global__ __launch_bounds__(256) void k_tbase(RunArgs a) {
-  constexpr int R = kTilesPerScanBlock / 256;
   __shared__ uint64_t s_w[2][4][4];
   __shared__ uint64_t s_base[4];
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
-  const uint32_t t0 = blockIdx.x * kTilesPerScanBlock + t;
+  const uint32_t t0 = blockIdx.x * (256 * R) + t;
   TileStat ts[R];
   uint32_t sg[R], sp[R], sn[R];
 #pragma unroll
@@ -834,10 +863,13 @@ __global__ __launch_bounds__(256) void k_tbase(RunArgs a) {
 }
 
 // ---- K1d: scatter staged slots into the global line arrays --------------------------
-// One wave per group of kScatterGroup consecutive tiles (~10 lines per 4 KiB tile would
-// leave most lanes of a wave-per-tile idle): lanes 0..G-1 read the group's records into
-// the wave's LDS table, then all lanes walk the group's lines.
-constexpr int kScatterGroup = 16;
+// One wave per group of 64 consecutive tiles (one lane per tile reads the tile's record
+// into the wave's LDS table; ~20 lines per 8 KiB tile would leave most lanes of a
+// wave-per-tile idle), then the lanes walk the group's lines, each line finding its tile by
+// binary search over the LDS prefix.  The walk loads kScatterBatch lines' slots before
+// storing any of them: the kernel is latency-bound on those dependent loads otherwise.
+constexpr int kScatterGroup = 64;
+constexpr int kScatterBatch = 8;
 struct ScatterEnt {
   uint64_t base;     // global line index of the tile's slot 0 (= tile line k0)
   uint64_t rel_lo;   // tile start, stream-relative
@@ -848,13 +880,14 @@ struct ScatterEnt {
 
 __global__ __launch_bounds__(256) void k_scatter(RunArgs a) {
   __shared__ ScatterEnt s_ent[4][kScatterGroup];
+  __shared__ uint32_t s_pre[4][kScatterGroup];  // inclusive line-count prefix of the group's tiles
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   uint32_t* err_flag = a.counters + 2;
   const uint32_t ngroups = (a.ntiles + kScatterGroup - 1) / kScatterGroup;
   for (uint32_t g = blockIdx.x * 4 + wv; g < ngroups; g += gridDim.x * 4) {
     const uint32_t tile = g * kScatterGroup + lane;
     uint32_t n = 0;
-    if (lane < kScatterGroup && tile < a.ntiles) {
+    if (tile < a.ntiles) {
       const TileStat ts = a.tstat[tile];
       const uint32_t s = a.tile_seg[tile];
       const SegDesc sd = a.segs[s];
@@ -881,7 +914,7 @@ __global__ __launch_bounds__(256) void k_scatter(RunArgs a) {
           const uint32_t pk0 = prel == 0 ? 0 : 1;
           const uint32_t pn = pst.events + 1 > pk0 ? pst.events + 1 - pk0 : 0;  // never the stream's last tile
           if (pn == 0) continue;
-          const uint32_t* psrc = (pst.flags & 1u) ? a.pool + pst.pool_base : a.slots + (size_t)pt * kSlots;
+          const uint32_t* psrc = (pst.flags & 1u) ? a.pool + pst.pool_base : a.slots + (size_t)pt * kSlotStride;
           const uint32_t v = psrc[pn - 1];
           const uint32_t mt = v >> 16;
           // a deferred line had its whole content searched by k_fixup
@@ -897,34 +930,46 @@ __global__ __launch_bounds__(256) void k_scatter(RunArgs a) {
         else atomicOr(err_flag, 1u);
       }
     }
-    // inclusive prefix of the group's line counts, then each line finds its tile
-    uint32_t incl = n;
-#pragma unroll
-    for (int d = 1; d < kScatterGroup; d <<= 1) {
-      const uint32_t o = __shfl_up(incl, d, 64);
-      if (lane >= d) incl += o;
-    }
-    uint32_t pre[kScatterGroup];
-#pragma unroll
-    for (int k = 0; k < kScatterGroup; ++k) pre[k] = (uint32_t)__builtin_amdgcn_readlane((int)incl, k);
-    const uint32_t total = pre[kScatterGroup - 1];
+    const uint32_t incl = wave_incl_scan_add(n, lane);
+    s_pre[wv][lane] = incl;
+    const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
     wave_lds_sync();
-    for (uint32_t l = lane; l < total; l += 64) {
-      uint32_t k = 0;
+    for (uint32_t l0 = 0; l0 < total; l0 += 64 * kScatterBatch) {
+      uint32_t sl[kScatterBatch], kk[kScatterBatch], jj[kScatterBatch];
 #pragma unroll
-      for (int kk = 0; kk < kScatterGroup - 1; ++kk) k += l >= pre[kk] ? 1u : 0u;
-      const uint32_t j = l - (k ? pre[k - 1] : 0u);
-      const ScatterEnt e = s_ent[wv][k];
-      const uint32_t* src = (e.src & 0x80000000u) ? a.pool + (e.src & 0x7FFFFFFFu)
-                                                  : a.slots + (size_t)(g * kScatterGroup + k) * kSlots;
-      const uint32_t sl = src[j];
-      const uint64_t li = e.base + j;
-      if (li >= a.cap_lines) { atomicOr(err_flag, 1u); continue; }
-      a.line_off[li + e.seg] = e.rel_lo + (sl & kSlotOff);
-      a.meta[li] = (uint16_t)(sl >> 16);
-      if (sl & kSlotHit) atomicOr(&a.bits[li >> 5], 1u << (li & 31));
+      for (int u = 0; u < kScatterBatch; ++u) {
+        const uint32_t l = l0 + (uint32_t)(u * 64 + lane);
+        sl[u] = 0;
+        kk[u] = 0;
+        jj[u] = 0;
+        if (l < total) {
+          uint32_t lo = 0, hi = kScatterGroup - 1;  // first tile whose inclusive prefix exceeds l
+          while (lo < hi) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (s_pre[wv][mid] > l) hi = mid; else lo = mid + 1;
+          }
+          const uint32_t j = l - (lo ? s_pre[wv][lo - 1] : 0u);
+          const uint32_t src = s_ent[wv][lo].src;
+          const uint32_t* sp = (src & 0x80000000u) ? a.pool + (src & 0x7FFFFFFFu)
+                                                   : a.slots + (size_t)(g * kScatterGroup + lo) * kSlotStride;
+          sl[u] = sp[j];
+          kk[u] = lo;
+          jj[u] = j;
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < kScatterBatch; ++u) {
+        const uint32_t l = l0 + (uint32_t)(u * 64 + lane);
+        if (l >= total) continue;
+        const ScatterEnt& e = s_ent[wv][kk[u]];
+        const uint64_t li = e.base + jj[u];
+        if (li >= a.cap_lines) { atomicOr(err_flag, 1u); continue; }
+        a.line_off[li + e.seg] = e.rel_lo + (sl[u] & kSlotOff);
+        a.meta[li] = (uint16_t)(sl[u] >> 16);
+        if (sl[u] & kSlotHit) atomicOr(&a.bits[li >> 5], 1u << (li & 31));
+      }
     }
-    asm volatile("" ::: "memory");  // the next group rewrites the wave's LDS table
+    asm volatile("" ::: "memory");  // the next group rewrites the wave's LDS tables
   }
 }
 
@@ -1021,7 +1066,7 @@ __device__ void verify_hit(const RunArgs& a, uint32_t tile, uint32_t s, int32_t 
     const bool first = rel_lo == 0, last = rel_lo + kTile >= (int64_t)sd.len;
     const uint32_t k0 = first ? 0 : 1, k1 = last ? ts.events : ts.events + 1;
     const uint32_t nl = k1 > k0 ? k1 - k0 : 0;
-    const uint32_t* list = (ts.flags & 1u) ? a.pool + ts.pool_base : a.slots + (size_t)tile * kSlots;
+    const uint32_t* list = (ts.flags & 1u) ? a.pool + ts.pool_base : a.slots + (size_t)tile * kSlotStride;
     int lo = 0, hi = x < 0 ? 0 : (int)nl;  // starts <= x
     while (lo < hi) {
       const int mid = (lo + hi) >> 1;
@@ -1665,7 +1710,7 @@ __global__ __launch_bounds__(kThreads) void k_cgather(RunArgs a) {
     const uint64_t ob1 = ob0 + s_wb[0] + s_wb[1] + s_wb[2] + s_wb[3];
     const uint64_t c0 = ob0 + (uint64_t)sub * kCopyChunk;
     const uint64_t c1 = c0 + kCopyChunk < ob1 ? c0 + kCopyChunk : ob1;
-    block_gather_copy(s_src, s_dst, s_len, c0, c1, a.bytes, a.out);
+    if (!(KLF_ABL & 1024)) block_gather_copy(s_src, s_dst, s_len, c0, c1, a.bytes, a.out);
   }
 }
 
@@ -1769,10 +1814,17 @@ hipError_t launch_pipeline(const RunArgs& a, hipStream_t st, hipEvent_t* ev, int
     KLF_TRY(hipEventRecord(ev[6], st));  // k_scan alone (the roofline kernel)
     hipLaunchKernelGGL(k_fixup, dim3(num_cus * 2), dim3(256), 0, st, a);
     KLF_TRY(hipGetLastError());
-    const uint32_t nb = (a.ntiles + kTilesPerScanBlock - 1) / kTilesPerScanBlock;
-    hipLaunchKernelGGL(k_tsum, dim3(nb), dim3(256), 0, st, a);
-    KLF_TRY(hipGetLastError());
-    hipLaunchKernelGGL(k_tbase, dim3(nb), dim3(256), 0, st, a);
+    if (a.ntiles <= kScanSmallTiles) {
+      const uint32_t nb = (a.ntiles + 1023) / 1024;
+      hipLaunchKernelGGL(k_tsum<4>, dim3(nb), dim3(256), 0, st, a);
+      KLF_TRY(hipGetLastError());
+      hipLaunchKernelGGL(k_tbase<4>, dim3(nb), dim3(256), 0, st, a);
+    } else {
+      const uint32_t nb = (a.ntiles + 4095) / 4096;
+      hipLaunchKernelGGL(k_tsum<16>, dim3(nb), dim3(256), 0, st, a);
+      KLF_TRY(hipGetLastError());
+      hipLaunchKernelGGL(k_tbase<16>, dim3(nb), dim3(256), 0, st, a);
+    }
     KLF_TRY(hipGetLastError());
     uint32_t sg = ((a.ntiles + kScatterGroup - 1) / kScatterGroup + 3) / 4;
     if (sg > (uint32_t)num_cus * 8) sg = num_cus * 8;

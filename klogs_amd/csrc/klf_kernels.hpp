@@ -22,6 +22,8 @@ constexpr uint32_t kCtrPool = 4;                    // counters[4]: dense-tile p
 constexpr uint32_t kMatchChunk = 8192;              // lines per k_mcount partial (256 words)
 
 constexpr int kSlots = kTile / 32 + 2;  // staged line slots per tile (>= 8 KiB / 32-byte kubelet line + 1)
+constexpr uint32_t kScanSmallTiles = 1u << 20;  // tile-scan blocks of 1,024 tiles up to this many tiles (8 GiB), 4,096 above
+constexpr int kSlotStride = (kSlots + 3) & ~3;  // u32 slots per tile region in HBM (16-B aligned regions)
 
 // q-gram prefilter of general pattern sets (klf_patterns.hpp CompiledSet::qf_*)
 constexpr int kQfBucketBits = 12;                    // bitmap words = verification buckets
@@ -36,7 +38,7 @@ constexpr uint32_t kCtrHits = 8;                     // counters[8]: spilled pre
 constexpr uint32_t kCtrHitsOver = 9;                 // counters[9]: hit list overflow -> k_match
 constexpr uint32_t kCtrFlatHits = 12;                // counters[12]: hit slots flattened by k_tbase
 constexpr uint32_t kCtrCopyChunks = 11;              // counters[11]: output copy chunks (k_cgather)
-constexpr uint64_t kCopyChunk = 16 * 1024;           // output bytes per k_cgather work item
+constexpr uint64_t kCopyChunk = 4 * 1024;            // output bytes per k_cgather work item
 constexpr uint32_t kCtrVerified = 10;                // counters[10]: hits k_verify walked (diagnostics)
 constexpr uint32_t kQfRegex = 1u << 24;              // entry flags: regex factor (else literal)
 constexpr uint32_t kQfLoose = 1u << 25;              //   compare OR 0x20 per byte
@@ -149,11 +151,11 @@ struct RunArgs {
   DevPatterns pats;
   // workspace (device)
   TileStat* tstat;      // [ntiles]
-  uint32_t* slots;      // [ntiles * kSlots] staged line slots
+  uint32_t* slots;      // [ntiles * kSlotStride] staged line slots
   uint32_t* pool;       // [pool_cap] slots of dense tiles
   uint64_t pool_cap;
   uint64_t* tile_base;  // [ntiles] global line index of each tile's line 0
-  uint64_t* bsum;       // [4 * (ntiles / 4096 + 1)] scan block sums (events, parsed, since_ok, hits)
+  uint64_t* bsum;       // [4 * (ntiles / 1024 + 1)] scan block sums (events, parsed, since_ok, hits)
   uint64_t* mpart;      // [cap_lines / kMatchChunk + 1] matched-line partial per line chunk
   uint64_t* csum;       // [3 * (max compaction blocks + 1)] per-block (bytes, lines), then their
                         // prefixes and the prefix of copy chunks
