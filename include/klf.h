@@ -127,6 +127,15 @@ int klf_run_device(klf_engine* e, const uint8_t* d_bytes, uint32_t n_streams,
                    const uint64_t* seg_base, const uint64_t* lens, const klf_filter* f,
                    klf_result** out);
 
+/* Re-applies the tail rule with a different N to the latest run (prev must be the
+ * engine's latest result): re-runs only matched counts, the tail window and the
+ * compaction on the line index, parse/since bits and match bitmap the run left in HBM.
+ * The byte-range shards of one stream need it: a rank's share of the
+ * global --tail is known only after the count exchange.  prev becomes stale
+ * (KLF_ESTATE on access) because the output buffer is rewritten.  Replaces nothing in
+ * the reference (kubelet applies --tail once, server-side: logs.go / tail.go). */
+int klf_retail(klf_engine* e, klf_result* prev, int64_t tail, klf_result** out);
+
 /* ---- results -------------------------------------------------------------------- */
 /* Selected bytes of one stream (host view, D2H on first access). */
 int klf_result_stream(klf_result* r, uint32_t stream_id, const uint8_t** bytes,

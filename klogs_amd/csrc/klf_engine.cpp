@@ -70,6 +70,8 @@ struct klf_engine {
       d_meta, d_bits, d_segout, d_wpre, d_out, d_mpart;
   uint64_t pool_cap = 1 << 20;
   hipEvent_t ev[7] = {};
+  klf::RunArgs last_args{};  // arguments of the latest completed run (klf_retail)
+  uint64_t last_gen = 0;     // gen of that run's result
 };
 
 struct klf_result {
@@ -345,7 +347,7 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
   }
   if (ntiles >= (1ull << 32)) { delete r; return set_err(e, KLF_EINVAL, "batch too large"); }
   const uint32_t nsegs = (uint32_t)segs.size();
-  if (nsegs == 0) { *out = r; return KLF_OK; }
+  if (nsegs == 0) { e->last_gen = r->gen; *out = r; return KLF_OK; }
 
   hipStream_t st = e->stream;
   bool same_layout = segs.size() == e->last_segs.size() && e->d_tile_seg.cap >= ntiles * 4 &&
@@ -481,6 +483,8 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
       e->pool_cap = std::max<uint64_t>(e->pool_cap, (uint64_t)counters[klf::kCtrPool] + 1024);
       continue;
     }
+    e->last_args = a;
+    e->last_gen = r->gen;
     break;
   }
   if (const char* path = getenv("KLF_TIMELINE_OUT")) {  // diagnostic builds only
@@ -509,6 +513,40 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
 extern "C" int klf_run_device(klf_engine* e, const uint8_t* d_bytes, uint32_t n, const uint64_t* seg_base,
                               const uint64_t* lens, const klf_filter* f, klf_result** out) {
   return run_device_impl(e, d_bytes, n, seg_base, lens, f, out);
+}
+
+extern "C" int klf_retail(klf_engine* e, klf_result* prev, int64_t tail, klf_result** out) {
+  if (!e || !prev || !out || prev->e != e || tail < -1) return KLF_EINVAL;
+  *out = nullptr;
+  if (prev->gen != e->gen || e->last_gen != prev->gen) return set_err(e, KLF_ESTATE, "klf_retail: not the latest run");
+  HIPCHK(e, hipSetDevice(e->device), "hipSetDevice");
+  auto* r = new (std::nothrow) klf_result();
+  if (!r) return KLF_ENOMEM;
+  r->e = e;
+  r->n_streams = prev->n_streams;
+  r->seg_of = prev->seg_of;
+  r->seg_base = prev->seg_base;
+  r->has_bits = prev->has_bits;
+  r->total_lines = prev->total_lines;
+  const uint32_t nsegs = (uint32_t)prev->so.size();
+  r->so.resize(nsegs);
+  if (nsegs) {
+    klf::RunArgs a = e->last_args;
+    a.tail = tail;
+    a.stage_times = 0;
+    hipStream_t st = e->stream;
+    hipError_t h = klf::launch_retail(a, st, e->ev, e->num_cus);
+    if (h == hipSuccess) h = hipMemcpyAsync(r->so.data(), e->d_segout.p, nsegs * sizeof(SegOut), hipMemcpyDeviceToHost, st);
+    if (h == hipSuccess) h = hipStreamSynchronize(st);
+    if (h != hipSuccess) { delete r; return hip_err(e, h, "klf_retail"); }
+    float ms;
+    if (hipEventElapsedTime(&ms, e->ev[0], e->ev[5]) == hipSuccess) r->ms[4] = ms;
+  }
+  for (auto& s : r->so) r->total_out = std::max(r->total_out, s.out_hi);
+  r->gen = ++e->gen;  // prev's output buffer is rewritten: prev is stale from here on
+  e->last_gen = r->gen;
+  *out = r;
+  return KLF_OK;
 }
 
 extern "C" int klf_run(klf_engine* e, const klf_filter* f, klf_result** out) {

@@ -1475,6 +1475,18 @@ __global__ __launch_bounds__(256) void k_wprefix(RunArgs a) {
   }
 }
 
+// Re-tail (klf_retail): clears what k_mcount .. k_cgather accumulate into the segment
+// records, leaving the line index, the parse/since counts and the match bitmap of the run.
+__global__ __launch_bounds__(256) void k_retail_init(RunArgs a) {
+  for (uint32_t s = blockIdx.x * 256 + threadIdx.x; s < a.nsegs; s += gridDim.x * 256) {
+    SegOut& so = a.segout[s];
+    so.matched = 0;
+    so.win_lo = so.win_hi = 0;
+    so.sel_lo = so.sel_hi = 0;
+    so.out_lo = so.out_hi = 0;
+  }
+}
+
 // Zeroes the run's counters and per-stream records (one launch instead of memsets).
 __global__ __launch_bounds__(256) void k_init(RunArgs a) {
   const uint32_t i = blockIdx.x * 256 + threadIdx.x;
@@ -1782,6 +1794,8 @@ hipError_t launch_scan(const RunArgs& a, hipStream_t st, int num_cus) {
   return hipGetLastError();
 }
 
+static hipError_t launch_tail_stage(const RunArgs& a, hipStream_t st, hipEvent_t* ev, int num_cus);
+
 hipError_t launch_pipeline(const RunArgs& a, hipStream_t st, hipEvent_t* ev, int num_cus) {
   hipError_t e;
 #define KLF_TRY(x) do { e = (x); if (e != hipSuccess) return e; } while (0)
@@ -1849,6 +1863,17 @@ hipError_t launch_pipeline(const RunArgs& a, hipStream_t st, hipEvent_t* ev, int
     KLF_TRY(hipGetLastError());
   }
   if (a.stage_times) KLF_TRY(hipEventRecord(ev[3], st));  // ~5 us of idle GPU each
+  KLF_TRY(launch_tail_stage(a, st, ev, num_cus));
+  KLF_TRY(hipEventRecord(ev[5], st));
+#undef KLF_TRY
+  return hipSuccess;
+}
+
+// Matched counts, kubelet tail window, window prefix, compaction + copy (the stages after
+// the matchers): shared by launch_pipeline and launch_retail.
+static hipError_t launch_tail_stage(const RunArgs& a, hipStream_t st, hipEvent_t* ev, int num_cus) {
+  hipError_t e;
+#define KLF_TRY(x) do { e = (x); if (e != hipSuccess) return e; } while (0)
   if (a.grep_mode != kGrepNone) {
     const uint64_t nchunks = a.cap_lines / kMatchChunk + 1;
     const uint32_t g = (uint32_t)(nchunks < (uint64_t)num_cus * 4 ? nchunks : (uint64_t)num_cus * 4);
@@ -1866,9 +1891,18 @@ hipError_t launch_pipeline(const RunArgs& a, hipStream_t st, hipEvent_t* ev, int
   KLF_TRY(hipGetLastError());
   hipLaunchKernelGGL(k_cgather, dim3(num_cus * 8), dim3(kThreads), 0, st, a);
   KLF_TRY(hipGetLastError());
-  KLF_TRY(hipEventRecord(ev[5], st));
 #undef KLF_TRY
   return hipSuccess;
+}
+
+hipError_t launch_retail(const RunArgs& a, hipStream_t st, hipEvent_t* ev, int num_cus) {
+  hipError_t e = hipEventRecord(ev[0], st);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_retail_init, dim3((a.nsegs + 255) / 256 < 1024 ? (a.nsegs + 255) / 256 : 1024), dim3(256), 0,
+                     st, a);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  if ((e = launch_tail_stage(a, st, ev, num_cus)) != hipSuccess) return e;
+  return hipEventRecord(ev[5], st);
 }
 
 }  // namespace klf

@@ -184,6 +184,8 @@ struct RunArgs {
 // scan, ev[3] after the general matcher, ev[4] after counts+tail+window prefix, ev[5]
 // after compaction.  Returns a hipError_t.
 hipError_t launch_pipeline(const RunArgs& a, hipStream_t stream, hipEvent_t* ev, int num_cus);
+// Re-runs matched counts, tail and compaction of the last pipeline with a.tail changed.
+hipError_t launch_retail(const RunArgs& a, hipStream_t stream, hipEvent_t* ev, int num_cus);
 // Gram sketch (kQfHistBins u32 bins, zeroed here) of the first `sample` bytes of each
 // of up to 16 segments, every position, grams folded / masked like the prefilter's.
 hipError_t launch_gramhist(const uint8_t* bytes, const SegDesc* segs, uint32_t nsegs, uint64_t sample, uint32_t fold,

@@ -75,6 +75,7 @@ SIGNATURES = {
     "klf_layout": (C.c_int, [C.c_uint32, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
     "klf_run_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.POINTER(C.c_uint64),
                                  C.POINTER(C.c_uint64), C.POINTER(_Filter), C.POINTER(C.c_void_p)]),
+    "klf_retail": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int64, C.POINTER(C.c_void_p)]),
     "klf_result_stream": (C.c_int, [C.c_void_p, C.c_uint32, C.POINTER(C.c_void_p), C.POINTER(C.c_uint64),
                                     C.POINTER(_Counts)]),
     "klf_result_lines": (C.c_int, [C.c_void_p, C.c_uint32, C.POINTER(C.c_void_p), C.POINTER(C.c_uint64)]),
@@ -249,6 +250,13 @@ class Result:
         c = _Counts()
         _check(_lib.klf_result_totals(self._p, C.byref(c)))
         return c.as_dict()
+
+    def retail(self, tail: int) -> "Result":
+        """The same run with --tail N re-applied (klf_retail): counts, tail window and
+        compaction only.  This result is stale afterwards (its output buffer is reused)."""
+        r = C.c_void_p()
+        _check(_lib.klf_retail(self._eng._h, self._p, int(tail), C.byref(r)), self._eng._h)
+        return Result(r.value or 0, self.n_streams, self._eng)
 
     def free(self):
         if self._p:

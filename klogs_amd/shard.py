@@ -119,3 +119,146 @@ def engine_runner(engine, since=None, tail: int = -1):
         finally:
             r.free()
     return run
+
+
+# ---------------------------------------------------------------------------------------
+# One huge stream split by byte range (SURVEY.md §8e, C2 at more than one GPU).
+#
+# Rank r owns the lines whose first byte lies in its byte range; the ranges are cut just
+# after a newline, so every shard but the last ends with '\n' and only the last can hold
+# the unterminated final fragment (kubelet tail.go: the fragment is emitted, not counted).
+# since and grep are per line; --tail is the only cross-shard rule.  Every rank filters its
+# shard with the global N (a superset of its share: the global window is a suffix of the
+# stream, so a shard's part of it is a suffix of the shard's own last-N window), then ONE
+# exchange of each shard's count of newline-terminated G lines (G = matching lines, every
+# line without patterns: the set kubelet's tail counts, SPEC.md S3/S4) gives every rank its
+# share n_r = clamp(N - sum of later shards' counts, 0, own count).  At most two shards
+# re-apply the tail rule (the one the window's first line falls in, and the end shard when
+# the fragment must be cut although its own count is below N); they re-run only the tail
+# and compaction stages on the line index already in HBM (klf_retail).
+# Output bytes never cross GPUs: the stream's file is the shards' outputs in rank order.
+# ---------------------------------------------------------------------------------------
+
+def split_bounds(n: int, world: int, find_nl: Callable[[int], int]) -> List[int]:
+    """Shard boundaries [b_0 = 0, ..., b_world = n] of an n-byte stream: b_r is just past
+    the first '\\n' at or after byte r*n//world - 1 (n when there is none), so a line
+    belongs to the shard its first byte is in.  find_nl(pos) -> index of the first '\\n'
+    at index >= pos, or -1."""
+    if world < 1:
+        raise ValueError("world must be >= 1")
+    b = [0]
+    for r in range(1, world):
+        c = r * n // world
+        p = find_nl(max(c - 1, 0)) if c > 0 else -1
+        cut = n if p < 0 else p + 1
+        b.append(max(cut, b[-1]))
+    b.append(n)
+    return b
+
+
+def end_shard(bounds: Sequence[int]) -> int:
+    """The shard holding the stream's last byte (the last non-empty one; the shards after
+    it are empty).  Every other non-empty shard ends with '\n'."""
+    w = len(bounds) - 1
+    ne = [r for r in range(w) if bounds[r] < bounds[r + 1]]
+    return ne[-1] if ne else w - 1
+
+
+def tail_shares(g_term: Sequence[int], tail: int, last: int = -1) -> List[int]:
+    """Each shard's share of the global --tail N (-1 = all lines: every shard -1).  An
+    earlier shard gets N minus the newline-terminated G lines of the shards after it,
+    clamped to [0, its own count].  The end shard `last` (default: the final one) holds
+    the fragment, which kubelet emits only when the whole stream has fewer than N
+    terminated G lines (the window then holds every line; otherwise ReadLogs stops after
+    N lines, before the fragment): it keeps N in that case, else min(N, own count), which
+    its own tail rule turns into "every terminated line of mine, fragment cut"."""
+    w = len(g_term)
+    last = w - 1 if last < 0 else last
+    if tail < 0:
+        return [-1] * w
+    total = sum(int(x) for x in g_term)
+    out = [0] * w
+    later = 0
+    for r in reversed(range(w)):
+        if r == last:
+            out[r] = tail if total < tail else min(tail, int(g_term[r]))
+        else:
+            out[r] = max(0, min(int(g_term[r]), tail - later))
+        later += int(g_term[r])
+    return out
+
+
+COUNT_FIELDS = ("lines", "parsed", "since_ok", "matched", "selected", "out_bytes")
+
+
+def _allgather_ints(vec: Sequence[int], world: int, device=None) -> np.ndarray:
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([int(x) for x in vec], dtype=torch.int64)
+    if device is not None:
+        t = t.to(device)
+    if world == 1:
+        return t.cpu().numpy().reshape(1, -1)
+    out = torch.empty(world * t.numel(), dtype=torch.int64, device=t.device)
+    dist.all_gather_into_tensor(out, t)
+    return out.cpu().numpy().reshape(world, -1)
+
+
+def run_split(n: int, find_nl: Callable[[int], int], runner, world: int, rank: int, tail: int,
+              allgather=None, device=None):
+    """Filters this rank's byte range of one stream; returns (this shard's output bytes,
+    whole-stream counts).  runner(lo, hi, tail) -> a shard handle with .out (bytes),
+    .counts (dict of COUNT_FIELDS), .g_term (newline-terminated G lines) and
+    .retail(n) -> handle (the same shard with the tail rule re-applied).
+    allgather(list of ints) -> [world, k] array (default: torch.distributed, RCCL on the
+    GPU box, gloo in the CPU tests)."""
+    ag = allgather or (lambda v: _allgather_ints(v, world, device))
+    b = split_bounds(n, world, find_nl)
+    h = runner(b[rank], b[rank + 1], tail)
+    g_term = ag([h.g_term])[:, 0]                       # the one exchange step
+    last = end_shard(b)
+    share = tail_shares(g_term, tail, last)[rank]
+    ran_as = tail if rank == last else min(tail, int(g_term[rank]))  # what the first run selected
+    if tail >= 0 and share != ran_as:
+        h = h.retail(share)
+    counts = ag([int(h.counts[f]) for f in COUNT_FIELDS])  # whole-stream counts (reporting)
+    return h.out, {f: int(counts[:, k].sum()) for k, f in enumerate(COUNT_FIELDS)}
+
+
+class EngineShard:
+    """runner handle over klogs_amd.engine.Engine (host-staged shard bytes)."""
+
+    def __init__(self, engine, data: bytes, since, tail: int, has_patterns: bool, result=None):
+        self._eng, self._data, self._since, self._pat = engine, data, since, has_patterns
+        if result is None:
+            engine.reset()
+            engine.set_streams(1)
+            if data:
+                engine.stage(0, data)
+            result = engine.run(since=since, tail=tail, n_streams=1)
+        self._r = result
+        so = result.stream(0)
+        self.out, self.counts = so.out, so.counts
+        frag = bool(data) and not data.endswith(b"\n")
+        frag_in_g = frag and (not has_patterns or self._last_bit())
+        self.g_term = int(self.counts["matched"]) - (1 if frag_in_g else 0)
+
+    def _last_bit(self) -> bool:
+        lines = int(self.counts["lines"])
+        bits = self._r.match_bits(0)
+        return lines > 0 and bool((bits[(lines - 1) >> 3] >> ((lines - 1) & 7)) & 1)
+
+    def retail(self, tail: int) -> "EngineShard":
+        r = self._r.retail(tail)
+        self._r.free()
+        return EngineShard(self._eng, self._data, self._since, tail, self._pat, result=r)
+
+    def free(self):
+        self._r.free()
+
+
+def engine_split_runner(engine, data: bytes, since=None, has_patterns: bool = False):
+    """runner for run_split: the engine on the shard data[lo:hi] (one GPU per process)."""
+    def run(lo: int, hi: int, tail: int):
+        return EngineShard(engine, data[lo:hi], since, tail, has_patterns)
+    return run

@@ -108,3 +108,116 @@ def test_gloo_world2_gather_matches_serial():
     for i, (out, c) in enumerate(serial):
         assert outs[i] == out
         assert tables[0][i].tolist() == [c[k] for k in shard.RECORD_FIELDS[1:]]
+
+
+# ---- one stream split by byte range (shard.run_split) ---------------------------------
+
+class _OracleShard:
+    """run_split handle over the C oracle (the CPU stand-in for one rank's engine)."""
+
+    def __init__(self, data, since, tail, grep):
+        self.data, self.since, self.grep = data, since, grep
+        self.out, _, bits, self.counts = co.filter_stream(data, since, tail, grep, want_lines=False, want_bits=True)
+        frag = bool(data) and not data.endswith(b"\n")
+        L = self.counts["lines"]
+        in_g = (not grep) or (L > 0 and (bits[(L - 1) >> 3] >> ((L - 1) & 7)) & 1)
+        self.g_term = self.counts["matched"] - (1 if frag and in_g else 0)
+
+    def retail(self, tail):
+        return _OracleShard(self.data, self.since, tail, self.grep)
+
+
+def _split_case(data, world, tail, grep):
+    """run_split over `world` simulated ranks (all-gather by direct exchange) -> output."""
+    find_nl = lambda p: data.find(b"\n", p)
+    handles = {}
+    stage = {}
+
+    # run every rank's first phase, then the exchange, then the second phase
+    b = shard.split_bounds(len(data), world, find_nl)
+    for r in range(world):
+        handles[r] = _OracleShard(data[b[r]:b[r + 1]], SINCE, tail, grep)
+    g = np.array([[handles[r].g_term] for r in range(world)])
+    outs, totals = [], {}
+    for r in range(world):
+        it = iter([g, np.array([[int(handles[k].counts[f]) for f in shard.COUNT_FIELDS] for k in range(world)])])
+
+        def ag(vec, _it=it, _r=r):
+            m = next(_it)
+            return m
+
+        runner = lambda lo, hi, t, _r=r: handles[_r]
+        out, tot = shard.run_split(len(data), find_nl, runner, world, r, tail, allgather=ag)
+        outs.append(out)
+        totals = tot
+    return b"".join(outs), totals
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 5])
+@pytest.mark.parametrize("tail", [-1, 0, 1, 7, 40, 10_000])
+@pytest.mark.parametrize("grep", [(), (b"pod",)])
+@pytest.mark.parametrize("frag", [False, True])
+def test_split_stream_equals_unsplit(world, tail, grep, frag):
+    data = synth.generate(synth.TEXT, 77, 3, 60_000)
+    if frag:
+        data = data + b"2024-10-22T00:59:59.000000000Z frag pod no newline"
+    want, _, _, wc = co.filter_stream(data, SINCE, tail, list(grep), want_lines=False, want_bits=False)
+    got, totals = _split_case(data, world, tail, list(grep))
+    # counts that do not depend on the tail rule add up across shards (selected / out_bytes
+    # are summed from the shards' own runs before any re-tail in this simulation)
+    for f in ("lines", "parsed", "since_ok", "matched"):
+        assert totals[f] == wc[f], f
+    assert got == want
+
+
+def test_split_bounds_edges():
+    data = b"a\nbb\nccc\n" * 3 + b"tail"
+    fn = lambda p: data.find(b"\n", p)
+    for w in (1, 2, 3, 4, 7, 50):
+        b = shard.split_bounds(len(data), w, fn)
+        assert b[0] == 0 and b[-1] == len(data) and all(x <= y for x, y in zip(b, b[1:]))
+        last = shard.end_shard(b)
+        for r in range(w):
+            if b[r] < b[r + 1] and r != last:
+                assert data[b[r + 1] - 1:b[r + 1]] == b"\n"
+    assert shard.split_bounds(0, 3, lambda p: -1) == [0, 0, 0, 0]
+    assert shard.tail_shares([5, 5, 5], 7) == [0, 2, 5]
+    assert shard.tail_shares([5, 5, 5], 3) == [0, 0, 3]
+    assert shard.tail_shares([1, 1, 1], 7) == [1, 1, 7]
+    assert shard.tail_shares([5, 5, 5], -1) == [-1, -1, -1]
+    assert shard.tail_shares([5, 5, 0], 7, last=1) == [2, 5, 0]
+
+
+def _split_worker(rank, world, port, q):
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        data = synth.generate(synth.TEXT, 78, 1, 80_000) + b"2024-10-22T00:59:59.5Z pod fragment"
+        find_nl = lambda p: data.find(b"\n", p)
+        runner = lambda lo, hi, t: _OracleShard(data[lo:hi], SINCE, t, [b"pod"])
+        out, tot = shard.run_split(len(data), find_nl, runner, world, rank, 33)
+        q.put((rank, out, tot))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_world2_split_stream():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_split_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = dict((r, (o, t)) for r, o, t in (q.get(timeout=300) for _ in range(world)))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    data = synth.generate(synth.TEXT, 78, 1, 80_000) + b"2024-10-22T00:59:59.5Z pod fragment"
+    want, _, _, wc = co.filter_stream(data, SINCE, 33, [b"pod"], want_lines=False, want_bits=False)
+    assert got[0][0] + got[1][0] == want
+    assert got[0][1] == got[1][1]
+    assert got[0][1]["selected"] == wc["selected"] and got[0][1]["out_bytes"] == wc["out_bytes"]
+    assert got[0][1]["matched"] == wc["matched"]
