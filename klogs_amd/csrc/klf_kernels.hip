@@ -562,7 +562,7 @@ __global__ __launch_bounds__(kThreads, MODE == kScanGen ? 3 : KLF_SCAN_OCC) void
     if (KLF_ABL & 128) {  // timing build: no line list / parse / literal
     } else if (!dense) {
       work(s_list);
-      if (KLF_ABL & 4096) {  // timing build: half the slot bytes (u16 slots)
+      if (KLF_ABL & 8192) {  // timing build: half the slot bytes (u16 slots); k_scatter ignores slots
         for (uint32_t j = lane; j < nlines; j += 64) reinterpret_cast<uint16_t*>(gslot)[j] = (uint16_t)s_list[j];
       } else if (!(KLF_ABL & 512)) {
         for (uint32_t j = lane; j < nlines; j += 64) gslot[j] = s_list[j];
@@ -739,7 +739,7 @@ __global__ __launch_bounds__(256) void k_fixup(RunArgs a) {
     if (lane == 0) {
       ts.parsed = (uint16_t)(ts.parsed + dp);
       ts.since_ok = (uint16_t)(ts.since_ok + dq);
-      if (!(KLF_ABL & 256)) a.tstat[tile] = ts;
+      a.tstat[tile] = ts;
     }
   }
 }
@@ -964,9 +964,14 @@ __global__ __launch_bounds__(256) void k_scatter(RunArgs a) {
         const ScatterEnt& e = s_ent[wv][kk[u]];
         const uint64_t li = e.base + jj[u];
         if (li >= a.cap_lines) { atomicOr(err_flag, 1u); continue; }
+#if KLF_ABL & (8192 | 16384)  // timing builds: slot contents ignored (no line selected downstream)
+        a.line_off[li + e.seg] = e.rel_lo;
+        a.meta[li] = (uint16_t)(sl[u] & 0u);
+#else
         a.line_off[li + e.seg] = e.rel_lo + (sl[u] & kSlotOff);
         a.meta[li] = (uint16_t)(sl[u] >> 16);
         if (sl[u] & kSlotHit) atomicOr(&a.bits[li >> 5], 1u << (li & 31));
+#endif
       }
     }
     asm volatile("" ::: "memory");  // the next group rewrites the wave's LDS tables

@@ -17,6 +17,7 @@ for name, grep in (("nogrep", []), ("lit", [synth.NEEDLE])):
         r = eng.run_device(dev.data_ptr(), base, [n], since=(synth.T0 + 3301, 0), tail=100, stage_times=True)
         ts.append(r.timing()); r.free()
     ts = np.array(ts[2:])
-    res[name] = {"scan_ms": float(np.median(ts[:, 0])), "total_ms": float(np.median(ts[:, 4]))}
+    res[name] = {"scan_ms": float(np.median(ts[:, 0])), "total_ms": float(np.median(ts[:, 4])),
+                 "k_scan_ms": float(np.median(ts[:, 6]))}
     eng.close()
 print(json.dumps(res))
