@@ -564,6 +564,7 @@ __global__ __launch_bounds__(kThreads, MODE == kScanGen ? 3 : KLF_SCAN_OCC) void
       work(s_list);
       if (KLF_ABL & 8192) {  // timing build: half the slot bytes (u16 slots); k_scatter ignores slots
         for (uint32_t j = lane; j < nlines; j += 64) reinterpret_cast<uint16_t*>(gslot)[j] = (uint16_t)s_list[j];
+      } else if ((KLF_ABL & 32768) && ((tile / nwaves) & 3u) != 0) {  // timing build: 1 tile in 4 stores
       } else if (!(KLF_ABL & 512)) {
         for (uint32_t j = lane; j < nlines; j += 64) gslot[j] = s_list[j];
       }
@@ -964,7 +965,7 @@ __global__ __launch_bounds__(256) void k_scatter(RunArgs a) {
         const ScatterEnt& e = s_ent[wv][kk[u]];
         const uint64_t li = e.base + jj[u];
         if (li >= a.cap_lines) { atomicOr(err_flag, 1u); continue; }
-#if KLF_ABL & (8192 | 16384)  // timing builds: slot contents ignored (no line selected downstream)
+#if KLF_ABL & (8192 | 16384 | 32768)  // timing builds: slot contents ignored (no line selected downstream)
         a.line_off[li + e.seg] = e.rel_lo;
         a.meta[li] = (uint16_t)(sl[u] & 0u);
 #else

@@ -221,3 +221,34 @@ def test_long_lines_copy_chunks(gpu, since, tail):
     """Selected output of 1-32 KiB lines: one compaction block spans many 64 KiB copy chunks."""
     streams = [synth.generate(synth.LONGJSON, 12, i, 3_000_000 + 777 * i, permille=5) for i in range(3)]
     check_against_c(streams, since, tail, [])
+
+
+def test_stream_over_4gib_offsets(gpu):
+    """one stream longer than 2^32 bytes (u64 line offsets past 4 GiB),
+    device-resident, since + tail + one literal: output, counts and every line offset
+    against the C oracle."""
+    import torch
+    target = (4 << 30) + (96 << 20)
+    n = synth.size(synth.JSON, 7, 0, target, permille=10)
+    assert n > (1 << 32)
+    host = np.empty(n + 1, dtype=np.uint8)
+    synth.generate_into(host, synth.JSON, 7, 0, target, permille=10)
+    host = host[:n]
+    base, total = E.layout([n])
+    dev = torch.empty(total, dtype=torch.uint8, device="cuda")
+    dev[:n].copy_(torch.from_numpy(host))
+    torch.cuda.synchronize()
+    since = (synth.T0 + synth.SPAN - 240, 0)
+    with E.Engine(0, grep=[synth.NEEDLE]) as eng:
+        r = eng.run_device(dev.data_ptr(), base, [n], since=since, tail=1000)
+        so = r.stream(0)
+        lo = r.lines(0)
+        r.free()
+    del dev
+    want, want_lo, _, wc = co.filter_stream(host, since, 1000, [synth.NEEDLE], want_lines=True, want_bits=False)
+    assert so.out == want
+    for k in ("lines", "parsed", "since_ok", "matched", "selected", "out_bytes"):
+        assert so.counts[k] == wc[k], k
+    assert lo.shape == want_lo.shape and int(lo[-1]) == n
+    assert np.array_equal(lo, want_lo)
+    assert int(np.count_nonzero(lo > (1 << 32))) > 0
