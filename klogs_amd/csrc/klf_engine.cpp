@@ -54,9 +54,21 @@ struct klf_engine {
   klf::CompiledSet cs;
   std::string err;
   uint64_t gen = 0;
-  // staging (host path)
+  // staging (host path): per stream, a list of pinned host chunks (hipHostMalloc, reused
+  // across runs), so klf_run's H2D is DMA from page-locked memory at PCIe rate instead of
+  // a bounce through pageable buffers; pageable only where pinning fails (no device).
   std::mutex mu;
-  std::vector<std::vector<uint8_t>> staged;
+  struct StageChunk {
+    uint8_t* p = nullptr;
+    size_t used = 0;
+    bool pinned = false;
+  };
+  struct StagedStream {
+    std::vector<StageChunk> chunks;
+    uint64_t len = 0;
+  };
+  std::vector<StagedStream> staged;
+  std::vector<StageChunk> chunk_pool;  // free chunks (used = 0)
   // device pattern tables
   DevBuf d_lit, d_ac_class, d_ac_next, d_ac_accept, d_rx_class, d_rx_b, d_rx_follow, d_rx_vec, d_rx_flags;
   DevBuf d_qf_bitmap, d_qf_head, d_qf_ent, d_qf_nbytes, d_cand, d_rx_vec4, d_qhits, d_hslots, d_hist, d_hflat;
@@ -248,6 +260,9 @@ extern "C" int klf_open(const klf_config* cfg, klf_engine** out) {
   return KLF_OK;
 }
 
+static void release_staged(klf_engine* e);
+static void free_chunk(klf_engine::StageChunk& c);
+
 extern "C" void klf_close(klf_engine* e) {
   if (!e) return;
   if (e->stream) (void)hipStreamSynchronize(e->stream);
@@ -257,6 +272,12 @@ extern "C" void klf_close(klf_engine* e) {
                     &e->d_slots, &e->d_pool, &e->d_tile_base, &e->d_bsum, &e->d_cstatus, &e->d_counters,
                     &e->d_line_off, &e->d_meta, &e->d_bits, &e->d_segout, &e->d_wpre, &e->d_out, &e->d_tile_seg, &e->d_mpart})
     b->release();
+  {
+    std::lock_guard<std::mutex> g(e->mu);
+    release_staged(e);
+    for (auto& c : e->chunk_pool) free_chunk(c);
+    e->chunk_pool.clear();
+  }
   for (auto& x : e->ev)
     if (x) (void)hipEventDestroy(x);
   if (e->own_stream && e->stream) (void)hipStreamDestroy(e->stream);
@@ -273,28 +294,84 @@ extern "C" int klf_set_streams(klf_engine* e, uint32_t n) {
   return KLF_OK;
 }
 
+static constexpr size_t kStageChunk = 64u << 20;  // pinned staging chunk
+
+static bool take_chunk(klf_engine* e, klf_engine::StageChunk* c) {
+  {
+    std::lock_guard<std::mutex> g(e->mu);
+    if (!e->chunk_pool.empty()) {
+      *c = e->chunk_pool.back();
+      e->chunk_pool.pop_back();
+      c->used = 0;
+      return true;
+    }
+  }
+  void* p = nullptr;
+  if (hipHostMalloc(&p, kStageChunk, hipHostMallocDefault) == hipSuccess && p) {
+    c->p = static_cast<uint8_t*>(p);
+    c->pinned = true;
+  } else {
+    (void)hipGetLastError();
+    c->p = static_cast<uint8_t*>(malloc(kStageChunk));
+    c->pinned = false;
+    if (!c->p) return false;
+  }
+  c->used = 0;
+  return true;
+}
+
+static void free_chunk(klf_engine::StageChunk& c) {
+  if (!c.p) return;
+  if (c.pinned) (void)hipHostFree(c.p);
+  else free(c.p);
+  c.p = nullptr;
+}
+
 extern "C" int klf_stage(klf_engine* e, uint32_t id, const uint8_t* p, size_t n) {
   if (!e || (n && !p)) return KLF_EINVAL;
-  std::vector<uint8_t>* dst;
+  klf_engine::StagedStream* dst;
   {
     std::lock_guard<std::mutex> g(e->mu);
     if (id >= e->staged.size()) e->staged.resize((size_t)id + 1);
     dst = &e->staged[id];
   }
-  // different ids never share a vector; the outer vector only grows under the lock and
-  // callers declare the table with klf_set_streams before staging concurrently.
-  try {
-    dst->insert(dst->end(), p, p + n);
-  } catch (...) {
-    return KLF_ENOMEM;
+  // different ids never share a stream record; the outer vector only grows under the
+  // lock and callers declare the table with klf_set_streams before staging concurrently.
+  while (n) {
+    if (dst->chunks.empty() || dst->chunks.back().used == kStageChunk) {
+      klf_engine::StageChunk c;
+      if (!take_chunk(e, &c)) return KLF_ENOMEM;
+      try {
+        dst->chunks.push_back(c);
+      } catch (...) {
+        free_chunk(c);
+        return KLF_ENOMEM;
+      }
+    }
+    auto& c = dst->chunks.back();
+    const size_t k = std::min(n, kStageChunk - c.used);
+    memcpy(c.p + c.used, p, k);
+    c.used += k;
+    dst->len += k;
+    p += k;
+    n -= k;
   }
   return KLF_OK;
+}
+
+static void release_staged(klf_engine* e) {  // caller holds e->mu
+  for (auto& s : e->staged)
+    for (auto& c : s.chunks) {
+      c.used = 0;
+      e->chunk_pool.push_back(c);
+    }
+  e->staged.clear();
 }
 
 extern "C" int klf_reset(klf_engine* e) {
   if (!e) return KLF_EINVAL;
   std::lock_guard<std::mutex> g(e->mu);
-  e->staged.clear();
+  release_staged(e);
   return KLF_OK;
 }
 
@@ -555,14 +632,18 @@ extern "C" int klf_run(klf_engine* e, const klf_filter* f, klf_result** out) {
   std::lock_guard<std::mutex> g(e->mu);
   const uint32_t n = (uint32_t)e->staged.size();
   std::vector<uint64_t> lens(n), base(n);
-  for (uint32_t i = 0; i < n; ++i) lens[i] = e->staged[i].size();
+  for (uint32_t i = 0; i < n; ++i) lens[i] = e->staged[i].len;
   uint64_t total = 0;
   klf_layout(n, lens.data(), base.data(), &total);
   HIPCHK(e, e->d_batch.ensure(total), "alloc batch");
-  for (uint32_t i = 0; i < n; ++i)
-    if (lens[i])
-      HIPCHK(e, hipMemcpyAsync(e->d_batch.as<uint8_t>() + base[i], e->staged[i].data(), lens[i], hipMemcpyHostToDevice,
-                               e->stream), "H2D stream");
+  for (uint32_t i = 0; i < n; ++i) {  // DMA from the pinned chunks, all queued back to back
+    uint64_t off = base[i];
+    for (const auto& c : e->staged[i].chunks) {
+      HIPCHK(e, hipMemcpyAsync(e->d_batch.as<uint8_t>() + off, c.p, c.used, hipMemcpyHostToDevice, e->stream),
+             "H2D stream");
+      off += c.used;
+    }
+  }
   return run_device_impl(e, e->d_batch.as<uint8_t>(), n, base.data(), lens.data(), f, out);
 }
 

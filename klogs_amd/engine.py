@@ -296,6 +296,11 @@ class Engine:
     def set_streams(self, n: int):
         _check(_lib.klf_set_streams(self._h, n), self._h)
 
+    def stage_array(self, stream_id: int, arr: np.ndarray):
+        """klf_stage straight from a contiguous uint8 numpy array (no intermediate copy)."""
+        a = np.ascontiguousarray(arr, dtype=np.uint8)
+        _check(_lib.klf_stage(self._h, stream_id, C.c_void_p(a.ctypes.data if a.size else 0), a.size), self._h)
+
     def stage(self, stream_id: int, data: bytes):
         buf = C.create_string_buffer(data, len(data) or 1)
         _check(_lib.klf_stage(self._h, stream_id, buf, len(data)), self._h)

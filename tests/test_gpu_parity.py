@@ -252,3 +252,31 @@ def test_stream_over_4gib_offsets(gpu):
     assert lo.shape == want_lo.shape and int(lo[-1]) == n
     assert np.array_equal(lo, want_lo)
     assert int(np.count_nonzero(lo > (1 << 32))) > 0
+
+
+def test_staging_across_pinned_chunks(gpu):
+    """klf_stage in odd-sized pieces that straddle the 64 MiB pinned staging chunks, two
+    streams interleaved, then klf_run: bit-exact with the C oracle."""
+    a = synth.generate(synth.JSON, 21, 0, 150 << 20, permille=10)
+    b = synth.generate(synth.TEXT, 22, 1, 70 << 20)
+    since = (synth.T0 + 3000, 0)
+    with E.Engine(0, grep=[synth.NEEDLE]) as eng:
+        for rep in range(2):  # the second run reuses the pooled chunks
+            eng.reset()
+            eng.set_streams(2)
+            pa = pb = 0
+            step = 7_777_777 + rep
+            while pa < len(a) or pb < len(b):
+                if pa < len(a):
+                    eng.stage_array(0, np.frombuffer(a, dtype=np.uint8)[pa:pa + step])
+                    pa += step
+                if pb < len(b):
+                    eng.stage(1, b[pb:pb + step // 3])
+                    pb += step // 3
+            r = eng.run(since=since, tail=5000, n_streams=2)
+            for i, s in enumerate((a, b)):
+                so = r.stream(i)
+                want, _, _, wc = co.filter_stream(s, since, 5000, [synth.NEEDLE], want_lines=False, want_bits=False)
+                assert so.out == want, (rep, i)
+                assert so.counts["lines"] == wc["lines"] and so.counts["selected"] == wc["selected"]
+            r.free()
