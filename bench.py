@@ -75,9 +75,18 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # Rehearsal knob for a one-GPU box: KLF_BENCH_BACKEND=gloo lets N ranks share cuda:0
+    # (RCCL refuses two ranks on one device).  The driver's runs use RCCL, one GPU per rank.
+    backend = os.environ.get("KLF_BENCH_BACKEND", "nccl")
+    if backend != "nccl":
+        local = local % torch.cuda.device_count()
     torch.cuda.set_device(local)
+    coll_dev = f"cuda:{local}" if backend == "nccl" else "cpu"
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
 
     # ---- synthetic input: stream `rank` of the C2 family, generated on the host ----
     assert shard.local_streams([args.bytes] * world, world, rank) == [rank]  # LPT: equal streams 1:1
@@ -104,7 +113,7 @@ def main():
     def step():
         r = eng.run_device(ptr, seg_base, [n], since=since, tail=TAIL)
         if world > 1:  # per-stream count records -> every rank (one all-gather, RCCL over xGMI)
-            shard.gather_counts({rank: r.totals()}, [n] * world, world, device=f"cuda:{local}")
+            shard.gather_counts({rank: r.totals()}, [n] * world, world, device=coll_dev)
         return r
 
     for _ in range(args.warmup):
@@ -130,7 +139,7 @@ def main():
         dist.barrier()
     dt = time.perf_counter() - t0
     if world > 1:
-        tt = torch.tensor([dt], dtype=torch.float64, device=f"cuda:{local}")
+        tt = torch.tensor([dt], dtype=torch.float64, device=coll_dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
 
