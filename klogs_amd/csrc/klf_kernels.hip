@@ -602,7 +602,8 @@ __global__ __launch_bounds__(kThreads, MODE == kScanGen ? 3 : KLF_SCAN_OCC) void
 #pragma unroll
         for (int d = 0; d < 4; ++d)
 #pragma unroll
-          for (int o = 0; o < 4; o += QS) {
+          for (int o = 0; o < 4; o += (QS < 4 ? QS : 4)) {
+            if ((4 * d + o) % QS != 0) continue;  // QS = 8: dwords 0 and 2 only
             const uint32_t g = o == 0 ? w[d] : __builtin_amdgcn_alignbyte(w[d + 1], w[d], o);
             hm |= probe(g) << (4 * d + o);
           }
@@ -1660,7 +1661,11 @@ __device__ void block_gather_copy(const uint64_t* s_src, const uint64_t* s_dst, 
       const int b0 = (int)(pos - d0), b1 = (int)(pend - d0);
       if (ad0 >= 16) {
         const uint64_t base = (uint64_t)ad0 & ~15ull;
+#if KLF_ABL & 65536  // timing build: source reads from the batch's first 64 KiB (wrong bytes, same work)
+        const uint4* wp = reinterpret_cast<const uint4*>(src + (base & 0xFFF0ull));
+#else
         const uint4* wp = reinterpret_cast<const uint4*>(src + base);
+#endif
         const uint4 v = extract16(wp[0], wp[1], (uint32_t)(ad0 - (int64_t)base));
         const uint32_t vv[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
@@ -1825,6 +1830,8 @@ hipError_t launch_pipeline(const RunArgs& a, hipStream_t st, hipEvent_t* ev, int
       KLF_TRY((launch_scan<kScanLit, 1>(a, st, num_cus)));
     else if (a.grep_mode == kGrepGeneral && a.pats.qf_on && a.pats.qf_stride == 4)
       KLF_TRY((launch_scan<kScanGen, 4>(a, st, num_cus)));
+    else if (a.grep_mode == kGrepGeneral && a.pats.qf_on && a.pats.qf_stride == 8)
+      KLF_TRY((launch_scan<kScanGen, 8>(a, st, num_cus)));
     else if (a.grep_mode == kGrepGeneral && a.pats.qf_on && a.pats.qf_stride == 2)
       KLF_TRY((launch_scan<kScanGen, 2>(a, st, num_cus)));
     else if (a.grep_mode == kGrepGeneral && a.pats.qf_on)

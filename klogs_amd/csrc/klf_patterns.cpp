@@ -980,10 +980,11 @@ void build_prefilter(const std::vector<std::vector<uint8_t>>& lits, const std::v
     loose |= (n.flags & kQfLoose) != 0;
   }
   if (minlen < kQfMinNeedle) { out.qf_why = "a needle is shorter than 3 bytes"; return; }
-  // the widest sampling stride that keeps grams of >= 3 bytes (the probes are LDS-bound),
-  // then the longest gram that stride allows
-  const size_t sw = std::min<size_t>(4, minlen - 2);
-  const uint32_t S = sw >= 4 ? 4 : (sw >= 2 ? 2 : 1);
+  // the widest sampling stride that keeps grams of >= 3 bytes (each probe costs ~18 VALU
+  // in the scan, so S = 8 halves the probe work of S = 4), then the longest gram that
+  // stride allows
+  const size_t sw = std::min<size_t>(8, minlen - 2);
+  const uint32_t S = sw >= 8 ? 8 : (sw >= 4 ? 4 : (sw >= 2 ? 2 : 1));
   const uint32_t q = (uint32_t)std::min<size_t>(4, minlen - S + 1);
   out.qf_q = q;
   out.qf_stride = S;

@@ -156,6 +156,16 @@ def test_c4_literal_set_mixed_lines(gpu, since, tail):
     check_against_c([d, synth.generate(synth.MIXED, 4, 1, 700_000, permille=50)], since, tail, lits)
 
 
+@pytest.mark.parametrize("since,tail", [(None, -1), ((synth.T0 + 1800, 0), 50)])
+def test_long_needles_stride8(gpu, since, tail):
+    """Literal sets whose shortest needle allows an 8-byte sampling stride (k_scan<gen, 8>)."""
+    lits = [l for l in synth.c4_literals(1024) if len(l) >= 12][:300]
+    info = E.debug_prefilter(b"", grep=lits)[1]
+    assert info["on"] and info["stride"] == 8
+    d = synth.generate(synth.MIXED, 9, 0, 3_000_000, permille=20)
+    check_against_c([d, synth.generate(synth.MIXED, 9, 1, 700_000, permille=80)], since, tail, lits)
+
+
 @pytest.mark.parametrize("since,tail", [(None, -1), ((synth.T0 + 1800, 0), 20)])
 def test_c5_regex_set_long_json(gpu, since, tail):
     """BASELINE config 5 shape at test size: 64 regexes over 1-32 KiB JSON lines (events

@@ -104,6 +104,9 @@ def test_prefilter_off_falls_back(grep, match, why):
     ([b"abcd", b"0123456789"], [], 3, 2),
     ([b"abc", b"0123456789"], [], 3, 1),
     ([], [rb"(?i)timeout"], 4, 4),
+    ([b"abcdefghij", b"0123456789AB"], [], 3, 8),
+    ([b"abcdefghijk"], [rb"x+connection reset"], 4, 8),
+    ([b"abcdefghi", b"0123456789AB"], [], 4, 4),
 ])
 def test_gram_and_stride_choice(grep, match, q, stride):
     _, info = E.debug_prefilter(b"", grep=grep, match=match)
