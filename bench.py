@@ -68,7 +68,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--no-capture", action="store_true", help="skip the host-staged capture-path timing")
-    ap.add_argument("--extra-configs", default="c4,c5", help="N=1 only: comma list of c4,c5 ('' = none)")
+    ap.add_argument("--extra-configs", default="c3,c4,c5", help="N=1 only: comma list of c3,c4,c5 ('' = none)")
     ap.add_argument("--extra-bytes", type=int, default=32 << 30, help="total bytes of each extra config")
     args = ap.parse_args()
 
@@ -277,7 +277,13 @@ def main():
 
 
 def extra_streams(name: str, total: int):
-    """(stream sizes, generator kind, patterns, description) of BASELINE configs 4 / 5."""
+    """(stream sizes, generator kind, patterns, permille, description) of BASELINE configs
+    3 / 4 / 5."""
+    if name == "c3":  # one GPU's share of C3 at 8 GPUs (fixed size: --extra-bytes is for C4/C5)
+        n = 128
+        return [64 << 20] * n, synth.TEXT, {}, 10, \
+            "C3 per-GPU share at 8 GPUs: 128 streams x 64 MiB (256 pods x 4 containers / 8), -l selection " \
+            "only: no --since, no --tail, no grep (every line out, prefix stripped)"
     if name == "c4":
         n = 8
         return [total // n] * n, synth.MIXED, dict(grep=synth.c4_literals(1024)), 5, \
@@ -309,18 +315,18 @@ def run_extra(name: str, args, local: int, now: int) -> dict:
         del h
     torch.cuda.synchronize()
     log(f"[{name}] generated + uploaded {sum(lens)} B in {time.time() - t:.1f}s")
-    since = (now - SINCE_S, 0)
+    since, tail = ((None, -1) if name == "c3" else ((now - SINCE_S, 0), TAIL))
     stream = torch.cuda.current_stream()
     eng = E.Engine(local, hip_stream=stream.cuda_stream, **pats)
     ptr = dev.data_ptr()
     for _ in range(args.warmup):
-        eng.run_device(ptr, seg_base, lens, since=since, tail=TAIL).free()
+        eng.run_device(ptr, seg_base, lens, since=since, tail=tail).free()
     torch.cuda.synchronize()
     scan_ms, total_ms = [], []
     t0 = time.perf_counter()
     last = None
     for i in range(args.steps):
-        r = eng.run_device(ptr, seg_base, lens, since=since, tail=TAIL)
+        r = eng.run_device(ptr, seg_base, lens, since=since, tail=tail)
         tm = r.timing()
         scan_ms.append(tm[6])
         total_ms.append(tm[4])
@@ -330,10 +336,20 @@ def run_extra(name: str, args, local: int, now: int) -> dict:
             last = r
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
-    staged = eng.run_device(ptr, seg_base, lens, since=since, tail=TAIL, stage_times=True)
+    verified = None
+    if name == "c3" and not args.no_verify:  # first and last stream against the C oracle
+        sys.path.insert(0, str(ROOT / "oracle"))
+        import c_oracle as co
+        verified = True
+        for i in (0, len(lens) - 1):
+            h = np.empty(lens[i] + 1, dtype=np.uint8)
+            synth.generate_into(h, kind, 42, i, sizes[i], permille=permille)
+            want = co.filter_stream(h[:lens[i]], co.GO_ZERO_TIME, -1, [], want_lines=False, want_bits=False)[0]
+            verified = verified and last.stream(i).out == want
+    tot = last.totals()
+    staged = eng.run_device(ptr, seg_base, lens, since=since, tail=tail, stage_times=True)
     stage = staged.timing()
     staged.free()
-    tot = last.totals()
     n = sum(lens)
     scan_s = float(np.mean(scan_ms)) / 1e3
     dev_s = float(np.mean(total_ms)) / 1e3
@@ -342,7 +358,7 @@ def run_extra(name: str, args, local: int, now: int) -> dict:
         "workload": desc, "streams": len(lens), "bytes": n, "lines": tot["lines"],
         "value_GBps": round(n * args.steps / dt / 1e9, 1), "ms_per_step": round(dt / args.steps * 1e3, 3),
         "device_ms_per_step": round(dev_s * 1e3, 3),
-        "roofline": {"bound": "hbm", "kernel": "k_scan<general, q-gram prefilter>",
+        "roofline": {"bound": "hbm", "kernel": "k_scan<plain>" if not pats else "k_scan<general, q-gram prefilter>",
                      "achieved": round(n / scan_s / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(n / scan_s / 1e9 / HBM_PEAK_GBS, 4), "avg_launch_ms": round(scan_s * 1e3, 4)},
         "matcher_ms": round(stage[1], 4),
@@ -350,6 +366,8 @@ def run_extra(name: str, args, local: int, now: int) -> dict:
         "matched_lines": tot["matched"], "selected_lines": tot["selected"], "out_bytes": tot["out_bytes"],
         "stage_ms": [round(x, 4) for x in stage],
     }
+    if verified is not None:
+        out["verified_vs_c_oracle"] = bool(verified)
     last.free()
     eng.close()
     del dev

@@ -78,6 +78,7 @@ struct klf_engine {
   // workspace
   std::vector<SegDesc> last_segs;  // tile_seg cache key
   DevBuf d_tile_seg;
+  DevBuf d_cmap, d_cseg;
   DevBuf d_batch, d_segs, d_tstat, d_slots, d_pool, d_tile_base, d_bsum, d_cstatus, d_counters, d_line_off,
       d_meta, d_bits, d_segout, d_wpre, d_out, d_mpart;
   uint64_t pool_cap = 1 << 20;
@@ -269,7 +270,7 @@ extern "C" void klf_close(klf_engine* e) {
   for (DevBuf* b : {&e->d_lit, &e->d_ac_class, &e->d_ac_next, &e->d_ac_accept, &e->d_rx_class, &e->d_rx_b,
                     &e->d_rx_follow, &e->d_rx_vec, &e->d_rx_flags, &e->d_qf_bitmap, &e->d_qf_head,
                     &e->d_qf_ent, &e->d_qf_nbytes, &e->d_rx_vec4, &e->d_qhits, &e->d_hslots, &e->d_hist, &e->d_hflat, &e->d_cand, &e->d_batch, &e->d_segs, &e->d_tstat,
-                    &e->d_slots, &e->d_pool, &e->d_tile_base, &e->d_bsum, &e->d_cstatus, &e->d_counters,
+                    &e->d_slots, &e->d_pool, &e->d_tile_base, &e->d_bsum, &e->d_cstatus, &e->d_counters, &e->d_cmap, &e->d_cseg,
                     &e->d_line_off, &e->d_meta, &e->d_bits, &e->d_segout, &e->d_wpre, &e->d_out, &e->d_tile_seg, &e->d_mpart})
     b->release();
   {
@@ -492,6 +493,9 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
     HIPCHK(e, e->d_meta.ensure(cap * 2 + 16), "alloc meta");
     HIPCHK(e, e->d_bits.ensure((cap / 32 + 1) * 4), "alloc bits");
     HIPCHK(e, e->d_cstatus.ensure((max_cblocks + 1) * 3 * 8), "alloc cstatus");
+    const uint64_t cmap_cap = max_cblocks + total_bytes / klf::kCopyChunk + 2;  // >= sum of ceil(bytes / chunk), >= 1 each
+    HIPCHK(e, e->d_cmap.ensure(cmap_cap * 4), "alloc cmap");
+    HIPCHK(e, e->d_cseg.ensure((max_cblocks + 1) * 4), "alloc cseg");
     HIPCHK(e, e->d_mpart.ensure((cap / klf::kMatchChunk + 2) * 8), "alloc mpart");
     HIPCHK(e, e->d_pool.ensure(e->pool_cap * 4), "alloc pool");
     klf::RunArgs a{};
@@ -527,6 +531,9 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
     a.bsum = e->d_bsum.as<uint64_t>();
     a.mpart = e->d_mpart.as<uint64_t>();
     a.csum = e->d_cstatus.as<uint64_t>();
+    a.cmap = e->d_cmap.as<uint32_t>();
+    a.cmap_cap = cmap_cap;
+    a.cseg = e->d_cseg.as<uint32_t>();
     a.counters = e->d_counters.as<uint32_t>();
     a.line_off = e->d_line_off.as<uint64_t>();
     a.meta = e->d_meta.as<uint16_t>();

@@ -269,6 +269,9 @@ __device__ __forceinline__ bool parse_fast(const uint8_t* lds, uint32_t o, const
 #ifndef KLF_ABL
 #define KLF_ABL 0
 #endif
+#ifndef KLF_COPY_U
+#define KLF_COPY_U 1
+#endif
 #ifndef KLF_SCAN_OCC
 #define KLF_SCAN_OCC 4
 #endif
@@ -1518,11 +1521,14 @@ struct WinLines {
   uint32_t nsel;
 };
 
-__device__ __forceinline__ void window_lines(const RunArgs& a, uint64_t w0, uint64_t W, WinLines& r) {
+// s_lo: a stream at or before the one holding window line w0 (0 = unknown; k_csum
+// records each block's first stream so that k_cgather's search starts there)
+__device__ __forceinline__ void window_lines(const RunArgs& a, uint64_t w0, uint64_t W, WinLines& r,
+                                             uint32_t s_lo = 0) {
   uint32_t s = 0;
   {
     const uint64_t wq = w0 < W ? w0 : (W ? W - 1 : 0);
-    uint32_t lo = 0, hi = a.nsegs;
+    uint32_t lo = s_lo, hi = a.nsegs;
     while (hi - lo > 1) {
       const uint32_t mid = (lo + hi) >> 1;
       if (a.wpre[mid] <= wq) lo = mid; else hi = mid;
@@ -1564,6 +1570,7 @@ __global__ __launch_bounds__(kThreads) void k_csum(RunArgs a) {
   for (uint32_t blk = blockIdx.x; blk < nblocks; blk += gridDim.x) {
     WinLines r;
     window_lines(a, (uint64_t)blk * kCompactLines + (uint64_t)t * 4, W, r);
+    if (t == 0) a.cseg[blk] = r.seg[0];
     const uint64_t b = wave_sum(r.bytes), c = wave_sum((uint64_t)r.nsel);
     __syncthreads();
     if (lane == 0) { s_wb[wv] = b; s_wc[wv] = c; }
@@ -1598,9 +1605,11 @@ __global__ __launch_bounds__(256) void k_cscan(RunArgs a) {
     a.csum[3 * i] = pb;
     a.csum[3 * i + 1] = pc;
     a.csum[3 * i + 2] = pk;
+    const uint64_t nk = chunks(xb);
+    for (uint64_t k = 0; k < nk && pk + k < a.cmap_cap; ++k) a.cmap[pk + k] = i;  // chunk -> block
     pb += xb;
     pc += xc;
-    pk += chunks(xb);
+    pk += nk;
   }
   if (t == 255) {
     a.csum[3 * nb] = pb;  // total output bytes
@@ -1640,53 +1649,91 @@ __device__ void block_gather_copy(const uint64_t* s_src, const uint64_t* s_dst, 
                                   uint64_t ob1, const uint8_t* __restrict__ src, uint8_t* __restrict__ dst) {
   if (ob1 <= ob0) return;
   const uint64_t c0 = ob0 >> 4, c1 = (ob1 + 15) >> 4;
-  int i = 0;  // line of the current position: monotone per thread
-  for (uint64_t c = c0 + threadIdx.x; c < c1; c += blockDim.x) {
-    const uint64_t d0 = c << 4;
-    const uint64_t lo = d0 > ob0 ? d0 : ob0, hi = d0 + 16 < ob1 ? d0 + 16 : ob1;
-    {  // last line with s_dst <= lo, searched in [i, kCompactLines)
-      int l = i, h = kCompactLines;
+  // U output chunks per thread and step, their source loads all in flight before the
+  // first is merged (the copy is latency-bound otherwise: a 16-B chunk per round trip)
+  constexpr int U = KLF_COPY_U;
+  int iu[U];  // line of each lane's chunk u: monotone per u
+#pragma unroll
+  for (int u = 0; u < U; ++u) iu[u] = 0;
+  auto piece = [&](uint32_t (&o)[4], int64_t ad0, const uint4& va, const uint4& vb, int b0, int b1)
+      __attribute__((always_inline)) {
+    if (ad0 >= 16) {
+      const uint64_t base = (uint64_t)ad0 & ~15ull;
+      const uint4 v = extract16(va, vb, (uint32_t)(ad0 - (int64_t)base));
+      const uint32_t vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const uint32_t m = byte_mask(b0, b1, k);
+        o[k] = (vv[k] & m) | (o[k] & ~m);
+      }
+    } else {
+      for (int b = b0; b < b1; ++b) {
+        const uint32_t byte = src[ad0 + b];
+        o[b >> 2] = (o[b >> 2] & ~(0xFFu << (8 * (b & 3)))) | (byte << (8 * (b & 3)));
+      }
+    }
+  };
+  for (uint64_t cb = c0 + threadIdx.x; cb < c1; cb += (uint64_t)U * blockDim.x) {
+    uint4 va[U], vb[U];
+    int liu[U];
+    uint64_t pend0[U];
+    int64_t a0[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {  // locate the first piece of every chunk, issue its loads
+      const uint64_t c = cb + (uint64_t)u * blockDim.x;
+      va[u] = vb[u] = make_uint4(0, 0, 0, 0);
+      liu[u] = iu[u];
+      pend0[u] = 0;
+      a0[u] = 0;
+      if (c >= c1) continue;
+      const uint64_t d0 = c << 4;
+      const uint64_t lo = d0 > ob0 ? d0 : ob0, hi = d0 + 16 < ob1 ? d0 + 16 : ob1;
+      int l = iu[u], h = kCompactLines;  // last line with s_dst <= lo, in [iu, kCompactLines)
       while (h - l > 1) {
         const int m = (l + h) >> 1;
         if (s_dst[m] <= lo) l = m; else h = m;
       }
-      i = l;
-    }
-    uint32_t o[4] = {0, 0, 0, 0};
-    int li = i;
-    for (uint64_t pos = lo; pos < hi;) {
-      while (s_dst[li] + s_len[li] <= pos) ++li;  // zero-length / finished lines
-      const uint64_t pend = s_dst[li] + s_len[li] < hi ? s_dst[li] + s_len[li] : hi;
-      const int64_t ad0 = (int64_t)s_src[li] - (int64_t)s_dst[li] + (int64_t)d0;  // source of chunk byte 0
-      const int b0 = (int)(pos - d0), b1 = (int)(pend - d0);
-      if (ad0 >= 16) {
-        const uint64_t base = (uint64_t)ad0 & ~15ull;
-#if KLF_ABL & 65536  // timing build: source reads from the batch's first 64 KiB (wrong bytes, same work)
-        const uint4* wp = reinterpret_cast<const uint4*>(src + (base & 0xFFF0ull));
-#else
-        const uint4* wp = reinterpret_cast<const uint4*>(src + base);
-#endif
-        const uint4 v = extract16(wp[0], wp[1], (uint32_t)(ad0 - (int64_t)base));
-        const uint32_t vv[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const uint32_t m = byte_mask(b0, b1, k);
-          o[k] = (vv[k] & m) | (o[k] & ~m);
-        }
-      } else {
-        for (int b = b0; b < b1; ++b) {
-          const uint32_t byte = src[ad0 + b];
-          o[b >> 2] = (o[b >> 2] & ~(0xFFu << (8 * (b & 3)))) | (byte << (8 * (b & 3)));
-        }
+      iu[u] = l;
+      int li = l;
+      while (s_dst[li] + s_len[li] <= lo) ++li;  // zero-length / finished lines
+      liu[u] = li;
+      pend0[u] = s_dst[li] + s_len[li] < hi ? s_dst[li] + s_len[li] : hi;
+      a0[u] = (int64_t)s_src[li] - (int64_t)s_dst[li] + (int64_t)d0;  // source of chunk byte 0
+      if (a0[u] >= 16) {
+        const uint4* wp = reinterpret_cast<const uint4*>(src + ((uint64_t)a0[u] & ~15ull));
+        va[u] = wp[0];
+        vb[u] = wp[1];
       }
-      pos = pend;
     }
-    if (lo == d0 && hi == d0 + 16) {
-      *reinterpret_cast<uint4*>(dst + d0) = make_uint4(o[0], o[1], o[2], o[3]);
-    } else {
-      for (uint64_t pos = lo; pos < hi; ++pos) {
-        const int b = (int)(pos - d0);
-        dst[pos] = (uint8_t)(o[b >> 2] >> (8 * (b & 3)));
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint64_t c = cb + (uint64_t)u * blockDim.x;
+      if (c >= c1) continue;
+      const uint64_t d0 = c << 4;
+      const uint64_t lo = d0 > ob0 ? d0 : ob0, hi = d0 + 16 < ob1 ? d0 + 16 : ob1;
+      uint32_t o[4] = {0, 0, 0, 0};
+      piece(o, a0[u], va[u], vb[u], (int)(lo - d0), (int)(pend0[u] - d0));
+      int li = liu[u];
+      for (uint64_t pos = pend0[u]; pos < hi;) {  // further lines inside the chunk (short lines)
+        while (s_dst[li] + s_len[li] <= pos) ++li;
+        const uint64_t pend = s_dst[li] + s_len[li] < hi ? s_dst[li] + s_len[li] : hi;
+        const int64_t ad0 = (int64_t)s_src[li] - (int64_t)s_dst[li] + (int64_t)d0;
+        uint4 xa = make_uint4(0, 0, 0, 0), xb = xa;
+        if (ad0 >= 16) {
+          const uint4* wp = reinterpret_cast<const uint4*>(src + ((uint64_t)ad0 & ~15ull));
+          xa = wp[0];
+          xb = wp[1];
+        }
+        piece(o, ad0, xa, xb, (int)(pos - d0), (int)(pend - d0));
+        pos = pend;
+      }
+      if (lo == d0 && hi == d0 + 16) {
+        *reinterpret_cast<uint4*>(dst + d0) = make_uint4(o[0], o[1], o[2], o[3]);
+      } else {
+        for (uint64_t pos = lo; pos < hi; ++pos) {
+          const int b = (int)(pos - d0);
+          dst[pos] = (uint8_t)(o[b >> 2] >> (8 * (b & 3)));
+        }
       }
     }
   }
@@ -1702,14 +1749,20 @@ __global__ __launch_bounds__(kThreads) void k_cgather(RunArgs a) {
   const uint64_t W = a.wpre[a.nsegs];
   const uint32_t nblocks = a.counters[3], nchunks = a.counters[kCtrCopyChunks];
   for (uint32_t w = blockIdx.x; w < nchunks; w += gridDim.x) {
-    uint32_t lo = 0, hi = nblocks;  // the compaction block of copy chunk w
-    while (hi - lo > 1) {
-      const uint32_t mid = (lo + hi) >> 1;
-      if (a.csum[3 * mid + 2] <= w) lo = mid; else hi = mid;
+    uint32_t blk;  // the compaction block of copy chunk w (k_cscan's map; search past its end)
+    if (w < a.cmap_cap) {
+      blk = a.cmap[w];
+    } else {
+      uint32_t lo = 0, hi = nblocks;
+      while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (a.csum[3 * mid + 2] <= w) lo = mid; else hi = mid;
+      }
+      blk = lo;
     }
-    const uint32_t blk = lo, sub = w - (uint32_t)a.csum[3 * blk + 2];
+    const uint32_t sub = w - (uint32_t)a.csum[3 * blk + 2];
     WinLines r;
-    window_lines(a, (uint64_t)blk * kCompactLines + (uint64_t)t * 4, W, r);
+    window_lines(a, (uint64_t)blk * kCompactLines + (uint64_t)t * 4, W, r, a.cseg[blk]);
     const uint64_t ib = wave_incl_scan_add(r.bytes, lane);
     const uint64_t ic = wave_incl_scan_add((uint64_t)r.nsel, lane);
     __syncthreads();  // the previous chunk's copy is done with the LDS tables

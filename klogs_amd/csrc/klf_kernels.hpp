@@ -38,7 +38,7 @@ constexpr uint32_t kCtrHits = 8;                     // counters[8]: spilled pre
 constexpr uint32_t kCtrHitsOver = 9;                 // counters[9]: hit list overflow -> k_match
 constexpr uint32_t kCtrFlatHits = 12;                // counters[12]: hit slots flattened by k_tbase
 constexpr uint32_t kCtrCopyChunks = 11;              // counters[11]: output copy chunks (k_cgather)
-constexpr uint64_t kCopyChunk = 4 * 1024;            // output bytes per k_cgather work item
+constexpr uint64_t kCopyChunk = 64 * 1024;           // output bytes per k_cgather work item
 constexpr uint32_t kCtrVerified = 10;                // counters[10]: hits k_verify walked (diagnostics)
 constexpr uint32_t kQfRegex = 1u << 24;              // entry flags: regex factor (else literal)
 constexpr uint32_t kQfLoose = 1u << 25;              //   compare OR 0x20 per byte
@@ -159,6 +159,9 @@ struct RunArgs {
   uint64_t* mpart;      // [cap_lines / kMatchChunk + 1] matched-line partial per line chunk
   uint64_t* csum;       // [3 * (max compaction blocks + 1)] per-block (bytes, lines), then their
                         // prefixes and the prefix of copy chunks
+  uint32_t* cmap;       // [cmap_cap] compaction block of every copy chunk (k_cscan -> k_cgather)
+  uint64_t cmap_cap;
+  uint32_t* cseg;       // [max compaction blocks] stream of each block's first window line
   uint32_t* counters;   // [kNumCounters]: 1 compact ticket, 2 error flags, 3 compact blocks,
                         // 4 dense-tile pool
   uint64_t* line_off;   // [cap_lines + nsegs]
