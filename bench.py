@@ -24,6 +24,7 @@ import argparse
 import json
 import os
 import sys
+import tempfile
 import time
 from pathlib import Path
 
@@ -337,7 +338,22 @@ def run_extra(name: str, args, local: int, now: int) -> dict:
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     verified = None
-    if name == "c3" and not args.no_verify:  # first and last stream against the C oracle
+    write = None
+    wdir = None
+    if name == "c3":  # §8f-3 output write path: every stream into its own file (klf_result_write)
+        wdir = tempfile.TemporaryDirectory(prefix="klf_c3_")
+        paths = [os.path.join(wdir.name, f"pod{i // 4}__c{i % 4}.log") for i in range(len(lens))]
+        tw = time.perf_counter()
+        try:
+            wbytes = last.write_files(paths)
+        except E.KlfError as ex:  # e.g. no room for 6.9 GB in the temp dir: reported, not fatal
+            wbytes, write = None, {"error": str(ex), "dir": wdir.name}
+        wdt = time.perf_counter() - tw
+    if write is None and wdir is not None:
+        write = {"GBps": round(wbytes / wdt / 1e9, 2), "bytes": wbytes, "files": len(paths), "s": round(wdt, 3),
+                 "how": "klf_result_write: 64 MiB pinned D2H chunks, double-buffered, 8 writer threads each owning whole files (own HIP stream + 2x32 MiB pinned halves), "
+                        "into page-cache files under " + os.path.dirname(wdir.name)}
+    if name == "c3" and not args.no_verify and wbytes is not None:  # first and last stream vs the C oracle
         sys.path.insert(0, str(ROOT / "oracle"))
         import c_oracle as co
         verified = True
@@ -345,7 +361,11 @@ def run_extra(name: str, args, local: int, now: int) -> dict:
             h = np.empty(lens[i] + 1, dtype=np.uint8)
             synth.generate_into(h, kind, 42, i, sizes[i], permille=permille)
             want = co.filter_stream(h[:lens[i]], co.GO_ZERO_TIME, -1, [], want_lines=False, want_bits=False)[0]
-            verified = verified and last.stream(i).out == want
+            with open(paths[i], "rb") as f:  # the written file, i.e. the D2H + write path too
+                verified = verified and f.read() == want
+        write["verified_vs_c_oracle"] = bool(verified)
+    if wdir is not None:
+        wdir.cleanup()
     tot = last.totals()
     staged = eng.run_device(ptr, seg_base, lens, since=since, tail=tail, stage_times=True)
     stage = staged.timing()
@@ -368,6 +388,8 @@ def run_extra(name: str, args, local: int, now: int) -> dict:
     }
     if verified is not None:
         out["verified_vs_c_oracle"] = bool(verified)
+    if write is not None:
+        out["write_path"] = write
     last.free()
     eng.close()
     del dev

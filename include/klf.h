@@ -36,6 +36,7 @@ extern "C" {
 #define KLF_EPATTERN -4    /* a --match pattern is outside the supported RE2 subset     */
 #define KLF_ETOOBIG -5     /* pattern set exceeds engine limits                         */
 #define KLF_ESTATE -6      /* call out of order (e.g. stage after run without reset)    */
+#define KLF_EIO -7         /* write(2) to a stream's file failed (klf_result_write)       */
 
 /* ---- instants ------------------------------------------------------------------- */
 /* An absolute UTC instant: seconds since the Unix epoch + nanoseconds in [0, 1e9).
@@ -150,6 +151,18 @@ int klf_result_match_bits(klf_result* r, uint32_t stream_id, const uint8_t** bit
 /* Device views (no copy): the concatenated output and the stream's [off, len) in it. */
 int klf_result_device_out(klf_result* r, uint32_t stream_id, const uint8_t** d_out,
                           uint64_t* off, uint64_t* len);
+/* Output write path: appends every stream's selected bytes to its open
+ * file, fds[i] for stream i (fds[i] < 0 skips the stream), at the descriptor's current
+ * offset with write(2), as io.Copy(logFile, logs) does in writeLogToDisk
+ * (cmd/root.go:359-374).  The device output is copied D2H through 64 MiB pinned chunks,
+ * double-buffered (DMA of the next 32 MiB while the current one is written).  With 8 MiB
+ * or more of output and distinct descriptors, up to 8 worker threads (KLF_WRITE_THREADS
+ * overrides) each own whole streams, so files are written in parallel and each file still
+ * sees one in-order write(2) sequence; a descriptor shared by several streams gets them in
+ * stream order from one thread.  EINTR and short writes are retried.  n_fds must equal
+ * the stream count.  *written (optional) = bytes written over all streams.  KLF_EIO
+ * (klf_last_error names the stream and errno text) reports the first failing write. */
+int klf_result_write(klf_result* r, const int* fds, uint32_t n_fds, uint64_t* written);
 /* Per-stage device time of the run in ms, HIP events on the launch stream:
  * [0] scan stage (newline + line index + timestamp + since + fused grep prefilter),
  * [1] pattern verification / matchers, [2] counts + tail + window prefix, [3] compaction

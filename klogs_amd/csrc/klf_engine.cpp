@@ -3,12 +3,16 @@
 // multi-GPU split happens above, in the host, by stream sharding — DESIGN.md §5).
 #include <hip/hip_runtime.h>
 
+#include <unistd.h>
+
 #include <algorithm>
+#include <cerrno>
 #include <atomic>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
+#include <thread>
 #include <string>
 #include <vector>
 
@@ -124,6 +128,7 @@ extern "C" const char* klf_strerror(int code) {
     case KLF_EPATTERN: return "pattern outside the supported RE2 subset";
     case KLF_ETOOBIG: return "pattern set exceeds engine limits";
     case KLF_ESTATE: return "call out of order";
+    case KLF_EIO: return "write to a stream's file failed";
     default: return "unknown error";
   }
 }
@@ -694,6 +699,149 @@ extern "C" int klf_result_stream(klf_result* r, uint32_t id, const uint8_t** byt
   if (bytes) *bytes = r->out.data() + off;
   if (len) *len = n;
   fill_counts(r, s, n, counts);
+  return KLF_OK;
+}
+
+static bool write_all(int fd, const uint8_t* p, uint64_t n) {  // io.Copy's write loop
+  while (n) {
+    const ssize_t k = ::write(fd, p, (size_t)std::min<uint64_t>(n, 1u << 30));
+    if (k < 0) {
+      if (errno == EINTR) continue;
+      return false;
+    }
+    if (k == 0) {
+      errno = EIO;
+      return false;
+    }
+    p += k;
+    n -= (uint64_t)k;
+  }
+  return true;
+}
+
+// §8f-3: device output -> per-stream files.  The output is one buffer in stream order;
+// it crosses PCIe once, through 64 MiB pinned chunks taken from the staging pool, with
+// the DMA of the next piece in flight while the host writes the current one.
+//
+// A page-cache write(2) is a host memcpy under the file's inode lock (≈ 7 GB/s on one
+// core, measured), far below the pinned D2H, so with several streams each worker thread
+// owns whole streams (files), with its own HIP stream and pinned chunk: files are written
+// in parallel and each file still sees one sequential write(2) sequence.  One descriptor
+// shared by several streams must see them in stream order: that case (and small outputs)
+// runs on the calling thread alone.
+namespace {
+struct WPiece { uint64_t lo, hi; int fd; uint32_t id; };
+
+struct WErr { std::atomic<int> id{-1}; int err = 0; std::string what; std::mutex mu; };
+
+// D2H [lo, hi) of d_out in two halves of `buf` (double-buffered on `st`) and write(2) each
+// half to fd.  Returns false with `werr` set on the first failure.
+bool copy_piece(klf_engine* e, const uint8_t* d_out, const WPiece& q, uint8_t* buf, uint64_t half,
+                hipStream_t st, hipEvent_t ev[2], WErr& werr, uint64_t& total) {
+  auto fail = [&](int err, const std::string& what) {
+    int exp = -1;
+    if (werr.id.compare_exchange_strong(exp, (int)q.id)) { werr.err = err; werr.what = what; }
+    return false;
+  };
+  const uint64_t n = q.hi - q.lo, nk = (n + half - 1) / half;
+  auto issue = [&](uint64_t k) {
+    const uint64_t o = k * half, m = std::min(half, n - o);
+    return hipMemcpyAsync(buf + (k & 1) * half, d_out + q.lo + o, m, hipMemcpyDeviceToHost, st) == hipSuccess &&
+           hipEventRecord(ev[k & 1], st) == hipSuccess;
+  };
+  if (!issue(0)) return fail(0, "D2H");
+  for (uint64_t k = 0; k < nk; ++k) {
+    if (werr.id.load() >= 0) return false;  // another worker failed: stop early
+    if (k + 1 < nk && !issue(k + 1)) return fail(0, "D2H");
+    if (hipEventSynchronize(ev[k & 1]) != hipSuccess) return fail(0, "D2H sync");
+    const uint64_t o = k * half, m = std::min(half, n - o);
+    if (!write_all(q.fd, buf + (k & 1) * half, m)) return fail(errno, "write");
+    total += m;
+  }
+  (void)e;
+  return true;
+}
+}  // namespace
+
+extern "C" int klf_result_write(klf_result* r, const int* fds, uint32_t n_fds, uint64_t* written) {
+  if (written) *written = 0;
+  if (!r || (n_fds && !fds) || n_fds != r->n_streams) return KLF_EINVAL;
+  klf_engine* e = r->e;
+  if (e->gen != r->gen) return KLF_ESTATE;
+  std::vector<WPiece> pcs;
+  for (uint32_t i = 0; i < n_fds; ++i) {
+    const int64_t s = r->seg_of[i];
+    if (fds[i] < 0 || s < 0 || r->so[s].out_hi == r->so[s].out_lo) continue;
+    pcs.push_back({r->so[s].out_lo, r->so[s].out_hi, fds[i], i});
+  }
+  if (pcs.empty()) return KLF_OK;
+  std::sort(pcs.begin(), pcs.end(), [](const WPiece& a, const WPiece& b) { return a.lo < b.lo; });
+  uint64_t out_bytes = 0;
+  for (const auto& q : pcs) out_bytes += q.hi - q.lo;
+  auto eio = [&](const WErr& w) {
+    return set_err(e, KLF_EIO, "write stream " + std::to_string(w.id.load()) + ": " + w.what +
+                                   (w.err ? std::string(": ") + strerror(w.err) : std::string()));
+  };
+  if (r->have_out) {  // already on the host (klf_result_stream ran)
+    uint64_t total = 0;
+    for (const auto& q : pcs) {
+      if (!write_all(q.fd, r->out.data() + q.lo, q.hi - q.lo))
+        return set_err(e, KLF_EIO, "write stream " + std::to_string(q.id) + ": " + strerror(errno));
+      total += q.hi - q.lo;
+    }
+    if (written) *written = total;
+    return KLF_OK;
+  }
+  int nthr = 8;
+  if (const char* v = getenv("KLF_WRITE_THREADS")) nthr = std::max(1, atoi(v));
+  nthr = (int)std::min<size_t>((size_t)nthr, pcs.size());
+  {
+    std::vector<int> f;
+    for (const auto& q : pcs) f.push_back(q.fd);
+    std::sort(f.begin(), f.end());
+    if (std::adjacent_find(f.begin(), f.end()) != f.end()) nthr = 1;  // shared fd: stream order
+  }
+  if (out_bytes < (8u << 20)) nthr = 1;
+  HIPCHK(e, hipStreamSynchronize(e->stream), "sync before write");  // d_out complete
+  const uint8_t* d_out = e->d_out.as<uint8_t>();
+  WErr werr;
+  std::atomic<size_t> next{0};
+  std::vector<uint64_t> totals((size_t)nthr, 0);
+  std::atomic<int> setup_fail{0};
+  auto worker = [&](int t) {
+    klf_engine::StageChunk c;
+    hipStream_t st = nullptr;
+    hipEvent_t ev[2] = {nullptr, nullptr};
+    bool ok = hipSetDevice(e->device) == hipSuccess && take_chunk(e, &c) &&
+              hipStreamCreateWithFlags(&st, hipStreamNonBlocking) == hipSuccess &&
+              hipEventCreateWithFlags(&ev[0], hipEventDisableTiming) == hipSuccess &&
+              hipEventCreateWithFlags(&ev[1], hipEventDisableTiming) == hipSuccess;
+    if (!ok) {
+      setup_fail = 1;
+    } else {
+      for (size_t j; (j = next.fetch_add(1)) < pcs.size();)
+        if (!copy_piece(e, d_out, pcs[j], c.p, kStageChunk / 2, st, ev, werr, totals[(size_t)t])) break;
+    }
+    if (st) (void)hipStreamSynchronize(st);  // no DMA into a chunk handed back below
+    for (auto& x : ev)
+      if (x) (void)hipEventDestroy(x);
+    if (st) (void)hipStreamDestroy(st);
+    if (c.p) {
+      std::lock_guard<std::mutex> g(e->mu);
+      c.used = 0;
+      e->chunk_pool.push_back(c);
+    }
+  };
+  std::vector<std::thread> th;
+  for (int t = 1; t < nthr; ++t) th.emplace_back(worker, t);
+  worker(0);
+  for (auto& x : th) x.join();
+  if (setup_fail && werr.id.load() < 0 && next.load() < pcs.size())
+    return set_err(e, KLF_ENOMEM, "write worker setup (pinned chunk / HIP stream)");
+  if (werr.id.load() >= 0) return eio(werr);
+  uint64_t total = 0;
+  for (auto x : totals) total += x;
+  if (written) *written = total;
   return KLF_OK;
 }
 

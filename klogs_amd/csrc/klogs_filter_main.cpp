@@ -195,14 +195,17 @@ int main(int argc, char** argv) {
     klf_result* r = nullptr;
     rc = klf_run(e, &filter, &r);
     if (rc != KLF_OK) panic_exit(std::string("klf_run: ") + klf_strerror(rc) + ": " + klf_last_error(e));
-    for (uint32_t i = 0; i < n; ++i) {  // writeLogToDisk (:359-374), file closed afterwards
-      const uint8_t* p = nullptr;
-      uint64_t len = 0;
-      if (klf_result_stream(r, i, &p, &len, nullptr) != KLF_OK) panic_exit("klf_result_stream");
-      if (!len) continue;
-      FILE* f = std::fopen(files[i].c_str(), "wb");
-      if (!f || std::fwrite(p, 1, len, f) != len || std::fclose(f) != 0) panic_exit("write " + files[i]);
+    // writeLogToDisk (:359-374): one klf_result_write over every stream's file (chunked,
+    // double-buffered D2H from pinned memory), files closed afterwards
+    std::vector<int> fds(n, -1);
+    for (uint32_t i = 0; i < n; ++i) {
+      fds[i] = ::open(files[i].c_str(), O_WRONLY | O_TRUNC);
+      if (fds[i] < 0) panic_exit("open " + files[i]);
     }
+    rc = klf_result_write(r, fds.data(), n, nullptr);
+    if (rc != KLF_OK) panic_exit(std::string("klf_result_write: ") + klf_strerror(rc) + ": " + klf_last_error(e));
+    for (uint32_t i = 0; i < n; ++i)
+      if (::close(fds[i]) != 0) panic_exit("close " + files[i]);
     klf_result_free(r);
     klf_close(e);
   }

@@ -24,6 +24,7 @@ KLF_EHIP = -3
 KLF_EPATTERN = -4
 KLF_ETOOBIG = -5
 KLF_ESTATE = -6
+KLF_EIO = -7
 KLF_PAT_LITERAL = 0
 KLF_PAT_REGEX = 1
 GO_ZERO_TIME = (-62135596800, 0)
@@ -82,6 +83,7 @@ SIGNATURES = {
     "klf_result_match_bits": (C.c_int, [C.c_void_p, C.c_uint32, C.POINTER(C.c_void_p), C.POINTER(C.c_uint64)]),
     "klf_result_device_out": (C.c_int, [C.c_void_p, C.c_uint32, C.POINTER(C.c_void_p), C.POINTER(C.c_uint64),
                                         C.POINTER(C.c_uint64)]),
+    "klf_result_write": (C.c_int, [C.c_void_p, C.POINTER(C.c_int), C.c_uint32, C.POINTER(C.c_uint64)]),
     "klf_result_timing": (C.c_int, [C.c_void_p, C.POINTER(C.c_double), C.c_uint32, C.POINTER(C.c_uint32)]),
     "klf_result_totals": (C.c_int, [C.c_void_p, C.POINTER(_Counts)]),
     "klf_result_free": (None, [C.c_void_p]),
@@ -239,6 +241,26 @@ class Result:
         n = C.c_uint64()
         _check(_lib.klf_result_device_out(self._p, i, C.byref(p), C.byref(off), C.byref(n)))
         return p.value or 0, off.value, n.value
+
+    def write_fds(self, fds: Sequence[int]) -> int:
+        """klf_result_write: append stream i's selected bytes to fds[i] (< 0 skips it);
+        returns the bytes written.  writeLogToDisk (cmd/root.go:359-374)."""
+        arr = (C.c_int * len(fds))(*[int(f) for f in fds])
+        n = C.c_uint64()
+        _check(_lib.klf_result_write(self._p, arr, len(fds), C.byref(n)), self._eng._h)
+        return n.value
+
+    def write_files(self, paths: Sequence[Optional[str]]) -> int:
+        """Create (truncate) paths[i] and write stream i into it (None skips the stream)."""
+        fds = []
+        try:
+            for pth in paths:
+                fds.append(-1 if pth is None else os.open(pth, os.O_WRONLY | os.O_CREAT | os.O_TRUNC, 0o644))
+            return self.write_fds(fds)
+        finally:
+            for f in fds:
+                if f >= 0:
+                    os.close(f)
 
     def timing(self) -> List[float]:
         ms = (C.c_double * 7)()
