@@ -269,6 +269,9 @@ __device__ __forceinline__ bool parse_fast(const uint8_t* lds, uint32_t o, const
 #ifndef KLF_ABL
 #define KLF_ABL 0
 #endif
+#ifndef KLF_CG_NT
+#define KLF_CG_NT 0
+#endif
 #ifndef KLF_COPY_U
 #define KLF_COPY_U 1
 #endif
@@ -1719,7 +1722,13 @@ __device__ void block_gather_copy(const uint64_t* s_src, const uint64_t* s_dst, 
         pos = pend;
       }
       if (lo == d0 && hi == d0 + 16) {
+#if KLF_CG_NT  // streaming store (written once, never re-read by this kernel)
+        typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+        u32x4 v = {o[0], o[1], o[2], o[3]};
+        __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(dst + d0));
+#else
         *reinterpret_cast<uint4*>(dst + d0) = make_uint4(o[0], o[1], o[2], o[3]);
+#endif
       } else {
         for (uint64_t pos = lo; pos < hi; ++pos) {
           const int b = (int)(pos - d0);

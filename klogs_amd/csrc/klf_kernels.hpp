@@ -38,7 +38,10 @@ constexpr uint32_t kCtrHits = 8;                     // counters[8]: spilled pre
 constexpr uint32_t kCtrHitsOver = 9;                 // counters[9]: hit list overflow -> k_match
 constexpr uint32_t kCtrFlatHits = 12;                // counters[12]: hit slots flattened by k_tbase
 constexpr uint32_t kCtrCopyChunks = 11;              // counters[11]: output copy chunks (k_cgather)
-constexpr uint64_t kCopyChunk = 64 * 1024;           // output bytes per k_cgather work item
+#ifndef KLF_COPY_CHUNK_KB
+#define KLF_COPY_CHUNK_KB 128  // measured on C3: 64 KiB 7.75 ms, 128 KiB 7.25, 256 KiB 8.39
+#endif
+constexpr uint64_t kCopyChunk = KLF_COPY_CHUNK_KB * 1024;  // output bytes per k_cgather work item
 constexpr uint32_t kCtrVerified = 10;                // counters[10]: hits k_verify walked (diagnostics)
 constexpr uint32_t kQfRegex = 1u << 24;              // entry flags: regex factor (else literal)
 constexpr uint32_t kQfLoose = 1u << 25;              //   compare OR 0x20 per byte
