@@ -272,6 +272,9 @@ __device__ __forceinline__ bool parse_fast(const uint8_t* lds, uint32_t o, const
 #ifndef KLF_CG_NT
 #define KLF_CG_NT 0
 #endif
+#ifndef KLF_CG_GRID
+#define KLF_CG_GRID 8  // k_cgather workgroups per CU
+#endif
 #ifndef KLF_CG_PF2
 #define KLF_CG_PF2 1  // C3 compaction 7.12 -> 6.78 ms (U=2 on top: 7.81)
 #endif
@@ -1999,7 +2002,7 @@ static hipError_t launch_tail_stage(const RunArgs& a, hipStream_t st, hipEvent_t
   KLF_TRY(hipGetLastError());
   hipLaunchKernelGGL(k_cscan, dim3(1), dim3(256), 0, st, a);
   KLF_TRY(hipGetLastError());
-  hipLaunchKernelGGL(k_cgather, dim3(num_cus * 8), dim3(kThreads), 0, st, a);
+  hipLaunchKernelGGL(k_cgather, dim3(num_cus * KLF_CG_GRID), dim3(kThreads), 0, st, a);
   KLF_TRY(hipGetLastError());
 #undef KLF_TRY
   return hipSuccess;
