@@ -1570,8 +1570,11 @@ __device__ __forceinline__ void window_lines(const RunArgs& a, uint64_t w0, uint
   }
 }
 
+constexpr uint32_t kCsegBoundary = 0x80000000u;  // cseg flag: block holds a stream's first/last window line
+
 __global__ __launch_bounds__(kThreads) void k_csum(RunArgs a) {
   __shared__ uint64_t s_wb[4], s_wc[4];
+  __shared__ uint32_t s_wf[4];
   if (a.counters[2]) return;
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const uint64_t W = a.wpre[a.nsegs];
@@ -1579,20 +1582,24 @@ __global__ __launch_bounds__(kThreads) void k_csum(RunArgs a) {
   for (uint32_t blk = blockIdx.x; blk < nblocks; blk += gridDim.x) {
     WinLines r;
     window_lines(a, (uint64_t)blk * kCompactLines + (uint64_t)t * 4, W, r);
-    if (t == 0) a.cseg[blk] = r.seg[0];
     const uint64_t b = wave_sum(r.bytes), c = wave_sum((uint64_t)r.nsel);
+    // does the block hold a stream's first or last window line? (k_cgather records the
+    // stream's output range there, so such a block gets a copy chunk even with no bytes)
+    const bool bnd = __any(r.first[0] || r.first[1] || r.first[2] || r.first[3] || r.last[0] || r.last[1] ||
+                           r.last[2] || r.last[3]);
     __syncthreads();
-    if (lane == 0) { s_wb[wv] = b; s_wc[wv] = c; }
+    if (lane == 0) { s_wb[wv] = b; s_wc[wv] = c; s_wf[wv] = bnd ? 1u : 0u; }
     __syncthreads();
     if (t == 0) {
       a.csum[3 * blk] = s_wb[0] + s_wb[1] + s_wb[2] + s_wb[3];
       a.csum[3 * blk + 1] = s_wc[0] + s_wc[1] + s_wc[2] + s_wc[3];
+      a.cseg[blk] = r.seg[0] | ((s_wf[0] | s_wf[1] | s_wf[2] | s_wf[3]) ? kCsegBoundary : 0u);
     }
   }
 }
 
 // Exclusive prefixes of the block sums (bytes, lines) and of the copy chunks per block
-// (ceil(bytes / kCopyChunk), at least 1): long selected lines spread their copy over many
+// (ceil(bytes / kCopyChunk); 0 or 1 for an empty block): long selected lines spread their copy over many
 // workgroups instead of the one that owns their 1024-line block.
 __global__ __launch_bounds__(256) void k_cscan(RunArgs a) {
   __shared__ uint64_t s_wb[4], s_wc[4], s_wk[4];
@@ -1601,9 +1608,13 @@ __global__ __launch_bounds__(256) void k_cscan(RunArgs a) {
   const uint32_t nb = a.counters[3];
   const uint32_t per = (nb + 255) / 256;
   const uint32_t i0 = t * per, i1 = i0 + per < nb ? i0 + per : nb;
-  auto chunks = [](uint64_t bytes) -> uint64_t { return bytes ? (bytes + kCopyChunk - 1) / kCopyChunk : 1; };
+  // a block with no output bytes gets a chunk only when it holds a stream boundary (C2:
+  // hundreds of empty blocks in the --since window, two of them with work)
+  auto chunks = [&](uint64_t bytes, uint32_t i) -> uint64_t {
+    return bytes ? (bytes + kCopyChunk - 1) / kCopyChunk : ((a.cseg[i] & kCsegBoundary) ? 1 : 0);
+  };
   uint64_t b = 0, c = 0, k = 0;
-  for (uint32_t i = i0; i < i1; ++i) { b += a.csum[3 * i]; c += a.csum[3 * i + 1]; k += chunks(a.csum[3 * i]); }
+  for (uint32_t i = i0; i < i1; ++i) { b += a.csum[3 * i]; c += a.csum[3 * i + 1]; k += chunks(a.csum[3 * i], i); }
   const uint64_t ib = wave_incl_scan_add(b, lane), ic = wave_incl_scan_add(c, lane), ik = wave_incl_scan_add(k, lane);
   if (lane == 63) { s_wb[wv] = ib; s_wc[wv] = ic; s_wk[wv] = ik; }
   __syncthreads();
@@ -1614,7 +1625,7 @@ __global__ __launch_bounds__(256) void k_cscan(RunArgs a) {
     a.csum[3 * i] = pb;
     a.csum[3 * i + 1] = pc;
     a.csum[3 * i + 2] = pk;
-    const uint64_t nk = chunks(xb);
+    const uint64_t nk = chunks(xb, i);
     for (uint64_t k = 0; k < nk && pk + k < a.cmap_cap; ++k) a.cmap[pk + k] = i;  // chunk -> block
     pb += xb;
     pc += xc;
@@ -1793,7 +1804,7 @@ __global__ __launch_bounds__(kThreads) void k_cgather(RunArgs a) {
     }
     const uint32_t sub = w - (uint32_t)a.csum[3 * blk + 2];
     WinLines r;
-    window_lines(a, (uint64_t)blk * kCompactLines + (uint64_t)t * 4, W, r, a.cseg[blk]);
+    window_lines(a, (uint64_t)blk * kCompactLines + (uint64_t)t * 4, W, r, a.cseg[blk] & ~kCsegBoundary);
     const uint64_t ib = wave_incl_scan_add(r.bytes, lane);
     const uint64_t ic = wave_incl_scan_add((uint64_t)r.nsel, lane);
     __syncthreads();  // the previous chunk's copy is done with the LDS tables
