@@ -15,8 +15,10 @@
  * until the owning object is freed.
  *
  * Threading: klf_stage may be called concurrently for DIFFERENT stream ids (one
- * goroutine per container stream, cmd/root.go:249/:261); everything else is
- * single-caller per engine.
+ * goroutine per container stream, cmd/root.go:249/:261), with no other precondition (the
+ * stream table grows as needed); calls for one id are in order.  Everything else is
+ * single-caller per engine, and klf_run starts after every klf_stage has returned
+ * (wg.Wait(), cmd/root.go:470).
  */
 #ifndef KLF_H
 #define KLF_H
@@ -83,7 +85,10 @@ const char* klf_strerror(int code);
 /* ---- host staging path (what the cgo glue calls) -------------------------------- */
 /* Appends n bytes of stream `stream_id`'s body (chunks arrive in order).  Replaces the
  * io.Copy in writeLogToDisk (cmd/root.go:366).  Ids are dense, 0-based, caller-chosen
- * (the stream-table order of getPodLogs, cmd/root.go:240-262). */
+ * (the stream-table order of getPodLogs, cmd/root.go:240-262).  The bytes are copied into
+ * pinned host chunks (large pieces striped over a few copy threads; KLF_STAGE_THREADS)
+ * and every chunk that fills (64 MiB) is DMA'd to HBM at once, overlapping the capture.
+ * KLF_ESTATE after klf_run until klf_reset. */
 int klf_stage(klf_engine* e, uint32_t stream_id, const uint8_t* p, size_t n);
 /* Declares stream ids [0, n_streams) (streams never staged are empty). */
 int klf_set_streams(klf_engine* e, uint32_t n_streams);
@@ -148,6 +153,12 @@ int klf_result_lines(klf_result* r, uint32_t stream_id, const uint64_t** off,
  * Returns KLF_EINVAL when the engine has no patterns. */
 int klf_result_match_bits(klf_result* r, uint32_t stream_id, const uint8_t** bits,
                           uint64_t* nbytes);
+/* Position of the stream's last unparseable newline-terminated line, counted from the end
+ * over the newline-terminated lines (1 = the last one; 0 = every terminated line parses).
+ * The byte-range shards of one stream need it: kubelet emits the trailing
+ * fragment when the --tail window holds an unparseable line (SPEC.md S4), and that line
+ * may sit in an earlier shard.  Reads the latest run's line meta (KLF_ESTATE otherwise). */
+int klf_result_last_unparsed(klf_result* r, uint32_t stream_id, uint64_t* rank);
 /* Device views (no copy): the concatenated output and the stream's [off, len) in it. */
 int klf_result_device_out(klf_result* r, uint32_t stream_id, const uint8_t** d_out,
                           uint64_t* off, uint64_t* len);
@@ -176,19 +187,6 @@ void klf_result_free(klf_result* r);
 /* ---- host-side helpers mirroring cmd/root.go (no GPU needed) ---------------------- */
 /* Go time.Parse(time.RFC3339Nano, s) restated (SPEC.md S2); 0 = ok. */
 int klf_parse_rfc3339nano(const uint8_t* s, size_t n, klf_time* out);
-
-/* ---- test hooks (host only, no GPU): the compiled pattern tables run on the CPU ---- */
-/* Compiles `pats` and reports the matcher mode: 0 none, 1 never, 2 all, 3 single
- * literal (fused scan), 4 general (AC + Glushkov).  err receives the compile message. */
-int klf_debug_compile(const klf_pattern* pats, uint32_t n, uint32_t* mode, char* err, size_t err_cap);
-/* Runs the compiled tables (the exact recurrences the GPU matcher runs) on one content. */
-int klf_debug_match(const klf_pattern* pats, uint32_t n, const uint8_t* content, size_t len, int* match);
-/* The prefiltered path of general sets on one content, as the scan runs it: q-gram
- * samples at positions = phase (mod stride), bitmap + bucket verification, literal hits
- * final, regex factor hits -> Glushkov NFA.  info (nullable) = {prefilter on, q, stride,
- * needles}; when the prefilter is off *match is the full matcher's answer. */
-int klf_debug_prefilter(const klf_pattern* pats, uint32_t n, const uint8_t* content, size_t len,
-                        uint32_t phase, int* match, uint32_t* info);
 
 #ifdef __cplusplus
 }

@@ -41,7 +41,7 @@ def _run(cmd, quiet):
 def build_engine(force=False, quiet=True) -> Path:
     LIB.mkdir(parents=True, exist_ok=True)
     out = LIB / "libklf.so"
-    hdrs = [CSRC / h for h in ENGINE_HDRS] + [ROOT / "include" / "klf.h"]
+    hdrs = [CSRC / h for h in ENGINE_HDRS] + [ROOT / "include" / "klf.h", ROOT / "include" / "klf_debug.h"]
     objs = []
     for src in ENGINE_SRCS:
         s = CSRC / src

@@ -6,17 +6,21 @@
 #include <unistd.h>
 
 #include <algorithm>
-#include <cerrno>
 #include <atomic>
+#include <cerrno>
+#include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
+#include <memory>
 #include <mutex>
-#include <thread>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/klf.h"
+#include "../../include/klf_debug.h"
 #include "klf_kernels.hpp"
 #include "klf_patterns.hpp"
 #include "klf_ts.hpp"
@@ -48,6 +52,85 @@ struct DevBuf {
 
 uint64_t align_up(uint64_t x, uint64_t a) { return (x + a - 1) / a * a; }
 
+// Host copy workers for klf_stage: one large piece is striped over a few threads, so
+// staging one stream is not bound by a single core's memcpy into page-locked memory.
+// The caller copies a stripe itself and waits for the rest; several callers share the
+// workers (their stripes queue up).
+class CopyPool {
+ public:
+  explicit CopyPool(int workers) {
+    for (int i = 0; i < workers; ++i) th_.emplace_back([this] { loop(); });
+  }
+  ~CopyPool() {
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto& t : th_) t.join();
+  }
+  int workers() const { return (int)th_.size(); }
+  void copy(uint8_t* dst, const uint8_t* src, size_t n) {
+    constexpr size_t kMinStripe = 512u << 10;
+    const size_t parts = std::min<size_t>((size_t)workers() + 1, n / kMinStripe);
+    if (parts < 2) {
+      memcpy(dst, src, n);
+      return;
+    }
+    const size_t step = (n / parts + 4095) & ~(size_t)4095;
+    Job job;
+    job.left = 0;
+    size_t o = step;  // stripe 0 is the caller's
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      for (; o < n; o += step) {
+        q_.push_back({dst + o, src + o, std::min(step, n - o), &job});
+        ++job.left;
+      }
+    }
+    cv_.notify_all();
+    memcpy(dst, src, std::min(step, n));
+    std::unique_lock<std::mutex> g(job.mu);
+    job.cv.wait(g, [&] { return job.left == 0; });
+  }
+
+ private:
+  struct Job {
+    std::mutex mu;
+    std::condition_variable cv;
+    int left = 0;
+  };
+  struct Stripe {
+    uint8_t* dst;
+    const uint8_t* src;
+    size_t n;
+    Job* job;
+  };
+  void loop() {
+    for (;;) {
+      Stripe s;
+      {
+        std::unique_lock<std::mutex> g(mu_);
+        cv_.wait(g, [&] { return stop_ || !q_.empty(); });
+        if (q_.empty()) return;
+        s = q_.front();
+        q_.pop_front();
+      }
+      memcpy(s.dst, s.src, s.n);
+      {
+        std::lock_guard<std::mutex> g(s.job->mu);
+        --s.job->left;
+      }
+      s.job->cv.notify_all();
+    }
+  }
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::deque<Stripe> q_;
+  bool stop_ = false;
+  std::vector<std::thread> th_;
+};
+
 }  // namespace
 
 struct klf_engine {
@@ -58,9 +141,13 @@ struct klf_engine {
   klf::CompiledSet cs;
   std::string err;
   uint64_t gen = 0;
-  // staging (host path): per stream, a list of pinned host chunks (hipHostMalloc, reused
-  // across runs), so klf_run's H2D is DMA from page-locked memory at PCIe rate instead of
-  // a bounce through pageable buffers; pageable only where pinning fails (no device).
+  // Staging (host path).  Each stream fills a pinned host chunk
+  // (hipHostMalloc, pooled across runs); a chunk that fills is DMA'd at once on the copy
+  // stream into a pooled 64 MiB device chunk, so the H2D overlaps the rest of the capture.
+  // klf_run DMAs the partly filled last chunk of every stream straight into the batch and
+  // one kernel (k_assemble) moves the device chunks into their places in the batch.
+  // Per-stream records are heap objects that never move (klf_stage on different ids runs
+  // concurrently while the table grows).
   std::mutex mu;
   struct StageChunk {
     uint8_t* p = nullptr;
@@ -68,11 +155,25 @@ struct klf_engine {
     bool pinned = false;
   };
   struct StagedStream {
-    std::vector<StageChunk> chunks;
+    std::vector<uint8_t*> dchunks;  // full chunks already DMA'd (device, kStageChunk each)
+    StageChunk cur;                 // pinned chunk being filled (p = null: none)
     uint64_t len = 0;
   };
-  std::vector<StagedStream> staged;
-  std::vector<StageChunk> chunk_pool;  // free chunks (used = 0)
+  std::vector<std::unique_ptr<StagedStream>> staged;
+  std::vector<StageChunk> chunk_pool;  // free pinned chunks (used = 0)
+  std::vector<uint8_t*> dchunk_pool;   // free device chunks
+  struct Inflight {
+    StageChunk c;
+    hipEvent_t ev;
+  };
+  std::deque<Inflight> inflight;       // pinned chunks whose H2D may still be running
+  std::vector<hipEvent_t> ev_pool;
+  hipStream_t copy_stream = nullptr;   // early H2D of full chunks
+  hipEvent_t copy_done = nullptr;
+  bool ran = false;                    // klf_run since the last klf_reset (stage -> ESTATE)
+  std::unique_ptr<CopyPool> copier;
+  DevBuf d_asm;                        // k_assemble piece table
+  DevBuf d_scratch;                    // small query results (klf_result_last_unparsed)
   // device pattern tables
   DevBuf d_lit, d_ac_class, d_ac_next, d_ac_accept, d_rx_class, d_rx_b, d_rx_follow, d_rx_vec, d_rx_flags;
   DevBuf d_qf_bitmap, d_qf_head, d_qf_ent, d_qf_nbytes, d_cand, d_rx_vec4, d_qhits, d_hslots, d_hist, d_hflat;
@@ -84,7 +185,7 @@ struct klf_engine {
   DevBuf d_tile_seg;
   DevBuf d_cmap, d_cseg;
   DevBuf d_batch, d_segs, d_tstat, d_slots, d_pool, d_tile_base, d_bsum, d_cstatus, d_counters, d_line_off,
-      d_meta, d_bits, d_segout, d_wpre, d_out, d_mpart;
+      d_meta, d_bits, d_segout, d_wpre, d_out, d_mpart, d_tkeep, d_kbase;
   uint64_t pool_cap = 1 << 20;
   hipEvent_t ev[7] = {};
   klf::RunArgs last_args{};  // arguments of the latest completed run (klf_retail)
@@ -184,6 +285,16 @@ extern "C" int klf_open(const klf_config* cfg, klf_engine** out) {
     h = hipEventCreate(&x);
     if (h != hipSuccess) { e->err = "hipEventCreate failed"; *out = e; return KLF_EHIP; }
   }
+  if ((h = hipStreamCreateWithFlags(&e->copy_stream, hipStreamNonBlocking)) != hipSuccess ||
+      (h = hipEventCreateWithFlags(&e->copy_done, hipEventDisableTiming)) != hipSuccess) {
+    *out = e;
+    return hip_err(e, h, "copy stream");
+  }
+  {
+    int nw = 3;  // staging copy workers (+ the calling thread)
+    if (const char* v = getenv("KLF_STAGE_THREADS")) nw = std::max(0, std::min(atoi(v), 32));
+    e->copier.reset(new CopyPool(nw));
+  }
   // 3) pattern tables to the device
   const auto& cs = e->cs;
   hipStream_t st = e->stream;
@@ -261,7 +372,6 @@ extern "C" int klf_open(const klf_config* cfg, klf_engine** out) {
     e->cand_cap = (uint32_t)std::max(1L, std::min(atol(cc), 1L << 28));
   if (const char* hc = getenv("KLF_HITS_CAP"))  // tests: force the hit-list overflow fallback
     e->hits_cap_max = (uint64_t)std::max(1L, std::min(atol(hc), 1L << 28));
-  if (cfg->staging_hint) e->staged.reserve(16);
   *out = e;
   return KLF_OK;
 }
@@ -272,45 +382,96 @@ static void free_chunk(klf_engine::StageChunk& c);
 extern "C" void klf_close(klf_engine* e) {
   if (!e) return;
   if (e->stream) (void)hipStreamSynchronize(e->stream);
+  if (e->copy_stream) (void)hipStreamSynchronize(e->copy_stream);
   for (DevBuf* b : {&e->d_lit, &e->d_ac_class, &e->d_ac_next, &e->d_ac_accept, &e->d_rx_class, &e->d_rx_b,
                     &e->d_rx_follow, &e->d_rx_vec, &e->d_rx_flags, &e->d_qf_bitmap, &e->d_qf_head,
                     &e->d_qf_ent, &e->d_qf_nbytes, &e->d_rx_vec4, &e->d_qhits, &e->d_hslots, &e->d_hist, &e->d_hflat, &e->d_cand, &e->d_batch, &e->d_segs, &e->d_tstat,
                     &e->d_slots, &e->d_pool, &e->d_tile_base, &e->d_bsum, &e->d_cstatus, &e->d_counters, &e->d_cmap, &e->d_cseg,
-                    &e->d_line_off, &e->d_meta, &e->d_bits, &e->d_segout, &e->d_wpre, &e->d_out, &e->d_tile_seg, &e->d_mpart})
+                    &e->d_line_off, &e->d_meta, &e->d_bits, &e->d_segout, &e->d_wpre, &e->d_out, &e->d_tile_seg, &e->d_mpart, &e->d_tkeep, &e->d_kbase})
     b->release();
+  e->d_asm.release();
+  e->d_scratch.release();
+  e->copier.reset();
   {
     std::lock_guard<std::mutex> g(e->mu);
     release_staged(e);
     for (auto& c : e->chunk_pool) free_chunk(c);
     e->chunk_pool.clear();
+    for (uint8_t* d : e->dchunk_pool) (void)hipFree(d);
+    e->dchunk_pool.clear();
+    for (auto x : e->ev_pool) (void)hipEventDestroy(x);
+    e->ev_pool.clear();
   }
   for (auto& x : e->ev)
     if (x) (void)hipEventDestroy(x);
+  if (e->copy_done) (void)hipEventDestroy(e->copy_done);
+  if (e->copy_stream) (void)hipStreamDestroy(e->copy_stream);
   if (e->own_stream && e->stream) (void)hipStreamDestroy(e->stream);
   delete e;
 }
 
 // ------------------------------------------------------------------------ staging ---
 
+static constexpr size_t kStageChunk = 64u << 20;  // pinned staging chunk = device chunk
+static constexpr size_t kMaxInflight = 8;         // pinned chunks with an H2D in flight (512 MiB)
+
+static void grow_table(klf_engine* e, size_t n) {  // caller holds e->mu
+  while (e->staged.size() < n) e->staged.emplace_back(new klf_engine::StagedStream());
+}
+
 extern "C" int klf_set_streams(klf_engine* e, uint32_t n) {
   if (!e) return KLF_EINVAL;
   std::lock_guard<std::mutex> g(e->mu);
+  if (e->ran) return set_err(e, KLF_ESTATE, "klf_set_streams after klf_run: klf_reset first");
   if (n < e->staged.size()) return set_err(e, KLF_ESTATE, "cannot shrink the stream table; klf_reset first");
-  e->staged.resize(n);
+  try {
+    grow_table(e, n);
+  } catch (...) {
+    return set_err(e, KLF_ENOMEM, "stream table");
+  }
   return KLF_OK;
 }
 
-static constexpr size_t kStageChunk = 64u << 20;  // pinned staging chunk
+static void free_chunk(klf_engine::StageChunk& c) {
+  if (!c.p) return;
+  if (c.pinned) (void)hipHostFree(c.p);
+  else free(c.p);
+  c.p = nullptr;
+}
 
+// A free pinned chunk: the pool, else a chunk whose H2D has finished, else (with
+// kMaxInflight chunks in flight) the oldest one once its DMA is done, else a new one.
 static bool take_chunk(klf_engine* e, klf_engine::StageChunk* c) {
+  klf_engine::Inflight wait{};
+  bool have_wait = false;
   {
     std::lock_guard<std::mutex> g(e->mu);
+    while (!e->inflight.empty() && hipEventQuery(e->inflight.front().ev) == hipSuccess) {
+      e->chunk_pool.push_back(e->inflight.front().c);
+      e->ev_pool.push_back(e->inflight.front().ev);
+      e->inflight.pop_front();
+    }
     if (!e->chunk_pool.empty()) {
       *c = e->chunk_pool.back();
       e->chunk_pool.pop_back();
       c->used = 0;
       return true;
     }
+    if (e->inflight.size() >= kMaxInflight) {
+      wait = e->inflight.front();
+      e->inflight.pop_front();
+      have_wait = true;
+    }
+  }
+  if (have_wait) {
+    (void)hipEventSynchronize(wait.ev);
+    {
+      std::lock_guard<std::mutex> g(e->mu);
+      e->ev_pool.push_back(wait.ev);
+    }
+    *c = wait.c;
+    c->used = 0;
+    return true;
   }
   void* p = nullptr;
   if (hipHostMalloc(&p, kStageChunk, hipHostMallocDefault) == hipSuccess && p) {
@@ -326,11 +487,38 @@ static bool take_chunk(klf_engine* e, klf_engine::StageChunk* c) {
   return true;
 }
 
-static void free_chunk(klf_engine::StageChunk& c) {
-  if (!c.p) return;
-  if (c.pinned) (void)hipHostFree(c.p);
-  else free(c.p);
-  c.p = nullptr;
+// The stream's full pinned chunk -> a device chunk, DMA'd now on the copy stream (the
+// capture keeps running meanwhile); the pinned chunk returns to the pool when the DMA ends.
+static int ship_chunk(klf_engine* e, klf_engine::StagedStream* s) {
+  uint8_t* d = nullptr;
+  hipEvent_t ev = nullptr;
+  {
+    std::lock_guard<std::mutex> g(e->mu);
+    if (!e->dchunk_pool.empty()) {
+      d = e->dchunk_pool.back();
+      e->dchunk_pool.pop_back();
+    }
+    if (!e->ev_pool.empty()) {
+      ev = e->ev_pool.back();
+      e->ev_pool.pop_back();
+    }
+  }
+  hipError_t h = hipSuccess;
+  if (!d) h = hipMalloc(reinterpret_cast<void**>(&d), kStageChunk);
+  if (h != hipSuccess) return hip_err(e, h, "device staging chunk");
+  if (!ev) h = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+  if (h == hipSuccess) h = hipMemcpyAsync(d, s->cur.p, kStageChunk, hipMemcpyHostToDevice, e->copy_stream);
+  if (h == hipSuccess) h = hipEventRecord(ev, e->copy_stream);
+  std::lock_guard<std::mutex> g(e->mu);
+  if (h != hipSuccess) {
+    e->dchunk_pool.push_back(d);
+    if (ev) e->ev_pool.push_back(ev);
+    return hip_err(e, h, "early H2D");
+  }
+  s->dchunks.push_back(d);
+  e->inflight.push_back({s->cur, ev});
+  s->cur = klf_engine::StageChunk{};
+  return KLF_OK;
 }
 
 extern "C" int klf_stage(klf_engine* e, uint32_t id, const uint8_t* p, size_t n) {
@@ -338,45 +526,52 @@ extern "C" int klf_stage(klf_engine* e, uint32_t id, const uint8_t* p, size_t n)
   klf_engine::StagedStream* dst;
   {
     std::lock_guard<std::mutex> g(e->mu);
-    if (id >= e->staged.size()) e->staged.resize((size_t)id + 1);
-    dst = &e->staged[id];
-  }
-  // different ids never share a stream record; the outer vector only grows under the
-  // lock and callers declare the table with klf_set_streams before staging concurrently.
-  while (n) {
-    if (dst->chunks.empty() || dst->chunks.back().used == kStageChunk) {
-      klf_engine::StageChunk c;
-      if (!take_chunk(e, &c)) return KLF_ENOMEM;
-      try {
-        dst->chunks.push_back(c);
-      } catch (...) {
-        free_chunk(c);
-        return KLF_ENOMEM;
-      }
+    if (e->ran) return set_err(e, KLF_ESTATE, "klf_stage after klf_run: klf_reset first");
+    try {
+      grow_table(e, (size_t)id + 1);
+    } catch (...) {
+      return set_err(e, KLF_ENOMEM, "stream table");
     }
-    auto& c = dst->chunks.back();
-    const size_t k = std::min(n, kStageChunk - c.used);
-    memcpy(c.p + c.used, p, k);
-    c.used += k;
+    dst = e->staged[id].get();  // stable: the table holds pointers, only the table moves
+  }
+  while (n) {
+    if (!dst->cur.p && !take_chunk(e, &dst->cur)) return set_err(e, KLF_ENOMEM, "pinned staging chunk");
+    const size_t k = std::min(n, kStageChunk - dst->cur.used);
+    e->copier->copy(dst->cur.p + dst->cur.used, p, k);
+    dst->cur.used += k;
     dst->len += k;
     p += k;
     n -= k;
+    if (dst->cur.used == kStageChunk) {
+      const int rc = ship_chunk(e, dst);
+      if (rc) return rc;
+    }
   }
   return KLF_OK;
 }
 
-static void release_staged(klf_engine* e) {  // caller holds e->mu
-  for (auto& s : e->staged)
-    for (auto& c : s.chunks) {
-      c.used = 0;
-      e->chunk_pool.push_back(c);
+static void release_staged(klf_engine* e) {  // caller holds e->mu; no H2D may be in flight
+  for (auto& s : e->staged) {
+    for (uint8_t* d : s->dchunks) e->dchunk_pool.push_back(d);
+    if (s->cur.p) {
+      s->cur.used = 0;
+      e->chunk_pool.push_back(s->cur);
     }
+  }
+  for (auto& f : e->inflight) {
+    e->chunk_pool.push_back(f.c);
+    e->ev_pool.push_back(f.ev);
+  }
+  e->inflight.clear();
   e->staged.clear();
+  e->ran = false;
 }
 
 extern "C" int klf_reset(klf_engine* e) {
   if (!e) return KLF_EINVAL;
   std::lock_guard<std::mutex> g(e->mu);
+  (void)hipStreamSynchronize(e->copy_stream);  // early DMAs read the pinned chunks
+  (void)hipStreamSynchronize(e->stream);       // k_assemble reads the device chunks
   release_staged(e);
   return KLF_OK;
 }
@@ -402,7 +597,8 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
   if (reinterpret_cast<uintptr_t>(d_bytes) % 16) return set_err(e, KLF_EINVAL, "device bytes must be 16-B aligned");
   *out = nullptr;
   HIPCHK(e, hipSetDevice(e->device), "hipSetDevice");
-  auto* r = new (std::nothrow) klf_result();
+  std::unique_ptr<klf_result> rp(new (std::nothrow) klf_result());  // freed on every error return
+  klf_result* r = rp.get();
   if (!r) return KLF_ENOMEM;
   r->e = e;
   r->gen = ++e->gen;
@@ -415,7 +611,7 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
   uint64_t total_bytes = 0, ntiles = 0, cap = 0;
   for (uint32_t i = 0; i < n_streams; ++i) {
     if (!lens[i]) continue;
-    if (seg_base[i] % klf::kSegAlign) { delete r; return set_err(e, KLF_EINVAL, "seg_base must be 256-B aligned"); }
+    if (seg_base[i] % klf::kSegAlign) return set_err(e, KLF_EINVAL, "seg_base must be 256-B aligned");
     SegDesc d;
     d.base = seg_base[i];
     d.len = lens[i];
@@ -428,9 +624,13 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
     total_bytes += lens[i];
     cap += lens[i] / 32 + 2;  // kubelet lines carry a >= 31-byte prefix; overflow -> exact rerun
   }
-  if (ntiles >= (1ull << 32)) { delete r; return set_err(e, KLF_EINVAL, "batch too large"); }
+  if (ntiles >= (1ull << 32)) return set_err(e, KLF_EINVAL, "batch too large");
   const uint32_t nsegs = (uint32_t)segs.size();
-  if (nsegs == 0) { e->last_gen = r->gen; *out = r; return KLF_OK; }
+  if (nsegs == 0) { e->last_gen = r->gen; *out = rp.release(); return KLF_OK; }
+  // tests: a line capacity clamped on every attempt forces the overflow error below
+  uint64_t cap_clamp = ~0ull;
+  if (const char* v = getenv("KLF_DEBUG_CAP_CLAMP")) cap_clamp = std::max(1L, atol(v));
+  cap = std::min(cap, cap_clamp);
 
   hipStream_t st = e->stream;
   bool same_layout = segs.size() == e->last_segs.size() && e->d_tile_seg.cap >= ntiles * 4 &&
@@ -476,6 +676,10 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
   HIPCHK(e, e->d_segout.ensure(nsegs * sizeof(SegOut)), "alloc segout");
   HIPCHK(e, e->d_wpre.ensure((nsegs + 1) * 8), "alloc wpre");
   HIPCHK(e, e->d_out.ensure(total_bytes + 64), "alloc out");
+  HIPCHK(e, e->d_tkeep.ensure(ntiles * 8), "alloc tkeep");
+  HIPCHK(e, e->d_kbase.ensure(ntiles * 16), "alloc kbase");
+  uint32_t compact_mode = 0;  // tests: force either compaction path
+  if (const char* v = getenv("KLF_COMPACT")) compact_mode = !strcmp(v, "sparse") ? 1u : !strcmp(v, "dense") ? 2u : 0u;
   const bool need_cand = mode == klf::CompiledSet::kGeneral && e->cs.qf_on && e->cs.rx_count;
   if (need_cand) HIPCHK(e, e->d_cand.ensure((size_t)e->cand_cap * 8), "alloc cand");
   const bool need_hits = mode == klf::CompiledSet::kGeneral && e->cs.qf_on;
@@ -492,6 +696,7 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
     HIPCHK(e, e->d_hflat.ensure((size_t)hflat_cap * 4), "alloc hflat");
   }
 
+  bool overflow = false;
   for (int attempt = 0; attempt < 2; ++attempt) {
     const uint64_t max_cblocks = cap / klf::kCompactLines + 2;
     HIPCHK(e, e->d_line_off.ensure((cap + nsegs + 1) * 8), "alloc line_off");
@@ -556,6 +761,9 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
     a.hflat = need_hits ? e->d_hflat.as<uint32_t>() : nullptr;
     a.hflat_cap = need_hits ? hflat_cap : 0;
     a.qhits_cap = need_hits ? qhits_cap : 0;
+    a.tkeep = e->d_tkeep.as<uint2>();
+    a.kbase = e->d_kbase.as<uint64_t>();
+    a.compact_mode = compact_mode;
     HIPCHK(e, klf::launch_pipeline(a, st, e->ev, e->num_cus), "launch");
     r->so.resize(nsegs);
     uint32_t counters[16];
@@ -567,8 +775,9 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
       fprintf(stderr, "[klf] hits=%u spilled=%u hits_over=%u nfa_queue=%u queue_over=%u deferred=%u\n",
               counters[klf::kCtrVerified], counters[klf::kCtrHits], counters[klf::kCtrHitsOver],
               counters[klf::kCtrQueue], counters[klf::kCtrQOver], counters[5]);
-    if (counters[2] & 1u) {  // more lines (or dense-tile slots) than estimated: rerun with exact sizes
-      cap = std::max<uint64_t>(cap, r->so[nsegs - 1].line_hi + 2);
+    overflow = (counters[2] & 1u) != 0;
+    if (overflow) {  // more lines (or dense-tile slots) than estimated: rerun with exact sizes
+      cap = std::min(std::max<uint64_t>(cap, r->so[nsegs - 1].line_hi + 2), cap_clamp);
       e->pool_cap = std::max<uint64_t>(e->pool_cap, (uint64_t)counters[klf::kCtrPool] + 1024);
       continue;
     }
@@ -576,6 +785,8 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
     e->last_gen = r->gen;
     break;
   }
+  if (overflow)  // the exact rerun overflowed too: never hand out the aborted run's records
+    return set_err(e, KLF_ENOMEM, "line index / dense-tile pool overflow after the exact rerun");
   if (const char* path = getenv("KLF_TIMELINE_OUT")) {  // diagnostic builds only
     std::vector<uint64_t> tl(300000 * 8);
     if (klf::dump_timeline(tl.data(), tl.size() * 8) == hipSuccess) {
@@ -595,7 +806,7 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
   if (hipEventElapsedTime(&ms, e->ev[1], e->ev[6]) == hipSuccess) r->ms[6] = ms;
   r->total_lines = r->so[nsegs - 1].line_hi;
   for (auto& s : r->so) r->total_out = std::max(r->total_out, s.out_hi);
-  *out = r;
+  *out = rp.release();
   return KLF_OK;
 }
 
@@ -644,19 +855,37 @@ extern "C" int klf_run(klf_engine* e, const klf_filter* f, klf_result** out) {
   std::lock_guard<std::mutex> g(e->mu);
   const uint32_t n = (uint32_t)e->staged.size();
   std::vector<uint64_t> lens(n), base(n);
-  for (uint32_t i = 0; i < n; ++i) lens[i] = e->staged[i].len;
+  for (uint32_t i = 0; i < n; ++i) lens[i] = e->staged[i]->len;
   uint64_t total = 0;
   klf_layout(n, lens.data(), base.data(), &total);
   HIPCHK(e, e->d_batch.ensure(total), "alloc batch");
-  for (uint32_t i = 0; i < n; ++i) {  // DMA from the pinned chunks, all queued back to back
+  uint8_t* batch = e->d_batch.as<uint8_t>();
+  std::vector<klf::AsmPiece> pieces;
+  for (uint32_t i = 0; i < n; ++i) {
     uint64_t off = base[i];
-    for (const auto& c : e->staged[i].chunks) {
-      HIPCHK(e, hipMemcpyAsync(e->d_batch.as<uint8_t>() + off, c.p, c.used, hipMemcpyHostToDevice, e->stream),
-             "H2D stream");
-      off += c.used;
+    for (uint8_t* d : e->staged[i]->dchunks) {
+      pieces.push_back({d, off, kStageChunk});
+      off += kStageChunk;
     }
   }
-  return run_device_impl(e, e->d_batch.as<uint8_t>(), n, base.data(), lens.data(), f, out);
+  if (!pieces.empty()) HIPCHK(e, upload(e->d_asm, pieces, e->stream), "upload pieces");
+  // early DMAs done -> k_assemble moves the device chunks into place, while the copy
+  // stream DMAs every stream's partly filled last chunk straight to its place
+  HIPCHK(e, hipEventRecord(e->copy_done, e->copy_stream), "record copy");
+  HIPCHK(e, hipStreamWaitEvent(e->stream, e->copy_done, 0), "wait copy");
+  if (!pieces.empty())
+    HIPCHK(e, klf::launch_assemble(e->d_asm.as<klf::AsmPiece>(), (uint32_t)pieces.size(), batch, e->stream),
+           "assemble");
+  for (uint32_t i = 0; i < n; ++i) {
+    const auto& s = *e->staged[i];
+    if (s.cur.p && s.cur.used)
+      HIPCHK(e, hipMemcpyAsync(batch + base[i] + s.dchunks.size() * kStageChunk, s.cur.p, s.cur.used,
+                               hipMemcpyHostToDevice, e->copy_stream), "H2D tail");
+  }
+  HIPCHK(e, hipEventRecord(e->copy_done, e->copy_stream), "record tail");
+  HIPCHK(e, hipStreamWaitEvent(e->stream, e->copy_done, 0), "wait tail");
+  e->ran = true;
+  return run_device_impl(e, batch, n, base.data(), lens.data(), f, out);
 }
 
 // ---------------------------------------------------------------------- results ---
@@ -899,6 +1128,26 @@ extern "C" int klf_result_match_bits(klf_result* r, uint32_t id, const uint8_t**
   }
   if (bits) *bits = r->stream_bits[id].data();
   if (nbytes) *nbytes = r->stream_bits[id].size();
+  return KLF_OK;
+}
+
+extern "C" int klf_result_last_unparsed(klf_result* r, uint32_t id, uint64_t* rank) {
+  int rc = check_result(r, id);
+  if (rc) return rc;
+  if (!rank) return KLF_EINVAL;
+  *rank = 0;
+  const int64_t s = r->seg_of[id];
+  if (s < 0) return KLF_OK;
+  klf_engine* e = r->e;
+  const SegOut& so = r->so[s];
+  const uint64_t hi = so.line_hi - (so.frag ? 1 : 0);  // newline-terminated lines only
+  if (hi <= so.line_lo) return KLF_OK;
+  HIPCHK(e, e->d_scratch.ensure(64), "alloc scratch");
+  uint64_t v = 0;
+  HIPCHK(e, klf::launch_lastbad(e->last_args, so.line_lo, hi, e->d_scratch.as<uint64_t>(), e->stream), "lastbad");
+  HIPCHK(e, hipMemcpyAsync(&v, e->d_scratch.p, 8, hipMemcpyDeviceToHost, e->stream), "D2H lastbad");
+  HIPCHK(e, hipStreamSynchronize(e->stream), "sync");
+  if (v) *rank = hi - (v - 1);
   return KLF_OK;
 }
 

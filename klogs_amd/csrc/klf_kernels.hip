@@ -1488,9 +1488,24 @@ __global__ __launch_bounds__(256) void k_wprefix(RunArgs a) {
   }
   const uint64_t nb0 = (carry + kCompactLines - 1) / kCompactLines;
   const uint32_t nb = (uint32_t)(nb0 < a.max_cblocks ? nb0 : a.max_cblocks);
+  // Compaction path: tile copy (k_tkeep / k_tcopy) when at least a quarter of the lines
+  // can be selected (every window line that is since_ok and matching at most), else the
+  // line gather (k_csum / k_cscan / k_cgather), which touches only the selected lines.
+  uint64_t est = 0;
+  for (uint32_t s = t; s < a.nsegs; s += 256) {
+    const SegOut& so = a.segout[s];
+    uint64_t w = so.win_hi - so.win_lo;
+    w = w < so.since_ok ? w : so.since_ok;
+    if (a.grep_mode != kGrepNone) w = w < so.matched ? w : so.matched;
+    est += w;
+  }
+  est = block_sum_u64(est, s_w64);
+  const uint64_t L = a.segout[a.nsegs - 1].line_hi;
+  const bool dense = a.compact_mode == 2 || (a.compact_mode == 0 && L > 0 && est * 4 >= L);
   if (t == 0) {
     a.wpre[a.nsegs] = carry;
     a.counters[3] = nb;
+    a.counters[kCtrDense] = dense ? 1u : 0u;
   }
 }
 
@@ -1575,7 +1590,7 @@ constexpr uint32_t kCsegBoundary = 0x80000000u;  // cseg flag: block holds a str
 __global__ __launch_bounds__(kThreads) void k_csum(RunArgs a) {
   __shared__ uint64_t s_wb[4], s_wc[4];
   __shared__ uint32_t s_wf[4];
-  if (a.counters[2]) return;
+  if (a.counters[2] || a.counters[kCtrDense]) return;
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const uint64_t W = a.wpre[a.nsegs];
   const uint32_t nblocks = a.counters[3];
@@ -1603,7 +1618,7 @@ __global__ __launch_bounds__(kThreads) void k_csum(RunArgs a) {
 // workgroups instead of the one that owns their 1024-line block.
 __global__ __launch_bounds__(256) void k_cscan(RunArgs a) {
   __shared__ uint64_t s_wb[4], s_wc[4], s_wk[4];
-  if (a.counters[2]) return;
+  if (a.counters[2] || a.counters[kCtrDense]) return;
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const uint32_t nb = a.counters[3];
   const uint32_t per = (nb + 255) / 256;
@@ -1787,7 +1802,7 @@ __global__ __launch_bounds__(kThreads) void k_cgather(RunArgs a) {
   __shared__ uint16_t s_map[kCopyChunk / 16 + 1];
   __shared__ uint64_t s_wb[4], s_wc[4];
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
-  if (a.counters[2]) return;
+  if (a.counters[2] || a.counters[kCtrDense]) return;
   const uint64_t W = a.wpre[a.nsegs];
   const uint32_t nblocks = a.counters[3], nchunks = a.counters[kCtrCopyChunks];
   for (uint32_t w = blockIdx.x; w < nchunks; w += gridDim.x) {
@@ -1848,6 +1863,239 @@ __global__ __launch_bounds__(kThreads) void k_cgather(RunArgs a) {
   }
 }
 
+
+// ============================================ K4': dense compaction (tile copy) ==
+// When most lines are selected (e.g. C3: -l only, every line out) the output is the input
+// minus the timestamp prefixes: a byte compaction.  It runs over the scan's 8 KiB tiles:
+//   k_tkeep   wave per tile: the tile's lines (tile_base .. + events) -> kept content bytes
+//             inside the tile and selected lines starting in it
+//   k_ksum / k_kbase   reduce-then-scan of those -> each tile's output / selected-line
+//             offsets, stream output ranges at the streams' first / last tiles
+//   k_tcopy   wave per tile with kept bytes: the tile is loaded into LDS with coalesced
+//             16-B loads, its kept runs are listed, and every 16-B output chunk of the
+//             tile's output range is assembled from LDS (any alignment: five dword reads +
+//             v_alignbyte) and stored with one 16-B store (coalesced across the wave); only
+//             the two chunks shared with the neighbouring tiles are stored bytewise.
+// Input read once, output written once, the line index read twice.
+struct TileLines {
+  uint32_t s;
+  SegDesc sd;
+  int64_t rel_lo;  // tile start, stream-relative
+  int32_t tlen;    // bytes of the stream in the tile
+  uint64_t l0;     // global index of the tile's first line (the one holding its byte 0)
+  uint32_t nl;     // lines holding bytes of the tile
+};
+__device__ __forceinline__ TileLines tile_lines(const RunArgs& a, uint32_t tile) {
+  TileLines g;
+  g.s = a.tile_seg[tile];
+  g.sd = a.segs[g.s];
+  g.rel_lo = (int64_t)(tile - g.sd.tile0) * kTile;
+  const int64_t rem = (int64_t)g.sd.len - g.rel_lo;
+  g.tlen = (int32_t)(rem < kTile ? rem : kTile);
+  const TileStat ts = a.tstat[tile];
+  g.l0 = a.tile_base[tile];
+  g.nl = rem <= kTile ? ts.events : ts.events + 1;  // the stream's end closes the last line
+  return g;
+}
+
+// Line l of tile g: is it selected, and its kept run [lo, hi) (stream offsets) in the tile.
+__device__ __forceinline__ bool line_run(const RunArgs& a, const TileLines& g, uint64_t wlo, uint64_t whi,
+                                         uint64_t l, int64_t& lo, int64_t& hi, int64_t& ls) {
+  if (l < wlo || l >= whi) return false;
+  const uint16_t m = a.meta[l];
+  if (!((m & Meta::kParsed) && (m & Meta::kSince) && gbit(a, l))) return false;
+  const uint64_t s0 = a.line_off[l + g.s], le = a.line_off[l + g.s + 1];
+  const uint64_t cs = s0 + line_plen(a, m, a.bytes + g.sd.base, s0, le);
+  ls = (int64_t)s0;
+  lo = (int64_t)cs > g.rel_lo ? (int64_t)cs : g.rel_lo;
+  hi = (int64_t)le < g.rel_lo + g.tlen ? (int64_t)le : g.rel_lo + g.tlen;
+  return true;
+}
+
+__global__ __launch_bounds__(256) void k_tkeep(RunArgs a) {
+  if (a.counters[2] || !a.counters[kCtrDense]) return;
+  const int lane = threadIdx.x & 63;
+  const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  for (uint32_t tile = blockIdx.x * 4 + wv; tile < a.ntiles; tile += gridDim.x * 4) {
+    const TileLines g = tile_lines(a, tile);
+    const uint64_t wlo = a.segout[g.s].win_lo, whi = a.segout[g.s].win_hi;
+    uint32_t kb = 0, kl = 0;
+    for (uint32_t j = lane; j < g.nl; j += 64) {
+      int64_t lo, hi, ls;
+      if (!line_run(a, g, wlo, whi, g.l0 + j, lo, hi, ls)) continue;
+      kb += hi > lo ? (uint32_t)(hi - lo) : 0u;
+      kl += (ls >= g.rel_lo && ls < g.rel_lo + g.tlen) ? 1u : 0u;
+    }
+    kb = wave_sum(kb);
+    kl = wave_sum(kl);
+    if (lane == 0) a.tkeep[tile] = make_uint2(kb, kl);
+  }
+}
+
+// Reduce-then-scan of the tiles' (kept bytes, selected lines): 256 x R tiles per block.
+template <int R>
+__global__ __launch_bounds__(256) void k_ksum(RunArgs a) {
+  __shared__ uint64_t s_w[2][4];
+  if (a.counters[2] || !a.counters[kCtrDense]) return;
+  const uint32_t t0 = blockIdx.x * (256 * R) + threadIdx.x;
+  uint64_t b = 0, c = 0;
+#pragma unroll
+  for (int r = 0; r < R; ++r)
+    if (t0 + r * 256 < a.ntiles) {
+      const uint2 k = a.tkeep[t0 + r * 256];
+      b += k.x;
+      c += k.y;
+    }
+  b = wave_sum(b);
+  c = wave_sum(c);
+  if ((threadIdx.x & 63) == 0) { s_w[0][threadIdx.x >> 6] = b; s_w[1][threadIdx.x >> 6] = c; }
+  __syncthreads();
+  if (threadIdx.x < 2) {
+    const int k = threadIdx.x;
+    a.bsum[2 * blockIdx.x + k] = s_w[k][0] + s_w[k][1] + s_w[k][2] + s_w[k][3];
+  }
+}
+
+template <int R>
+__global__ __launch_bounds__(256) void k_kbase(RunArgs a) {
+  __shared__ uint64_t s_w[2][2][4];
+  __shared__ uint64_t s_base[2];
+  if (a.counters[2] || !a.counters[kCtrDense]) return;
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const uint32_t t0 = blockIdx.x * (256 * R) + t;
+  {
+    uint64_t b = 0, c = 0;
+    for (uint32_t k = t; k < blockIdx.x; k += 256) { b += a.bsum[2 * k]; c += a.bsum[2 * k + 1]; }
+    b = wave_sum(b);
+    c = wave_sum(c);
+    if (lane == 0) { s_w[0][0][wv] = b; s_w[0][1][wv] = c; }
+    __syncthreads();
+    if (t < 2) s_base[t] = s_w[0][t][0] + s_w[0][t][1] + s_w[0][t][2] + s_w[0][t][3];
+    __syncthreads();
+  }
+  uint64_t cb = s_base[0], cc = s_base[1];
+  for (int r = 0; r < R; ++r) {
+    const uint32_t tile = t0 + r * 256;
+    uint2 k = make_uint2(0, 0);
+    if (tile < a.ntiles) k = a.tkeep[tile];
+    const uint64_t ib = wave_incl_scan_add((uint64_t)k.x, lane), ic = wave_incl_scan_add((uint64_t)k.y, lane);
+    const int pb = r & 1;
+    if (lane == 63) { s_w[pb][0][wv] = ib; s_w[pb][1][wv] = ic; }
+    __syncthreads();
+    uint64_t ob = cb + ib - k.x, oc = cc + ic - k.y;
+    for (int w = 0; w < wv; ++w) { ob += s_w[pb][0][w]; oc += s_w[pb][1][w]; }
+    cb += s_w[pb][0][0] + s_w[pb][0][1] + s_w[pb][0][2] + s_w[pb][0][3];
+    cc += s_w[pb][1][0] + s_w[pb][1][1] + s_w[pb][1][2] + s_w[pb][1][3];
+    if (tile < a.ntiles) {
+      a.kbase[2 * tile] = ob;
+      a.kbase[2 * tile + 1] = oc;
+      const uint32_t s = a.tile_seg[tile];
+      const SegDesc& sd = a.segs[s];
+      if (tile == sd.tile0) { a.segout[s].out_lo = ob; a.segout[s].sel_lo = oc; }
+      if (tile + 1 == sd.tile0 + sd.ntiles) { a.segout[s].out_hi = ob + k.x; a.segout[s].sel_hi = oc + k.y; }
+    }
+  }
+}
+
+// LDS per wave: the tile (16 B of front pad, 8 KiB, 32 B of back pad: the unaligned reads of
+// a piece start up to 15 B before its chunk and end up to 20 B after it), the kept runs
+// (src | dst << 16, tile-relative; a selected line carries a >= 20-B prefix, so at most
+// kTile / 20 + 2 runs), and the chunk -> first run map.
+constexpr int kTcRuns = kTile / 20 + 4;
+constexpr int kTcChunks = kTile / 16 + 2;
+__global__ __launch_bounds__(256) void k_tcopy(RunArgs a) {
+  __shared__ __attribute__((aligned(16))) uint8_t s_buf_all[4][kTile + 48];
+  __shared__ uint32_t s_run_all[4][kTcRuns];
+  __shared__ uint16_t s_map_all[4][kTcChunks];
+  if (a.counters[2] || !a.counters[kCtrDense]) return;
+  const int lane = threadIdx.x & 63;
+  const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  uint8_t* s_buf = s_buf_all[wv] + 16;
+  uint32_t* s_run = s_run_all[wv];
+  uint16_t* s_map = s_map_all[wv];
+  const uint32_t* s32 = reinterpret_cast<const uint32_t*>(s_buf_all[wv]);  // dword k = s_buf[4k - 16]
+  for (uint32_t tile = blockIdx.x * 4 + wv; tile < a.ntiles; tile += gridDim.x * 4) {
+    const uint2 kt = a.tkeep[tile];
+    if (kt.x == 0) continue;
+    const TileLines g = tile_lines(a, tile);
+    const uint64_t obase = a.kbase[2 * tile];
+    // the tile's bytes: all loads in flight while the runs are worked out
+    const uint4* gp = reinterpret_cast<const uint4*>(a.bytes + g.sd.base + g.rel_lo);
+    uint4 v[8];
+#pragma unroll
+    for (int r = 0; r < 8; ++r) v[r] = gp[r * 64 + lane];
+    const uint64_t wlo = a.segout[g.s].win_lo, whi = a.segout[g.s].win_hi;
+    uint32_t nr = 0, dacc = 0;  // runs listed, kept bytes before the current group of lines
+    for (uint32_t j0 = 0; j0 < g.nl; j0 += 64) {
+      const uint32_t j = j0 + lane;
+      int64_t lo = 0, hi = 0, ls;
+      bool has = j < g.nl && line_run(a, g, wlo, whi, g.l0 + j, lo, hi, ls) && hi > lo;
+      const uint32_t len = has ? (uint32_t)(hi - lo) : 0u;
+      const uint32_t incl = wave_incl_scan_add(len, lane);
+      const uint64_t bm = __ballot(has);
+      if (has) {
+        const uint32_t idx = nr + (uint32_t)__popcll(bm & ((1ull << lane) - 1ull));
+        s_run[idx] = (uint32_t)(lo - g.rel_lo) | ((dacc + incl - len) << 16);
+      }
+      nr += (uint32_t)__popcll(bm);
+      dacc += (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+    }
+    {
+      uint4* l = reinterpret_cast<uint4*>(s_buf);
+#pragma unroll
+      for (int r = 0; r < 8; ++r) l[r * 64 + lane] = v[r];
+    }
+    const uint32_t kept = kt.x;
+    const uint32_t o15 = (uint32_t)(obase & 15u);
+    wave_lds_sync();
+    // chunk c covers output [16 * (obase / 16 + c), +16); its first byte inside this tile's
+    // output, x0(c) = (c ? 16c - o15 : 0), lies in exactly one run
+    for (uint32_t k = lane; k < nr; k += 64) {
+      const uint32_t r = s_run[k], d = r >> 16;
+      const uint32_t e = k + 1 < nr ? (s_run[k + 1] >> 16) : kept;
+      if (d == 0) s_map[0] = (uint16_t)k;
+      for (uint32_t c = (d + o15 + 15) >> 4; 16 * c - o15 < e; ++c)
+        if (c) s_map[c] = (uint16_t)k;
+    }
+    wave_lds_sync();
+    const uint32_t nch = (uint32_t)(((obase + kept + 15) >> 4) - (obase >> 4));
+    uint8_t* outc = a.out + ((obase >> 4) << 4);
+    for (uint32_t c = lane; c < nch; c += 64) {
+      const uint32_t x0 = c ? 16 * c - o15 : 0u;
+      const uint32_t x1 = (16 * c + 16 - o15) < kept ? 16 * c + 16 - o15 : kept;
+      uint32_t o[4] = {0u, 0u, 0u, 0u};
+      uint32_t k = s_map[c];
+      for (uint32_t x = x0; x < x1;) {
+        const uint32_t r = s_run[k], src = r & 0xFFFFu, d = r >> 16;
+        const uint32_t e = k + 1 < nr ? (s_run[k + 1] >> 16) : kept;
+        const uint32_t pe = e < x1 ? e : x1;
+        // the 16 bytes that land on chunk bytes 0..15 for this run: LDS from va on
+        const int32_t va = (int32_t)src + (int32_t)(x - d) - (int32_t)(x + o15 - 16 * c);
+        const int32_t wa = (va + 16) >> 2;  // dword index (the buffer starts 16 B early)
+        const uint32_t sh = (uint32_t)(va + 16) & 3u;
+        const uint32_t w0 = s32[wa], w1 = s32[wa + 1], w2 = s32[wa + 2], w3 = s32[wa + 3], w4 = s32[wa + 4];
+        const uint32_t y[4] = {__builtin_amdgcn_alignbyte(w1, w0, sh), __builtin_amdgcn_alignbyte(w2, w1, sh),
+                               __builtin_amdgcn_alignbyte(w3, w2, sh), __builtin_amdgcn_alignbyte(w4, w3, sh)};
+        const int b0 = (int)(x + o15 - 16 * c), b1 = (int)(pe + o15 - 16 * c);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const uint32_t m = byte_mask(b0, b1, q);
+          o[q] = (y[q] & m) | (o[q] & ~m);
+        }
+        x = pe;
+        ++k;
+      }
+      const int b0 = (int)(x0 + o15 - 16 * c), b1 = (int)(x1 + o15 - 16 * c);
+      if (b0 == 0 && b1 == 16) {
+        *reinterpret_cast<uint4*>(outc + 16 * (uint64_t)c) = make_uint4(o[0], o[1], o[2], o[3]);
+      } else {  // shared with a neighbouring tile: only this tile's bytes
+        for (int b = b0; b < b1; ++b) outc[16 * (uint64_t)c + b] = (uint8_t)(o[b >> 2] >> (8 * (b & 3)));
+      }
+    }
+    asm volatile("" ::: "memory");  // the next tile rewrites the wave's LDS
+  }
+}
+
 // Gram statistics for the prefilter's window choice: every byte position of a sample of
 // the batch into a count-min sketch (two rows, global atomics; one-off, first batch).
 __global__ __launch_bounds__(256) void k_gramhist(const uint8_t* bytes, const SegDesc* segs, uint32_t nsegs,
@@ -1870,7 +2118,55 @@ __global__ __launch_bounds__(256) void k_gramhist(const uint8_t* bytes, const Se
   }
 }
 
+// Capture assembly: block b copies 1 MiB of piece b / kAsmBlocks (pieces are 64 MiB
+// device chunks); 16-B loads, four in flight per thread.
+constexpr uint32_t kAsmSpan = 1u << 20;
+__global__ __launch_bounds__(256) void k_assemble(const AsmPiece* __restrict__ pieces, uint32_t n,
+                                                  uint8_t* __restrict__ batch, uint32_t per) {
+  const uint32_t pi = blockIdx.x / per, sub = blockIdx.x % per;
+  if (pi >= n) return;
+  const AsmPiece p = pieces[pi];
+  const uint64_t lo = (uint64_t)sub * kAsmSpan;
+  if (lo >= p.len) return;
+  const uint64_t m = (p.len - lo < kAsmSpan ? p.len - lo : kAsmSpan) / 16;
+  const uint4* s = reinterpret_cast<const uint4*>(p.src + lo);
+  uint4* d = reinterpret_cast<uint4*>(batch + p.dst + lo);
+  for (uint64_t i = threadIdx.x; i < m; i += 4 * 256) {
+    uint4 v[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (i + k * 256 < m) v[k] = s[i + k * 256];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (i + k * 256 < m) d[i + k * 256] = v[k];
+  }
+}
+
+__global__ __launch_bounds__(256) void k_lastbad(const uint16_t* __restrict__ meta, uint64_t lo, uint64_t hi,
+                                                 unsigned long long* res) {
+  uint64_t best = 0;
+  for (uint64_t l = lo + (uint64_t)blockIdx.x * 256 + threadIdx.x; l < hi; l += (uint64_t)gridDim.x * 256)
+    if (!(meta[l] & Meta::kParsed)) best = l + 1;
+  if (best) atomicMax(res, (unsigned long long)best);
+}
+
 }  // namespace
+
+hipError_t launch_assemble(const AsmPiece* pieces, uint32_t n, uint8_t* batch, hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  constexpr uint32_t per = (64u << 20) / kAsmSpan;  // = the engine's staging chunk / span
+  hipLaunchKernelGGL(k_assemble, dim3(n * per), dim3(256), 0, st, pieces, n, batch, per);
+  return hipGetLastError();
+}
+
+hipError_t launch_lastbad(const RunArgs& a, uint64_t lo, uint64_t hi, uint64_t* res, hipStream_t st) {
+  hipError_t e = hipMemsetAsync(res, 0, 8, st);
+  if (e != hipSuccess || hi <= lo) return e;
+  const uint64_t nb = (hi - lo + 255) / 256;
+  hipLaunchKernelGGL(k_lastbad, dim3((uint32_t)(nb < 2048 ? nb : 2048)), dim3(256), 0, st, a.meta, lo, hi,
+                     reinterpret_cast<unsigned long long*>(res));
+  return hipGetLastError();
+}
 
 hipError_t dump_timeline(void* host, size_t bytes) {
 #if KLF_TIMELINE
@@ -2009,12 +2305,25 @@ static hipError_t launch_tail_stage(const RunArgs& a, hipStream_t st, hipEvent_t
   hipLaunchKernelGGL(k_wprefix, dim3(1), dim3(256), 0, st, a);
   KLF_TRY(hipGetLastError());
   if (a.stage_times) KLF_TRY(hipEventRecord(ev[4], st));  // ~5 us of idle GPU each
+  // k_wprefix chose the path (counters[kCtrDense]); the other path's kernels exit at once
   hipLaunchKernelGGL(k_csum, dim3(num_cus * 4), dim3(kThreads), 0, st, a);
   KLF_TRY(hipGetLastError());
   hipLaunchKernelGGL(k_cscan, dim3(1), dim3(256), 0, st, a);
   KLF_TRY(hipGetLastError());
   hipLaunchKernelGGL(k_cgather, dim3(num_cus * KLF_CG_GRID), dim3(kThreads), 0, st, a);
   KLF_TRY(hipGetLastError());
+  if (a.compact_mode != 1) {
+    const uint32_t gk = (a.ntiles + 3) / 4;
+    hipLaunchKernelGGL(k_tkeep, dim3(gk < (uint32_t)num_cus * 8 ? gk : num_cus * 8), dim3(256), 0, st, a);
+    KLF_TRY(hipGetLastError());
+    const uint32_t nb = (a.ntiles + 4095) / 4096;
+    hipLaunchKernelGGL(k_ksum<16>, dim3(nb), dim3(256), 0, st, a);
+    KLF_TRY(hipGetLastError());
+    hipLaunchKernelGGL(k_kbase<16>, dim3(nb), dim3(256), 0, st, a);
+    KLF_TRY(hipGetLastError());
+    hipLaunchKernelGGL(k_tcopy, dim3(gk < (uint32_t)num_cus * 12 ? gk : num_cus * 12), dim3(256), 0, st, a);
+    KLF_TRY(hipGetLastError());
+  }
 #undef KLF_TRY
   return hipSuccess;
 }

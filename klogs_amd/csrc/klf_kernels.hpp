@@ -43,6 +43,7 @@ constexpr uint32_t kCtrCopyChunks = 11;              // counters[11]: output cop
 #endif
 constexpr uint64_t kCopyChunk = KLF_COPY_CHUNK_KB * 1024;  // output bytes per k_cgather work item
 constexpr uint32_t kCtrVerified = 10;                // counters[10]: hits k_verify walked (diagnostics)
+constexpr uint32_t kCtrDense = 14;                   // counters[14]: dense compaction (k_tkeep / k_tcopy)
 constexpr uint32_t kQfRegex = 1u << 24;              // entry flags: regex factor (else literal)
 constexpr uint32_t kQfLoose = 1u << 25;              //   compare OR 0x20 per byte
 constexpr size_t kNfaMaxLds = 64 * 1024;            // k_nfa stages its tables in LDS up to this
@@ -183,6 +184,11 @@ struct RunArgs {
   uint64_t hflat_cap;
   uint64_t* qhits;      // [qhits_cap] spilled hits (batch byte offsets of the samples)
   uint32_t qhits_cap;
+  // dense compaction (most lines selected): per tile kept bytes / selected lines, their
+  // exclusive prefixes (out offset, selected-line offset per tile)
+  uint2* tkeep;         // [ntiles]
+  uint64_t* kbase;      // [2 * ntiles]
+  uint32_t compact_mode;  // 0 auto, 1 line gather (sparse), 2 tile copy (dense)
 };
 
 // Enqueues the whole pipeline on `stream`; `ev` (6 events) brackets the stages for
@@ -196,6 +202,16 @@ hipError_t launch_retail(const RunArgs& a, hipStream_t stream, hipEvent_t* ev, i
 // of up to 16 segments, every position, grams folded / masked like the prefilter's.
 hipError_t launch_gramhist(const uint8_t* bytes, const SegDesc* segs, uint32_t nsegs, uint64_t sample, uint32_t fold,
                            uint32_t qmask, uint32_t* hist, hipStream_t stream);
+// Staged capture (klf_run): device chunks of the early H2D -> their places in the batch.
+struct AsmPiece {
+  const uint8_t* src;  // device chunk (16-B aligned)
+  uint64_t dst;        // batch byte offset (16-B aligned)
+  uint64_t len;        // bytes (a multiple of 16)
+};
+hipError_t launch_assemble(const AsmPiece* pieces, uint32_t n, uint8_t* batch, hipStream_t stream);
+// Global index of the last line in [lo, hi) whose meta has no parsed bit, +1 (0 = none),
+// atomically max-ed into *res (zeroed here).  Needs the latest run's meta (a.meta).
+hipError_t launch_lastbad(const RunArgs& a, uint64_t lo, uint64_t hi, uint64_t* res, hipStream_t stream);
 // Diagnostic builds (-DKLF_TIMELINE=1): per-tile scan timeline; hipErrorNotSupported otherwise.
 hipError_t dump_timeline(void* host, size_t bytes);
 hipError_t clear_timeline();

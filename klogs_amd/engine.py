@@ -63,7 +63,8 @@ class _Counts(C.Structure):
         return {k: int(getattr(self, k)) for k, _ in self._fields_}
 
 
-# Every symbol include/klf.h declares, with its ctypes signature (checked by the CPU tests).
+# Every symbol include/klf.h and include/klf_debug.h declare, with its ctypes signature
+# (checked by the CPU tests).
 SIGNATURES = {
     "klf_open": (C.c_int, [C.POINTER(_Config), C.POINTER(C.c_void_p)]),
     "klf_close": (None, [C.c_void_p]),
@@ -81,6 +82,7 @@ SIGNATURES = {
                                     C.POINTER(_Counts)]),
     "klf_result_lines": (C.c_int, [C.c_void_p, C.c_uint32, C.POINTER(C.c_void_p), C.POINTER(C.c_uint64)]),
     "klf_result_match_bits": (C.c_int, [C.c_void_p, C.c_uint32, C.POINTER(C.c_void_p), C.POINTER(C.c_uint64)]),
+    "klf_result_last_unparsed": (C.c_int, [C.c_void_p, C.c_uint32, C.POINTER(C.c_uint64)]),
     "klf_result_device_out": (C.c_int, [C.c_void_p, C.c_uint32, C.POINTER(C.c_void_p), C.POINTER(C.c_uint64),
                                         C.POINTER(C.c_uint64)]),
     "klf_result_write": (C.c_int, [C.c_void_p, C.POINTER(C.c_int), C.c_uint32, C.POINTER(C.c_uint64)]),
@@ -234,6 +236,13 @@ class Result:
         n = C.c_uint64()
         _check(_lib.klf_result_match_bits(self._p, i, C.byref(p), C.byref(n)))
         return C.string_at(p.value, n.value) if n.value else b""
+
+    def last_unparsed(self, i: int) -> int:
+        """klf_result_last_unparsed: rank from the end (over newline-terminated lines) of the
+        stream's last unparseable terminated line, 0 = none."""
+        v = C.c_uint64()
+        _check(_lib.klf_result_last_unparsed(self._p, i, C.byref(v)))
+        return int(v.value)
 
     def device_out(self, i: int) -> Tuple[int, int, int]:
         p = C.c_void_p()

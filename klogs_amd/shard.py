@@ -70,12 +70,17 @@ def unpack_records(blocks: np.ndarray, n_streams: int) -> np.ndarray:
     return out
 
 
-def gather_counts(counts: Dict[int, dict], lens: Sequence[int], world: int, device=None) -> np.ndarray:
-    """All-gathers every rank's per-stream records (one collective) -> [n_streams, 6]."""
+def gather_counts(counts: Dict[int, dict], lens: Sequence[int], world: int, device=None,
+                  allgather=None) -> np.ndarray:
+    """All-gathers every rank's per-stream records (one collective) -> [n_streams, 6].
+    allgather(block [cap, NREC] int64) -> [world * cap, NREC] replaces the collective (the
+    in-process simulations of several ranks)."""
+    cap = max(len(local_streams(lens, world, r)) for r in range(world)) or 1
+    if allgather is not None:
+        return unpack_records(np.asarray(allgather(pack_records(counts, cap))), len(lens))
     import torch
     import torch.distributed as dist
 
-    cap = max(len(local_streams(lens, world, r)) for r in range(world)) or 1
     rec = torch.from_numpy(pack_records(counts, cap))
     if device is not None:
         rec = rec.to(device)
@@ -88,7 +93,7 @@ def gather_counts(counts: Dict[int, dict], lens: Sequence[int], world: int, devi
 
 
 def run_shard(lens: Sequence[int], fetch: Callable[[int], bytes], runner, world: int, rank: int,
-              device=None):
+              device=None, allgather=None):
     """Filters this rank's streams and gathers every stream's counts.
 
     fetch(stream_id) -> the stream's captured bytes; runner(list of bytes) -> list of
@@ -98,7 +103,7 @@ def run_shard(lens: Sequence[int], fetch: Callable[[int], bytes], runner, world:
     res = runner([fetch(i) for i in mine]) if mine else []
     outs = {sid: r[0] for sid, r in zip(mine, res)}
     counts = {sid: r[1] for sid, r in zip(mine, res)}
-    return outs, gather_counts(counts, lens, world, device)
+    return outs, gather_counts(counts, lens, world, device, allgather)
 
 
 def engine_runner(engine, since=None, tail: int = -1):
@@ -164,14 +169,19 @@ def end_shard(bounds: Sequence[int]) -> int:
     return ne[-1] if ne else w - 1
 
 
-def tail_shares(g_term: Sequence[int], tail: int, last: int = -1) -> List[int]:
+def tail_shares(g_term: Sequence[int], tail: int, last: int = -1, unparsed=None) -> List[int]:
     """Each shard's share of the global --tail N (-1 = all lines: every shard -1).  An
     earlier shard gets N minus the newline-terminated G lines of the shards after it,
     clamped to [0, its own count].  The end shard `last` (default: the final one) holds
-    the fragment, which kubelet emits only when the whole stream has fewer than N
-    terminated G lines (the window then holds every line; otherwise ReadLogs stops after
-    N lines, before the fragment): it keeps N in that case, else min(N, own count), which
-    its own tail rule turns into "every terminated line of mine, fragment cut"."""
+    the fragment.  kubelet (SPEC.md S4) reads from G-rank max(0, T - N), counts parsed lines
+    only and stops after N of them, so the fragment is emitted iff the window's terminated
+    lines hold fewer than N parsed ones: when T < N, or when some terminated line of the
+    window is unparseable.  The end shard applies that rule to its own part of the window
+    with its share; an unparseable line in an EARLIER shard's part is visible to it only
+    through unparsed[r] (rank from the end of shard r's last unparseable terminated line,
+    0 = none; klf_result_last_unparsed): when one lies inside shard r's share, the end
+    shard gets share N, which keeps all of its terminated lines (its share was its whole
+    count anyway) and makes its own rule emit the fragment."""
     w = len(g_term)
     last = w - 1 if last < 0 else last
     if tail < 0:
@@ -185,6 +195,8 @@ def tail_shares(g_term: Sequence[int], tail: int, last: int = -1) -> List[int]:
         else:
             out[r] = max(0, min(int(g_term[r]), tail - later))
         later += int(g_term[r])
+    if unparsed is not None and any(r != last and 0 < int(unparsed[r]) <= out[r] for r in range(w)):
+        out[last] = tail
     return out
 
 
@@ -208,16 +220,18 @@ def run_split(n: int, find_nl: Callable[[int], int], runner, world: int, rank: i
               allgather=None, device=None):
     """Filters this rank's byte range of one stream; returns (this shard's output bytes,
     whole-stream counts).  runner(lo, hi, tail) -> a shard handle with .out (bytes),
-    .counts (dict of COUNT_FIELDS), .g_term (newline-terminated G lines) and
-    .retail(n) -> handle (the same shard with the tail rule re-applied).
+    .counts (dict of COUNT_FIELDS), .g_term (newline-terminated G lines), .u_rank (rank
+    from the end of its last unparseable terminated G line, 0 = none) and .retail(n) ->
+    handle (the same shard with the tail rule re-applied).
     allgather(list of ints) -> [world, k] array (default: torch.distributed, RCCL on the
     GPU box, gloo in the CPU tests)."""
     ag = allgather or (lambda v: _allgather_ints(v, world, device))
     b = split_bounds(n, world, find_nl)
     h = runner(b[rank], b[rank + 1], tail)
-    g_term = ag([h.g_term])[:, 0]                       # the one exchange step
+    ex = ag([h.g_term, h.u_rank])                        # the one exchange step
+    g_term, u_rank = ex[:, 0], ex[:, 1]
     last = end_shard(b)
-    share = tail_shares(g_term, tail, last)[rank]
+    share = tail_shares(g_term, tail, last, u_rank)[rank]
     ran_as = tail if rank == last else min(tail, int(g_term[rank]))  # what the first run selected
     if tail >= 0 and share != ran_as:
         h = h.retail(share)
@@ -242,6 +256,8 @@ class EngineShard:
         frag = bool(data) and not data.endswith(b"\n")
         frag_in_g = frag and (not has_patterns or self._last_bit())
         self.g_term = int(self.counts["matched"]) - (1 if frag_in_g else 0)
+        # with patterns every G line is parsed; without, G is every line
+        self.u_rank = 0 if has_patterns else result.last_unparsed(0)
 
     def _last_bit(self) -> bool:
         lines = int(self.counts["lines"])

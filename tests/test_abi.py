@@ -20,8 +20,9 @@ def _declared(header: Path):
 
 
 def test_every_declared_symbol_is_exported():
-    names = _declared(ROOT / "include" / "klf.h")
+    names = _declared(ROOT / "include" / "klf.h") + _declared(ROOT / "include" / "klf_debug.h")
     assert len(names) >= 20
+    assert not [n for n in _declared(ROOT / "include" / "klf.h") if n.startswith("klf_debug")]
     lib = C.CDLL(str(ROOT / "klogs_amd" / "_lib" / "libklf.so"))
     for n in names:
         assert hasattr(lib, n), n

@@ -21,7 +21,7 @@ def _split_on_engines(data, world, tail, grep):
     try:
         b = shard.split_bounds(len(data), world, find_nl)
         hs = [shard.EngineShard(engines[r], data[b[r]:b[r + 1]], SINCE, tail, bool(grep)) for r in range(world)]
-        g = np.array([[h.g_term] for h in hs])
+        g = np.array([[h.g_term, h.u_rank] for h in hs])
         outs, counts = [], []
         for r in range(world):
             calls = iter([g])
@@ -76,3 +76,21 @@ def test_retail_equals_fresh_run(gpu, grep):
             r.free()
             r = r2
         r.free()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("tail", [1, 3, 8, 13])
+@pytest.mark.parametrize("where", ["early", "late", "many"])
+def test_split_unparseable_in_window_on_engines(gpu, world, tail, where):
+    """An unparseable terminated line in an earlier shard's part of the tail window makes
+    kubelet emit the trailing fragment (SPEC.md S4): klf_result_last_unparsed carries it."""
+    good = [b"2024-10-22T00:%02d:00.000000000Z line %d\n" % (40 + i // 10, i) for i in range(12)]
+    bad = b"garbage-without-a-timestamp\n"
+    lines = list(good)
+    for p in {"early": (3,), "late": (10,), "many": (2, 6, 11)}[where]:
+        lines.insert(p, bad)
+    data = b"".join(lines) + b"2024-10-22T00:59:59Z the fragment"
+    for grep in ([], [b"line"]):
+        want, _, _, _ = co.filter_stream(data, SINCE, tail, grep, want_lines=False, want_bits=False)
+        got, _ = _split_on_engines(data, world, tail, grep)
+        assert got == want, (grep, got, want)

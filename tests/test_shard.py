@@ -122,9 +122,21 @@ class _OracleShard:
         L = self.counts["lines"]
         in_g = (not grep) or (L > 0 and (bits[(L - 1) >> 3] >> ((L - 1) & 7)) & 1)
         self.g_term = self.counts["matched"] - (1 if frag and in_g else 0)
+        self.u_rank = 0 if grep else _last_unparsed(data)
 
     def retail(self, tail):
         return _OracleShard(self.data, self.since, tail, self.grep)
+
+
+def _last_unparsed(data):
+    """Rank from the end (over newline-terminated lines) of the last unparseable one, 0 = none
+    (SPEC.md S2: no space, or a prefix Go time.Parse rejects)."""
+    lines = data.split(b"\n")[:-1]  # the terminated lines (the last piece is the fragment or b"")
+    for k, ln in enumerate(reversed(lines), start=1):
+        sp = ln.find(b" ")
+        if sp < 0 or co.parse_ts(ln[:sp]) is None:
+            return k
+    return 0
 
 
 def _split_case(data, world, tail, grep):
@@ -137,7 +149,7 @@ def _split_case(data, world, tail, grep):
     b = shard.split_bounds(len(data), world, find_nl)
     for r in range(world):
         handles[r] = _OracleShard(data[b[r]:b[r + 1]], SINCE, tail, grep)
-    g = np.array([[handles[r].g_term] for r in range(world)])
+    g = np.array([[handles[r].g_term, handles[r].u_rank] for r in range(world)])
     outs, totals = [], {}
     for r in range(world):
         it = iter([g, np.array([[int(handles[k].counts[f]) for f in shard.COUNT_FIELDS] for k in range(world)])])
@@ -168,6 +180,38 @@ def test_split_stream_equals_unsplit(world, tail, grep, frag):
     for f in ("lines", "parsed", "since_ok", "matched"):
         assert totals[f] == wc[f], f
     assert got == want
+
+
+@pytest.mark.parametrize("world", [2, 3, 4])
+@pytest.mark.parametrize("tail", [1, 2, 3, 5, 8, 13])
+@pytest.mark.parametrize("where", ["early", "late", "none", "many"])
+def test_split_unparseable_in_window_emits_fragment(world, tail, where):
+    """kubelet emits the fragment when the tail window holds an unparseable terminated line
+    (SPEC.md S4); that line may sit in an earlier shard than the fragment (advisor r01)."""
+    good = [b"2024-10-22T00:%02d:00.000000000Z line %d\n" % (40 + i // 10, i) for i in range(12)]
+    bad = b"garbage-without-a-timestamp\n"
+    lines = list(good)
+    if where == "early":
+        lines.insert(3, bad)
+    elif where == "late":
+        lines.insert(10, bad)
+    elif where == "many":
+        for p in (2, 6, 11):
+            lines.insert(p, bad)
+    data = b"".join(lines) + b"2024-10-22T00:59:59Z the fragment"
+    for grep in ((), (b"line",)):
+        want, _, _, _ = co.filter_stream(data, SINCE, tail, list(grep), want_lines=False, want_bits=False)
+        got, _ = _split_case(data, world, tail, list(grep))
+        assert got == want, (grep, got, want)
+
+
+def test_tail_shares_unparsed():
+    # shard 0's last unparseable line is 2 lines from its end, inside its share of 3
+    assert shard.tail_shares([5, 2], 5, unparsed=[2, 0]) == [3, 5]
+    # outside its share: no fragment from it
+    assert shard.tail_shares([5, 2], 5, unparsed=[4, 0]) == [3, 2]
+    # the end shard's own unparseable lines are its own rule's business
+    assert shard.tail_shares([5, 2], 5, unparsed=[0, 1]) == [3, 2]
 
 
 def test_split_bounds_edges():
