@@ -68,7 +68,9 @@ def main():
     ap.add_argument("--bytes", type=int, default=STREAM_BYTES, help="stream bytes per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-verify", action="store_true")
+    ap.add_argument("--no-write", action="store_true", help="skip C3's file write path")
     ap.add_argument("--no-capture", action="store_true", help="skip the host-staged capture-path timing")
+    ap.add_argument("--capture-piece", type=int, default=4 << 20, help="klf_stage piece size of the capture path")
     ap.add_argument("--extra-configs", default="c3,c4,c5", help="N=1 only: comma list of c3,c4,c5 ('' = none)")
     ap.add_argument("--extra-bytes", type=int, default=32 << 30, help="total bytes of each extra config")
     args = ap.parse_args()
@@ -158,6 +160,7 @@ def main():
     dev_avg_s = float(np.mean(total_ms)) / 1e3
     achieved = scan_alg / scan_avg_s / 1e9
 
+    log(f"[rank {rank}] timed {args.steps} steps: {dt / args.steps * 1e3:.3f} ms/step")
     verified = None
     if rank == 0 and not args.no_verify and world == 1:
         sys.path.insert(0, str(ROOT / "oracle"))
@@ -191,10 +194,11 @@ def main():
     # klf_run (DMA H2D from the pinned chunks + the whole filter) and the output D2H.
     # Reported beside `value`, never as it (device-resident is the metric).
     capture = None
+    log(f"[rank {rank}] verified={verified} cpu_baseline={cpu and cpu['value']}")
     if rank == 0 and world == 1 and not args.no_capture:
         ceng = E.Engine(local, grep=[synth.NEEDLE])
         want = last.stream(0).out
-        piece = 1 << 20
+        piece = args.capture_piece
         runs = []
         for _ in range(2):  # the first pays the pinned-chunk allocation
             ceng.reset()
@@ -280,6 +284,9 @@ def main():
 def extra_streams(name: str, total: int):
     """(stream sizes, generator kind, patterns, permille, description) of BASELINE configs
     3 / 4 / 5."""
+    if name == "c2":  # the headline workload, for scripts/run_config.py
+        return [STREAM_BYTES], synth.JSON, dict(grep=[synth.NEEDLE]), 10, \
+            "C2: one 4 GiB JSON log stream, --since 5m --tail 100 --grep " + synth.NEEDLE.decode()
     if name == "c3":  # one GPU's share of C3 at 8 GPUs (fixed size: --extra-bytes is for C4/C5)
         n = 128
         return [64 << 20] * n, synth.TEXT, {}, 10, \
@@ -340,7 +347,7 @@ def run_extra(name: str, args, local: int, now: int) -> dict:
     verified = None
     write = None
     wdir = None
-    if name == "c3":  # §8f-3 output write path: every stream into its own file (klf_result_write)
+    if name == "c3" and not args.no_write:  # §8f-3 output write path: every stream into its own file (klf_result_write)
         wdir = tempfile.TemporaryDirectory(prefix="klf_c3_")
         paths = [os.path.join(wdir.name, f"pod{i // 4}__c{i % 4}.log") for i in range(len(lens))]
         tw = time.perf_counter()
@@ -353,7 +360,7 @@ def run_extra(name: str, args, local: int, now: int) -> dict:
         write = {"GBps": round(wbytes / wdt / 1e9, 2), "bytes": wbytes, "files": len(paths), "s": round(wdt, 3),
                  "how": "klf_result_write: 64 MiB pinned D2H chunks, double-buffered, 8 writer threads each owning whole files (own HIP stream + 2x32 MiB pinned halves), "
                         "into page-cache files under " + os.path.dirname(wdir.name)}
-    if name == "c3" and not args.no_verify and wbytes is not None:  # first and last stream vs the C oracle
+    if name == "c3" and not args.no_verify and write is not None and wbytes is not None:  # first and last stream vs the C oracle
         sys.path.insert(0, str(ROOT / "oracle"))
         import c_oracle as co
         verified = True

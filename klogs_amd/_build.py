@@ -22,7 +22,7 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("KLF_OFFLOAD_ARCH", "gfx950")
 
 ENGINE_SRCS = ["klf_kernels.hip", "klf_engine.cpp", "klf_patterns.cpp"]
-ENGINE_HDRS = ["klf_kernels.hpp", "klf_patterns.hpp", "klf_ts.hpp"]
+ENGINE_HDRS = ["klf_kernels.hpp", "klf_patterns.hpp", "klf_ts.hpp", "klf_copypool.hpp"]
 
 
 def _stale(out: Path, deps) -> bool:

@@ -21,6 +21,7 @@
 
 #include "../../include/klf.h"
 #include "../../include/klf_debug.h"
+#include "klf_copypool.hpp"
 #include "klf_kernels.hpp"
 #include "klf_patterns.hpp"
 #include "klf_ts.hpp"
@@ -51,85 +52,6 @@ struct DevBuf {
 };
 
 uint64_t align_up(uint64_t x, uint64_t a) { return (x + a - 1) / a * a; }
-
-// Host copy workers for klf_stage: one large piece is striped over a few threads, so
-// staging one stream is not bound by a single core's memcpy into page-locked memory.
-// The caller copies a stripe itself and waits for the rest; several callers share the
-// workers (their stripes queue up).
-class CopyPool {
- public:
-  explicit CopyPool(int workers) {
-    for (int i = 0; i < workers; ++i) th_.emplace_back([this] { loop(); });
-  }
-  ~CopyPool() {
-    {
-      std::lock_guard<std::mutex> g(mu_);
-      stop_ = true;
-    }
-    cv_.notify_all();
-    for (auto& t : th_) t.join();
-  }
-  int workers() const { return (int)th_.size(); }
-  void copy(uint8_t* dst, const uint8_t* src, size_t n) {
-    constexpr size_t kMinStripe = 512u << 10;
-    const size_t parts = std::min<size_t>((size_t)workers() + 1, n / kMinStripe);
-    if (parts < 2) {
-      memcpy(dst, src, n);
-      return;
-    }
-    const size_t step = (n / parts + 4095) & ~(size_t)4095;
-    Job job;
-    job.left = 0;
-    size_t o = step;  // stripe 0 is the caller's
-    {
-      std::lock_guard<std::mutex> g(mu_);
-      for (; o < n; o += step) {
-        q_.push_back({dst + o, src + o, std::min(step, n - o), &job});
-        ++job.left;
-      }
-    }
-    cv_.notify_all();
-    memcpy(dst, src, std::min(step, n));
-    std::unique_lock<std::mutex> g(job.mu);
-    job.cv.wait(g, [&] { return job.left == 0; });
-  }
-
- private:
-  struct Job {
-    std::mutex mu;
-    std::condition_variable cv;
-    int left = 0;
-  };
-  struct Stripe {
-    uint8_t* dst;
-    const uint8_t* src;
-    size_t n;
-    Job* job;
-  };
-  void loop() {
-    for (;;) {
-      Stripe s;
-      {
-        std::unique_lock<std::mutex> g(mu_);
-        cv_.wait(g, [&] { return stop_ || !q_.empty(); });
-        if (q_.empty()) return;
-        s = q_.front();
-        q_.pop_front();
-      }
-      memcpy(s.dst, s.src, s.n);
-      {
-        std::lock_guard<std::mutex> g(s.job->mu);
-        --s.job->left;
-      }
-      s.job->cv.notify_all();
-    }
-  }
-  std::mutex mu_;
-  std::condition_variable cv_;
-  std::deque<Stripe> q_;
-  bool stop_ = false;
-  std::vector<std::thread> th_;
-};
 
 }  // namespace
 
@@ -171,7 +93,7 @@ struct klf_engine {
   hipStream_t copy_stream = nullptr;   // early H2D of full chunks
   hipEvent_t copy_done = nullptr;
   bool ran = false;                    // klf_run since the last klf_reset (stage -> ESTATE)
-  std::unique_ptr<CopyPool> copier;
+  std::unique_ptr<klf::CopyPool> copier;
   DevBuf d_asm;                        // k_assemble piece table
   DevBuf d_scratch;                    // small query results (klf_result_last_unparsed)
   // device pattern tables
@@ -185,7 +107,7 @@ struct klf_engine {
   DevBuf d_tile_seg;
   DevBuf d_cmap, d_cseg;
   DevBuf d_batch, d_segs, d_tstat, d_slots, d_pool, d_tile_base, d_bsum, d_cstatus, d_counters, d_line_off,
-      d_meta, d_bits, d_segout, d_wpre, d_out, d_mpart, d_tkeep, d_kbase;
+      d_meta, d_bits, d_segout, d_wpre, d_out, d_mpart, d_trec, d_truns, d_kbase;
   uint64_t pool_cap = 1 << 20;
   hipEvent_t ev[7] = {};
   klf::RunArgs last_args{};  // arguments of the latest completed run (klf_retail)
@@ -293,7 +215,7 @@ extern "C" int klf_open(const klf_config* cfg, klf_engine** out) {
   {
     int nw = 3;  // staging copy workers (+ the calling thread)
     if (const char* v = getenv("KLF_STAGE_THREADS")) nw = std::max(0, std::min(atoi(v), 32));
-    e->copier.reset(new CopyPool(nw));
+    e->copier.reset(new klf::CopyPool(nw));
   }
   // 3) pattern tables to the device
   const auto& cs = e->cs;
@@ -387,7 +309,7 @@ extern "C" void klf_close(klf_engine* e) {
                     &e->d_rx_follow, &e->d_rx_vec, &e->d_rx_flags, &e->d_qf_bitmap, &e->d_qf_head,
                     &e->d_qf_ent, &e->d_qf_nbytes, &e->d_rx_vec4, &e->d_qhits, &e->d_hslots, &e->d_hist, &e->d_hflat, &e->d_cand, &e->d_batch, &e->d_segs, &e->d_tstat,
                     &e->d_slots, &e->d_pool, &e->d_tile_base, &e->d_bsum, &e->d_cstatus, &e->d_counters, &e->d_cmap, &e->d_cseg,
-                    &e->d_line_off, &e->d_meta, &e->d_bits, &e->d_segout, &e->d_wpre, &e->d_out, &e->d_tile_seg, &e->d_mpart, &e->d_tkeep, &e->d_kbase})
+                    &e->d_line_off, &e->d_meta, &e->d_bits, &e->d_segout, &e->d_wpre, &e->d_out, &e->d_tile_seg, &e->d_mpart, &e->d_trec, &e->d_truns, &e->d_kbase})
     b->release();
   e->d_asm.release();
   e->d_scratch.release();
@@ -676,7 +598,8 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
   HIPCHK(e, e->d_segout.ensure(nsegs * sizeof(SegOut)), "alloc segout");
   HIPCHK(e, e->d_wpre.ensure((nsegs + 1) * 8), "alloc wpre");
   HIPCHK(e, e->d_out.ensure(total_bytes + 64), "alloc out");
-  HIPCHK(e, e->d_tkeep.ensure(ntiles * 8), "alloc tkeep");
+  HIPCHK(e, e->d_trec.ensure(ntiles * sizeof(klf::TRec)), "alloc trec");
+  HIPCHK(e, e->d_truns.ensure(ntiles * klf::kRunSlots * 4), "alloc truns");
   HIPCHK(e, e->d_kbase.ensure(ntiles * 16), "alloc kbase");
   uint32_t compact_mode = 0;  // tests: force either compaction path
   if (const char* v = getenv("KLF_COMPACT")) compact_mode = !strcmp(v, "sparse") ? 1u : !strcmp(v, "dense") ? 2u : 0u;
@@ -761,7 +684,8 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
     a.hflat = need_hits ? e->d_hflat.as<uint32_t>() : nullptr;
     a.hflat_cap = need_hits ? hflat_cap : 0;
     a.qhits_cap = need_hits ? qhits_cap : 0;
-    a.tkeep = e->d_tkeep.as<uint2>();
+    a.trec = e->d_trec.as<klf::TRec>();
+    a.truns = e->d_truns.as<uint32_t>();
     a.kbase = e->d_kbase.as<uint64_t>();
     a.compact_mode = compact_mode;
     HIPCHK(e, klf::launch_pipeline(a, st, e->ev, e->num_cus), "launch");

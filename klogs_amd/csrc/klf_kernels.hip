@@ -89,6 +89,19 @@ __device__ __forceinline__ uint32_t wave_max(uint32_t x) {
             mx((uint32_t)__builtin_amdgcn_readlane((int)x, 47), (uint32_t)__builtin_amdgcn_readlane((int)x, 63)));
 }
 
+__device__ __forceinline__ uint32_t wave_incl_scan_max(uint32_t x, int lane) {
+  auto mx = [](uint32_t a, uint32_t b) { return a > b ? a : b; };
+  x = mx(x, dpp0<0x111>(x));  // row_shr:1 (lanes without a source read 0)
+  x = mx(x, dpp0<0x112>(x));
+  x = mx(x, dpp0<0x114>(x));
+  x = mx(x, dpp0<0x118>(x));
+  const uint32_t r0 = (uint32_t)__builtin_amdgcn_readlane((int)x, 15);
+  const uint32_t r1 = mx(r0, (uint32_t)__builtin_amdgcn_readlane((int)x, 31));
+  const uint32_t r2 = mx(r1, (uint32_t)__builtin_amdgcn_readlane((int)x, 47));
+  const int row = lane >> 4;
+  return mx(x, row == 0 ? 0u : row == 1 ? r0 : row == 2 ? r1 : r2);
+}
+
 __device__ __forceinline__ uint32_t find_seg_by_tile(const SegDesc* segs, uint32_t n, uint32_t tile) {
   uint32_t lo = 0, hi = n;
   while (hi - lo > 1) {
@@ -1867,16 +1880,18 @@ __global__ __launch_bounds__(kThreads) void k_cgather(RunArgs a) {
 // ============================================ K4': dense compaction (tile copy) ==
 // When most lines are selected (e.g. C3: -l only, every line out) the output is the input
 // minus the timestamp prefixes: a byte compaction.  It runs over the scan's 8 KiB tiles:
-//   k_tkeep   wave per tile: the tile's lines (tile_base .. + events) -> kept content bytes
-//             inside the tile and selected lines starting in it
+//   k_tkeep   wave per tile: the tile's lines (tile_base .. + events) -> its kept runs
+//             (content bytes of selected lines inside the tile, with their offsets in the
+//             tile's output), kept bytes and selected lines starting in it (TRec + runs)
 //   k_ksum / k_kbase   reduce-then-scan of those -> each tile's output / selected-line
 //             offsets, stream output ranges at the streams' first / last tiles
-//   k_tcopy   wave per tile with kept bytes: the tile is loaded into LDS with coalesced
-//             16-B loads, its kept runs are listed, and every 16-B output chunk of the
-//             tile's output range is assembled from LDS (any alignment: five dword reads +
-//             v_alignbyte) and stored with one 16-B store (coalesced across the wave); only
-//             the two chunks shared with the neighbouring tiles are stored bytewise.
-// Input read once, output written once, the line index read twice.
+//   k_tcopy   wave per tile with kept bytes, the next tile's bytes and runs in flight in
+//             registers: the tile goes to LDS (coalesced 16-B loads), and every 16-B output
+//             chunk of the tile's output range is assembled from LDS (any alignment: five
+//             dword reads + v_alignbyte) and stored with one 16-B store (coalesced across
+//             the wave); only the two chunks shared with the neighbouring tiles are stored
+//             bytewise.
+// Input read once, output written once, the line index read once.
 struct TileLines {
   uint32_t s;
   SegDesc sd;
@@ -1898,37 +1913,118 @@ __device__ __forceinline__ TileLines tile_lines(const RunArgs& a, uint32_t tile)
   return g;
 }
 
-// Line l of tile g: is it selected, and its kept run [lo, hi) (stream offsets) in the tile.
-__device__ __forceinline__ bool line_run(const RunArgs& a, const TileLines& g, uint64_t wlo, uint64_t whi,
-                                         uint64_t l, int64_t& lo, int64_t& hi, int64_t& ls) {
-  if (l < wlo || l >= whi) return false;
-  const uint16_t m = a.meta[l];
-  if (!((m & Meta::kParsed) && (m & Meta::kSince) && gbit(a, l))) return false;
-  const uint64_t s0 = a.line_off[l + g.s], le = a.line_off[l + g.s + 1];
-  const uint64_t cs = s0 + line_plen(a, m, a.bytes + g.sd.base, s0, le);
-  ls = (int64_t)s0;
-  lo = (int64_t)cs > g.rel_lo ? (int64_t)cs : g.rel_lo;
-  hi = (int64_t)le < g.rel_lo + g.tlen ? (int64_t)le : g.rel_lo + g.tlen;
-  return true;
+// The kept run of line j of tile g (lane = line): the line's index data is loaded first
+// (LineData, all loads of a line in one round trip; k_tkeep loads the next tile's first
+// lines ahead), then tested.  has = non-empty run.
+struct LineData {
+  uint64_t s0, le;  // line start / end (stream offsets)
+  uint32_t bw;      // match bitmap word of the line
+  uint32_t m;       // meta
+};
+struct LineRun {
+  uint32_t src, len;  // tile offset of the run, bytes
+  bool has, starts;   // non-empty run; a selected line starting in the tile
+};
+// Line l0 + j's data; l clamped into the index (lines past the tile are loaded but unused).
+__device__ __forceinline__ LineData load_line(const RunArgs& a, uint32_t s, uint64_t l) {
+  l = l < a.cap_lines ? l : a.cap_lines - 1;
+  LineData d;
+  d.m = a.meta[l];
+  d.s0 = a.line_off[l + s];
+  d.le = a.line_off[l + s + 1];
+  d.bw = a.grep_mode == kGrepNone ? ~0u : a.bits[l >> 5];
+  return d;
+}
+__device__ __forceinline__ LineRun eval_line(const RunArgs& a, const TileLines& g, uint64_t wlo, uint64_t whi,
+                                             uint32_t j, const LineData& d) {
+  LineRun r{0u, 0u, false, false};
+  const uint64_t l = g.l0 + j;
+  const bool sel = j < g.nl && l >= wlo && l < whi && (d.m & Meta::kParsed) && (d.m & Meta::kSince) &&
+                   ((d.bw >> (l & 31)) & 1u);
+  if (!sel) return r;
+  const uint64_t cs = d.s0 + line_plen(a, (uint16_t)d.m, a.bytes + g.sd.base, d.s0, d.le);
+  const int64_t lo = (int64_t)cs > g.rel_lo ? (int64_t)cs : g.rel_lo;
+  const int64_t hi = (int64_t)d.le < g.rel_lo + g.tlen ? (int64_t)d.le : g.rel_lo + g.tlen;
+  r.has = hi > lo;
+  r.src = r.has ? (uint32_t)(lo - g.rel_lo) : 0u;
+  r.len = r.has ? (uint32_t)(hi - lo) : 0u;
+  r.starts = (int64_t)d.s0 >= g.rel_lo && (int64_t)d.s0 < g.rel_lo + g.tlen;
+  return r;
 }
 
-__global__ __launch_bounds__(256) void k_tkeep(RunArgs a) {
+// Lists the tile's runs: to `runs` (at most cap entries; the count is returned whatever
+// it is), with each run's offset in the tile's output.  *kept, *nsel: totals.  pre: the
+// lane's line of the first group, already loaded (null: load it here).
+__device__ __forceinline__ uint32_t list_runs(const RunArgs& a, const TileLines& g, uint64_t wlo, uint64_t whi,
+                                              uint32_t* runs, uint32_t cap, int lane, uint32_t* kept, uint32_t* nsel,
+                                              const LineData* pre = nullptr) {
+  uint32_t nr = 0, dacc = 0, ns = 0;
+  for (uint32_t j0 = 0; j0 < g.nl; j0 += 64) {
+    const uint32_t j = j0 + (uint32_t)lane;
+    const LineData d = (j0 == 0 && pre) ? *pre : load_line(a, g.s, g.l0 + j);
+    const LineRun r = eval_line(a, g, wlo, whi, j, d);
+    const uint32_t incl = wave_incl_scan_add(r.len, lane);
+    const uint64_t bm = __ballot(r.has);
+    if (r.has) {
+      const uint32_t idx = nr + (uint32_t)__popcll(bm & ((1ull << lane) - 1ull));
+      if (idx < cap) runs[idx] = r.src | ((dacc + incl - r.len) << 16);
+    }
+    nr += (uint32_t)__popcll(bm);
+    dacc += (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+    ns += (uint32_t)__popcll(__ballot(r.starts));
+  }
+  *kept = dacc;
+  *nsel = ns;
+  return nr;
+}
+
+// The per-tile descriptors come in as __restrict__ const parameters: their wave-uniform
+// reads compile to scalar loads (lgkmcnt), so waiting for them never waits for the
+// vector memory traffic in flight.  A wave takes kTkBatch tiles per round: the first 64
+// lines' index data of all of them is loaded before any is listed (vmcnt counts loads and
+// the previous round's record stores in issue order, so a round costs one memory round
+// trip, not one per tile).
+constexpr int kTkBatch = 4;
+__global__ __launch_bounds__(256) void k_tkeep(RunArgs a, const uint32_t* __restrict__ tseg,
+                                               const SegDesc* __restrict__ segs, const TileStat* __restrict__ tstat,
+                                               const uint64_t* __restrict__ tbase, const SegOut* __restrict__ sout) {
   if (a.counters[2] || !a.counters[kCtrDense]) return;
   const int lane = threadIdx.x & 63;
   const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  for (uint32_t tile = blockIdx.x * 4 + wv; tile < a.ntiles; tile += gridDim.x * 4) {
-    const TileLines g = tile_lines(a, tile);
-    const uint64_t wlo = a.segout[g.s].win_lo, whi = a.segout[g.s].win_hi;
-    uint32_t kb = 0, kl = 0;
-    for (uint32_t j = lane; j < g.nl; j += 64) {
-      int64_t lo, hi, ls;
-      if (!line_run(a, g, wlo, whi, g.l0 + j, lo, hi, ls)) continue;
-      kb += hi > lo ? (uint32_t)(hi - lo) : 0u;
-      kl += (ls >= g.rel_lo && ls < g.rel_lo + g.tlen) ? 1u : 0u;
+  const uint32_t nw = gridDim.x * 4;
+  for (uint32_t t0 = (blockIdx.x * 4 + wv) * kTkBatch; t0 < a.ntiles; t0 += nw * kTkBatch) {
+    TileLines g[kTkBatch];
+    LineData pre[kTkBatch];
+#pragma unroll
+    for (int u = 0; u < kTkBatch; ++u) {
+      const uint32_t tile = t0 + u < a.ntiles ? t0 + u : a.ntiles - 1;
+      g[u].s = tseg[tile];
+      g[u].sd = segs[g[u].s];
+      g[u].rel_lo = (int64_t)(tile - g[u].sd.tile0) * kTile;
+      const int64_t rem = (int64_t)g[u].sd.len - g[u].rel_lo;
+      g[u].tlen = (int32_t)(rem < kTile ? rem : kTile);
+      g[u].l0 = tbase[tile];
+      const uint32_t ev = tstat[tile].events;
+      g[u].nl = rem <= kTile ? ev : ev + 1;
+      pre[u] = load_line(a, g[u].s, g[u].l0 + (uint64_t)lane);
     }
-    kb = wave_sum(kb);
-    kl = wave_sum(kl);
-    if (lane == 0) a.tkeep[tile] = make_uint2(kb, kl);
+#pragma unroll
+    for (int u = 0; u < kTkBatch; ++u) {
+      const uint32_t tile = t0 + u;
+      if (tile >= a.ntiles) break;
+      const uint64_t wlo = sout[g[u].s].win_lo, whi = sout[g[u].s].win_hi;
+      uint32_t kept, nsel;
+      const uint32_t nr = list_runs(a, g[u], wlo, whi, a.truns + (size_t)tile * kRunSlots, kRunSlots, lane, &kept,
+                                    &nsel, &pre[u]);
+      if (lane == 0) {
+        TRec rec;
+        rec.src = g[u].sd.base + (uint64_t)g[u].rel_lo;
+        rec.kept = kept;
+        rec.nruns = nr <= (uint32_t)kRunSlots ? (uint16_t)nr : kRunsRecompute;
+        rec.nsel = (uint16_t)nsel;
+        a.trec[tile] = rec;
+      }
+    }
   }
 }
 
@@ -1942,9 +2038,9 @@ __global__ __launch_bounds__(256) void k_ksum(RunArgs a) {
 #pragma unroll
   for (int r = 0; r < R; ++r)
     if (t0 + r * 256 < a.ntiles) {
-      const uint2 k = a.tkeep[t0 + r * 256];
-      b += k.x;
-      c += k.y;
+      const TRec k = a.trec[t0 + r * 256];
+      b += k.kept;
+      c += k.nsel;
     }
   b = wave_sum(b);
   c = wave_sum(c);
@@ -1976,13 +2072,17 @@ __global__ __launch_bounds__(256) void k_kbase(RunArgs a) {
   uint64_t cb = s_base[0], cc = s_base[1];
   for (int r = 0; r < R; ++r) {
     const uint32_t tile = t0 + r * 256;
-    uint2 k = make_uint2(0, 0);
-    if (tile < a.ntiles) k = a.tkeep[tile];
-    const uint64_t ib = wave_incl_scan_add((uint64_t)k.x, lane), ic = wave_incl_scan_add((uint64_t)k.y, lane);
+    uint32_t kb = 0, kc = 0;
+    if (tile < a.ntiles) {
+      const TRec k = a.trec[tile];
+      kb = k.kept;
+      kc = k.nsel;
+    }
+    const uint64_t ib = wave_incl_scan_add((uint64_t)kb, lane), ic = wave_incl_scan_add((uint64_t)kc, lane);
     const int pb = r & 1;
     if (lane == 63) { s_w[pb][0][wv] = ib; s_w[pb][1][wv] = ic; }
     __syncthreads();
-    uint64_t ob = cb + ib - k.x, oc = cc + ic - k.y;
+    uint64_t ob = cb + ib - kb, oc = cc + ic - kc;
     for (int w = 0; w < wv; ++w) { ob += s_w[pb][0][w]; oc += s_w[pb][1][w]; }
     cb += s_w[pb][0][0] + s_w[pb][0][1] + s_w[pb][0][2] + s_w[pb][0][3];
     cc += s_w[pb][1][0] + s_w[pb][1][1] + s_w[pb][1][2] + s_w[pb][1][3];
@@ -1992,108 +2092,231 @@ __global__ __launch_bounds__(256) void k_kbase(RunArgs a) {
       const uint32_t s = a.tile_seg[tile];
       const SegDesc& sd = a.segs[s];
       if (tile == sd.tile0) { a.segout[s].out_lo = ob; a.segout[s].sel_lo = oc; }
-      if (tile + 1 == sd.tile0 + sd.ntiles) { a.segout[s].out_hi = ob + k.x; a.segout[s].sel_hi = oc + k.y; }
+      if (tile + 1 == sd.tile0 + sd.ntiles) { a.segout[s].out_hi = ob + kb; a.segout[s].sel_hi = oc + kc; }
     }
   }
 }
 
 // LDS per wave: the tile (16 B of front pad, 8 KiB, 32 B of back pad: the unaligned reads of
 // a piece start up to 15 B before its chunk and end up to 20 B after it), the kept runs
-// (src | dst << 16, tile-relative; a selected line carries a >= 20-B prefix, so at most
-// kTile / 20 + 2 runs), and the chunk -> first run map.
-constexpr int kTcRuns = kTile / 20 + 4;
-constexpr int kTcChunks = kTile / 16 + 2;
-__global__ __launch_bounds__(256) void k_tcopy(RunArgs a) {
+// (a selected line carries a >= 20-B prefix, so at most kTile / 20 + 2 runs), and the
+// chunk -> first run map.
+#ifndef KLF_TC_ABL
+#define KLF_TC_ABL 0  // timing builds: 1 no copy loop, 2 no map and no copy, 4 no tile loads
+#endif
+constexpr int kTcRuns = kTile / 20 + 8;     // + the two sentinels
+constexpr int kTcChunks = kTile / 16 + 8;   // 513 chunks at most, in groups of 8 (16-B LDS accesses)
+__global__ __launch_bounds__(256) void k_tcopy(RunArgs a, const uint4* __restrict__ trec,
+                                               const uint64_t* __restrict__ kbase, const uint32_t* __restrict__ truns) {
   __shared__ __attribute__((aligned(16))) uint8_t s_buf_all[4][kTile + 48];
   __shared__ uint32_t s_run_all[4][kTcRuns];
-  __shared__ uint16_t s_map_all[4][kTcChunks];
+  __shared__ __attribute__((aligned(16))) uint32_t s_map_all[4][kTcChunks];
   if (a.counters[2] || !a.counters[kCtrDense]) return;
   const int lane = threadIdx.x & 63;
   const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   uint8_t* s_buf = s_buf_all[wv] + 16;
   uint32_t* s_run = s_run_all[wv];
-  uint16_t* s_map = s_map_all[wv];
+  uint32_t* s_map = s_map_all[wv];
   const uint32_t* s32 = reinterpret_cast<const uint32_t*>(s_buf_all[wv]);  // dword k = s_buf[4k - 16]
-  for (uint32_t tile = blockIdx.x * 4 + wv; tile < a.ntiles; tile += gridDim.x * 4) {
-    const uint2 kt = a.tkeep[tile];
-    if (kt.x == 0) continue;
-    const TileLines g = tile_lines(a, tile);
-    const uint64_t obase = a.kbase[2 * tile];
-    // the tile's bytes: all loads in flight while the runs are worked out
-    const uint4* gp = reinterpret_cast<const uint4*>(a.bytes + g.sd.base + g.rel_lo);
-    uint4 v[8];
-#pragma unroll
-    for (int r = 0; r < 8; ++r) v[r] = gp[r * 64 + lane];
-    const uint64_t wlo = a.segout[g.s].win_lo, whi = a.segout[g.s].win_hi;
-    uint32_t nr = 0, dacc = 0;  // runs listed, kept bytes before the current group of lines
-    for (uint32_t j0 = 0; j0 < g.nl; j0 += 64) {
-      const uint32_t j = j0 + lane;
-      int64_t lo = 0, hi = 0, ls;
-      bool has = j < g.nl && line_run(a, g, wlo, whi, g.l0 + j, lo, hi, ls) && hi > lo;
-      const uint32_t len = has ? (uint32_t)(hi - lo) : 0u;
-      const uint32_t incl = wave_incl_scan_add(len, lane);
-      const uint64_t bm = __ballot(has);
-      if (has) {
-        const uint32_t idx = nr + (uint32_t)__popcll(bm & ((1ull << lane) - 1ull));
-        s_run[idx] = (uint32_t)(lo - g.rel_lo) | ((dacc + incl - len) << 16);
-      }
-      nr += (uint32_t)__popcll(bm);
-      dacc += (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+  const uint32_t stride = gridDim.x * 4;
+  // software pipeline: tile t's bytes and runs are in registers while tile t - stride is
+  // copied; the records run one tile further ahead
+  // (named registers: an array here is put on the scratch stack)
+#define KLF_TC_ROWS(X) X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7)
+#define KLF_TC_DECL(q) uint4 v##q = make_uint4(0, 0, 0, 0);
+#define KLF_TC_LOAD(q) v##q = gp[q * 64 + lane];
+#define KLF_TC_STORE(q) l[q * 64 + lane] = v##q;
+  KLF_TC_ROWS(KLF_TC_DECL)
+  uint32_t rw0 = 0, rw1 = 0;
+  auto load_rec = [&](uint32_t t) __attribute__((always_inline)) {  // one scalar 16-B load
+    const uint4 q = trec[t];
+    TRec r;
+    r.src = (uint64_t)q.x | ((uint64_t)q.y << 32);
+    r.kept = q.z;
+    r.nruns = (uint16_t)(q.w & 0xFFFFu);
+    r.nsel = (uint16_t)(q.w >> 16);
+    return r;
+  };
+  auto issue = [&](uint32_t t, const TRec& r) __attribute__((always_inline)) {
+    if (r.kept == 0) return;
+    const uint4* gp = reinterpret_cast<const uint4*>(a.bytes + r.src);
+    if (!(KLF_TC_ABL & 4)) { KLF_TC_ROWS(KLF_TC_LOAD) }
+    if (r.nruns != kRunsRecompute) {
+      const uint32_t* rp = truns + (size_t)t * kRunSlots;
+      rw0 = (uint32_t)lane < r.nruns ? rp[lane] : 0u;
+      rw1 = (uint32_t)lane + 64 < r.nruns ? rp[lane + 64] : 0u;
     }
-    {
+  };
+  uint32_t tile = blockIdx.x * 4 + wv;
+  TRec rec{}, nrec{};
+  uint64_t ob = 0, nob = 0;
+  if (tile < a.ntiles) {
+    rec = load_rec(tile);
+    ob = kbase[2 * tile];
+    issue(tile, rec);
+  }
+  if (tile + stride < a.ntiles) {
+    nrec = load_rec(tile + stride);
+    nob = kbase[2 * (tile + stride)];
+  }
+  for (; tile < a.ntiles; tile += stride) {
+    const TRec cr = rec;
+    const uint64_t obase = ob;
+    if (cr.kept) {
       uint4* l = reinterpret_cast<uint4*>(s_buf);
-#pragma unroll
-      for (int r = 0; r < 8; ++r) l[r * 64 + lane] = v[r];
+      KLF_TC_ROWS(KLF_TC_STORE)
+      if (cr.nruns != kRunsRecompute) {
+        if ((uint32_t)lane < cr.nruns) s_run[lane] = rw0;
+        if ((uint32_t)lane + 64 < cr.nruns) s_run[lane + 64] = rw1;
+      }
     }
-    const uint32_t kept = kt.x;
+    // the next tile's loads go out before this tile's copy
+    rec = nrec;
+    ob = nob;
+    const uint32_t nt = tile + stride;
+    if (nt < a.ntiles) issue(nt, rec);
+    if (nt + stride < a.ntiles) {
+      nrec = load_rec(nt + stride);
+      nob = kbase[2 * (nt + stride)];
+    }
+    if (!cr.kept) continue;
+    uint32_t nr = cr.nruns;
+    if (nr == kRunsRecompute) {  // more runs than the record holds: list them again here
+      const TileLines g = tile_lines(a, tile);
+      uint32_t kept, nsel;
+      nr = list_runs(a, g, a.segout[g.s].win_lo, a.segout[g.s].win_hi, s_run, kTcRuns, lane, &kept, &nsel);
+    }
+    const uint32_t kept = cr.kept;
     const uint32_t o15 = (uint32_t)(obase & 15u);
-    wave_lds_sync();
+    const uint32_t nch = (uint32_t)(((obase + kept + 15) >> 4) - (obase >> 4));
     // chunk c covers output [16 * (obase / 16 + c), +16); its first byte inside this tile's
-    // output, x0(c) = (c ? 16c - o15 : 0), lies in exactly one run
-    for (uint32_t k = lane; k < nr; k += 64) {
-      const uint32_t r = s_run[k], d = r >> 16;
-      const uint32_t e = k + 1 < nr ? (s_run[k + 1] >> 16) : kept;
-      if (d == 0) s_map[0] = (uint16_t)k;
-      for (uint32_t c = (d + o15 + 15) >> 4; 16 * c - o15 < e; ++c)
-        if (c) s_map[c] = (uint16_t)k;
+    // output, x0(c) = (c ? 16c - o15 : 0), lies in exactly one run.  The map: run k marks
+    // the first chunk whose x0 is at or past its start (LDS max: several short runs may
+    // mark one chunk; the last of them holds x0), then a running max over the chunks.
+    if (KLF_TC_ABL & 2) continue;
+    // two sentinel runs past the last (start = kept) spare the bounds checks below
+    if (lane < 2) s_run[nr + lane] = kept << 16;
+    for (uint32_t c = 8 * (uint32_t)lane; c < nch; c += 512) {
+      *reinterpret_cast<uint4*>(&s_map[c]) = make_uint4(0, 0, 0, 0);
+      *reinterpret_cast<uint4*>(&s_map[c + 4]) = make_uint4(0, 0, 0, 0);
     }
     wave_lds_sync();
-    const uint32_t nch = (uint32_t)(((obase + kept + 15) >> 4) - (obase >> 4));
+    for (uint32_t k = lane; k < nr; k += 64) {
+      const uint32_t d = s_run[k] >> 16;
+      const uint32_t c = d ? (d + o15 + 15) >> 4 : 0u;
+      if (c < nch) atomicMax(&s_map[c], k);
+    }
+    wave_lds_sync();
+    // running max: 8 consecutive entries per lane, one wave scan of the lanes' maxima
+    for (uint32_t c0 = 0, carry = 0; c0 < nch; c0 += 512) {
+      const uint32_t c = c0 + 8 * (uint32_t)lane;
+      uint4 p = *reinterpret_cast<const uint4*>(&s_map[c]), q = *reinterpret_cast<const uint4*>(&s_map[c + 4]);
+      auto mx = [](uint32_t x, uint32_t y) { return x > y ? x : y; };
+      p.y = mx(p.y, p.x); p.z = mx(p.z, p.y); p.w = mx(p.w, p.z);
+      q.x = mx(q.x, p.w); q.y = mx(q.y, q.x); q.z = mx(q.z, q.y); q.w = mx(q.w, q.z);
+      const uint32_t incl = mx(wave_incl_scan_max(q.w, lane), carry);
+      uint32_t pre = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)incl, 0x138, 0xF, 0xF, false);  // wave_shr:1
+      pre = mx(lane ? pre : 0u, carry);
+      p.x = mx(p.x, pre); p.y = mx(p.y, pre); p.z = mx(p.z, pre); p.w = mx(p.w, pre);
+      q.x = mx(q.x, pre); q.y = mx(q.y, pre); q.z = mx(q.z, pre); q.w = mx(q.w, pre);
+      if (c < nch) {
+        *reinterpret_cast<uint4*>(&s_map[c]) = p;
+        *reinterpret_cast<uint4*>(&s_map[c + 4]) = q;
+      }
+      carry = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+    }
+    wave_lds_sync();
+    if (KLF_TC_ABL & 1) continue;
     uint8_t* outc = a.out + ((obase >> 4) << 4);
-    for (uint32_t c = lane; c < nch; c += 64) {
-      const uint32_t x0 = c ? 16 * c - o15 : 0u;
-      const uint32_t x1 = (16 * c + 16 - o15) < kept ? 16 * c + 16 - o15 : kept;
-      uint32_t o[4] = {0u, 0u, 0u, 0u};
-      uint32_t k = s_map[c];
-      for (uint32_t x = x0; x < x1;) {
-        const uint32_t r = s_run[k], src = r & 0xFFFFu, d = r >> 16;
-        const uint32_t e = k + 1 < nr ? (s_run[k + 1] >> 16) : kept;
-        const uint32_t pe = e < x1 ? e : x1;
-        // the 16 bytes that land on chunk bytes 0..15 for this run: LDS from va on
-        const int32_t va = (int32_t)src + (int32_t)(x - d) - (int32_t)(x + o15 - 16 * c);
-        const int32_t wa = (va + 16) >> 2;  // dword index (the buffer starts 16 B early)
-        const uint32_t sh = (uint32_t)(va + 16) & 3u;
-        const uint32_t w0 = s32[wa], w1 = s32[wa + 1], w2 = s32[wa + 2], w3 = s32[wa + 3], w4 = s32[wa + 4];
-        const uint32_t y[4] = {__builtin_amdgcn_alignbyte(w1, w0, sh), __builtin_amdgcn_alignbyte(w2, w1, sh),
-                               __builtin_amdgcn_alignbyte(w3, w2, sh), __builtin_amdgcn_alignbyte(w4, w3, sh)};
-        const int b0 = (int)(x + o15 - 16 * c), b1 = (int)(pe + o15 - 16 * c);
+    // 16 B of run r's bytes as they land on the chunk whose byte 0 is tile output x0: the
+    // LDS window at any alignment (five dword reads + v_alignbyte; +16: the front pad)
+    auto window = [&](uint32_t r, uint32_t x0, uint32_t (&y)[4]) __attribute__((always_inline)) {
+      const int32_t va = (int32_t)(r & 0xFFFFu) + (int32_t)x0 - (int32_t)(r >> 16) + 16;
+      const int32_t wa = va >> 2;
+      const uint32_t w0 = s32[wa], w1 = s32[wa + 1], w2 = s32[wa + 2], w3 = s32[wa + 3], w4 = s32[wa + 4];
+      y[0] = __builtin_amdgcn_alignbyte(w1, w0, (uint32_t)va);
+      y[1] = __builtin_amdgcn_alignbyte(w2, w1, (uint32_t)va);
+      y[2] = __builtin_amdgcn_alignbyte(w3, w2, (uint32_t)va);
+      y[3] = __builtin_amdgcn_alignbyte(w4, w3, (uint32_t)va);
+    };
+    // Chunk bytes [b0, b1) (tile output x0 + b - b0 ...) of a chunk spanning any number of
+    // runs, starting with run k: piecewise (the head and tail chunks, and chunks of three
+    // or more runs).  o[] bytes outside [b0, b1) are left as they were.
+    auto pieces = [&](uint32_t k, uint32_t xs, uint32_t xe, uint32_t xc, uint32_t (&o)[4]) __attribute__((always_inline)) {
+      // xc = tile output position of chunk byte 0 (may be "negative": unsigned wrap)
+      for (uint32_t x = xs; x < xe; ++k) {
+        const uint32_t r = s_run[k];
+        const uint32_t e = s_run[k + 1] >> 16;
+        const uint32_t pe = e < xe ? e : xe;
+        uint32_t y[4];
+        window(r, xc, y);
+        const int b0 = (int)(x - xc), b1 = (int)(pe - xc);
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          const uint32_t m = byte_mask(b0, b1, q);
-          o[q] = (y[q] & m) | (o[q] & ~m);
+          const uint32_t mm = byte_mask(b0, b1, q);
+          o[q] = (y[q] & mm) | (o[q] & ~mm);
         }
         x = pe;
-        ++k;
       }
-      const int b0 = (int)(x0 + o15 - 16 * c), b1 = (int)(x1 + o15 - 16 * c);
-      if (b0 == 0 && b1 == 16) {
-        *reinterpret_cast<uint4*>(outc + 16 * (uint64_t)c) = make_uint4(o[0], o[1], o[2], o[3]);
-      } else {  // shared with a neighbouring tile: only this tile's bytes
-        for (int b = b0; b < b1; ++b) outc[16 * (uint64_t)c + b] = (uint8_t)(o[b >> 2] >> (8 * (b & 3)));
+    };
+    // interior chunks (all 16 bytes from this tile): c in [c_lo, c_end), x0 = 16c - o15
+    const uint32_t c_lo = o15 ? 1u : 0u, c_end = (kept + o15) >> 4;
+    for (uint32_t c = c_lo + lane; c < c_end; c += 64) {
+      const uint32_t x0 = 16 * c - o15, x1 = x0 + 16;
+      const uint32_t k = s_map[c];
+      const uint32_t r0 = s_run[k], r1 = s_run[k + 1], d2 = s_run[k + 2] >> 16;
+      uint32_t o[4];
+      if (x1 <= d2) {  // at most two runs: both windows, blended where run k + 1 starts
+        uint32_t y0[4], y1[4];
+        window(r0, x0, y0);
+        const uint32_t d1 = r1 >> 16;
+        const bool two = d1 < x1;
+        window(two ? r1 : r0, x0, y1);
+        const int32_t split8 = 8 * (two ? (int32_t)(d1 - x0) : 16);  // bits of the chunk from run k
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int32_t sq = split8 - 32 * q;
+          const uint32_t lo = sq <= 0 ? 0u : sq >= 32 ? ~0u : ((1u << sq) - 1u);
+          o[q] = (y0[q] & lo) | (y1[q] & ~lo);
+        }
+      } else {
+        o[0] = o[1] = o[2] = o[3] = 0u;
+        pieces(k, x0, x1, x0, o);
+      }
+      *reinterpret_cast<uint4*>(outc + 16 * (uint64_t)c) = make_uint4(o[0], o[1], o[2], o[3]);
+    }
+    // head / tail chunks shared with the neighbouring tiles: only this tile's bytes (lane 0
+    // the head chunk, lane 1 the tail chunk; one chunk holding both is the head's)
+    {
+      const uint32_t ct = (kept + o15) >> 4;
+      bool edge = false;
+      uint32_t c = 0, xs = 0, xe = 0;
+      if (lane == 0 && o15) {
+        edge = true;
+        xe = kept < 16 - o15 ? kept : 16 - o15;
+      }
+      if (lane == 1 && ((kept + o15) & 15u) && (ct > 0 || !o15)) {
+        edge = true;
+        c = ct;
+        xs = 16 * ct - o15;
+        xe = kept;
+      }
+      if (edge) {
+        const uint32_t xc = 16 * c - o15;  // tile output position of chunk byte 0 (wraps for c = 0)
+        uint32_t o[4] = {0u, 0u, 0u, 0u};
+        pieces(s_map[c], xs, xe, xc, o);
+        for (uint32_t x = xs; x < xe; ++x) {
+          const uint32_t b = x - xc;
+          outc[16 * (uint64_t)c + b] = (uint8_t)(o[b >> 2] >> (8 * (b & 3)));
+        }
       }
     }
     asm volatile("" ::: "memory");  // the next tile rewrites the wave's LDS
   }
+#undef KLF_TC_ROWS
+#undef KLF_TC_DECL
+#undef KLF_TC_LOAD
+#undef KLF_TC_STORE
 }
 
 // Gram statistics for the prefilter's window choice: every byte position of a sample of
@@ -2313,15 +2536,25 @@ static hipError_t launch_tail_stage(const RunArgs& a, hipStream_t st, hipEvent_t
   hipLaunchKernelGGL(k_cgather, dim3(num_cus * KLF_CG_GRID), dim3(kThreads), 0, st, a);
   KLF_TRY(hipGetLastError());
   if (a.compact_mode != 1) {
-    const uint32_t gk = (a.ntiles + 3) / 4;
-    hipLaunchKernelGGL(k_tkeep, dim3(gk < (uint32_t)num_cus * 8 ? gk : num_cus * 8), dim3(256), 0, st, a);
+    const uint32_t gk = (a.ntiles + 3) / 4, gt = (a.ntiles + 4 * kTkBatch - 1) / (4 * kTkBatch);
+    hipLaunchKernelGGL(k_tkeep, dim3(gt < (uint32_t)num_cus * 8 ? gt : num_cus * 8), dim3(256), 0, st, a,
+                       a.tile_seg, a.segs, a.tstat, a.tile_base, a.segout);
     KLF_TRY(hipGetLastError());
     const uint32_t nb = (a.ntiles + 4095) / 4096;
     hipLaunchKernelGGL(k_ksum<16>, dim3(nb), dim3(256), 0, st, a);
     KLF_TRY(hipGetLastError());
     hipLaunchKernelGGL(k_kbase<16>, dim3(nb), dim3(256), 0, st, a);
     KLF_TRY(hipGetLastError());
-    hipLaunchKernelGGL(k_tcopy, dim3(gk < (uint32_t)num_cus * 12 ? gk : num_cus * 12), dim3(256), 0, st, a);
+    // persistent grid: one resident generation of blocks, so every wave's prefetch
+    // pipeline runs over its whole share of tiles
+    static int occ = 0;
+    if (occ == 0) {
+      (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_tcopy, 256, 0);
+      occ = occ < 1 ? 1 : (occ > 8 ? 8 : occ);
+    }
+    const uint32_t gc = (uint32_t)num_cus * (uint32_t)occ;
+    hipLaunchKernelGGL(k_tcopy, dim3(gk < gc ? gk : gc), dim3(256), 0, st, a,
+                       reinterpret_cast<const uint4*>(a.trec), a.kbase, a.truns);
     KLF_TRY(hipGetLastError());
   }
 #undef KLF_TRY

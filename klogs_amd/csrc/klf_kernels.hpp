@@ -69,6 +69,20 @@ __host__ __device__ inline uint32_t qf_bits(uint32_t h1, uint32_t h2) {
   return (1u << ((h1 >> 15) & 31u)) | (1u << (h2 & 31u)) | (1u << ((h2 >> 5) & 31u));
 }
 
+// Dense compaction: per-tile copy record written by k_tkeep, read by k_ksum / k_kbase /
+// k_tcopy (16 B), and up to kRunSlots kept runs per tile (u32: tile offset of the run's
+// first byte | its offset in the tile's output << 16); a tile with more runs has
+// nruns = kRunsRecompute and k_tcopy lists them again from the line index.
+constexpr int kRunSlots = 128;
+constexpr uint16_t kRunsRecompute = 0xFFFF;
+struct TRec {
+  uint64_t src;    // batch offset of the tile's first byte
+  uint32_t kept;   // content bytes of selected lines inside the tile
+  uint16_t nruns;  // kept runs (or kRunsRecompute)
+  uint16_t nsel;   // selected lines starting in the tile
+};
+static_assert(sizeof(TRec) == 16, "TRec is one 16-B record");
+
 // Per-tile record of the scan (K1a), 16 B.
 struct TileStat {
   uint32_t events;     // line-end events in the tile
@@ -186,7 +200,8 @@ struct RunArgs {
   uint32_t qhits_cap;
   // dense compaction (most lines selected): per tile kept bytes / selected lines, their
   // exclusive prefixes (out offset, selected-line offset per tile)
-  uint2* tkeep;         // [ntiles]
+  struct TRec* trec;    // [ntiles] per-tile copy record (k_tkeep)
+  uint32_t* truns;      // [ntiles * kRunSlots] the tiles' kept runs (k_tkeep -> k_tcopy)
   uint64_t* kbase;      // [2 * ntiles]
   uint32_t compact_mode;  // 0 auto, 1 line gather (sparse), 2 tile copy (dense)
 };
