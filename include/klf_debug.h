@@ -24,6 +24,14 @@ int klf_debug_match(const klf_pattern* pats, uint32_t n, const uint8_t* content,
 int klf_debug_prefilter(const klf_pattern* pats, uint32_t n, const uint8_t* content, size_t len,
                         uint32_t phase, int* match, uint32_t* info);
 
+/* The required factor set of one regex (SPEC.md S5) as the prefilter uses it: the
+ * strings '\0'-separated into buf (cap bytes), *pre = bound on the distance from a match's
+ * start to its first factor occurrence (0xFFFFFFFF: none), *loose = compared OR 0x20;
+ * want = the shortest string length preferred (0 = the longest set).  *n = strings.
+ * KLF_EINVAL when the regex has no factor. */
+int klf_debug_factors(const uint8_t* pat, size_t len, uint32_t want, char* buf, size_t cap, uint32_t* n,
+                      uint32_t* pre, uint32_t* loose);
+
 #ifdef __cplusplus
 }
 #endif

@@ -97,7 +97,7 @@ struct klf_engine {
   DevBuf d_asm;                        // k_assemble piece table
   DevBuf d_scratch;                    // small query results (klf_result_last_unparsed)
   // device pattern tables
-  DevBuf d_lit, d_ac_class, d_ac_next, d_ac_accept, d_rx_class, d_rx_b, d_rx_follow, d_rx_vec, d_rx_flags;
+  DevBuf d_lit, d_ac_class, d_ac_next, d_ac_accept, d_rx_class, d_rx_b, d_rx_follow, d_rx_vec, d_rx_flags, d_rx_pre;
   DevBuf d_qf_bitmap, d_qf_head, d_qf_ent, d_qf_nbytes, d_cand, d_rx_vec4, d_qhits, d_hslots, d_hist, d_hflat;
   uint32_t cand_cap = 1u << 22;  // NFA candidate queue (32 MiB); overflow -> k_match
   uint64_t hits_cap_max = 1u << 26;  // prefilter hit list (512 MiB at most); overflow -> k_match
@@ -250,7 +250,9 @@ extern "C" int klf_open(const klf_config* cfg, klf_engine** out) {
           (h = upload(e->d_rx_b, cs.rx_b, st)) != hipSuccess ||
           (h = upload(e->d_rx_follow, cs.rx_follow, st)) != hipSuccess ||
           (h = upload(e->d_rx_vec, vec, st)) != hipSuccess ||
-          (h = upload(e->d_rx_flags, cs.rx_flags, st)) != hipSuccess) {
+          (h = upload(e->d_rx_flags, cs.rx_flags, st)) != hipSuccess ||
+          (h = upload(e->d_rx_pre, cs.rx_pre.empty() ? std::vector<uint32_t>(cs.rx_count, klf::kRxPreUnbounded) : cs.rx_pre,
+                      st)) != hipSuccess) {
         *out = e;
         return hip_err(e, h, "upload regex tables");
       }
@@ -263,6 +265,9 @@ extern "C" int klf_open(const klf_config* cfg, klf_engine** out) {
       P.rx_init0 = v + 2 * cs.rx_count;
       P.rx_end = v + 3 * cs.rx_count;
       P.rx_flags = e->d_rx_flags.as<uint32_t>();
+      P.rx_pre = e->d_rx_pre.as<uint32_t>();
+      P.rx_unbounded = cs.rx_pre.empty() ? cs.rx_count
+                                         : (uint32_t)std::count(cs.rx_pre.begin(), cs.rx_pre.end(), klf::kRxPreUnbounded);
       std::vector<uint64_t> vec4;  // [rx][4] interleaved for k_nfa
       for (uint32_t r = 0; r < cs.rx_count; ++r)
         for (const auto* v : {&cs.rx_first, &cs.rx_last, &cs.rx_init0, &cs.rx_end}) vec4.push_back((*v)[r]);
@@ -306,7 +311,7 @@ extern "C" void klf_close(klf_engine* e) {
   if (e->stream) (void)hipStreamSynchronize(e->stream);
   if (e->copy_stream) (void)hipStreamSynchronize(e->copy_stream);
   for (DevBuf* b : {&e->d_lit, &e->d_ac_class, &e->d_ac_next, &e->d_ac_accept, &e->d_rx_class, &e->d_rx_b,
-                    &e->d_rx_follow, &e->d_rx_vec, &e->d_rx_flags, &e->d_qf_bitmap, &e->d_qf_head,
+                    &e->d_rx_follow, &e->d_rx_vec, &e->d_rx_flags, &e->d_rx_pre, &e->d_qf_bitmap, &e->d_qf_head,
                     &e->d_qf_ent, &e->d_qf_nbytes, &e->d_rx_vec4, &e->d_qhits, &e->d_hslots, &e->d_hist, &e->d_hflat, &e->d_cand, &e->d_batch, &e->d_segs, &e->d_tstat,
                     &e->d_slots, &e->d_pool, &e->d_tile_base, &e->d_bsum, &e->d_cstatus, &e->d_counters, &e->d_cmap, &e->d_cseg,
                     &e->d_line_off, &e->d_meta, &e->d_bits, &e->d_segout, &e->d_wpre, &e->d_out, &e->d_tile_seg, &e->d_mpart, &e->d_trec, &e->d_truns, &e->d_kbase})
@@ -604,7 +609,7 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
   uint32_t compact_mode = 0;  // tests: force either compaction path
   if (const char* v = getenv("KLF_COMPACT")) compact_mode = !strcmp(v, "sparse") ? 1u : !strcmp(v, "dense") ? 2u : 0u;
   const bool need_cand = mode == klf::CompiledSet::kGeneral && e->cs.qf_on && e->cs.rx_count;
-  if (need_cand) HIPCHK(e, e->d_cand.ensure((size_t)e->cand_cap * 8), "alloc cand");
+  if (need_cand) HIPCHK(e, e->d_cand.ensure((size_t)e->cand_cap * 16), "alloc cand");
   const bool need_hits = mode == klf::CompiledSet::kGeneral && e->cs.qf_on;
   // bitmap hits: < 1 per 8 KiB tile on log text, kHitSlots per tile recorded in place;
   // spills beyond 1 per 1 KiB of input -> k_match decides
@@ -1214,4 +1219,24 @@ extern "C" int klf_debug_compile(const klf_pattern* pats, uint32_t n, uint32_t* 
   if (err && err_cap) { strncpy(err, e.c_str(), err_cap - 1); err[err_cap - 1] = 0; }
   *mode = (uint32_t)cs.mode;
   return ok ? KLF_OK : code;
+}
+
+extern "C" int klf_debug_factors(const uint8_t* pat, size_t len, uint32_t want, char* buf, size_t cap, uint32_t* n,
+                                 uint32_t* pre, uint32_t* loose) {
+  if ((len && !pat) || (cap && !buf) || !n || !pre || !loose) return KLF_EINVAL;
+  std::vector<std::string> alts;
+  bool l = false;
+  uint32_t p = 0;
+  if (!klf::regex_factors(pat, len, alts, l, &p, want ? want : SIZE_MAX)) return KLF_EINVAL;
+  size_t o = 0;
+  for (auto& a : alts) {
+    if (o + a.size() + 1 > cap) return KLF_ETOOBIG;
+    memcpy(buf + o, a.data(), a.size());
+    o += a.size();
+    buf[o++] = 0;
+  }
+  *n = (uint32_t)alts.size();
+  *pre = p;
+  *loose = l ? 1u : 0u;
+  return KLF_OK;
 }

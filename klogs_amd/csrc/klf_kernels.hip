@@ -1123,7 +1123,10 @@ __device__ void verify_hit(const RunArgs& a, uint32_t tile, uint32_t s, int32_t 
     }
     if ((a.bits[l >> 5] >> (l & 31)) & 1u) continue;
     const uint32_t qi = atomicAdd(&a.counters[kCtrQueue], 1u);
-    if (qi < a.cand_cap) a.cand[qi] = l | ((uint64_t)E.z << 40);
+    if (qi < a.cand_cap) {
+      a.cand[2 * (size_t)qi] = l | ((uint64_t)E.z << 40);
+      a.cand[2 * (size_t)qi + 1] = (uint64_t)(rel_lo + x);  // the occurrence (stream offset)
+    }
     else atomicOr(&a.counters[kCtrQOver], 1u);
   }
 }
@@ -1269,9 +1272,10 @@ __global__ __launch_bounds__(256) void k_nfa(RunArgs a) {
   const int lane = threadIdx.x & 63;
   const uint32_t nw = gridDim.x * (blockDim.x / 64);
   for (uint32_t i = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6); i < nq; i += nw) {
-    const uint64_t e = a.cand[i];
+    const uint64_t e = a.cand[2 * (size_t)i];
     const uint64_t l = e & ((1ull << 40) - 1);
     const uint32_t r = (uint32_t)(e >> 40);
+    if (P.rx_pre[r] != kRxPreNone) continue;  // bounded window: k_nfa_win
     const uint32_t s = find_seg_by_line(a.segout, a.nsegs, l);
     if ((a.bits[l >> 5] >> (l & 31)) & 1u) continue;
     const uint16_t m = a.meta[l];
@@ -1284,6 +1288,80 @@ __global__ __launch_bounds__(256) void k_nfa(RunArgs a) {
     if (ce <= cs) continue;  // factor-bearing regexes never match empty content
     const bool hit = (P.rx_flags[r] & 1u) || nfa_wave(T, r, segp + cs, ce - cs, lane);
     if (hit && lane == 0) atomicOr(&a.bits[l >> 5], 1u << (l & 31));
+  }
+}
+
+// K2c: the windowed NFA (regexes whose factor set bounds the match start, rx_pre): one
+// thread per candidate occurrence x.  Matches holding that occurrence start in
+// [x - rx_pre, x]; the run enters `first` only up to x and stops as soon as the entered
+// set dies (or at the content's end, where the EOT closure decides).  Every match holds
+// its first factor occurrence and every occurrence is a candidate, so the union of the
+// windows decides the line (klf_patterns.cpp nfa_window is the host twin).  Tens of bytes
+// per candidate instead of the whole (1-32 KiB) line.
+template <bool LDS>
+__global__ __launch_bounds__(256) void k_nfa_win(RunArgs a) {
+  extern __shared__ uint64_t s_nfa[];
+  if (a.counters[2] || a.counters[kCtrQOver] || a.counters[kCtrHitsOver]) return;
+  const uint32_t nq = a.counters[kCtrQueue] < a.cand_cap ? a.counters[kCtrQueue] : a.cand_cap;
+  if (nq == 0) return;
+  const DevPatterns& P = a.pats;
+  const uint32_t R = P.rx_count, C = P.rx_classes, FS = LDS ? P.rx_maxpos : 64;
+  NfaTables T;
+  if (LDS) {
+    uint64_t* sb = s_nfa;
+    uint64_t* sf = sb + (size_t)R * C;
+    uint64_t* sv = sf + (size_t)R * FS;
+    uint8_t* sc = reinterpret_cast<uint8_t*>(sv + 4 * (size_t)R);
+    for (uint32_t i = threadIdx.x; i < R * C; i += blockDim.x) sb[i] = P.rx_b[i];
+    for (uint32_t i = threadIdx.x; i < R * FS; i += blockDim.x) sf[i] = P.rx_follow[(size_t)(i / FS) * 64 + i % FS];
+    for (uint32_t i = threadIdx.x; i < R; i += blockDim.x) {
+      sv[4 * i] = P.rx_first[i];
+      sv[4 * i + 1] = P.rx_last[i];
+      sv[4 * i + 2] = P.rx_init0[i];
+      sv[4 * i + 3] = P.rx_end[i];
+    }
+    for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) sc[i] = P.rx_class[i];
+    __syncthreads();
+    T = NfaTables{sc, sb, sf, sv, C, FS};
+  } else {
+    T = NfaTables{P.rx_class, P.rx_b, P.rx_follow, P.rx_vec, C, 64};
+  }
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nq; i += gridDim.x * blockDim.x) {
+    const uint64_t e = a.cand[2 * (size_t)i];
+    const uint64_t l = e & ((1ull << 40) - 1);
+    const uint32_t r = (uint32_t)(e >> 40);
+    const uint32_t pre = P.rx_pre[r];
+    if (pre == kRxPreNone) continue;  // k_nfa runs those over the whole line
+    if ((a.bits[l >> 5] >> (l & 31)) & 1u) continue;
+    const uint16_t m = a.meta[l];
+    if (!(m & Meta::kParsed)) continue;
+    const uint32_t s = find_seg_by_line(a.segout, a.nsegs, l);
+    const uint8_t* segp = a.bytes + a.segs[s].base;
+    const uint64_t ls = a.line_off[l + s], le = a.line_off[l + s + 1];
+    const uint64_t cs = ls + line_plen(a, m, segp, ls, le);
+    uint64_t ce = le;
+    if (ce > cs && segp[ce - 1] == '\n') --ce;
+    const uint64_t x = a.cand[2 * (size_t)i + 1];
+    if (x < cs || x >= ce) continue;  // an occurrence in the timestamp prefix: no match holds it
+    bool hit = (P.rx_flags[r] & 1u) != 0;
+    if (!hit) {
+      const uint64_t* V = T.vec + 4 * (size_t)r;
+      const uint64_t first = V[0], lastm = V[1];
+      const uint64_t* B = T.b + (size_t)r * T.classes;
+      const uint64_t* F = T.fol + (size_t)r * T.fstride;
+      const uint64_t ws = x - cs > pre ? x - pre : cs;
+      uint64_t d = ws == cs ? V[2] : first;
+      uint64_t p = ws;
+      for (; p < ce && d; ++p) {
+        const uint64_t c = d & B[T.cls[segp[p]]];
+        if (c & lastm) { hit = true; break; }
+        uint64_t nd = p + 1 <= x ? first : 0ull;
+        for (uint64_t mm = c; mm; mm &= mm - 1) nd |= F[__ffsll((unsigned long long)mm) - 1];
+        d = nd;
+      }
+      if (!hit && p == ce) hit = (d & V[3]) != 0;
+    }
+    if (hit) atomicOr(&a.bits[l >> 5], 1u << (l & 31));
   }
 }
 
@@ -2495,10 +2573,17 @@ hipError_t launch_pipeline(const RunArgs& a, hipStream_t st, hipEvent_t* ev, int
   }
   if (a.grep_mode == kGrepGeneral && a.pats.qf_on && a.pats.rx_count) {
     const size_t lds = nfa_lds_bytes(a.pats);
-    if (lds <= kNfaMaxLds)
-      hipLaunchKernelGGL(k_nfa<true>, dim3(num_cus * 4), dim3(256), lds, st, a);
-    else
-      hipLaunchKernelGGL(k_nfa<false>, dim3(num_cus * 4), dim3(256), 0, st, a);
+    if (lds <= kNfaMaxLds) {
+      if (a.pats.rx_unbounded < a.pats.rx_count)
+        hipLaunchKernelGGL(k_nfa_win<true>, dim3(num_cus * 2), dim3(256), lds, st, a);
+      KLF_TRY(hipGetLastError());
+      if (a.pats.rx_unbounded) hipLaunchKernelGGL(k_nfa<true>, dim3(num_cus * 4), dim3(256), lds, st, a);
+    } else {
+      if (a.pats.rx_unbounded < a.pats.rx_count)
+        hipLaunchKernelGGL(k_nfa_win<false>, dim3(num_cus * 2), dim3(256), 0, st, a);
+      KLF_TRY(hipGetLastError());
+      if (a.pats.rx_unbounded) hipLaunchKernelGGL(k_nfa<false>, dim3(num_cus * 4), dim3(256), 0, st, a);
+    }
     KLF_TRY(hipGetLastError());
   }
   if (a.grep_mode == kGrepGeneral || a.grep_mode == kGrepAll) {

@@ -47,7 +47,8 @@ constexpr uint32_t kCtrDense = 14;                   // counters[14]: dense comp
 constexpr uint32_t kQfRegex = 1u << 24;              // entry flags: regex factor (else literal)
 constexpr uint32_t kQfLoose = 1u << 25;              //   compare OR 0x20 per byte
 constexpr size_t kNfaMaxLds = 64 * 1024;            // k_nfa stages its tables in LDS up to this
-constexpr uint32_t kCarryBias = 256;                 // TileStat.carry_off = hit offset + 1 + bias
+constexpr uint32_t kCarryBias = 256;
+constexpr uint32_t kRxPreNone = 0xFFFFFFFFu;         // rx_pre: no bound (= klf_patterns.hpp kRxPreUnbounded)                 // TileStat.carry_off = hit offset + 1 + bias
 // Blocked Bloom filter, one 32-bit bitmap word per probe.  The gram is folded to 24 bits
 // (byte 3 xor-ed into bits 11..18) so that both hashes are full-rate 24-bit multiplies:
 // word = top 12 bits of the low product (also the verification bucket), three bits inside
@@ -137,7 +138,9 @@ struct DevPatterns {  // device copies of CompiledSet tables (kGrepGeneral)
   const uint64_t* rx_end = nullptr;
   const uint64_t* rx_vec = nullptr;   // [rx_count][4]: first, last, init0, end
   const uint32_t* rx_flags = nullptr;
+  const uint32_t* rx_pre = nullptr;   // [rx_count] match start -> first factor occurrence bound
   uint32_t rx_count = 0, rx_classes = 0, rx_maxpos = 64;
+  uint32_t rx_unbounded = 0;          // regexes without a bound (k_nfa runs their whole lines)
   // q-gram prefilter (qf_on): bitmap, buckets, needles
   uint32_t qf_on = 0, qf_stride = 1, qf_fold = 0, qf_mask = ~0u;
   const uint32_t* qf_bitmap = nullptr;
@@ -191,7 +194,8 @@ struct RunArgs {
   uint8_t* out;         // output bytes (capacity >= total input)
   uint32_t max_cblocks; // compaction block capacity
   uint32_t stage_times; // record the inner stage events (ev[2..4])
-  uint64_t* cand;       // [cand_cap] NFA candidates: global line index | regex << 40
+  uint64_t* cand;       // [2 * cand_cap] NFA candidates: {global line index | regex << 40,
+                        //  stream offset of the factor occurrence}
   uint32_t cand_cap;
   uint16_t* hslots;     // [ntiles * kHitSlots] prefilter hits (tile offsets of the samples)
   uint32_t* hflat;      // [hflat_cap] hit slot ids (tile * kHitSlots + j), flattened by k_tbase

@@ -580,13 +580,30 @@ uint64_t closure(uint64_t entered, uint64_t holds, const std::vector<uint64_t>& 
 // one ASCII case pair counts as one byte; zero-width assertions are ""), and `req`, an
 // OR-set of strings one of which every match contains.  Case pairs make the factor loose
 // (stored OR 0x20).  The same analysis as RE2's prefilter, restricted to what the q-gram
-// scan can use: the best set maximises its shortest alternative.
+// scan can use.
+//
+// Each set also carries `pre`: an upper bound on the distance from the start of a match
+// of the node to the start of the first factor occurrence in it (kUnbounded when a
+// repetition precedes it).  The GPU runs the NFA only over a window around each factor
+// occurrence the prefilter verified: match starts in [x - pre, x], then on without new
+// starts until the automaton dies (every match holds its first factor occurrence, and
+// each occurrence is a candidate of its own), instead of over the whole line.
+//
+// Choice among a node's sets: those with at least `want` bytes in their shortest string
+// first (the sampling stride of the whole pattern set needs that many; regex_factors runs
+// the analysis once with want = unbounded to find each regex's best length), then a
+// bounded `pre`, then the longest shortest string, then fewer strings.
+constexpr uint32_t kUnbounded = 0xFFFFFFFFu;
+uint32_t sat_add(uint32_t a, uint32_t b) { return (a == kUnbounded || b == kUnbounded) ? kUnbounded : a + b; }
+
 struct FInfo {
   bool has_exact = false;
   std::string exact;
   bool exact_loose = false;
   std::vector<std::string> req;
   bool req_loose = false;
+  uint32_t req_pre = kUnbounded;
+  uint32_t maxlen = 0;  // longest match of the node (kUnbounded: no bound)
 };
 
 size_t req_score(const std::vector<std::string>& r) {
@@ -596,21 +613,36 @@ size_t req_score(const std::vector<std::string>& r) {
   return m;
 }
 
-void consider(FInfo& f, const std::vector<std::string>& r, bool loose) {
+struct FactorCtx {
+  size_t want = SIZE_MAX;  // shortest string the stride needs
+};
+
+void consider(const FactorCtx& cx, FInfo& f, const std::vector<std::string>& r, bool loose, uint32_t pre) {
   const size_t a = req_score(r), b = req_score(f.req);
-  if (a > b || (a == b && a > 0 && r.size() < f.req.size())) {
+  if (a == 0) return;
+  auto key = [&](size_t len, uint32_t p, size_t n) {
+    return std::make_tuple(len >= cx.want ? 1 : 0, (len >= cx.want && p != kUnbounded) ? 1 : 0, len,
+                           -(long)n);
+  };
+  if (b == 0 || key(a, pre, r.size()) > key(b, f.req_pre, f.req.size())) {
     f.req = r;
     f.req_loose = loose;
+    f.req_pre = pre;
   }
 }
 
-std::vector<std::string> req_or_exact(const FInfo& f, bool& loose) {
-  if (f.has_exact) { loose = f.exact_loose; return {f.exact}; }
+std::vector<std::string> req_or_exact(const FInfo& f, bool& loose, uint32_t* pre = nullptr) {
+  if (f.has_exact) {
+    loose = f.exact_loose;
+    if (pre) *pre = 0;
+    return {f.exact};
+  }
   loose = f.req_loose;
+  if (pre) *pre = f.req_pre;
   return f.req;
 }
 
-FInfo factor_of(const std::vector<RNode>& pool, int x) {
+FInfo factor_of(const FactorCtx& cx, const std::vector<RNode>& pool, int x) {
   const RNode& n = pool[x];
   FInfo f;
   switch (n.k) {
@@ -618,6 +650,7 @@ FInfo factor_of(const std::vector<RNode>& pool, int x) {
       f.has_exact = true;
       return f;
     case RNode::kSet: {
+      f.maxlen = 1;
       const size_t c = n.set.count();
       int b0 = -1, b1 = -1;
       for (int b = 0; b < 256 && c <= 2; ++b)
@@ -635,78 +668,106 @@ FInfo factor_of(const std::vector<RNode>& pool, int x) {
     case RNode::kCat: {
       std::string run;
       bool run_loose = false, all = true;
+      uint32_t off = 0, run_pre = 0;  // offset of the kid (bound), of the current exact run
       for (int k : n.kids) {
-        const FInfo kf = factor_of(pool, k);
-        consider(f, kf.req, kf.req_loose);
+        const FInfo kf = factor_of(cx, pool, k);
+        consider(cx, f, kf.req, kf.req_loose, sat_add(off, kf.req_pre));
         if (kf.has_exact) {
+          if (run.empty()) run_pre = off;
           run += kf.exact;
           run_loose |= kf.exact_loose;
         } else {
-          if (!run.empty()) consider(f, {run}, run_loose);
+          if (!run.empty()) consider(cx, f, {run}, run_loose, run_pre);
           run.clear();
           run_loose = false;
           all = false;
         }
+        off = sat_add(off, kf.maxlen);
       }
-      if (!run.empty()) consider(f, {run}, run_loose);
+      if (!run.empty()) consider(cx, f, {run}, run_loose, run_pre);
       if (all) { f.has_exact = true; f.exact = run; f.exact_loose = run_loose; }
+      f.maxlen = off;
       return f;
     }
     case RNode::kAlt: {
       std::vector<std::string> u;
       bool loose = false;
+      uint32_t pre = 0;
+      bool none = false;
       for (int k : n.kids) {
         bool l = false;
-        const std::vector<std::string> r = req_or_exact(factor_of(pool, k), l);
-        if (req_score(r) == 0) return f;  // some branch needs no byte at all
+        uint32_t p = 0;
+        const FInfo kf = factor_of(cx, pool, k);
+        f.maxlen = std::max(f.maxlen, kf.maxlen);
+        const std::vector<std::string> r = req_or_exact(kf, l, &p);
+        if (req_score(r) == 0) { none = true; continue; }  // some branch needs no byte at all
         loose |= l;
+        pre = std::max(pre, p);
         for (auto& s : r)
           if (std::find(u.begin(), u.end(), s) == u.end()) u.push_back(s);
       }
-      if (u.size() <= 16) { f.req = u; f.req_loose = loose; }
+      if (!none && u.size() <= 16) { f.req = u; f.req_loose = loose; f.req_pre = pre; }
       return f;
     }
     case RNode::kPlus: {
-      f.req = req_or_exact(factor_of(pool, n.kids[0]), f.req_loose);
+      const FInfo kf = factor_of(cx, pool, n.kids[0]);
+      f.req = req_or_exact(kf, f.req_loose, &f.req_pre);  // the first repetition holds one
+      f.maxlen = kf.maxlen == 0 ? 0 : kUnbounded;
       return f;
     }
     case RNode::kRepeat: {
+      const FInfo kf = factor_of(cx, pool, n.kids[0]);
+      f.maxlen = n.hi < 0 ? (kf.maxlen == 0 ? 0 : kUnbounded)
+                          : (kf.maxlen == kUnbounded ? kUnbounded : kf.maxlen * (uint32_t)n.hi);
       if (n.lo == 0) return f;
-      const FInfo kf = factor_of(pool, n.kids[0]);
       if (kf.has_exact) {
         std::string rep;
         for (int r = 0; r < n.lo && rep.size() <= kQfMaxFactor; ++r) rep += kf.exact;
         if (n.hi == n.lo) { f.has_exact = true; f.exact = rep; f.exact_loose = kf.exact_loose; }
-        else { f.req = {rep}; f.req_loose = kf.exact_loose; }
+        else { f.req = {rep}; f.req_loose = kf.exact_loose; f.req_pre = 0; }
         if (rep.empty()) f.req.clear();
       } else {
         f.req = kf.req;
         f.req_loose = kf.req_loose;
+        f.req_pre = kf.req_pre;
       }
       return f;
     }
-    default:  // kStar, kQuest: a match may skip the node
+    case RNode::kStar: {
+      const FInfo kf = factor_of(cx, pool, n.kids[0]);
+      f.maxlen = kf.maxlen == 0 ? 0 : kUnbounded;
       return f;
+    }
+    default: {  // kQuest: a match may skip the node
+      f.maxlen = factor_of(cx, pool, n.kids[0]).maxlen;
+      return f;
+    }
   }
 }
 
 }  // namespace
 
-bool regex_factors(const uint8_t* pat, size_t n, std::vector<std::string>& alts, bool& loose) {
+bool regex_factors(const uint8_t* pat, size_t n, std::vector<std::string>& alts, bool& loose, uint32_t* pre,
+                   size_t want) {
   alts.clear();
   loose = false;
+  if (pre) *pre = kUnbounded;
   Parser ps(pat, n);
   const int root = ps.parse();
   if (root < 0) return false;
-  alts = req_or_exact(factor_of(ps.pool, root), loose);
+  FactorCtx cx;
+  cx.want = want;
+  uint32_t p = kUnbounded;
+  alts = req_or_exact(factor_of(cx, ps.pool, root), loose, &p);
   if (req_score(alts) == 0) { alts.clear(); return false; }
   for (auto& s : alts) {
-    if (s.size() > kQfMaxFactor) s.resize(kQfMaxFactor);  // a substring of a factor is one too
+    if (s.size() > kQfMaxFactor) s.resize(kQfMaxFactor);  // a substring of a factor is one too (its own start: same pre)
     if (loose)
       for (auto& c : s) c = (char)((uint8_t)c | 0x20);
   }
   std::sort(alts.begin(), alts.end());
   alts.erase(std::unique(alts.begin(), alts.end()), alts.end());
+  if (pre) *pre = p;
   return true;
 }
 
@@ -800,7 +861,14 @@ bool compile_set(const std::vector<std::vector<uint8_t>>& pats, const std::vecto
   std::vector<GlushkovTables> rxs;
   std::vector<std::vector<std::string>> rx_fac;  // required factors per regex (prefilter)
   std::vector<bool> rx_loose;
+  std::vector<uint32_t> rx_pre;
+  std::vector<size_t> rx_src;  // pattern index of each kept regex
   bool always = false;
+  auto drop_nl = [](std::vector<std::string>& alts) {  // content never holds '\n'
+    alts.erase(std::remove_if(alts.begin(), alts.end(),
+                              [](const std::string& f) { return f.find('\n') != std::string::npos; }),
+               alts.end());
+  };
   for (size_t k = 0; k < pats.size(); ++k) {
     if (kinds[k] == KLF_PAT_LITERAL) {
       const auto& l = pats[k];
@@ -817,15 +885,16 @@ bool compile_set(const std::vector<std::vector<uint8_t>>& pats, const std::vecto
       rxs.push_back(std::move(g));
       std::vector<std::string> alts;
       bool loose = false;
-      if (regex_factors(pats[k].data(), pats[k].size(), alts, loose)) {
-        // content never holds '\n': such alternatives cannot occur; none left = no match ever
-        alts.erase(std::remove_if(alts.begin(), alts.end(),
-                                  [](const std::string& f) { return f.find('\n') != std::string::npos; }),
-                   alts.end());
+      uint32_t pre = kRxPreUnbounded;
+      if (regex_factors(pats[k].data(), pats[k].size(), alts, loose, &pre)) {
+        // such alternatives cannot occur; none left = no match ever
+        drop_nl(alts);
         if (alts.empty()) { rxs.pop_back(); continue; }
       }
       rx_fac.push_back(alts);
       rx_loose.push_back(loose);
+      rx_pre.push_back(pre);
+      rx_src.push_back(k);
     } else {
       err = "unknown pattern kind";
       err_code = KLF_EINVAL;
@@ -837,6 +906,30 @@ bool compile_set(const std::vector<std::vector<uint8_t>>& pats, const std::vecto
     err_code = KLF_ETOOBIG;
     return false;
   }
+  {  // second pass: the sampling stride follows the shortest needle of the first pass; keep
+     // it, and per regex prefer factor sets with a bounded match-start window (rx_pre)
+    size_t g = SIZE_MAX;
+    for (auto& l : lits) g = std::min(g, l.size());
+    for (auto& f : rx_fac)
+      for (auto& x : f) g = std::min(g, x.size());
+    const size_t want = g >= 10 ? 10 : g >= 6 ? 6 : g >= 4 ? 4 : 3;  // = build_prefilter's stride rule
+    for (size_t r = 0; r < rx_fac.size(); ++r) {
+      if (rx_fac[r].empty()) continue;
+      std::vector<std::string> alts;
+      bool loose = false;
+      uint32_t pre = kRxPreUnbounded;
+      const size_t k = rx_src[r];
+      if (!regex_factors(pats[k].data(), pats[k].size(), alts, loose, &pre, want)) continue;
+      drop_nl(alts);
+      size_t m = SIZE_MAX;
+      for (auto& x : alts) m = std::min(m, x.size());
+      if (alts.empty() || m < want) continue;
+      rx_fac[r] = alts;
+      rx_loose[r] = loose;
+      rx_pre[r] = pre;
+    }
+  }
+  out.rx_pre = rx_pre;
   if (always) { out.mode = CompiledSet::kAll; return true; }
   // dedupe literals
   std::sort(lits.begin(), lits.end());
@@ -1083,11 +1176,28 @@ void place_needles(CompiledSet& out, const std::vector<uint32_t>* hist) {
   out.qf_head[buckets.size()] = (uint32_t)(out.qf_ent.size() / 4);
 }
 
+bool nfa_window(const CompiledSet& cs, uint32_t r, const uint8_t* s, size_t n, size_t x) {
+  // matches holding the factor occurrence at x start in [x - pre, x]; past x no new start
+  // is entered and the run ends when the automaton dies
+  const uint32_t pre = cs.rx_pre.empty() ? kRxPreUnbounded : cs.rx_pre[r];
+  const size_t ws = (pre == kRxPreUnbounded || (size_t)pre >= x) ? 0 : x - pre;
+  const uint64_t first = cs.rx_first[r];
+  uint64_t d = ws == 0 ? cs.rx_init0[r] : first;
+  for (size_t i = ws; i < n; ++i) {
+    const uint64_t c = d & cs.rx_b[(size_t)r * cs.rx_classes + cs.rx_class[s[i]]];
+    if (c & cs.rx_last[r]) return true;
+    uint64_t nd = i + 1 <= x ? first : 0;
+    for (uint64_t m = c; m; m &= m - 1) nd |= cs.rx_follow[(size_t)r * 64 + __builtin_ctzll(m)];
+    d = nd;
+    if (!d) return false;
+  }
+  return (d & cs.rx_end[r]) != 0;
+}
+
 bool prefilter_match(const CompiledSet& cs, const uint8_t* s, size_t n, uint32_t phase) {
   // Any window of S consecutive positions holds a sample, and every needle's chosen
   // window is q + S - 1 long, so each occurrence spans one sample with its gram inside
   // the window (the scan's tiles own their samples; the occurrence may start before).
-  std::vector<uint8_t> cand(cs.rx_count, 0);
   const uint32_t S = cs.qf_stride;
   for (size_t p = phase % S; p < n; p += S) {
     uint32_t g = 0;
@@ -1107,23 +1217,9 @@ bool prefilter_match(const CompiledSet& cs, const uint8_t* s, size_t n, uint32_t
       for (uint32_t j = 0; j < m && eq; ++j) eq = (uint8_t)(s[x + j] | lm) == nb[j];
       if (!eq) continue;
       if (!(E[1] & kQfRegex)) return true;  // literal: final
-      cand[E[2]] = 1;
+      // regex factor occurrence: the NFA over its window (k_nfa on the GPU)
+      if ((cs.rx_flags[E[2]] & 1u) || nfa_window(cs, E[2], s, n, (size_t)x)) return true;
     }
-  }
-  for (uint32_t r = 0; r < cs.rx_count; ++r) {
-    if (!cand[r]) continue;
-    const uint32_t fl = cs.rx_flags[r];
-    if (n == 0) { if (fl & 2u) return true; continue; }
-    if (fl & 1u) return true;
-    uint64_t d = cs.rx_init0[r];
-    for (size_t i = 0; i < n; ++i) {
-      const uint64_t c = d & cs.rx_b[(size_t)r * cs.rx_classes + cs.rx_class[s[i]]];
-      if (c & cs.rx_last[r]) return true;
-      uint64_t nd = cs.rx_first[r];
-      for (uint64_t m = c; m; m &= m - 1) nd |= cs.rx_follow[(size_t)r * 64 + __builtin_ctzll(m)];
-      d = nd;
-    }
-    if (d & cs.rx_end[r]) return true;
   }
   return false;
 }

@@ -11,6 +11,7 @@
 // satisfy them (SPEC.md S5).
 #pragma once
 #include <stdint.h>
+#include <stddef.h>
 
 #include <string>
 #include <vector>
@@ -60,6 +61,7 @@ struct CompiledSet {
   std::vector<uint64_t> rx_follow;    // [rx_count * 64]
   std::vector<uint64_t> rx_first, rx_last, rx_init0, rx_end;  // [rx_count]
   std::vector<uint32_t> rx_flags;     // bit0 accept_at_start, bit1 accept_empty
+  std::vector<uint32_t> rx_pre;       // bound on match start -> first factor occurrence (prefilter on)
   uint32_t rx_maxpos = 0;             // most Glushkov positions of any regex
 
   // kGeneral: q-gram prefilter fused into the scan (qf_on).  Needles = the literals
@@ -86,16 +88,26 @@ struct CompiledSet {
 
 // Required literal factors of one regex (Go syntax, SPEC.md S5): every match contains
 // one of `alts`; `loose` when some byte is an ASCII case pair ((?i)), then every byte is
-// stored OR 0x20 and compared that way.  False when the regex has no factor.
-bool regex_factors(const uint8_t* pat, size_t n, std::vector<std::string>& alts, bool& loose);
+// stored OR 0x20 and compared that way.  *pre (nullable): bound on the distance from a
+// match's start to its first factor occurrence (kRxPreUnbounded: none).  want: sets
+// whose shortest string has at least `want` bytes are preferred (then a bounded pre,
+// then length).  False when the regex has no factor.
+constexpr uint32_t kRxPreUnbounded = 0xFFFFFFFFu;
+bool regex_factors(const uint8_t* pat, size_t n, std::vector<std::string>& alts, bool& loose,
+                   uint32_t* pre = nullptr, size_t want = SIZE_MAX);
 
 // (Re)places every needle's sampling window and rebuilds the bitmap and buckets; hist =
 // gram count-min sketch of a data sample (kQfHistBins bins) or null for the byte-class
 // estimate.
 void place_needles(CompiledSet& cs, const std::vector<uint32_t>* hist);
 
+// Regex r over content s[0, n) restricted to matches holding the factor occurrence that
+// starts at x: starts in [x - rx_pre[r], x], then no new start (the GPU's k_nfa).
+bool nfa_window(const CompiledSet& cs, uint32_t r, const uint8_t* s, size_t n, size_t x);
+
 // Host emulation of the prefiltered matcher on one content (tests): sampled positions
-// p = phase mod stride, bitmap probe, bucket verification, NFA on factor hits.
+// p = phase mod stride, bitmap probe, bucket verification, NFA over each factor
+// occurrence's window.
 bool prefilter_match(const CompiledSet& cs, const uint8_t* s, size_t n, uint32_t phase);
 
 // Parses one Go-syntax regex (SPEC.md S5) and builds its Glushkov tables.

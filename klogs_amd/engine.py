@@ -94,6 +94,8 @@ SIGNATURES = {
                                     C.c_size_t]),
     "klf_debug_match": (C.c_int, [C.POINTER(_Pattern), C.c_uint32, C.c_void_p, C.c_size_t,
                                   C.POINTER(C.c_int)]),
+    "klf_debug_factors": (C.c_int, [C.c_void_p, C.c_size_t, C.c_uint32, C.c_char_p, C.c_size_t,
+                                    C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]),
     "klf_debug_prefilter": (C.c_int, [C.POINTER(_Pattern), C.c_uint32, C.c_void_p, C.c_size_t, C.c_uint32,
                                       C.POINTER(C.c_int), C.POINTER(C.c_uint32)]),
 }
@@ -199,6 +201,19 @@ def debug_prefilter(content: bytes, grep=(), match=(), phase: int = 0):
     buf = C.create_string_buffer(content, len(content) or 1)
     _check(_lib.klf_debug_prefilter(arr, n, buf, len(content), phase, C.byref(m), info))
     return bool(m.value), dict(on=bool(info[0]), q=info[1], stride=info[2], needles=info[3])
+
+
+def debug_factors(pattern: bytes, want: int = 0):
+    """(factor strings, pre bound or None, loose) of one regex, or None without a factor."""
+    buf = C.create_string_buffer(4096)
+    n, pre, loose = C.c_uint32(), C.c_uint32(), C.c_uint32()
+    p = C.create_string_buffer(pattern, len(pattern) or 1)
+    rc = _lib.klf_debug_factors(p, len(pattern), want, buf, 4096, C.byref(n), C.byref(pre), C.byref(loose))
+    if rc == KLF_EINVAL:
+        return None
+    _check(rc)
+    alts = buf.raw.split(b"\0")[: n.value]
+    return alts, (None if pre.value == 0xFFFFFFFF else pre.value), bool(loose.value)
 
 
 @dataclass

@@ -122,3 +122,45 @@ def test_c4_c5_sets_are_prefiltered():
     assert len(rx) == 64
     _, info = E.debug_prefilter(b"", match=rx)
     assert info["on"], info
+
+
+# ---- the NFA window around each factor occurrence (rx_pre) ------------------------------
+WINDOW_SETS = [
+    [rb"ab{2,3}cd\d+xyz", rb"(?i)k(ey|ay)=v\d{1,3}:done"],
+    [rb"p[qr]{0,4}STARTtail\w+", rb"(x|yy|zzz)marker\d"],
+    [rb"(?i)panic: \w+ error in mod\d", rb"tx-[0-9a-f]{8}-commit\d"],
+    [rb"^headFACTOR\d", rb"FACTOR2x$", rb"a*FACTOR3"],  # anchors; an unbounded prefix
+]
+
+
+@pytest.mark.parametrize("idx", range(len(WINDOW_SETS)))
+def test_nfa_windows_equal_full_search(idx):
+    """Matches whose factor occurs several times, lookalike prefixes before it, a match
+    right at the content's start or end: the windowed NFA equals the full search."""
+    rng = random.Random(300 + idx)
+    match = WINDOW_SETS[idx]
+    parts = [b"abbcd12xyz", b"abbbbcd1xyz", b"abcd1xyz", b"KAY=v12:done", b"key=v1234:done", b"pqqSTARTtailx",
+             b"prrrrrSTARTtail", b"zzzmarker7", b"yymarker", b"PANIC: foo error in mod3", b"panic: error in mod3",
+             b"tx-0123abcd-commit5", b"tx-0123abc-commit5", b"headFACTOR1", b"xheadFACTOR1", b"FACTOR2x",
+             b"FACTOR2xy", b"aaaFACTOR3", b"FACTOR", b"cd1xyz", b":done", b"-commit"]
+    contents = []
+    for _ in range(400):
+        s = _text(rng, rng.randint(0, 30))
+        for _ in range(rng.randint(0, 3)):
+            k = rng.randint(0, len(s))
+            s = s[:k] + rng.choice(parts) + s[k:]
+        contents.append(s)
+    _check([], match, contents + parts)
+
+
+@pytest.mark.parametrize("pat,want,pre", [
+    (rb"status=5\d\d path=/api/v0/\w+", 0, 10),
+    (rb"tx-[0-9a-f]{8}-commit0", 0, 11),
+    (rb"(?i)panic: \w+ error in mod0", 0, None),  # the longest factor follows \w+
+    (rb"(?i)panic: \w+ error in mod0", 6, 0),     # a bounded one long enough for stride 4
+    (rb"x(ab|cde)+y", 0, 1),
+    (rb"a{2,5}bcd", 0, 5),                        # "bcd" after up to five a
+])
+def test_factor_prefix_bounds(pat, want, pre):
+    alts, got_pre, _ = E.debug_factors(pat, want)
+    assert got_pre == pre, (pat, alts, got_pre)
