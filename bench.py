@@ -114,9 +114,11 @@ def main():
     ptr = dev.data_ptr()
 
     def step():
-        r = eng.run_device(ptr, seg_base, [n], since=since, tail=TAIL)
+        # per-pattern counts ride along (one literal: no extra kernel work, SPEC.md S6)
+        r = eng.run_device(ptr, seg_base, [n], since=since, tail=TAIL, pattern_counts=True)
         if world > 1:  # per-stream count records -> every rank (one all-gather, RCCL over xGMI)
-            shard.gather_counts({rank: r.totals()}, [n] * world, world, device=coll_dev)
+            rec = dict(r.totals(), patterns=r.pattern_counts(0))
+            step.table = shard.gather_counts({rank: rec}, [n] * world, world, device=coll_dev, n_patterns=1)
         return r
 
     for _ in range(args.warmup):
@@ -173,7 +175,12 @@ def main():
         verified = ref_out == so.out and ref_c["selected"] == tot["selected"] and ref_c["lines"] == lines
         lo = last.lines(0)
         verified = bool(verified and lo.shape[0] == lines + 1 and int(lo[-1]) == n)
+    records_ok = None
+    if world > 1:  # the gathered table: every rank's row equals what that rank computed
+        mine = step.table[rank].tolist()
+        records_ok = mine == [tot[k] for k in shard.RECORD_FIELDS[1:]] + last.pattern_counts(0)
     cpu = None
+    cpu_more = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         sys.path.insert(0, str(ROOT / "oracle"))
         import c_oracle as co
@@ -188,6 +195,7 @@ def main():
                "sample": f"{passes} full passes over this run's {n} B stream with oracle/klf_oracle_c.c "
                          f"(memchr line split, Go time.Parse restated, memmem grep, kubelet tail+since) "
                          f"on 1 host core, {cpu_t:.1f} s"}
+        cpu_more = cpu_variants(host, since)
 
     # Capture path, N = 1 only: the product's host entry points on this
     # run's bytes -- klf_stage in 1 MiB pieces (io.Copy's role) into pinned chunks, then
@@ -264,6 +272,8 @@ def main():
                   "selected_lines": tot["selected"], "matched_lines": tot["matched"], "out_bytes": out_bytes,
                   "h2d_inclusive_GBps": round(n / (h2d_s + dev_avg_s) / 1e9, 3),
                   "capture_path": capture,
+                  "cpu_baseline_variants": cpu_more,
+                  "gathered_records_consistent": records_ok,
                   "verified_vs_c_oracle": verified},
     }
     last.free()
@@ -275,10 +285,122 @@ def main():
         for name in [x for x in args.extra_configs.split(",") if x]:
             res["extra"]["configs"][name] = run_extra(name, args, local, now)
             torch.cuda.empty_cache()
+    if world > 1 and "c3" in args.extra_configs.split(","):
+        res["extra"]["configs"] = {"c3_sharded": run_c3_sharded(args, world, rank, local, coll_dev)}
+        torch.cuda.empty_cache()
     if rank == 0:
         print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def cpu_variants(host: np.ndarray, since) -> dict:
+    """More CPU reference points on the same stream, rank 0 at N = 1 (bounded, ~10 s):
+    the C restatement on T host threads over line-aligned pieces (each piece with the run's
+    --tail: the same per-line work; the split-tail exchange is O(1)), and the reference
+    client's own ceiling -- klogs only io.Copy's each body into its file (cmd/root.go:359-374)
+    -- as a host memcpy bound (1 and T threads) and a page-cache file write of the stream."""
+    from concurrent.futures import ThreadPoolExecutor
+    sys.path.insert(0, str(ROOT / "oracle"))
+    import c_oracle as co
+    threads = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", "16") or 16)))
+    n = len(host)
+    cuts = [0]
+    for k in range(1, threads):
+        j = int(np.flatnonzero(host[k * n // threads:k * n // threads + (1 << 20)] == 10)[0]) + 1
+        cuts.append(k * n // threads + j)
+    cuts.append(n)
+    pieces = [host[a:b] for a, b in zip(cuts, cuts[1:])]
+    with ThreadPoolExecutor(threads) as ex:
+        passes, t_mt = 0, 0.0
+        while t_mt < 4.0 and passes < 64:
+            t = time.perf_counter()
+            list(ex.map(lambda p: co.filter_stream(p, since, TAIL, [synth.NEEDLE], want_lines=False,
+                                                   want_bits=False), pieces))
+            t_mt += time.perf_counter() - t
+            passes += 1
+        dst = np.empty_like(host)
+        t = time.perf_counter()
+        np.copyto(dst, host)
+        t_cp1 = time.perf_counter() - t
+        t = time.perf_counter()
+        list(ex.map(lambda ab: np.copyto(dst[ab[0]:ab[1]], host[ab[0]:ab[1]]), zip(cuts, cuts[1:])))
+        t_cpn = time.perf_counter() - t
+    del dst
+    wn = min(n, 1 << 30)
+    with tempfile.NamedTemporaryFile(prefix="klf_cpy_") as f:
+        t = time.perf_counter()
+        mv = memoryview(host[:wn])
+        off = 0
+        while off < wn:
+            off += os.write(f.fileno(), mv[off:off + (64 << 20)])
+        t_w = time.perf_counter() - t
+    return {
+        "port_threads": {"value": round(n * passes / t_mt / 1e9, 3), "unit": "GB/s", "cores": threads,
+                         "kind": "port", "sample": f"{passes} passes, {threads} line-aligned pieces of this run's "
+                                                   f"stream, one host thread each, {t_mt:.1f} s"},
+        "copy_bound_1t_GBps": round(n / t_cp1 / 1e9, 2),
+        "copy_bound_threads_GBps": round(n / t_cpn / 1e9, 2),
+        "file_write_GBps": round(wn / t_w / 1e9, 2),
+        "copy_note": "the reference client's own work is io.Copy of each body into a file; host memcpy and "
+                     "a page-cache write of the stream bound it from above",
+    }
+
+
+def run_c3_sharded(args, world: int, rank: int, local: int, coll_dev) -> dict:
+    """BASELINE config 3 across ranks: 128 x 64 MiB TEXT streams per rank
+    (the per-GPU share at 8 GPUs; weak scaling at fewer), LPT-assigned (shard.assign), each
+    rank one device batch of its streams, then the one all-gather of per-stream count
+    records.  value = all ranks' bytes / max-over-ranks time."""
+    size, per = 64 << 20, 128
+    lens_all = [synth.size(synth.TEXT, 42, i, size) for i in range(per * world)]
+    mine = shard.local_streams(lens_all, world, rank)
+    lens = [lens_all[i] for i in mine]
+    seg_base, total = E.layout(lens)
+    dev = torch.empty(total, dtype=torch.uint8, device=f"cuda:{local}")
+    h = np.empty(max(lens) + 1, dtype=np.uint8)
+    t = time.time()
+    for j, i in enumerate(mine):
+        synth.generate_into(h, synth.TEXT, 42, i, size)
+        dev[int(seg_base[j]):int(seg_base[j]) + lens[j]].copy_(torch.from_numpy(h[:lens[j]]))
+    torch.cuda.synchronize()
+    log(f"[rank {rank}] c3 share: {len(mine)} streams, {sum(lens)} B in {time.time() - t:.1f}s")
+    eng = E.Engine(local, hip_stream=torch.cuda.current_stream().cuda_stream)
+    ptr = dev.data_ptr()
+
+    def step():
+        r = eng.run_device(ptr, seg_base, lens)
+        recs = {sid: r.stream_counts(j) for j, sid in enumerate(mine)}
+        step.table = shard.gather_counts(recs, lens_all, world, device=coll_dev)
+        return r
+    for _ in range(args.warmup):
+        step().free()
+    torch.cuda.synchronize()
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        r = step()
+        r.free()
+    torch.cuda.synchronize()
+    dist.barrier()
+    dt = time.perf_counter() - t0
+    tt = torch.tensor([dt], dtype=torch.float64, device=coll_dev)
+    dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+    dt = float(tt.item())
+    # every rank's own rows of the gathered table equal its own counts; totals add up
+    r = eng.run_device(ptr, seg_base, lens)
+    ok = all(step.table[sid].tolist() == [r.stream_counts(j)[k] for k in shard.RECORD_FIELDS[1:]]
+             for j, sid in enumerate(mine))
+    ok = ok and int(step.table[:, 0].sum()) > 0 and int(step.table[:, 5].sum()) > 0
+    r.free()
+    eng.close()
+    del dev
+    return {"workload": "C3 at N GPUs: 128 x 64 MiB TEXT streams per GPU, LPT-sharded, -l only (every line out), "
+                        "one all-gather of per-stream count records per step",
+            "streams": per * world, "bytes": int(sum(lens_all)),
+            "value_GBps": round(sum(lens_all) * args.steps / dt / 1e9, 1),
+            "ms_per_step": round(dt / args.steps * 1e3, 3), "records_consistent": bool(ok)}
 
 
 def extra_streams(name: str, total: int):

@@ -105,6 +105,8 @@ typedef struct klf_filter {
 /* klf_filter.flags: record the inner stage boundaries (klf_result_timing [0]-[3]).
  * Each boundary costs a few microseconds of idle GPU; off, only [4]-[6] are measured. */
 #define KLF_FILTER_STAGE_TIMES 1u
+/* klf_filter.flags: count matching lines per pattern (klf_result_pattern_counts). */
+#define KLF_FILTER_PATTERN_COUNTS 2u
 
 typedef struct klf_counts {
   uint64_t lines;      /* all lines (a trailing fragment counts)                       */
@@ -143,7 +145,8 @@ int klf_run_device(klf_engine* e, const uint8_t* d_bytes, uint32_t n_streams,
 int klf_retail(klf_engine* e, klf_result* prev, int64_t tail, klf_result** out);
 
 /* ---- results -------------------------------------------------------------------- */
-/* Selected bytes of one stream (host view, D2H on first access). */
+/* Selected bytes of one stream (host view, D2H on first access; bytes == NULL: len and
+ * counts only, no D2H). */
 int klf_result_stream(klf_result* r, uint32_t stream_id, const uint8_t** bytes,
                       uint64_t* len, klf_counts* counts);
 /* Line-start offsets of one stream: n_lines+1 u64 (last = stream length). */
@@ -153,6 +156,15 @@ int klf_result_lines(klf_result* r, uint32_t stream_id, const uint64_t** off,
  * Returns KLF_EINVAL when the engine has no patterns. */
 int klf_result_match_bits(klf_result* r, uint32_t stream_id, const uint8_t** bits,
                           uint64_t* nbytes);
+/* Per-pattern match counts of one stream (SURVEY.md §8a K4/K5 `count[stream][pattern]`, the
+ * per-stream record the ranks gather, §8e): counts[p] = parsed lines whose content matches
+ * pattern p (klf_config order; a line matching several patterns counts for each), for
+ * p < min(cap, n_patterns); *n = n_patterns.  Independent of --since / --tail, like
+ * klf_counts.matched.  The run must set KLF_FILTER_PATTERN_COUNTS (KLF_ESTATE otherwise).
+ * KLF_EINVAL when a pattern that matches every line (an empty --grep) sits beside others:
+ * the set is then not evaluated.  Extends the size report of printLogSize
+ * (cmd/root.go:279-309) with the new --grep / --match flags (:485-497). */
+int klf_result_pattern_counts(klf_result* r, uint32_t stream_id, uint64_t* counts, uint32_t cap, uint32_t* n);
 /* Position of the stream's last unparseable newline-terminated line, counted from the end
  * over the newline-terminated lines (1 = the last one; 0 = every terminated line parses).
  * The byte-range shards of one stream need it: kubelet emits the trailing
@@ -183,6 +195,28 @@ int klf_result_timing(const klf_result* r, double* ms, uint32_t cap, uint32_t* n
 /* Totals across streams. */
 int klf_result_totals(const klf_result* r, klf_counts* totals);
 void klf_result_free(klf_result* r);
+
+/* ---- follow mode (-f) -------------------------------------------- */
+/* The reference streams each container until EOF with Follow set (cmd/root.go:217-218,
+ * streamLog :312-339, the "ended prematurely" warning :314-318) while the main goroutine
+ * waits for 'q' (pressKeyToExit :399-421).  In follow mode the server keeps applying
+ * SinceSeconds / TailLines to the backlog, so the engine applies what is per line: since
+ * and the grep set (tail is -1; the filter's tail is ignored).  A session carries every
+ * stream's open (unterminated) line across the chunks fed to it; each flush runs ONE engine
+ * batch over the complete lines all streams received since the previous flush. */
+typedef struct klf_follow klf_follow;
+int klf_follow_open(klf_engine* e, const klf_filter* f, klf_follow** out);
+/* Appends bytes read from stream `stream_id` (any split; concurrent calls for different
+ * ids are safe, as klf_stage).  Complete lines are staged on the engine at once. */
+int klf_follow_feed(klf_follow* fw, uint32_t stream_id, const uint8_t* p, size_t n);
+/* Filters what is complete; final != 0 also flushes every stream's open line (the streams'
+ * EOF: kubelet emits the last unterminated line).  *out covers stream ids [0, max id fed];
+ * a stream fed nothing since the last flush has 0 lines.  The previous flush's result
+ * stays valid until this call (results of the session share the engine's workspace). */
+int klf_follow_flush(klf_follow* fw, int final, klf_result** out);
+/* Bytes of the stream's open line (received, not yet filtered). */
+uint64_t klf_follow_open_bytes(const klf_follow* fw, uint32_t stream_id);
+void klf_follow_close(klf_follow* fw);
 
 /* ---- host-side helpers mirroring cmd/root.go (no GPU needed) ---------------------- */
 /* Go time.Parse(time.RFC3339Nano, s) restated (SPEC.md S2); 0 = ok. */

@@ -96,6 +96,9 @@ struct klf_engine {
   std::unique_ptr<klf::CopyPool> copier;
   DevBuf d_asm;                        // k_assemble piece table
   DevBuf d_scratch;                    // small query results (klf_result_last_unparsed)
+  DevBuf d_ac_out, d_ac_dict, d_pcount, d_pairs;  // per-pattern counts
+  uint32_t pairs_log2 = 20;            // (line, pattern) pair set: 2^20 entries, grows on overflow
+  uint32_t n_user = 0;                 // patterns as given to klf_open
   // device pattern tables
   DevBuf d_lit, d_ac_class, d_ac_next, d_ac_accept, d_rx_class, d_rx_b, d_rx_follow, d_rx_vec, d_rx_flags, d_rx_pre;
   DevBuf d_qf_bitmap, d_qf_head, d_qf_ent, d_qf_nbytes, d_cand, d_rx_vec4, d_qhits, d_hslots, d_hist, d_hflat;
@@ -131,6 +134,9 @@ struct klf_result {
   std::vector<uint32_t> bits;
   std::vector<std::vector<uint8_t>> stream_bits;
   std::vector<uint8_t> have_stream_bits;
+  // per-pattern counts (KLF_FILTER_PATTERN_COUNTS): [segment][compiled id]
+  bool counted = false, pcount_ok = false;
+  std::vector<uint32_t> pcount;
 };
 
 static int set_err(klf_engine* e, int code, const std::string& m) {
@@ -191,6 +197,9 @@ extern "C" int klf_open(const klf_config* cfg, klf_engine** out) {
   }
   // 2) device
   e->device = cfg->device;
+  e->n_user = cfg->n_patterns;
+  e->dpats.n_cids = e->cs.n_cids;
+  e->dpats.n_lits = e->cs.n_lits;
   hipError_t h = hipSetDevice(cfg->device);
   if (h != hipSuccess) { e->err = std::string("hipSetDevice: ") + hipGetErrorString(h); *out = e; return KLF_EHIP; }
   hipDeviceProp_t prop;
@@ -237,6 +246,12 @@ extern "C" int klf_open(const klf_config* cfg, klf_engine** out) {
       P.ac_class = e->d_ac_class.as<uint8_t>();
       P.ac_next = e->d_ac_next.as<uint32_t>();
       P.ac_accept = e->d_ac_accept.as<uint8_t>();
+      if ((h = upload(e->d_ac_out, cs.ac_out, st)) != hipSuccess || (h = upload(e->d_ac_dict, cs.ac_dict, st)) != hipSuccess) {
+        *out = e;
+        return hip_err(e, h, "upload AC output tables");
+      }
+      P.ac_out = e->d_ac_out.as<int32_t>();
+      P.ac_dict = e->d_ac_dict.as<uint32_t>();
       P.ac_states = cs.ac_states;
       P.ac_classes = cs.ac_classes;
     }
@@ -289,6 +304,8 @@ extern "C" int klf_open(const klf_config* cfg, klf_engine** out) {
       P.qf_stride = cs.qf_stride;
       P.qf_fold = cs.qf_fold;
       P.qf_mask = cs.qf_mask;
+      P.qf_w24 = cs.qf_q == 4 ? 24u : 0u;
+      P.qf_k = cs.qf_k;
       P.qf_bitmap = e->d_qf_bitmap.as<uint32_t>();
       P.qf_head = e->d_qf_head.as<uint32_t>();
       P.qf_ent = e->d_qf_ent.as<uint4>();
@@ -297,6 +314,8 @@ extern "C" int klf_open(const klf_config* cfg, klf_engine** out) {
   }
   if (const char* cc = getenv("KLF_CAND_CAP"))  // tests: force the queue-overflow fallback
     e->cand_cap = (uint32_t)std::max(1L, std::min(atol(cc), 1L << 28));
+  if (const char* pl = getenv("KLF_PAIRS_LOG2"))  // tests: a small per-pattern pair set (grows on overflow)
+    e->pairs_log2 = (uint32_t)std::max(4L, std::min(atol(pl), 28L));
   if (const char* hc = getenv("KLF_HITS_CAP"))  // tests: force the hit-list overflow fallback
     e->hits_cap_max = (uint64_t)std::max(1L, std::min(atol(hc), 1L << 28));
   *out = e;
@@ -318,6 +337,7 @@ extern "C" void klf_close(klf_engine* e) {
     b->release();
   e->d_asm.release();
   e->d_scratch.release();
+  for (DevBuf* b : {&e->d_ac_out, &e->d_ac_dict, &e->d_pcount, &e->d_pairs}) b->release();
   e->copier.reset();
   {
     std::lock_guard<std::mutex> g(e->mu);
@@ -590,6 +610,7 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
       HIPCHK(e, upload(e->d_qf_bitmap, e->cs.qf_bitmap, st), "upload bitmap");
       HIPCHK(e, upload(e->d_qf_head, e->cs.qf_head, st), "upload buckets");
       HIPCHK(e, upload(e->d_qf_ent, e->cs.qf_ent, st), "upload entries");
+      e->dpats.qf_k = e->cs.qf_k;
       e->dpats.qf_bitmap = e->d_qf_bitmap.as<uint32_t>();
       e->dpats.qf_head = e->d_qf_head.as<uint32_t>();
       e->dpats.qf_ent = e->d_qf_ent.as<uint4>();
@@ -624,9 +645,17 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
     HIPCHK(e, e->d_hflat.ensure((size_t)hflat_cap * 4), "alloc hflat");
   }
 
-  bool overflow = false;
-  for (int attempt = 0; attempt < 2; ++attempt) {
+  const bool count = (f->flags & KLF_FILTER_PATTERN_COUNTS) && mode == klf::CompiledSet::kGeneral && e->cs.n_cids;
+  r->counted = (f->flags & KLF_FILTER_PATTERN_COUNTS) != 0;
+  bool overflow = false, pairs_over = false;
+  for (int attempt = 0, line_reruns = 0, pair_reruns = 0; attempt < 4; ++attempt) {
     const uint64_t max_cblocks = cap / klf::kCompactLines + 2;
+    if (count) {
+      HIPCHK(e, e->d_pcount.ensure((size_t)nsegs * e->cs.n_cids * 4), "alloc pcount");
+      HIPCHK(e, e->d_pairs.ensure((size_t)8 << e->pairs_log2), "alloc pairs");
+      HIPCHK(e, hipMemsetAsync(e->d_pcount.p, 0, (size_t)nsegs * e->cs.n_cids * 4, st), "zero pcount");
+      HIPCHK(e, hipMemsetAsync(e->d_pairs.p, 0, (size_t)8 << e->pairs_log2, st), "zero pairs");
+    }
     HIPCHK(e, e->d_line_off.ensure((cap + nsegs + 1) * 8), "alloc line_off");
     HIPCHK(e, e->d_meta.ensure(cap * 2 + 16), "alloc meta");
     HIPCHK(e, e->d_bits.ensure((cap / 32 + 1) * 4), "alloc bits");
@@ -693,6 +722,10 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
     a.truns = e->d_truns.as<uint32_t>();
     a.kbase = e->d_kbase.as<uint64_t>();
     a.compact_mode = compact_mode;
+    a.count_pats = count ? 1u : 0u;
+    a.pcount = count ? e->d_pcount.as<uint32_t>() : nullptr;
+    a.pairs = count ? e->d_pairs.as<uint64_t>() : nullptr;
+    a.pairs_log2 = e->pairs_log2;
     HIPCHK(e, klf::launch_pipeline(a, st, e->ev, e->num_cus), "launch");
     r->so.resize(nsegs);
     uint32_t counters[16];
@@ -706,13 +739,25 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
               counters[klf::kCtrQueue], counters[klf::kCtrQOver], counters[5]);
     overflow = (counters[2] & 1u) != 0;
     if (overflow) {  // more lines (or dense-tile slots) than estimated: rerun with exact sizes
+      if (line_reruns++) break;
       cap = std::min(std::max<uint64_t>(cap, r->so[nsegs - 1].line_hi + 2), cap_clamp);
       e->pool_cap = std::max<uint64_t>(e->pool_cap, (uint64_t)counters[klf::kCtrPool] + 1024);
+      continue;
+    }
+    pairs_over = count && counters[klf::kCtrPairsOver] != 0;
+    if (pairs_over && pair_reruns < 2 && e->pairs_log2 < 28) {  // the pair set filled: a larger one
+      ++pair_reruns;
+      e->pairs_log2 = std::min(28u, e->pairs_log2 + 3);
       continue;
     }
     e->last_args = a;
     e->last_gen = r->gen;
     break;
+  }
+  if (count && !overflow && !pairs_over) {
+    r->pcount.resize((size_t)nsegs * e->cs.n_cids);
+    HIPCHK(e, hipMemcpy(r->pcount.data(), e->d_pcount.p, r->pcount.size() * 4, hipMemcpyDeviceToHost), "D2H pcount");
+    r->pcount_ok = true;
   }
   if (overflow)  // the exact rerun overflowed too: never hand out the aborted run's records
     return set_err(e, KLF_ENOMEM, "line index / dense-tile pool overflow after the exact rerun");
@@ -757,6 +802,9 @@ extern "C" int klf_retail(klf_engine* e, klf_result* prev, int64_t tail, klf_res
   r->seg_base = prev->seg_base;
   r->has_bits = prev->has_bits;
   r->total_lines = prev->total_lines;
+  r->counted = prev->counted;
+  r->pcount_ok = prev->pcount_ok;
+  r->pcount = prev->pcount;
   const uint32_t nsegs = (uint32_t)prev->so.size();
   r->so.resize(nsegs);
   if (nsegs) {
@@ -843,7 +891,7 @@ extern "C" int klf_result_stream(klf_result* r, uint32_t id, const uint8_t** byt
   int rc = check_result(r, id);
   if (rc) return rc;
   klf_engine* e = r->e;
-  if (!r->have_out) {
+  if (bytes && !r->have_out) {  // counts only: no D2H
     r->out.resize(r->total_out + 1);
     if (r->total_out) {
       HIPCHK(e, hipMemcpyAsync(r->out.data(), e->d_out.p, r->total_out, hipMemcpyDeviceToHost, e->stream), "D2H out");
@@ -1060,6 +1108,32 @@ extern "C" int klf_result_match_bits(klf_result* r, uint32_t id, const uint8_t**
   return KLF_OK;
 }
 
+extern "C" int klf_result_pattern_counts(klf_result* r, uint32_t id, uint64_t* counts, uint32_t cap, uint32_t* n) {
+  if (!r || id >= r->n_streams || (cap && !counts)) return KLF_EINVAL;
+  klf_engine* e = r->e;
+  if (n) *n = e->n_user;
+  if (!r->counted) return set_err(e, KLF_ESTATE, "the run did not ask for per-pattern counts (KLF_FILTER_PATTERN_COUNTS)");
+  const auto& cs = e->cs;
+  const int64_t s = r->seg_of[id];
+  const bool general = cs.mode == klf::CompiledSet::kGeneral;
+  if (general && !r->pcount_ok)
+    return set_err(e, KLF_ETOOBIG, "per-pattern counts: the (line, pattern) pair set overflowed");
+  for (uint32_t u = 0; u < std::min(cap, e->n_user); ++u) {
+    const int32_t m = u < cs.user_map.size() ? cs.user_map[u] : klf::CompiledSet::kCidNever;
+    uint64_t v = 0;
+    if (m == klf::CompiledSet::kCidUncounted)
+      return set_err(e, KLF_EINVAL, "per-pattern counts: not counted when another pattern matches every line");
+    if (s >= 0) {
+      const SegOut& so = r->so[s];
+      if (m == klf::CompiledSet::kCidAlways) v = so.parsed;
+      else if (m >= 0 && cs.mode == klf::CompiledSet::kLiteral1) v = so.matched;  // the one literal
+      else if (m >= 0 && general) v = r->pcount[(size_t)s * cs.n_cids + (size_t)m];
+    }
+    counts[u] = v;
+  }
+  return KLF_OK;
+}
+
 extern "C" int klf_result_last_unparsed(klf_result* r, uint32_t id, uint64_t* rank) {
   int rc = check_result(r, id);
   if (rc) return rc;
@@ -1117,6 +1191,82 @@ extern "C" int klf_result_totals(const klf_result* r, klf_counts* t) {
 }
 
 extern "C" void klf_result_free(klf_result* r) { delete r; }
+
+// ------------------------------------------------------------------ follow mode ---
+
+struct klf_follow {
+  klf_engine* e = nullptr;
+  klf_filter f{};
+  std::mutex mu;  // guards the carry table's growth (feeds of different ids run concurrently)
+  std::vector<std::unique_ptr<std::string>> carry;
+};
+
+static std::string* follow_carry(klf_follow* w, uint32_t id) {
+  std::lock_guard<std::mutex> g(w->mu);
+  while (w->carry.size() <= id) w->carry.emplace_back(new std::string());
+  return w->carry[id].get();
+}
+
+extern "C" int klf_follow_open(klf_engine* e, const klf_filter* f, klf_follow** out) {
+  if (!e || !f || !out) return KLF_EINVAL;
+  *out = nullptr;
+  auto* w = new (std::nothrow) klf_follow();
+  if (!w) return KLF_ENOMEM;
+  w->e = e;
+  w->f = *f;
+  w->f.tail = -1;  // per-line rules only: the server applies --tail to the backlog
+  const int rc = klf_reset(e);
+  if (rc) { delete w; return rc; }
+  *out = w;
+  return KLF_OK;
+}
+
+extern "C" int klf_follow_feed(klf_follow* w, uint32_t id, const uint8_t* p, size_t n) {
+  if (!w || (n && !p)) return KLF_EINVAL;
+  std::string* c;
+  try {
+    c = follow_carry(w, id);
+  } catch (...) {
+    return KLF_ENOMEM;
+  }
+  if (!n) return KLF_OK;
+  const uint8_t* nl = static_cast<const uint8_t*>(memrchr(p, '\n', n));
+  if (!nl) {  // still inside the open line
+    c->append(reinterpret_cast<const char*>(p), n);
+    return KLF_OK;
+  }
+  const size_t cut = (size_t)(nl - p) + 1;
+  int rc = KLF_OK;
+  if (!c->empty()) rc = klf_stage(w->e, id, reinterpret_cast<const uint8_t*>(c->data()), c->size());
+  if (!rc) rc = klf_stage(w->e, id, p, cut);
+  if (rc) return rc;
+  c->assign(reinterpret_cast<const char*>(p + cut), n - cut);
+  return KLF_OK;
+}
+
+extern "C" int klf_follow_flush(klf_follow* w, int final, klf_result** out) {
+  if (!w || !out) return KLF_EINVAL;
+  *out = nullptr;
+  const uint32_t n = (uint32_t)w->carry.size();
+  if (final)
+    for (uint32_t i = 0; i < n; ++i) {
+      std::string& c = *w->carry[i];
+      if (c.empty()) continue;
+      const int rc = klf_stage(w->e, i, reinterpret_cast<const uint8_t*>(c.data()), c.size());
+      if (rc) return rc;
+      c.clear();
+    }
+  int rc = klf_set_streams(w->e, n);
+  if (!rc) rc = klf_run(w->e, &w->f, out);
+  const int rr = klf_reset(w->e);  // the result keeps its outputs; the staging is released
+  return rc ? rc : rr;
+}
+
+extern "C" uint64_t klf_follow_open_bytes(const klf_follow* w, uint32_t id) {
+  return (w && id < w->carry.size()) ? w->carry[id]->size() : 0;
+}
+
+extern "C" void klf_follow_close(klf_follow* w) { delete w; }
 
 // ---------------------------------------------------------------- host helpers ---
 

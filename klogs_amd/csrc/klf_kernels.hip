@@ -304,7 +304,7 @@ constexpr int kScanPlain = 0, kScanLit = 1, kScanGen = 2;
 // The tile descriptors come in as separate __restrict__ const parameters so that their
 // (wave-uniform) reads compile to scalar loads: a vector load of them would be ordered
 // behind the in-flight prefetch by vmcnt and stall every tile on the next tile's bytes.
-template <int MODE, int QS>
+template <int MODE, int QS, int QK>
 __global__ __launch_bounds__(kThreads, MODE == kScanGen ? 3 : KLF_SCAN_OCC) void k_scan(RunArgs a, const uint32_t* __restrict__ tseg,
                                                                const SegDesc* __restrict__ segs) {
   constexpr bool LIT = MODE == kScanLit;
@@ -606,38 +606,56 @@ __global__ __launch_bounds__(kThreads, MODE == kScanGen ? 3 : KLF_SCAN_OCC) void
     // the scan keeps no verification code, and the latency-bound bucket walks run with
     // the whole GPU's parallelism.
     if (GEN) {
-      const uint32_t fold = a.pats.qf_fold, qmask = a.pats.qf_mask;
+      const uint32_t fold = a.pats.qf_fold, w24 = a.pats.qf_w24;
       const uint32_t* s32 = reinterpret_cast<const uint32_t*>(s_tile);
-      auto probe = [&](uint32_t g) __attribute__((always_inline)) -> uint32_t {
-        const uint32_t gf = (g | fold) & qmask;
-        const uint32_t h1 = qf_h1(gf), bits = qf_bits(h1, qf_h2(gf));
-        return (s_qf[qf_word(h1)] & bits) == bits ? 1u : 0u;
+      // bit 0 of the result: gram g has all K bits of its bitmap word set (qf_hash / qf_bits)
+      auto hbits = [&](uint32_t g) __attribute__((always_inline)) -> uint32_t {
+        const uint32_t gf = g | fold;
+        const uint32_t f = QK == 3 ? gf ^ __builtin_amdgcn_ubfe(gf, 13, 11) : gf;  // qf_fold3 (bits >= 24 unused)
+        const uint32_t h = __umul24(f, 0x9E3779u) + __umul24(__builtin_amdgcn_ubfe(gf, 8, w24), 0x7F4A7Du);
+        const uint32_t w = s_qf[h >> (32 - kQfBucketBits)];
+        uint32_t t = (w >> ((h >> 15) & 31u)) & (w >> ((h >> 10) & 31u));
+        if (QK == 3) t &= w >> ((uint32_t)(((uint64_t)(f & 0xFFFFFFu) * 0xC2B2AEu) >> 32) & 31u);
+        return t;
       };
-      // bitmap probes of my samples -> a 128-bit hit mask (bit = byte offset in my range)
-      uint32_t hq0 = 0, hq1 = 0, hq2 = 0, hq3 = 0;
-      const uint32_t rot = ((uint32_t)lane >> 1) & 7u;
-#pragma unroll
-      for (int v = 0; v < ((KLF_ABL & 4) ? 0 : 8); ++v) {
-        const uint32_t c = ((uint32_t)v + rot) & 7u;
+      // the samples of chunk c (16 B) -> their grams, in order (QS = 8: dwords 0 and 2)
+      auto chunk_grams = [&](uint32_t c, auto&& f) __attribute__((always_inline)) {
         const uint32_t o0 = my0 + 16u * c;
         const uint4 x = *reinterpret_cast<const uint4*>(s_tile + o0);
         const uint32_t w4 = QS < 4 ? s32[(o0 >> 2) + 4] : 0u;
         const uint32_t w[5] = {x.x, x.y, x.z, x.w, w4};
-        uint32_t hm = 0;
 #pragma unroll
         for (int d = 0; d < 4; ++d)
 #pragma unroll
           for (int o = 0; o < 4; o += (QS < 4 ? QS : 4)) {
-            if ((4 * d + o) % QS != 0) continue;  // QS = 8: dwords 0 and 2 only
-            const uint32_t g = o == 0 ? w[d] : __builtin_amdgcn_alignbyte(w[d + 1], w[d], o);
-            hm |= probe(g) << (4 * d + o);
+            if ((4 * d + o) % QS != 0) continue;
+            f(o == 0 ? w[d] : __builtin_amdgcn_alignbyte(w[d + 1], w[d], o), 4 * d + o);
           }
-        hm = clip(hm, c) << ((c & 1u) * 16u);
-        const uint32_t q = c >> 1;
-        hq0 |= q == 0 ? hm : 0u;
-        hq1 |= q == 1 ? hm : 0u;
-        hq2 |= q == 2 ? hm : 0u;
-        hq3 |= q == 3 ? hm : 0u;
+      };
+      // fast pass: one OR-accumulated bit per chunk (no positions); most tiles stop here
+      uint32_t chit = 0;
+      const uint32_t rot = ((uint32_t)lane >> 1) & 7u;
+#pragma unroll
+      for (int v = 0; v < ((KLF_ABL & 4) ? 0 : 8); ++v) {
+        const uint32_t c = ((uint32_t)v + rot) & 7u;
+        uint32_t acc = 0;
+        chunk_grams(c, [&](uint32_t g, int) __attribute__((always_inline)) { acc |= hbits(g); });
+        chit |= (acc & 1u) << c;
+      }
+      // chunks with a possible hit: the sample positions (past the tile's end clipped)
+      uint32_t hq0 = 0, hq1 = 0, hq2 = 0, hq3 = 0;
+      if (__any(chit != 0)) {
+        for (uint32_t m = chit; m; m &= m - 1u) {
+          const uint32_t c = (uint32_t)__builtin_ctz(m);
+          uint32_t hm = 0;
+          chunk_grams(c, [&](uint32_t g, int pos) __attribute__((always_inline)) { hm |= (hbits(g) & 1u) << pos; });
+          hm = clip(hm, c) << ((c & 1u) * 16u);
+          const uint32_t q = c >> 1;
+          hq0 |= q == 0 ? hm : 0u;
+          hq1 |= q == 1 ? hm : 0u;
+          hq2 |= q == 2 ? hm : 0u;
+          hq3 |= q == 3 ? hm : 0u;
+        }
       }
 #if KLF_ABL & 8
       any_defer |= (hq0 | hq1 | hq2 | hq3) == 0xFFFFFFFFu;  // timing build: probes only
@@ -716,6 +734,50 @@ __device__ bool general_match(const DevPatterns& P, const uint8_t* p, int64_t n)
   for (uint32_t r = 0; r < P.rx_count; ++r)
     if (rx_match(P, r, p, n)) return true;
   return false;
+}
+
+// ---- per-pattern counts (KLF_FILTER_PATTERN_COUNTS) -------------------------------------
+// Line l of segment s matches compiled pattern cid: count it once.  The (line, cid) pairs
+// go through an open-addressing set (key + 1, 0 = empty; atomicCAS), so the several
+// occurrences the prefilter verifies in one line, and the deferred lines the fix-up
+// re-matches, add one line each.
+__device__ void count_pair(const RunArgs& a, uint64_t l, uint32_t s, uint32_t cid) {
+  const uint64_t key = ((l << 20) | cid) + 1;
+  const uint32_t mask = (1u << a.pairs_log2) - 1u;
+  uint32_t h = (uint32_t)((key * 0x9E3779B97F4A7C15ull) >> 32) & mask;
+  for (int probe = 0; probe < 128; ++probe) {
+    const unsigned long long prev = atomicCAS(reinterpret_cast<unsigned long long*>(&a.pairs[h]), 0ull, key);
+    if (prev == 0ull) {
+      atomicAdd(&a.pcount[(size_t)s * a.pats.n_cids + cid], 1u);
+      return;
+    }
+    if (prev == key) return;
+    h = (h + 1u) & mask;
+  }
+  atomicOr(&a.counters[kCtrPairsOver], 1u);  // the host re-runs with a larger set
+}
+
+// Every pattern of the set on one content (deferred lines, the fallback matcher): counts
+// each matching pattern of line l; true when one matches.  AC reports every literal that
+// ends at each position (dictionary links), every regex runs on its own.
+__device__ bool general_count(const RunArgs& a, const uint8_t* p, int64_t n, uint64_t l, uint32_t s) {
+  const DevPatterns& P = a.pats;
+  bool any = false;
+  if (P.ac_states) {
+    uint32_t st = 0;
+    for (int64_t i = 0; i < n; ++i) {
+      st = P.ac_next[(size_t)st * P.ac_classes + P.ac_class[p[i]]];
+      if (!P.ac_accept[st]) continue;
+      any = true;
+      for (uint32_t t = P.ac_out[st] >= 0 ? st : P.ac_dict[st]; t; t = P.ac_dict[t]) count_pair(a, l, s, (uint32_t)P.ac_out[t]);
+    }
+  }
+  for (uint32_t r = 0; r < P.rx_count; ++r)
+    if (rx_match(P, r, p, n)) {
+      any = true;
+      count_pair(a, l, s, P.n_lits + r);
+    }
+  return any;
 }
 
 __global__ __launch_bounds__(256) void k_fixup(RunArgs a) {
@@ -1073,7 +1135,7 @@ __device__ void verify_hit(const RunArgs& a, uint32_t tile, uint32_t s, int32_t 
   const uint8_t* segp = a.bytes + sd.base;
   const int64_t rel_lo = (int64_t)(tile - sd.tile0) * kTile;
   const uint32_t g = (gword(segp + rel_lo + p) | P.qf_fold) & P.qf_mask;
-  const uint32_t b = qf_word(qf_h1(g));
+  const uint32_t b = qf_word(qf_hash(g, P.qf_w24, P.qf_k));
   const uint32_t e1 = P.qf_head[b + 1];
   for (uint32_t e = P.qf_head[b]; e < e1; ++e) {
     const uint4 E = P.qf_ent[e];
@@ -1118,10 +1180,13 @@ __device__ void verify_hit(const RunArgs& a, uint32_t tile, uint32_t s, int32_t 
     if (!(mt & Meta::kParsed)) continue;
     if (!(E.y & kQfRegex)) {  // literal: a match when it starts inside the content
       const uint32_t plen = (mt >> 2) == kPlenEscape ? line_plen(a, mt, segp, ls, a.line_off[l + s + 1]) : mt >> 2;
-      if ((uint64_t)(rel_lo + x) >= ls + plen) atomicOr(&a.bits[l >> 5], 1u << (l & 31));
+      if ((uint64_t)(rel_lo + x) >= ls + plen) {
+        atomicOr(&a.bits[l >> 5], 1u << (l & 31));
+        if (a.count_pats) count_pair(a, l, s, E.z);
+      }
       continue;
     }
-    if ((a.bits[l >> 5] >> (l & 31)) & 1u) continue;
+    if (!a.count_pats && ((a.bits[l >> 5] >> (l & 31)) & 1u)) continue;  // counting: every regex decides
     const uint32_t qi = atomicAdd(&a.counters[kCtrQueue], 1u);
     if (qi < a.cand_cap) {
       a.cand[2 * (size_t)qi] = l | ((uint64_t)E.z << 40);
@@ -1277,7 +1342,7 @@ __global__ __launch_bounds__(256) void k_nfa(RunArgs a) {
     const uint32_t r = (uint32_t)(e >> 40);
     if (P.rx_pre[r] != kRxPreNone) continue;  // bounded window: k_nfa_win
     const uint32_t s = find_seg_by_line(a.segout, a.nsegs, l);
-    if ((a.bits[l >> 5] >> (l & 31)) & 1u) continue;
+    if (!a.count_pats && ((a.bits[l >> 5] >> (l & 31)) & 1u)) continue;
     const uint16_t m = a.meta[l];
     if (!(m & Meta::kParsed)) continue;
     const uint8_t* segp = a.bytes + a.segs[s].base;
@@ -1287,7 +1352,41 @@ __global__ __launch_bounds__(256) void k_nfa(RunArgs a) {
     if (ce > cs && segp[ce - 1] == '\n') --ce;
     if (ce <= cs) continue;  // factor-bearing regexes never match empty content
     const bool hit = (P.rx_flags[r] & 1u) || nfa_wave(T, r, segp + cs, ce - cs, lane);
-    if (hit && lane == 0) atomicOr(&a.bits[l >> 5], 1u << (l & 31));
+    if (hit && lane == 0) {
+      atomicOr(&a.bits[l >> 5], 1u << (l & 31));
+      if (a.count_pats) count_pair(a, l, s, P.n_lits + r);
+    }
+  }
+}
+
+// Per-pattern counts of the lines k_fixup decided (non-canonical timestamp prefix, general
+// sets): k_fixup runs before the tile line bases exist, so the counting pass over those
+// lines runs here, one wave per tile that deferred a line, once the line index is built.
+__global__ __launch_bounds__(256) void k_fixcount(RunArgs a) {
+  if (!a.counters[kCtrDefer] || a.counters[2]) return;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  for (uint32_t tile = blockIdx.x * 4 + wv; tile < a.ntiles; tile += gridDim.x * 4) {
+    const TileStat ts = a.tstat[tile];
+    if (!(ts.flags & 4u)) continue;
+    const uint32_t s = a.tile_seg[tile];
+    const SegDesc sd = a.segs[s];
+    const int64_t rel_lo = (int64_t)(tile - sd.tile0) * kTile;
+    const bool first = rel_lo == 0, last = rel_lo + kTile >= (int64_t)sd.len;
+    const uint32_t k0 = first ? 0 : 1, k1 = last ? ts.events : ts.events + 1;
+    const uint32_t nlines = k1 > k0 ? k1 - k0 : 0;
+    const uint32_t* list = (ts.flags & 1u) ? a.pool + ts.pool_base : a.slots + (size_t)tile * kSlotStride;
+    const uint8_t* segp = a.bytes + sd.base;
+    for (uint32_t j = lane; j < nlines; j += 64) {
+      const uint32_t sl = list[j];
+      if (!(sl & kSlotDefer) || !(sl & kSlotHit)) continue;  // only deferred lines that matched
+      const uint64_t l = a.tile_base[tile] + k0 + j;
+      const uint16_t m = a.meta[l];
+      const uint64_t ls = a.line_off[l + s], le = a.line_off[l + s + 1];
+      const uint64_t cs = ls + line_plen(a, m, segp, ls, le);
+      uint64_t ce = le;
+      if (ce > cs && segp[ce - 1] == '\n') --ce;
+      if (ce > cs) general_count(a, segp + cs, (int64_t)(ce - cs), l, s);
+    }
   }
 }
 
@@ -1332,7 +1431,7 @@ __global__ __launch_bounds__(256) void k_nfa_win(RunArgs a) {
     const uint32_t r = (uint32_t)(e >> 40);
     const uint32_t pre = P.rx_pre[r];
     if (pre == kRxPreNone) continue;  // k_nfa runs those over the whole line
-    if ((a.bits[l >> 5] >> (l & 31)) & 1u) continue;
+    if (!a.count_pats && ((a.bits[l >> 5] >> (l & 31)) & 1u)) continue;
     const uint16_t m = a.meta[l];
     if (!(m & Meta::kParsed)) continue;
     const uint32_t s = find_seg_by_line(a.segout, a.nsegs, l);
@@ -1361,7 +1460,10 @@ __global__ __launch_bounds__(256) void k_nfa_win(RunArgs a) {
       }
       if (!hit && p == ce) hit = (d & V[3]) != 0;
     }
-    if (hit) atomicOr(&a.bits[l >> 5], 1u << (l & 31));
+    if (hit) {
+      atomicOr(&a.bits[l >> 5], 1u << (l & 31));
+      if (a.count_pats) count_pair(a, l, s, P.n_lits + r);
+    }
   }
 }
 
@@ -1384,8 +1486,12 @@ __global__ __launch_bounds__(256) void k_match(RunArgs a) {
       if (ce > cs && segp[ce - 1] == '\n') --ce;
       const uint8_t* p = segp + cs;
       const int64_t n = (int64_t)(ce - cs);
-      if (a.pats.ac_states) hit = ac_match(a.pats, p, n);
-      for (uint32_t r = 0; !hit && r < a.pats.rx_count; ++r) hit = rx_match(a.pats, r, p, n);
+      if (a.count_pats) {
+        hit = general_count(a, p, n, l, s);
+      } else {
+        if (a.pats.ac_states) hit = ac_match(a.pats, p, n);
+        for (uint32_t r = 0; !hit && r < a.pats.rx_count; ++r) hit = rx_match(a.pats, r, p, n);
+      }
     }
     if (hit) atomicOr(&a.bits[l >> 5], 1u << (l & 31));
   }
@@ -2500,17 +2606,21 @@ size_t nfa_lds_bytes(const DevPatterns& P) {
   return 8ull * P.rx_count * (P.rx_classes + P.rx_maxpos + 4) + 256;
 }
 
-template <int MODE, int QS>
+template <int MODE, int QS, int QK = 3>
 hipError_t launch_scan(const RunArgs& a, hipStream_t st, int num_cus) {
   static int occ = 0;  // queried once per variant: the host query delays the launch
   if (occ == 0) {
-    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_scan<MODE, QS>, kThreads, 0);
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_scan<MODE, QS, QK>, kThreads, 0);
     occ = occ < 1 ? 1 : (occ > 8 ? 8 : occ);
   }
   uint32_t grid = (uint32_t)(num_cus * occ);
   if (grid > a.ntiles) grid = a.ntiles;
-  hipLaunchKernelGGL((k_scan<MODE, QS>), dim3(grid), dim3(kThreads), 0, st, a, a.tile_seg, a.segs);
+  hipLaunchKernelGGL((k_scan<MODE, QS, QK>), dim3(grid), dim3(kThreads), 0, st, a, a.tile_seg, a.segs);
   return hipGetLastError();
+}
+template <int QS>
+hipError_t launch_gen(const RunArgs& a, hipStream_t st, int num_cus) {
+  return a.pats.qf_k == 2 ? launch_scan<kScanGen, QS, 2>(a, st, num_cus) : launch_scan<kScanGen, QS, 3>(a, st, num_cus);
 }
 
 static hipError_t launch_tail_stage(const RunArgs& a, hipStream_t st, hipEvent_t* ev, int num_cus);
@@ -2537,13 +2647,13 @@ hipError_t launch_pipeline(const RunArgs& a, hipStream_t st, hipEvent_t* ev, int
     if (a.grep_mode == kGrepLit1)
       KLF_TRY((launch_scan<kScanLit, 1>(a, st, num_cus)));
     else if (a.grep_mode == kGrepGeneral && a.pats.qf_on && a.pats.qf_stride == 4)
-      KLF_TRY((launch_scan<kScanGen, 4>(a, st, num_cus)));
+      KLF_TRY((launch_gen<4>(a, st, num_cus)));
     else if (a.grep_mode == kGrepGeneral && a.pats.qf_on && a.pats.qf_stride == 8)
-      KLF_TRY((launch_scan<kScanGen, 8>(a, st, num_cus)));
+      KLF_TRY((launch_gen<8>(a, st, num_cus)));
     else if (a.grep_mode == kGrepGeneral && a.pats.qf_on && a.pats.qf_stride == 2)
-      KLF_TRY((launch_scan<kScanGen, 2>(a, st, num_cus)));
+      KLF_TRY((launch_gen<2>(a, st, num_cus)));
     else if (a.grep_mode == kGrepGeneral && a.pats.qf_on)
-      KLF_TRY((launch_scan<kScanGen, 1>(a, st, num_cus)));
+      KLF_TRY((launch_gen<1>(a, st, num_cus)));
     else
       KLF_TRY((launch_scan<kScanPlain, 1>(a, st, num_cus)));
     KLF_TRY(hipEventRecord(ev[6], st));  // k_scan alone (the roofline kernel)
@@ -2570,6 +2680,10 @@ hipError_t launch_pipeline(const RunArgs& a, hipStream_t st, hipEvent_t* ev, int
   if (a.grep_mode == kGrepGeneral && a.pats.qf_on) {
     hipLaunchKernelGGL(k_verify, dim3(num_cus * 8), dim3(256), 0, st, a);
     KLF_TRY(hipGetLastError());
+    if (a.count_pats) {
+      hipLaunchKernelGGL(k_fixcount, dim3(num_cus * 2), dim3(256), 0, st, a);
+      KLF_TRY(hipGetLastError());
+    }
   }
   if (a.grep_mode == kGrepGeneral && a.pats.qf_on && a.pats.rx_count) {
     const size_t lds = nfa_lds_bytes(a.pats);

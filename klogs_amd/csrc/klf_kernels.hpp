@@ -44,6 +44,7 @@ constexpr uint32_t kCtrCopyChunks = 11;              // counters[11]: output cop
 constexpr uint64_t kCopyChunk = KLF_COPY_CHUNK_KB * 1024;  // output bytes per k_cgather work item
 constexpr uint32_t kCtrVerified = 10;                // counters[10]: hits k_verify walked (diagnostics)
 constexpr uint32_t kCtrDense = 14;                   // counters[14]: dense compaction (k_tkeep / k_tcopy)
+constexpr uint32_t kCtrPairsOver = 15;               // counters[15]: the per-pattern pair set overflowed
 constexpr uint32_t kQfRegex = 1u << 24;              // entry flags: regex factor (else literal)
 constexpr uint32_t kQfLoose = 1u << 25;              //   compare OR 0x20 per byte
 constexpr size_t kNfaMaxLds = 64 * 1024;            // k_nfa stages its tables in LDS up to this
@@ -65,10 +66,29 @@ __host__ __device__ inline uint32_t qf_hist_bin0(uint32_t g) { return qf_h1(g) >
 __host__ __device__ inline uint32_t qf_hist_bin1(uint32_t g) {
   return (1u << kQfHistBits) + ((g * 0x85EBCA77u) >> (32 - kQfHistBits));
 }
-__host__ __device__ inline uint32_t qf_word(uint32_t h1) { return h1 >> (32 - kQfBucketBits); }
-__host__ __device__ inline uint32_t qf_bits(uint32_t h1, uint32_t h2) {
-  return (1u << ((h1 >> 15) & 31u)) | (1u << (h2 & 31u)) | (1u << ((h2 >> 5) & 31u));
+// The scan's probe (k_scan<gen>): the gram's bytes 0..2 (for K = 3 folded, f = x ^ x >> 13,
+// so that the bit positions see all of them: measured offline on the C4 set, 1.7 false
+// hits per 8 KiB tile folded against 9.9 unfolded; the K = 2 sets are small and do as
+// well without) and, for 4-byte grams, bytes 1..3 (v_bfe extracts them, width 0 for
+// 3-byte grams, so no mask is applied), hashed with two full-rate 24-bit
+// multiply(-add)s; a blocked Bloom word (top 12 bits = also the verification bucket)
+// with K = 2 bits at hash bits 15..19 / 10..14, or K = 3 with a third from the high half
+// of f's product.  ~11 (K = 2) / 15 (K = 3) VALU per probe (the previous design: ~19).
+__host__ __device__ inline uint32_t qf_fold3(uint32_t g, uint32_t k) {
+  return (k == 3 ? g ^ ((g & 0xFFFFFFu) >> 13) : g) & 0xFFFFFFu;
 }
+__host__ __device__ inline uint32_t qf_hash(uint32_t g, uint32_t w24, uint32_t k) {  // w24 = 24 (q = 4) or 0 (q = 3)
+  const uint32_t hi = w24 ? (g >> 8) & 0xFFFFFFu : 0u;
+  return qf_fold3(g, k) * 0x9E3779u + hi * 0x7F4A7Du;
+}
+__host__ __device__ inline uint32_t qf_hash3(uint32_t g) {  // the third bit (K = 3)
+  return (uint32_t)(((uint64_t)qf_fold3(g, 3) * 0xC2B2AEu) >> 32);  // v_mul_hi_u32_u24
+}
+__host__ __device__ inline uint32_t qf_word(uint32_t h) { return h >> (32 - kQfBucketBits); }
+__host__ __device__ inline uint32_t qf_bits(uint32_t g, uint32_t h, uint32_t k) {
+  return (1u << ((h >> 15) & 31u)) | (1u << ((h >> 10) & 31u)) | (k == 3 ? 1u << (qf_hash3(g) & 31u) : 0u);
+}
+constexpr uint32_t kQfK2MaxGrams = 1536;  // up to this many sampled grams K = 2 bits, else 3
 
 // Dense compaction: per-tile copy record written by k_tkeep, read by k_ksum / k_kbase /
 // k_tcopy (16 B), and up to kRunSlots kept runs per tile (u32: tile offset of the run's
@@ -128,7 +148,10 @@ struct DevPatterns {  // device copies of CompiledSet tables (kGrepGeneral)
   const uint8_t* ac_class = nullptr;
   const uint32_t* ac_next = nullptr;
   const uint8_t* ac_accept = nullptr;
+  const int32_t* ac_out = nullptr;    // [states] literal id ending here, -1 none
+  const uint32_t* ac_dict = nullptr;  // [states] dictionary link (0 none)
   uint32_t ac_states = 0, ac_classes = 0;
+  uint32_t n_cids = 0, n_lits = 0;    // compiled pattern ids: literals, then regexes
   const uint8_t* rx_class = nullptr;
   const uint64_t* rx_b = nullptr;
   const uint64_t* rx_follow = nullptr;
@@ -143,6 +166,7 @@ struct DevPatterns {  // device copies of CompiledSet tables (kGrepGeneral)
   uint32_t rx_unbounded = 0;          // regexes without a bound (k_nfa runs their whole lines)
   // q-gram prefilter (qf_on): bitmap, buckets, needles
   uint32_t qf_on = 0, qf_stride = 1, qf_fold = 0, qf_mask = ~0u;
+  uint32_t qf_w24 = 24, qf_k = 3;     // probe: 4-byte grams (24) or 3-byte (0); bits per gram
   const uint32_t* qf_bitmap = nullptr;
   const uint32_t* qf_head = nullptr;
   const uint4* qf_ent = nullptr;
@@ -208,6 +232,12 @@ struct RunArgs {
   uint32_t* truns;      // [ntiles * kRunSlots] the tiles' kept runs (k_tkeep -> k_tcopy)
   uint64_t* kbase;      // [2 * ntiles]
   uint32_t compact_mode;  // 0 auto, 1 line gather (sparse), 2 tile copy (dense)
+  // per-pattern counts (KLF_FILTER_PATTERN_COUNTS): pcount[segment * n_cids + cid] lines,
+  // each (line, cid) counted once through the `pairs` hash set (open addressing, u64 keys)
+  uint32_t count_pats;
+  uint32_t* pcount;
+  uint64_t* pairs;
+  uint32_t pairs_log2;
 };
 
 // Enqueues the whole pipeline on `stream`; `ev` (6 events) brackets the stages for

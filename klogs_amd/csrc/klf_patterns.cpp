@@ -930,10 +930,41 @@ bool compile_set(const std::vector<std::vector<uint8_t>>& pats, const std::vecto
     }
   }
   out.rx_pre = rx_pre;
-  if (always) { out.mode = CompiledSet::kAll; return true; }
   // dedupe literals
   std::sort(lits.begin(), lits.end());
   lits.erase(std::unique(lits.begin(), lits.end()), lits.end());
+  {  // per-pattern counts: user pattern -> compiled id (literals, then regexes)
+    out.n_cids = (uint32_t)(lits.size() + rxs.size());
+    out.n_lits = (uint32_t)lits.size();
+    out.user_map.assign(pats.size(), CompiledSet::kCidNever);
+    size_t r = 0;
+    for (size_t k = 0; k < pats.size(); ++k) {
+      if (kinds[k] == KLF_PAT_LITERAL) {
+        const auto& l = pats[k];
+        if (l.empty()) { out.user_map[k] = CompiledSet::kCidAlways; continue; }
+        if (std::find(l.begin(), l.end(), (uint8_t)'\n') != l.end()) continue;
+        out.user_map[k] = (int32_t)(std::lower_bound(lits.begin(), lits.end(), l) - lits.begin());
+      } else {
+        while (r < rx_src.size() && rx_src[r] < k) ++r;
+        if (r < rx_src.size() && rx_src[r] == k) out.user_map[k] = (int32_t)(lits.size() + r);
+      }
+    }
+    // regexes that match every content
+    for (size_t k = 0; k < pats.size(); ++k)
+      if (kinds[k] == KLF_PAT_REGEX && out.user_map[k] == CompiledSet::kCidNever) {
+        GlushkovTables g;
+        std::string e2;
+        int c2 = 0;
+        if (compile_regex(pats[k].data(), pats[k].size(), g, e2, c2) && g.accept_at_start && g.accept_empty)
+          out.user_map[k] = CompiledSet::kCidAlways;
+      }
+  }
+  if (always) {
+    out.mode = CompiledSet::kAll;
+    for (auto& m : out.user_map)  // the set is not evaluated: only the always-patterns are counted
+      if (m >= 0) m = CompiledSet::kCidUncounted;
+    return true;
+  }
   if (lits.empty() && rxs.empty()) { out.mode = CompiledSet::kNever; return true; }
   if (rxs.empty() && lits.size() == 1 && lits[0].size() <= 256) {
     out.mode = CompiledSet::kLiteral1;
@@ -961,6 +992,7 @@ bool compile_set(const std::vector<std::vector<uint8_t>>& pats, const std::vecto
     }
     std::vector<std::map<int, int>> go(1);
     std::vector<uint8_t> term(1, 0);
+    std::vector<int32_t> term_id(1, -1);  // literal id ending exactly at a state
     for (auto& l : lits) {
       int s = 0;
       for (uint8_t c : l) {
@@ -976,6 +1008,8 @@ bool compile_set(const std::vector<std::vector<uint8_t>>& pats, const std::vecto
         }
       }
       term[s] = 1;
+      term_id.resize(go.size(), -1);
+      term_id[s] = (int32_t)(&l - &lits[0]);
     }
     const size_t ns = go.size();
     if (ns >= (1u << 31)) { err = "AC automaton too large"; err_code = KLF_ETOOBIG; return false; }
@@ -983,6 +1017,9 @@ bool compile_set(const std::vector<std::vector<uint8_t>>& pats, const std::vecto
     out.ac_classes = (uint32_t)ncls;
     out.ac_next.assign(ns * ncls, 0);
     out.ac_accept.assign(ns, 0);
+    term_id.resize(ns, -1);
+    out.ac_out.assign(term_id.begin(), term_id.end());
+    out.ac_dict.assign(ns, 0u);
     std::vector<int> fail(ns, 0);
     std::queue<int> q;
     for (int c = 0; c < ncls; ++c) {
@@ -996,6 +1033,8 @@ bool compile_set(const std::vector<std::vector<uint8_t>>& pats, const std::vecto
       int s = q.front();
       q.pop();
       out.ac_accept[s] = term[s] | out.ac_accept[fail[s]];
+      // dictionary link: the nearest state on the fail chain where a literal ends
+      out.ac_dict[s] = (uint32_t)(term_id[fail[s]] >= 0 ? fail[s] : (int)out.ac_dict[fail[s]]);
       for (int c = 0; c < ncls; ++c) {
         auto it = go[s].find(c);
         if (it != go[s].end()) {
@@ -1059,7 +1098,7 @@ void build_prefilter(const std::vector<std::vector<uint8_t>>& lits, const std::v
     uint32_t flags, rx;
   };
   std::vector<Needle> nd;
-  for (auto& l : lits) nd.push_back({std::string(l.begin(), l.end()), 0u, 0u});
+  for (size_t i = 0; i < lits.size(); ++i) nd.push_back({std::string(lits[i].begin(), lits[i].end()), 0u, (uint32_t)i});
   for (size_t r = 0; r < rx_fac.size(); ++r) {
     if (rx_fac[r].empty()) { out.qf_why = "regex " + std::to_string(r) + " has no required literal factor"; return; }
     for (auto& f : rx_fac[r]) nd.push_back({f, kQfRegex | (rx_loose[r] ? kQfLoose : 0u), (uint32_t)r});
@@ -1122,6 +1161,8 @@ void place_needles(CompiledSet& out, const std::vector<uint32_t>* hist) {
   std::map<uint32_t, int> used;  // gram -> needles sampling it so far
   std::vector<std::vector<uint32_t>> buckets(kQfWords);
   const size_t n = out.qf_needle.size();
+  out.qf_k = n * S <= kQfK2MaxGrams ? 2u : 3u;  // few grams: two bits per gram keep the false hits rare
+  const uint32_t w24 = q == 4 ? 24u : 0u;
   for (uint32_t i = 0; i < n; ++i) {
     const std::string& s = out.qf_needle[i];
     const uint32_t amax = (uint32_t)std::min<size_t>(s.size() - (q + S - 1), 255 - (S - 1));
@@ -1147,9 +1188,9 @@ void place_needles(CompiledSet& out, const std::vector<uint32_t>* hist) {
     for (uint32_t j = 0; j < S; ++j) {
       const uint32_t k = best_a + j, g = gram_at(s, k);
       used[g]++;
-      const uint32_t h1 = qf_h1(g);
-      out.qf_bitmap[qf_word(h1)] |= qf_bits(h1, qf_h2(g));
-      buckets[qf_word(h1)].push_back(i << 8 | k);
+      const uint32_t h = qf_hash(g, w24, out.qf_k);
+      out.qf_bitmap[qf_word(h)] |= qf_bits(g, h, out.qf_k);
+      buckets[qf_word(h)].push_back(i << 8 | k);
     }
   }
   // needle bytes (loose needles are already stored OR 0x20), then 16-B entries per bucket
@@ -1203,9 +1244,9 @@ bool prefilter_match(const CompiledSet& cs, const uint8_t* s, size_t n, uint32_t
     uint32_t g = 0;
     for (uint32_t b = 0; b < 4; ++b) g |= (uint32_t)(p + b < n ? s[p + b] : 0) << (8 * b);
     g = (g | cs.qf_fold) & cs.qf_mask;
-    const uint32_t h1 = qf_h1(g), bits = qf_bits(h1, qf_h2(g));
-    if ((cs.qf_bitmap[qf_word(h1)] & bits) != bits) continue;
-    const uint32_t b = qf_word(h1);
+    const uint32_t h = qf_hash(g, cs.qf_q == 4 ? 24u : 0u, cs.qf_k), bits = qf_bits(g, h, cs.qf_k);
+    if ((cs.qf_bitmap[qf_word(h)] & bits) != bits) continue;
+    const uint32_t b = qf_word(h);
     for (uint32_t e = cs.qf_head[b]; e < cs.qf_head[b + 1]; ++e) {
       const uint32_t* E = cs.qf_ent.data() + 4 * (size_t)e;
       const uint32_t m = E[1] & 0xFFFFu, k = (E[1] >> 16) & 0xFFu;

@@ -52,6 +52,13 @@ struct CompiledSet {
   std::vector<uint8_t> ac_class;    // [256] byte -> class
   std::vector<uint32_t> ac_next;    // [states * classes]
   std::vector<uint8_t> ac_accept;   // [states] 1 if a literal ends here (via fail links)
+  std::vector<int32_t> ac_out;      // [states] id of the literal ending exactly here, -1 none
+  std::vector<uint32_t> ac_dict;    // [states] nearest fail-chain state with ac_out >= 0 (0 none)
+
+  // per-pattern counts: compiled ids = literals (sorted, deduplicated) then regexes
+  static constexpr int32_t kCidNever = -1, kCidAlways = -2, kCidUncounted = -3;
+  uint32_t n_cids = 0, n_lits = 0;
+  std::vector<int32_t> user_map;    // [patterns] compiled id, or kCid* for the special cases
 
   // kGeneral: regexes.  Byte classes shared by all regexes (partition refinement).
   uint32_t rx_count = 0;
@@ -74,7 +81,8 @@ struct CompiledSet {
   uint32_t qf_stride = 1;    // 1, 2 or 4
   uint32_t qf_fold = 0;      // 0x20202020 when some needle compares case-insensitively
   uint32_t qf_mask = ~0u;    // gram bytes (q < 4: low q bytes)
-  std::vector<uint32_t> qf_bitmap;   // [kQfWords]: 2 bits of word qf_word(qf_h1) per gram
+  uint32_t qf_k = 3;         // bitmap bits per gram (qf_bits)
+  std::vector<uint32_t> qf_bitmap;   // [kQfWords]: qf_k bits of word qf_word(qf_hash) per gram
   std::vector<uint32_t> qf_head;     // [kQfWords + 1] bucket (= bitmap word) -> first entry
   std::vector<uint32_t> qf_ent;      // 16-B entries {needle dword offset, len | k << 16 | flags,
                                      //  regex, first needle dword}; k = offset of the gram

@@ -82,6 +82,8 @@ SIGNATURES = {
                                     C.POINTER(_Counts)]),
     "klf_result_lines": (C.c_int, [C.c_void_p, C.c_uint32, C.POINTER(C.c_void_p), C.POINTER(C.c_uint64)]),
     "klf_result_match_bits": (C.c_int, [C.c_void_p, C.c_uint32, C.POINTER(C.c_void_p), C.POINTER(C.c_uint64)]),
+    "klf_result_pattern_counts": (C.c_int, [C.c_void_p, C.c_uint32, C.POINTER(C.c_uint64), C.c_uint32,
+                                            C.POINTER(C.c_uint32)]),
     "klf_result_last_unparsed": (C.c_int, [C.c_void_p, C.c_uint32, C.POINTER(C.c_uint64)]),
     "klf_result_device_out": (C.c_int, [C.c_void_p, C.c_uint32, C.POINTER(C.c_void_p), C.POINTER(C.c_uint64),
                                         C.POINTER(C.c_uint64)]),
@@ -89,6 +91,11 @@ SIGNATURES = {
     "klf_result_timing": (C.c_int, [C.c_void_p, C.POINTER(C.c_double), C.c_uint32, C.POINTER(C.c_uint32)]),
     "klf_result_totals": (C.c_int, [C.c_void_p, C.POINTER(_Counts)]),
     "klf_result_free": (None, [C.c_void_p]),
+    "klf_follow_open": (C.c_int, [C.c_void_p, C.POINTER(_Filter), C.POINTER(C.c_void_p)]),
+    "klf_follow_feed": (C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p, C.c_size_t]),
+    "klf_follow_flush": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(C.c_void_p)]),
+    "klf_follow_open_bytes": (C.c_uint64, [C.c_void_p, C.c_uint32]),
+    "klf_follow_close": (None, [C.c_void_p]),
     "klf_parse_rfc3339nano": (C.c_int, [C.c_void_p, C.c_size_t, C.POINTER(_Time)]),
     "klf_debug_compile": (C.c_int, [C.POINTER(_Pattern), C.c_uint32, C.POINTER(C.c_uint32), C.c_char_p,
                                     C.c_size_t]),
@@ -150,14 +157,16 @@ def _patterns(grep: Sequence[bytes], match: Sequence[bytes]):
 
 
 KLF_FILTER_STAGE_TIMES = 1
+KLF_FILTER_PATTERN_COUNTS = 2
 
 
-def _filter(since: Optional[Tuple[int, int]], tail: int, stage_times: bool = False) -> _Filter:
+def _filter(since: Optional[Tuple[int, int]], tail: int, stage_times: bool = False,
+            pattern_counts: bool = False) -> _Filter:
     f = _Filter()
     s = GO_ZERO_TIME if since is None else since
     f.since.sec, f.since.nsec = int(s[0]), int(s[1])
     f.tail = int(tail)
-    f.flags = KLF_FILTER_STAGE_TIMES if stage_times else 0
+    f.flags = (KLF_FILTER_STAGE_TIMES if stage_times else 0) | (KLF_FILTER_PATTERN_COUNTS if pattern_counts else 0)
     return f
 
 
@@ -252,6 +261,15 @@ class Result:
         _check(_lib.klf_result_match_bits(self._p, i, C.byref(p), C.byref(n)))
         return C.string_at(p.value, n.value) if n.value else b""
 
+    def pattern_counts(self, i: int) -> List[int]:
+        """klf_result_pattern_counts: matching lines of stream i per pattern (the run needs
+        pattern_counts=True)."""
+        n = C.c_uint32()
+        _check(_lib.klf_result_pattern_counts(self._p, i, None, 0, C.byref(n)), self._eng._h)
+        buf = (C.c_uint64 * max(1, n.value))()
+        _check(_lib.klf_result_pattern_counts(self._p, i, buf, n.value, C.byref(n)), self._eng._h)
+        return [int(x) for x in buf[: n.value]]
+
     def last_unparsed(self, i: int) -> int:
         """klf_result_last_unparsed: rank from the end (over newline-terminated lines) of the
         stream's last unparseable terminated line, 0 = none."""
@@ -291,6 +309,13 @@ class Result:
         k = C.c_uint32()
         _check(_lib.klf_result_timing(self._p, ms, 7, C.byref(k)))
         return list(ms[: k.value])
+
+    def stream_counts(self, i: int) -> dict:
+        """The stream's counts alone (klf_result_stream with bytes NULL: no output D2H)."""
+        n = C.c_uint64()
+        c = _Counts()
+        _check(_lib.klf_result_stream(self._p, i, None, C.byref(n), C.byref(c)))
+        return c.as_dict()
 
     def totals(self) -> dict:
         c = _Counts()
@@ -354,18 +379,19 @@ class Engine:
     def reset(self):
         _check(_lib.klf_reset(self._h), self._h)
 
-    def run(self, since=None, tail: int = -1, n_streams: Optional[int] = None, stage_times: bool = False) -> Result:
-        f = _filter(since, tail, stage_times)
+    def run(self, since=None, tail: int = -1, n_streams: Optional[int] = None, stage_times: bool = False,
+            pattern_counts: bool = False) -> Result:
+        f = _filter(since, tail, stage_times, pattern_counts)
         r = C.c_void_p()
         _check(_lib.klf_run(self._h, C.byref(f), C.byref(r)), self._h)
         return Result(r.value or 0, n_streams if n_streams is not None else 0, self)
 
     def run_device(self, d_ptr: int, seg_base: Sequence[int], lens: Sequence[int], since=None,
-                   tail: int = -1, stage_times: bool = False) -> Result:
+                   tail: int = -1, stage_times: bool = False, pattern_counts: bool = False) -> Result:
         n = len(lens)
         B = (C.c_uint64 * max(1, n))(*[int(x) for x in seg_base])
         L = (C.c_uint64 * max(1, n))(*[int(x) for x in lens])
-        f = _filter(since, tail, stage_times)
+        f = _filter(since, tail, stage_times, pattern_counts)
         r = C.c_void_p()
         _check(_lib.klf_run_device(self._h, C.c_void_p(d_ptr), n, B, L, C.byref(f), C.byref(r)), self._h)
         return Result(r.value or 0, n, self)

@@ -9,6 +9,11 @@ client side cannot tell backlog bytes from new ones, so in follow mode the serve
 applies what is per line: the since cutoff (idempotent with the server's) and the grep
 set, prefix strip included (SPEC.md S1/S2/S5).
 
+`Follow` is the product path: a thin wrapper over the C ABI's follow session
+(klf_follow_open / feed / flush / close, include/klf.h), which carries the open lines and
+stages complete ones on the engine as they arrive.  `FollowBatch` restates the same
+carry rules in Python over any batch runner (the CPU tests drive it with the oracle).
+
 `FollowBatch` is the incremental chunked engine: `feed(stream, chunk)` carries each
 stream's open (unterminated) line across chunks; `flush()` runs ONE engine pass over the
 complete lines every stream has received since the last flush (one device batch for all
@@ -18,7 +23,8 @@ flush outputs equal the filter of the whole stream with tail -1 (tests/test_foll
 """
 from __future__ import annotations
 
-from typing import Callable, Dict, List, Sequence
+import ctypes as C
+from typing import Callable, Dict, List, Optional, Sequence, Tuple
 
 
 class FollowBatch:
@@ -77,3 +83,56 @@ def engine_runner(engine, since=None) -> Callable[[Sequence[bytes]], List[bytes]
         finally:
             r.free()
     return run
+
+
+class Follow:
+    """A follow session on one Engine (klf_follow_*): feed(stream, chunk) from any thread
+    (different streams concurrently), flush(final) -> {stream_id: output bytes} for the
+    streams that received input since the previous flush."""
+
+    def __init__(self, engine, since: Optional[Tuple[int, int]] = None):
+        from . import engine as E
+        self._E = E
+        self._eng = engine
+        f = E._filter(since, -1)
+        h = C.c_void_p()
+        E._check(E._lib.klf_follow_open(engine._h, C.byref(f), C.byref(h)), engine._h)
+        self._h = h
+
+    def feed(self, stream_id: int, chunk: bytes) -> None:
+        E = self._E
+        buf = C.create_string_buffer(chunk, len(chunk) or 1)
+        E._check(E._lib.klf_follow_feed(self._h, stream_id, buf, len(chunk)), self._eng._h)
+
+    def open_bytes(self, stream_id: int) -> int:
+        return int(self._E._lib.klf_follow_open_bytes(self._h, stream_id))
+
+    def flush(self, final: bool = False) -> Dict[int, bytes]:
+        E = self._E
+        r = C.c_void_p()
+        E._check(E._lib.klf_follow_flush(self._h, 1 if final else 0, C.byref(r)), self._eng._h)
+        res = E.Result(r.value or 0, 0, self._eng)
+        try:
+            out = {}
+            i = 0
+            while True:  # the result covers ids [0, max id fed]
+                p, n, c = C.c_void_p(), C.c_uint64(), E._Counts()
+                if E._lib.klf_result_stream(res._p, i, C.byref(p), C.byref(n), C.byref(c)):
+                    break
+                if c.lines:
+                    out[i] = C.string_at(p.value, n.value) if n.value else b""
+                i += 1
+            return out
+        finally:
+            res.free()
+
+    def close(self) -> None:
+        if self._h:
+            self._E._lib.klf_follow_close(self._h)
+            self._h = C.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()

@@ -42,22 +42,28 @@ def local_streams(lens: Sequence[int], world: int, rank: int) -> List[int]:
     return [i for i, r in enumerate(own) if r == rank]
 
 
-def pack_records(counts: Dict[int, dict], cap: int) -> np.ndarray:
-    """Fixed-size [cap, NREC] int64 block of this rank's records (stream_id -1 = padding)."""
-    rec = np.zeros((cap, NREC), dtype=np.int64)
+def pack_records(counts: Dict[int, dict], cap: int, n_patterns: int = 0) -> np.ndarray:
+    """Fixed-size [cap, NREC + n_patterns] int64 block of this rank's records (stream_id -1
+    = padding).  With n_patterns > 0 every counts dict also holds "patterns": the lines of
+    the stream each --grep/--match pattern matches (klf_result_pattern_counts)."""
+    rec = np.zeros((cap, NREC + n_patterns), dtype=np.int64)
     rec[:, 0] = -1
     for j, (sid, c) in enumerate(sorted(counts.items())):
         rec[j, 0] = sid
         for k, f in enumerate(RECORD_FIELDS[1:], start=1):
             rec[j, k] = int(c[f])
+        if n_patterns:
+            rec[j, NREC:] = np.asarray(c["patterns"], dtype=np.int64)
     return rec
 
 
-def unpack_records(blocks: np.ndarray, n_streams: int) -> np.ndarray:
-    """[world * cap, NREC] gathered blocks -> dense [n_streams, NREC - 1] count table."""
-    out = np.zeros((n_streams, NREC - 1), dtype=np.int64)
+def unpack_records(blocks: np.ndarray, n_streams: int, n_patterns: int = 0) -> np.ndarray:
+    """[world * cap, NREC + n_patterns] gathered blocks -> dense [n_streams, NREC - 1 +
+    n_patterns] count table."""
+    w = NREC + n_patterns
+    out = np.zeros((n_streams, w - 1), dtype=np.int64)
     seen = np.zeros(n_streams, dtype=bool)
-    for row in blocks.reshape(-1, NREC):
+    for row in blocks.reshape(-1, w):
         sid = int(row[0])
         if sid < 0:
             continue
@@ -71,42 +77,43 @@ def unpack_records(blocks: np.ndarray, n_streams: int) -> np.ndarray:
 
 
 def gather_counts(counts: Dict[int, dict], lens: Sequence[int], world: int, device=None,
-                  allgather=None) -> np.ndarray:
-    """All-gathers every rank's per-stream records (one collective) -> [n_streams, 6].
-    allgather(block [cap, NREC] int64) -> [world * cap, NREC] replaces the collective (the
-    in-process simulations of several ranks)."""
+                  allgather=None, n_patterns: int = 0) -> np.ndarray:
+    """All-gathers every rank's per-stream records (one collective) -> [n_streams, 6 +
+    n_patterns].  allgather(block [cap, width] int64) -> [world * cap, width] replaces the
+    collective (the in-process simulations of several ranks)."""
     cap = max(len(local_streams(lens, world, r)) for r in range(world)) or 1
     if allgather is not None:
-        return unpack_records(np.asarray(allgather(pack_records(counts, cap))), len(lens))
+        return unpack_records(np.asarray(allgather(pack_records(counts, cap, n_patterns))), len(lens), n_patterns)
     import torch
     import torch.distributed as dist
 
-    rec = torch.from_numpy(pack_records(counts, cap))
+    rec = torch.from_numpy(pack_records(counts, cap, n_patterns))
     if device is not None:
         rec = rec.to(device)
     if world > 1:
-        out = torch.empty(world * cap, NREC, dtype=torch.int64, device=rec.device)
+        out = torch.empty(world * cap, NREC + n_patterns, dtype=torch.int64, device=rec.device)
         dist.all_gather_into_tensor(out, rec)
     else:
         out = rec
-    return unpack_records(out.cpu().numpy(), len(lens))
+    return unpack_records(out.cpu().numpy(), len(lens), n_patterns)
 
 
 def run_shard(lens: Sequence[int], fetch: Callable[[int], bytes], runner, world: int, rank: int,
-              device=None, allgather=None):
+              device=None, allgather=None, n_patterns: int = 0):
     """Filters this rank's streams and gathers every stream's counts.
 
     fetch(stream_id) -> the stream's captured bytes; runner(list of bytes) -> list of
     (out bytes, counts dict) in the same order (the engine on a GPU; the CPU tests pass
-    a checker).  Returns ({stream_id: out bytes} for the local streams, count table)."""
+    a checker).  With n_patterns the counts carry per-pattern line counts ("patterns").
+    Returns ({stream_id: out bytes} for the local streams, count table)."""
     mine = local_streams(lens, world, rank)
     res = runner([fetch(i) for i in mine]) if mine else []
     outs = {sid: r[0] for sid, r in zip(mine, res)}
     counts = {sid: r[1] for sid, r in zip(mine, res)}
-    return outs, gather_counts(counts, lens, world, device, allgather)
+    return outs, gather_counts(counts, lens, world, device, allgather, n_patterns)
 
 
-def engine_runner(engine, since=None, tail: int = -1):
+def engine_runner(engine, since=None, tail: int = -1, pattern_counts: bool = False):
     """runner for run_shard over a klogs_amd.engine.Engine (one GPU per process)."""
     def run(streams: List[bytes]):
         engine.reset()
@@ -114,12 +121,15 @@ def engine_runner(engine, since=None, tail: int = -1):
         for i, s in enumerate(streams):
             if s:
                 engine.stage(i, s)
-        r = engine.run(since=since, tail=tail, n_streams=len(streams))
+        r = engine.run(since=since, tail=tail, n_streams=len(streams), pattern_counts=pattern_counts)
         try:
             out = []
             for i in range(len(streams)):
                 so = r.stream(i)
-                out.append((so.out, so.counts))
+                c = dict(so.counts)
+                if pattern_counts:
+                    c["patterns"] = r.pattern_counts(i)
+                out.append((so.out, c))
             return out
         finally:
             r.free()

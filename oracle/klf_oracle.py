@@ -560,6 +560,23 @@ def compile_patterns(grep: Sequence[bytes] = (), match: Sequence[bytes] = ()) ->
     return [Pattern("literal", g) for g in grep] + [Pattern("regex", m) for m in match]
 
 
+def pattern_counts(data: bytes, pats: Sequence[Pattern]) -> List[int]:
+    """Per-pattern match counts of one stream (klf_result_pattern_counts; SURVEY.md §8a
+    K4/K5 `count[stream][pattern]`): parsed lines whose content, without its '\\n'
+    (SPEC.md S5), matches pattern p -- a line matching several patterns counts for each,
+    since and tail play no part (like the `matched` count, SPEC.md S6)."""
+    counts = [0] * len(pats)
+    for lo, hi in split_lines(data):
+        p = parse_line(data[lo:hi])
+        if p is None:
+            continue
+        c = content_for_match(p[1])
+        for k, pat in enumerate(pats):
+            if pat.matches(c):
+                counts[k] += 1
+    return counts
+
+
 # ----------------------------------------------------------------------------------
 # kubelet restated
 # ----------------------------------------------------------------------------------

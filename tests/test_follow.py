@@ -23,9 +23,9 @@ def _oracle_runner(streams):
     return [co.filter_stream(x, SINCE, -1, GREP, want_lines=False, want_bits=False)[0] for x in streams]
 
 
-def _drive(runner, streams, seed):
+def _drive(runner, streams, seed, fb=None):
     rng = random.Random(seed)
-    fb = follow.FollowBatch(runner)
+    fb = fb or follow.FollowBatch(runner)
     pos = [0] * len(streams)
     got = [b""] * len(streams)
     while any(p < len(s) for p, s in zip(pos, streams)):
@@ -61,7 +61,57 @@ def test_follow_carry_and_empty_flush():
 
 
 @pytest.mark.gpu
-def test_follow_on_engine(gpu):
+@pytest.mark.parametrize("seed", [11, 12, 13])
+def test_follow_on_engine(gpu, seed):
+    """The C follow session (klf_follow_open / feed / flush / close) against the oracle."""
+    from klogs_amd import engine as E
+    streams = _streams()
+    with E.Engine(0, grep=GREP) as eng, follow.Follow(eng, since=SINCE) as fw:
+        got = _drive(None, streams, seed, fb=fw)
+    assert got == _oracle_runner(streams)
+
+
+@pytest.mark.gpu
+def test_follow_on_engine_carry_and_empty_flush(gpu):
+    from klogs_amd import engine as E
+    with E.Engine(0, grep=GREP) as eng, follow.Follow(eng, since=SINCE) as fw:
+        assert fw.flush() == {} and fw.flush(final=True) == {}
+        fw.feed(3, b"2024-10-22T00:59:00Z pod a")
+        assert fw.open_bytes(3) == len(b"2024-10-22T00:59:00Z pod a") and fw.flush() == {}
+        fw.feed(3, b"bc\n2024-10-22T00:59:01Z pod d")
+        assert fw.flush() == {3: b"pod abc\n"}
+        assert fw.flush(final=True) == {3: b"pod d"}
+        fw.feed(0, b"x\n")  # a session continues after a final flush
+        assert fw.flush() == {0: b""}
+
+
+@pytest.mark.gpu
+def test_follow_on_engine_concurrent_feeds(gpu):
+    """One reader thread per stream (cmd/root.go:249) feeding the same session."""
+    import threading
+    from klogs_amd import engine as E
+    streams = [synth.generate(synth.TEXT, 60 + i, i, 400_000 + 1_000 * i) for i in range(12)]
+    with E.Engine(0, grep=GREP) as eng, follow.Follow(eng, since=SINCE) as fw:
+        def reader(i):
+            rng = random.Random(i)
+            s, p = streams[i], 0
+            while p < len(s):
+                k = rng.choice([5, 999, 65_536, 300_000])
+                fw.feed(i, s[p:p + k])
+                p += k
+        th = [threading.Thread(target=reader, args=(i,)) for i in range(len(streams))]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        got = fw.flush(final=True)
+    assert sorted(got) == list(range(len(streams)))
+    assert [got[i] for i in range(len(streams))] == _oracle_runner(streams)
+
+
+@pytest.mark.gpu
+def test_follow_engine_runner(gpu):
+    """FollowBatch over the batch API (engine_runner) agrees too."""
     from klogs_amd import engine as E
     streams = _streams()
     with E.Engine(0, grep=GREP) as eng:

@@ -48,6 +48,12 @@ def test_records_roundtrip_and_duplicates():
         shard.unpack_records(np.concatenate([rec, rec]), 4)
     with pytest.raises(RuntimeError):
         shard.unpack_records(rec, 4)
+    # per-pattern columns ride after the fixed fields
+    pc = {k: dict(v, patterns=[k, 7]) for k, v in counts.items()}
+    rec = shard.pack_records(pc, 2, n_patterns=2)
+    assert rec.shape == (2, shard.NREC + 2)
+    table = shard.unpack_records(np.concatenate([rec, shard.pack_records({1: pc[0], 2: pc[3]}, 2, 2)]), 4, 2)
+    assert table[3].tolist() == [5, 4, 3, 2, 1, 9, 3, 7] and table[1].tolist()[-2:] == [0, 7]
 
 
 def _streams():
@@ -55,9 +61,12 @@ def _streams():
 
 
 def _oracle_runner(streams):
+    from oracle import klf_oracle as ko
+    pats = ko.compile_patterns([b"pod"])
     res = []
     for s in streams:
         out, _, _, c = co.filter_stream(s, SINCE, TAIL, [b"pod"], want_lines=False, want_bits=False)
+        c = dict(c, patterns=ko.pattern_counts(s, pats))
         res.append((out, c))
     return res
 
@@ -70,7 +79,7 @@ def _worker(rank, world, port, q):
     try:
         streams = _streams()
         lens = [len(s) for s in streams]
-        outs, table = shard.run_shard(lens, lambda i: streams[i], _oracle_runner, world, rank)
+        outs, table = shard.run_shard(lens, lambda i: streams[i], _oracle_runner, world, rank, n_patterns=1)
         q.put((rank, {k: v for k, v in outs.items()}, table))
     finally:
         dist.destroy_process_group()
@@ -107,7 +116,8 @@ def test_gloo_world2_gather_matches_serial():
     assert sorted(outs) == list(range(len(streams)))
     for i, (out, c) in enumerate(serial):
         assert outs[i] == out
-        assert tables[0][i].tolist() == [c[k] for k in shard.RECORD_FIELDS[1:]]
+        assert tables[0][i].tolist() == [c[k] for k in shard.RECORD_FIELDS[1:]] + c["patterns"]
+        assert c["patterns"][0] == c["matched"]  # one literal: its count is `matched`
 
 
 # ---- one stream split by byte range (shard.run_split) ---------------------------------
