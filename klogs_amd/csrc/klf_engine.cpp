@@ -746,8 +746,12 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
     }
     pairs_over = count && counters[klf::kCtrPairsOver] != 0;
     if (pairs_over && pair_reruns < 2 && e->pairs_log2 < 28) {  // the pair set filled: a larger one
+      // distinct pairs <= the set's capacity + the failed inserts; size for load <= 1/2
       ++pair_reruns;
-      e->pairs_log2 = std::min(28u, e->pairs_log2 + 3);
+      const uint64_t need = 2 * (((uint64_t)1 << e->pairs_log2) + counters[klf::kCtrPairsOver]);
+      uint32_t lg = e->pairs_log2 + 1;
+      while (lg < 28 && ((uint64_t)1 << lg) < need) ++lg;
+      e->pairs_log2 = lg;
       continue;
     }
     e->last_args = a;

@@ -754,7 +754,7 @@ __device__ void count_pair(const RunArgs& a, uint64_t l, uint32_t s, uint32_t ci
     if (prev == key) return;
     h = (h + 1u) & mask;
   }
-  atomicOr(&a.counters[kCtrPairsOver], 1u);  // the host re-runs with a larger set
+  atomicAdd(&a.counters[kCtrPairsOver], 1u);  // failed inserts: the host re-runs with a set sized from them
 }
 
 // Every pattern of the set on one content (deferred lines, the fallback matcher): counts

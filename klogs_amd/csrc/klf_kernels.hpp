@@ -44,7 +44,7 @@ constexpr uint32_t kCtrCopyChunks = 11;              // counters[11]: output cop
 constexpr uint64_t kCopyChunk = KLF_COPY_CHUNK_KB * 1024;  // output bytes per k_cgather work item
 constexpr uint32_t kCtrVerified = 10;                // counters[10]: hits k_verify walked (diagnostics)
 constexpr uint32_t kCtrDense = 14;                   // counters[14]: dense compaction (k_tkeep / k_tcopy)
-constexpr uint32_t kCtrPairsOver = 15;               // counters[15]: the per-pattern pair set overflowed
+constexpr uint32_t kCtrPairsOver = 15;               // counters[15]: failed (line, pattern) pair inserts (set full)
 constexpr uint32_t kQfRegex = 1u << 24;              // entry flags: regex factor (else literal)
 constexpr uint32_t kQfLoose = 1u << 25;              //   compare OR 0x20 per byte
 constexpr size_t kNfaMaxLds = 64 * 1024;            // k_nfa stages its tables in LDS up to this
