@@ -1,0 +1,19 @@
+#!/bin/bash
+# One round's profiles, on the GPU box (each step its own time limit, chained):
+#     bash scripts/profile_round.sh OUT
+#   OUT/trace   rocprofv3 --kernel-trace --stats of the driver's exact bench command
+#   OUT/bench.json, bench.err   that run's bench line
+#   OUT/pmc_<cfg>/...           counter passes (scripts/pmc.sh) for C2, C3 and C5
+# then, in the build container: python3 scripts/collect_profiles.py OUT profiles/rNN
+set -e
+cd "$(dirname "$0")/.."
+out=$1
+export TMPDIR=/tmp
+mkdir -p "$out"
+timeout -k 10 700 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/trace" -o run \
+  -- python3 bench.py > "$out/bench.json" 2> "$out/bench.err"
+echo "trace done"
+for c in c2 c3 c5; do
+  bash scripts/pmc.sh "$out/pmc_$c" "$c" "k_scan|k_tcopy|k_tkeep|k_scatter|k_verify|k_nfa"
+done
+echo "profile_round done: $out"
