@@ -56,6 +56,17 @@ def pmc_traffic():
     return int(t["traffic_bytes"]), str(files[-1].relative_to(ROOT))
 
 
+def committed_trace_frac(cfg: str = "c2"):
+    """The same roofline fraction from the newest committed kernel trace
+    (profiles/<round>/summary.json, scripts/collect_profiles.py): bytes / rocprofv3's average
+    launch / peak, measured on the profiling box -- reported beside the live HIP-event one."""
+    files = sorted(ROOT.glob("profiles/r*/summary.json"))
+    if not files:
+        return None, None
+    s = json.loads(files[-1].read_text()).get(cfg)
+    return (s and s["frac_rocprof"]), str(files[-1].relative_to(ROOT))
+
+
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
@@ -239,6 +250,7 @@ def main():
     staged.free()
     k1_avg_s = float(np.mean(k1_ms)) / 1e3
     traffic, traffic_src = pmc_traffic()
+    trace_frac, trace_src = committed_trace_frac("c2")
     value = world * n * args.steps / dt / 1e9
     res = {
         "metric": METRIC,
@@ -261,7 +273,9 @@ def main():
         "roofline": {"bound": "hbm", "kernel": "k_scan<literal>", "achieved": round(achieved, 1),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic, "traffic_source": traffic_src, "alg_bytes_per_launch": scan_alg,
-                     "avg_launch_ms": round(scan_avg_s * 1e3, 4)},
+                     "avg_launch_ms": round(scan_avg_s * 1e3, 4),
+                     "frac_source": "HIP events on the launch stream around k_scan, this run",
+                     "frac_rocprof_committed": trace_frac, "rocprof_source": trace_src},
         "cpu_baseline": cpu,
         "extra": {"device_ms_per_step": round(dev_avg_s * 1e3, 4),
                   "k1_stage": {"kernels": "k_scan+k_fixup+k_tsum+k_tbase+k_scatter", "alg_bytes": k1_alg,
@@ -432,6 +446,52 @@ def extra_streams(name: str, total: int):
     raise ValueError(name)
 
 
+def cpu_extra(name: str, kind: int, pats: dict, permille: int, since, tail: int) -> dict:
+    """CPU reference points for configs 3-5 (rank 0, N = 1; bounded, a few seconds each) on
+    samples of the same generator and shape: the C restatement (literal paths) on 1 and on
+    T host threads (one stream per thread, as the reference runs one goroutine per stream),
+    and for the regex set the Python restatement (one core: Python `re` holds the GIL)."""
+    from concurrent.futures import ThreadPoolExecutor
+    sys.path.insert(0, str(ROOT / "oracle"))
+    import c_oracle as co
+    threads = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", "16") or 16)))
+    sample = {"c3": 64 << 20, "c4": 2 << 20, "c5": 2 << 20}[name]
+    streams = [synth.generate(kind, 7, i, sample, permille=permille) for i in range(threads)]
+    grep = pats.get("grep", [])
+    sn = since if since is not None else co.GO_ZERO_TIME
+
+    def one(b):
+        return co.filter_stream(b, sn, tail, grep, want_lines=False, want_bits=False)
+
+    def timed(f, budget):
+        n, t = 0, 0.0
+        while t < budget and n < 64:
+            t0 = time.perf_counter()
+            f()
+            t += time.perf_counter() - t0
+            n += 1
+        return n, t
+    res = {}
+    if name == "c5":
+        from oracle import klf_oracle as ko
+        cp = ko.compile_patterns(match=pats["match"])
+        n, t = timed(lambda: ko.filter_stream(streams[0], sn, tail, cp), 3.0)
+        res["port_1_core"] = {"value": round(sample * n / t / 1e9, 4), "unit": "GB/s", "cores": 1,
+                              "kind": "port", "sample": f"{n} passes over one {sample >> 20} MiB stream of the "
+                                                        f"C5 generator, oracle/klf_oracle.py (Python re), {t:.1f} s"}
+        return res
+    n, t = timed(lambda: one(streams[0]), 3.0)
+    res["port_1_core"] = {"value": round(sample * n / t / 1e9, 4), "unit": "GB/s", "cores": 1, "kind": "port",
+                          "sample": f"{n} passes over one {sample >> 20} MiB stream of the {name.upper()} generator, "
+                                    f"oracle/klf_oracle_c.c, {t:.1f} s"}
+    with ThreadPoolExecutor(threads) as ex:
+        n, t = timed(lambda: list(ex.map(one, streams)), 3.0)
+    res["port_threads"] = {"value": round(sample * threads * n / t / 1e9, 4), "unit": "GB/s", "cores": threads,
+                           "kind": "port", "sample": f"{n} passes over {threads} streams of {sample >> 20} MiB, "
+                                                     f"one host thread per stream, {t:.1f} s"}
+    return res
+
+
 def run_extra(name: str, args, local: int, now: int) -> dict:
     sizes, kind, pats, permille, desc = extra_streams(name, args.extra_bytes)
     t = time.time()
@@ -515,6 +575,8 @@ def run_extra(name: str, args, local: int, now: int) -> dict:
         "matched_lines": tot["matched"], "selected_lines": tot["selected"], "out_bytes": tot["out_bytes"],
         "stage_ms": [round(x, 4) for x in stage],
     }
+    if not getattr(args, "no_cpu_baseline", True):
+        out["cpu_baseline"] = cpu_extra(name, kind, pats, permille, since, tail)
     if verified is not None:
         out["verified_vs_c_oracle"] = bool(verified)
     if write is not None:

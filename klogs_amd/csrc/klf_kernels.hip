@@ -2469,30 +2469,29 @@ __global__ __launch_bounds__(256) void k_tcopy(RunArgs a, const uint4* __restric
       }
       *reinterpret_cast<uint4*>(outc + 16 * (uint64_t)c) = make_uint4(o[0], o[1], o[2], o[3]);
     }
-    // head / tail chunks shared with the neighbouring tiles: only this tile's bytes (lane 0
-    // the head chunk, lane 1 the tail chunk; one chunk holding both is the head's)
+    // head / tail chunks shared with the neighbouring tiles: only this tile's bytes, one
+    // byte per lane (lanes 0-15 the head chunk, 16-31 the tail chunk; a chunk holding both
+    // ends is the head's), so both go out in ONE byte-store instruction
     {
-      const uint32_t ct = (kept + o15) >> 4;
-      bool edge = false;
-      uint32_t c = 0, xs = 0, xe = 0;
-      if (lane == 0 && o15) {
-        edge = true;
+      const uint32_t ct = (kept + o15) >> 4, i = (uint32_t)lane & 15u;
+      bool act = false;
+      uint32_t c = 0, xe = 0;
+      if (lane < 16 && o15) {
+        act = true;
         xe = kept < 16 - o15 ? kept : 16 - o15;
-      }
-      if (lane == 1 && ((kept + o15) & 15u) && (ct > 0 || !o15)) {
-        edge = true;
+      } else if (lane >= 16 && lane < 32 && ((kept + o15) & 15u) && (ct > 0 || !o15)) {
+        act = true;
         c = ct;
-        xs = 16 * ct - o15;
         xe = kept;
       }
-      if (edge) {
-        const uint32_t xc = 16 * c - o15;  // tile output position of chunk byte 0 (wraps for c = 0)
-        uint32_t o[4] = {0u, 0u, 0u, 0u};
-        pieces(s_map[c], xs, xe, xc, o);
-        for (uint32_t x = xs; x < xe; ++x) {
-          const uint32_t b = x - xc;
-          outc[16 * (uint64_t)c + b] = (uint8_t)(o[b >> 2] >> (8 * (b & 3)));
-        }
+      // tile output position of chunk byte i (wraps below 0 for the head chunk's bytes
+      // that belong to the previous tile: then x >= xe)
+      const uint32_t x = 16 * c - o15 + i;
+      if (act && x < xe) {
+        uint32_t k = s_map[c];
+        while ((s_run[k + 1] >> 16) <= x) ++k;  // the sentinels end the walk
+        const uint32_t r = s_run[k];
+        outc[16 * (uint64_t)c + i] = s_buf[(r & 0xFFFFu) + x - (r >> 16)];
       }
     }
     asm volatile("" ::: "memory");  // the next tile rewrites the wave's LDS
