@@ -24,6 +24,7 @@ namespace {
 #ifndef KLF_TIMELINE
 #define KLF_TIMELINE 0
 #endif
+__device__ uint32_t g_abl_waves;  // timing builds: k_scan waves finished so far
 #if KLF_TIMELINE
 // Diagnostic build only: per tile {claim, loaded, A published, prefix known, done,
 // look-back rounds, spins, cu/xcc} stamps (s_memtime), dumped by the engine.
@@ -329,6 +330,11 @@ __global__ __launch_bounds__(kThreads, MODE == kScanGen ? 3 : KLF_SCAN_OCC) void
     for (uint32_t i = t; i < kQfWords; i += kThreads) s_qf[i] = a.pats.qf_bitmap[i];
   __syncthreads();  // the kernel's only block barrier
   const uint32_t nwaves = gridDim.x * kWaves;
+  // Timing builds 512 / 65536 drop the slot / tile-record stores from the second launch on
+  // (the first launch's records stay valid for identical batches): a wave skips once every
+  // wave of an earlier launch has finished.
+  const bool abl_skip = (KLF_ABL & (512 | 65536)) &&
+                        __hip_atomic_load(&g_abl_waves, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= nwaves;
 
   // the prefetch registers are named (an array here was put on the scratch stack)
   static_assert(kRows == 8, "KLF_ROWS lists the 8 prefetch rows");
@@ -352,6 +358,18 @@ __global__ __launch_bounds__(kThreads, MODE == kScanGen ? 3 : KLF_SCAN_OCC) void
     const uint4* gp = reinterpret_cast<const uint4*>(a.bytes + pf_sd.base + (uint64_t)(tile - pf_sd.tile0) * kTile);
     KLF_ROWS(KLF_LOAD)
     if (lane < kHalo / 16) pfh = gp[kTile / 16 + lane];
+  }
+  // Each tile ends with exactly two unconditional store instructions (its first 64 line
+  // slots and its TileStat, through buffer descriptors whose out-of-range lanes the hardware
+  // drops): two dropped stores here give the loop entry the same count behind the first
+  // prefetch, so the compiler's wait for the prefetched rows (vmcnt in issue order) stops
+  // short of the previous tile's stores instead of waiting for them to complete.
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  {
+    const __amdgpu_buffer_rsrc_t none = __builtin_amdgcn_make_buffer_rsrc(a.tstat, 0, 0, 0x00020000);
+    __builtin_amdgcn_raw_buffer_store_b32(0u, none, 0x7FFF0000u, 0, 0);
+    const u32x4 z = {0u, 0u, 0u, 0u};
+    __builtin_amdgcn_raw_buffer_store_b128(z, none, 0x7FFF0100u, 0, 0);
   }
   bool any_defer = false;
   for (; tile < a.ntiles; tile += nwaves) {
@@ -590,8 +608,8 @@ __global__ __launch_bounds__(kThreads, MODE == kScanGen ? 3 : KLF_SCAN_OCC) void
       if (KLF_ABL & 8192) {  // timing build: half the slot bytes (u16 slots); k_scatter ignores slots
         for (uint32_t j = lane; j < nlines; j += 64) reinterpret_cast<uint16_t*>(gslot)[j] = (uint16_t)s_list[j];
       } else if ((KLF_ABL & 32768) && ((tile / nwaves) & 3u) != 0) {  // timing build: 1 tile in 4 stores
-      } else if (!(KLF_ABL & 512)) {
-        for (uint32_t j = lane; j < nlines; j += 64) gslot[j] = s_list[j];
+      } else if (!((KLF_ABL & 512) && abl_skip)) {
+        for (uint32_t j = lane + 64; j < nlines; j += 64) gslot[j] = s_list[j];
       }
     } else if (pool_ok) {
       work(gslot);
@@ -691,22 +709,30 @@ __global__ __launch_bounds__(kThreads, MODE == kScanGen ? 3 : KLF_SCAN_OCC) void
       }
     }
 
-    // ---- per-tile record ----
+    // ---- per-tile record: the first 64 slots and the TileStat, two store instructions
+    // on every path (see the loop entry) ----
     const uint32_t pp = wave_sum(n_parsed), qq = wave_sum(n_since), dd = wave_sum(n_defer);
     any_defer |= dd != 0;
-    if (lane == 0) {
-      TileStat ts;
-      ts.events = agg;
-      ts.pool_base = dense ? pool_base : 0;
-      ts.parsed = (uint16_t)pp;
-      ts.since_ok = (uint16_t)qq;
-      ts.flags = (uint16_t)((dense ? 1u : 0u) | (carry ? 2u : 0u) | (dd ? 4u : 0u));
-      ts.carry_off = (uint16_t)(GEN ? tile_hits : carry);  // GEN: hit slots used
-      a.tstat[tile] = ts;
+    {
+      const bool slot_st = !dense && !(KLF_ABL & (128 | 8192 | 32768)) && !((KLF_ABL & 512) && abl_skip);
+      const uint32_t ns = __builtin_amdgcn_readfirstlane(slot_st ? (nlines < 64u ? nlines : 64u) * 4u : 0u);
+      const __amdgpu_buffer_rsrc_t srs = __builtin_amdgcn_make_buffer_rsrc(gslot, 0, (int)ns, 0x00020000);
+      const uint32_t sv = s_list[lane];
+      __builtin_amdgcn_raw_buffer_store_b32(sv, srs, 4u * (uint32_t)lane, 0, 0);
+      const uint32_t w0 = agg, w1 = dense ? pool_base : 0u;
+      const uint32_t w2 = (pp & 0xFFFFu) | (qq << 16);
+      const uint32_t w3 = ((dense ? 1u : 0u) | (carry ? 2u : 0u) | (dd ? 4u : 0u)) |
+                          ((uint32_t)(uint16_t)(GEN ? tile_hits : carry) << 16);  // GEN: hit slots used
+      const bool ts_st = !((KLF_ABL & 65536) && abl_skip);
+      const __amdgpu_buffer_rsrc_t trs =
+          __builtin_amdgcn_make_buffer_rsrc(a.tstat + tile, 0, ts_st ? (int)sizeof(TileStat) : 0, 0x00020000);
+      const u32x4 tv = {w0, w1, w2, w3};
+      __builtin_amdgcn_raw_buffer_store_b128(tv, trs, lane == 0 ? 0u : 0x7FFF0000u, 0, 0);
     }
     asm volatile("" ::: "memory");  // the next stage overwrites the LDS region read above
   }
   if (any_defer && lane == 0) a.counters[kCtrDefer] = 1u;
+  if ((KLF_ABL & (512 | 65536)) && lane == 0) atomicAdd(&g_abl_waves, 1u);
 }
 
 // ---- K1e: general parse of the deferred lines (non-canonical timestamp shapes) ---------
@@ -2343,6 +2369,16 @@ __global__ __launch_bounds__(256) void k_tcopy(RunArgs a, const uint4* __restric
     nrec = load_rec(tile + stride);
     nob = kbase[2 * (tile + stride)];
   }
+  {  // nine dropped stores behind the first loads: the loop is entered with the same count
+     // of stores after the prefetched rows as every iteration ends with (the waits for the
+     // rows are computed over both paths)
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    const __amdgpu_buffer_rsrc_t none = __builtin_amdgcn_make_buffer_rsrc(a.out, 0, 0, 0x00020000);
+    const u32x4 z = {0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int u = 0; u < 8; ++u) __builtin_amdgcn_raw_buffer_store_b128(z, none, 0x7FFF0000u + 16u * u, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b8((uint8_t)0, none, 0x7FFF0100u, 0, 0);
+  }
   for (; tile < a.ntiles; tile += stride) {
     const TRec cr = rec;
     const uint64_t obase = ob;
@@ -2363,7 +2399,8 @@ __global__ __launch_bounds__(256) void k_tcopy(RunArgs a, const uint4* __restric
       nrec = load_rec(nt + stride);
       nob = kbase[2 * (nt + stride)];
     }
-    if (!cr.kept) continue;
+    // (no early exit for a tile with nothing kept: every iteration issues the same nine
+    // stores, so the compiler's vmcnt waits for the prefetched rows count past them)
     uint32_t nr = cr.nruns;
     if (nr == kRunsRecompute) {  // more runs than the record holds: list them again here
       const TileLines g = tile_lines(a, tile);
@@ -2412,6 +2449,18 @@ __global__ __launch_bounds__(256) void k_tcopy(RunArgs a, const uint4* __restric
     wave_lds_sync();
     if (KLF_TC_ABL & 1) continue;
     uint8_t* outc = a.out + ((obase >> 4) << 4);
+    // Every store goes through a per-tile buffer descriptor over the tile's output chunks
+    // (wave-uniform): lanes with nothing to store pass an offset past its range and the
+    // hardware drops them, so there is no branch around any store and each tile issues
+    // exactly 8 + 1 store instructions.  The compiler then counts them: the wait for the
+    // next tile's prefetched rows no longer waits for this tile's stores to complete.
+    const uint64_t ob_u = (uint64_t)(uintptr_t)outc;
+    const uint32_t ob_lo = __builtin_amdgcn_readfirstlane((uint32_t)ob_u);
+    const uint32_t ob_hi = __builtin_amdgcn_readfirstlane((uint32_t)(ob_u >> 32));
+    const uint32_t nrec = __builtin_amdgcn_readfirstlane(cr.kept ? nch * 16u : 0u);
+    const __amdgpu_buffer_rsrc_t orsrc = __builtin_amdgcn_make_buffer_rsrc(
+        reinterpret_cast<void*>((uint64_t)ob_lo | ((uint64_t)ob_hi << 32)), 0, (int)nrec, 0x00020000);
+    constexpr uint32_t kDrop = 0x7FFFFFF0u;
     // 16 B of run r's bytes as they land on the chunk whose byte 0 is tile output x0: the
     // LDS window at any alignment (five dword reads + v_alignbyte; +16: the front pad)
     auto window = [&](uint32_t r, uint32_t x0, uint32_t (&y)[4]) __attribute__((always_inline)) {
@@ -2443,9 +2492,14 @@ __global__ __launch_bounds__(256) void k_tcopy(RunArgs a, const uint4* __restric
         x = pe;
       }
     };
-    // interior chunks (all 16 bytes from this tile): c in [c_lo, c_end), x0 = 16c - o15
+    // interior chunks (all 16 bytes from this tile): c in [c_lo, c_end), x0 = 16c - o15;
+    // at most 512 of them: eight rounds of 64 lanes
     const uint32_t c_lo = o15 ? 1u : 0u, c_end = (kept + o15) >> 4;
-    for (uint32_t c = c_lo + lane; c < c_end; c += 64) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const uint32_t c = c_lo + (uint32_t)lane + 64u * (uint32_t)u;
+      uint32_t o[4] = {0u, 0u, 0u, 0u};
+      if (c < c_end) {
       const uint32_t x0 = 16 * c - o15, x1 = x0 + 16;
       const uint32_t k = s_map[c];
       const uint32_t r0 = s_run[k], r1 = s_run[k + 1], d2 = s_run[k + 2] >> 16;
@@ -2464,10 +2518,12 @@ __global__ __launch_bounds__(256) void k_tcopy(RunArgs a, const uint4* __restric
           o[q] = (y0[q] & lo) | (y1[q] & ~lo);
         }
       } else {
-        o[0] = o[1] = o[2] = o[3] = 0u;
         pieces(k, x0, x1, x0, o);
       }
-      *reinterpret_cast<uint4*>(outc + 16 * (uint64_t)c) = make_uint4(o[0], o[1], o[2], o[3]);
+      }
+      typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+      const u32x4 ov = {o[0], o[1], o[2], o[3]};
+      __builtin_amdgcn_raw_buffer_store_b128(ov, orsrc, c < c_end ? 16u * c : kDrop, 0, 0);
     }
     // head / tail chunks shared with the neighbouring tiles: only this tile's bytes, one
     // byte per lane (lanes 0-15 the head chunk, 16-31 the tail chunk; a chunk holding both
@@ -2487,12 +2543,15 @@ __global__ __launch_bounds__(256) void k_tcopy(RunArgs a, const uint4* __restric
       // tile output position of chunk byte i (wraps below 0 for the head chunk's bytes
       // that belong to the previous tile: then x >= xe)
       const uint32_t x = 16 * c - o15 + i;
-      if (act && x < xe) {
+      const bool st = act && x < xe;
+      uint8_t b = 0;
+      if (st) {
         uint32_t k = s_map[c];
         while ((s_run[k + 1] >> 16) <= x) ++k;  // the sentinels end the walk
         const uint32_t r = s_run[k];
-        outc[16 * (uint64_t)c + i] = s_buf[(r & 0xFFFFu) + x - (r >> 16)];
+        b = s_buf[(r & 0xFFFFu) + x - (r >> 16)];
       }
+      __builtin_amdgcn_raw_buffer_store_b8(b, orsrc, st ? 16u * c + i : kDrop, 0, 0);
     }
     asm volatile("" ::: "memory");  // the next tile rewrites the wave's LDS
   }
