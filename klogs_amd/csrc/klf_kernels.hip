@@ -2457,9 +2457,9 @@ __global__ __launch_bounds__(256) void k_tcopy(RunArgs a, const uint4* __restric
     const uint64_t ob_u = (uint64_t)(uintptr_t)outc;
     const uint32_t ob_lo = __builtin_amdgcn_readfirstlane((uint32_t)ob_u);
     const uint32_t ob_hi = __builtin_amdgcn_readfirstlane((uint32_t)(ob_u >> 32));
-    const uint32_t nrec = __builtin_amdgcn_readfirstlane(cr.kept ? nch * 16u : 0u);
+    const uint32_t nout = __builtin_amdgcn_readfirstlane(cr.kept ? nch * 16u : 0u);
     const __amdgpu_buffer_rsrc_t orsrc = __builtin_amdgcn_make_buffer_rsrc(
-        reinterpret_cast<void*>((uint64_t)ob_lo | ((uint64_t)ob_hi << 32)), 0, (int)nrec, 0x00020000);
+        reinterpret_cast<void*>((uint64_t)ob_lo | ((uint64_t)ob_hi << 32)), 0, (int)nout, 0x00020000);
     constexpr uint32_t kDrop = 0x7FFFFFF0u;
     // 16 B of run r's bytes as they land on the chunk whose byte 0 is tile output x0: the
     // LDS window at any alignment (five dword reads + v_alignbyte; +16: the front pad)
@@ -2503,7 +2503,6 @@ __global__ __launch_bounds__(256) void k_tcopy(RunArgs a, const uint4* __restric
       const uint32_t x0 = 16 * c - o15, x1 = x0 + 16;
       const uint32_t k = s_map[c];
       const uint32_t r0 = s_run[k], r1 = s_run[k + 1], d2 = s_run[k + 2] >> 16;
-      uint32_t o[4];
       if (x1 <= d2) {  // at most two runs: both windows, blended where run k + 1 starts
         uint32_t y0[4], y1[4];
         window(r0, x0, y0);
