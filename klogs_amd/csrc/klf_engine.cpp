@@ -617,7 +617,7 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
     }
   }
   HIPCHK(e, e->d_tstat.ensure(ntiles * sizeof(klf::TileStat)), "alloc tstat");
-  HIPCHK(e, e->d_slots.ensure(ntiles * klf::kSlotStride * 4), "alloc slots");
+  HIPCHK(e, e->d_slots.ensure(ntiles * klf::kRecStride * 4), "alloc slots");
   HIPCHK(e, e->d_tile_base.ensure(ntiles * 8), "alloc tile_base");
   HIPCHK(e, e->d_bsum.ensure((ntiles / 1024 + 2) * 4 * 8), "alloc bsum");
   HIPCHK(e, e->d_counters.ensure(klf::kNumCounters * 4), "alloc counters");

@@ -330,11 +330,16 @@ __global__ __launch_bounds__(kThreads, MODE == kScanGen ? 3 : KLF_SCAN_OCC) void
     for (uint32_t i = t; i < kQfWords; i += kThreads) s_qf[i] = a.pats.qf_bitmap[i];
   __syncthreads();  // the kernel's only block barrier
   const uint32_t nwaves = gridDim.x * kWaves;
-  // Timing builds 512 / 65536 drop the slot / tile-record stores from the second launch on
-  // (the first launch's records stay valid for identical batches): a wave skips once every
-  // wave of an earlier launch has finished.
-  const bool abl_skip = (KLF_ABL & (512 | 65536)) &&
-                        __hip_atomic_load(&g_abl_waves, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= nwaves;
+  // Timing builds (KLF_ABL != 0, scripts/variant.sh): the first launch is the full scan;
+  // from the second launch on (a wave knows once every wave of an earlier launch has
+  // finished) the ablated scan runs and stores nothing, so the first launch's records feed
+  // the downstream kernels (identical batches) and no ablation can misdirect them.
+  // KLF_ABL bits: 2 no literal anchor test, 64 staging + any-test only, 1 no timestamp
+  // parse, 128 no line list / parse / literal, 4 no prefilter fast pass, 8 prefilter
+  // probes only; 4096 = nothing removed (the scan without its stores).
+  const bool abl = (KLF_ABL != 0) &&
+                   __hip_atomic_load(&g_abl_waves, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= nwaves;
+#define ABL(x) ((KLF_ABL & (x)) && abl)
 
   // the prefetch registers are named (an array here was put on the scratch stack)
   static_assert(kRows == 8, "KLF_ROWS lists the 8 prefetch rows");
@@ -359,17 +364,14 @@ __global__ __launch_bounds__(kThreads, MODE == kScanGen ? 3 : KLF_SCAN_OCC) void
     KLF_ROWS(KLF_LOAD)
     if (lane < kHalo / 16) pfh = gp[kTile / 16 + lane];
   }
-  // Each tile ends with exactly two unconditional store instructions (its first 64 line
-  // slots and its TileStat, through buffer descriptors whose out-of-range lanes the hardware
-  // drops): two dropped stores here give the loop entry the same count behind the first
+  // Each tile ends with exactly one unconditional store instruction (the first two 128-B
+  // lines of its record region, through a buffer descriptor so that an ablated launch can
+  // drop it): a dropped store here gives the loop entry the same count behind the first
   // prefetch, so the compiler's wait for the prefetched rows (vmcnt in issue order) stops
-  // short of the previous tile's stores instead of waiting for them to complete.
-  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  // short of the previous tile's store instead of waiting for it to complete.
   {
-    const __amdgpu_buffer_rsrc_t none = __builtin_amdgcn_make_buffer_rsrc(a.tstat, 0, 0, 0x00020000);
+    const __amdgpu_buffer_rsrc_t none = __builtin_amdgcn_make_buffer_rsrc(a.slots, 0, 0, 0x00020000);
     __builtin_amdgcn_raw_buffer_store_b32(0u, none, 0x7FFF0000u, 0, 0);
-    const u32x4 z = {0u, 0u, 0u, 0u};
-    __builtin_amdgcn_raw_buffer_store_b128(z, none, 0x7FFF0100u, 0, 0);
   }
   bool any_defer = false;
   for (; tile < a.ntiles; tile += nwaves) {
@@ -417,7 +419,7 @@ __global__ __launch_bounds__(kThreads, MODE == kScanGen ? 3 : KLF_SCAN_OCC) void
       for (int v = 0; v < 8; ++v) {
         const uint32_t c = ((uint32_t)v + rot) & 7u;
         nlc |= any_eq16(xs[v], 0x0A0A0A0Au) ? (1u << c) : 0u;
-        if (LIT && !(KLF_ABL & 2)) anc |= any_eq16(xs[v], pat) ? (1u << c) : 0u;
+        if (LIT && !ABL(2)) anc |= any_eq16(xs[v], pat) ? (1u << c) : 0u;
       }
       if (nvalid < kLaneBytes) {
         const uint32_t vm = (1u << ((nvalid + 15) >> 4)) - 1u;
@@ -425,18 +427,10 @@ __global__ __launch_bounds__(kThreads, MODE == kScanGen ? 3 : KLF_SCAN_OCC) void
         anc &= vm;
       }
     }
-#if KLF_ABL & 64  // timing build: staging + any-test only
-    {
-      const uint32_t ev = wave_sum((uint32_t)__popc(nlc | anc));
-      if (lane == 0) {
-        TileStat ts{};
-        ts.events = ev;
-        a.tstat[tile] = ts;
-      }
-      asm volatile("" ::: "memory");
+    if (ABL(64)) {  // timing build: staging + any-test only
+      asm volatile("" ::"v"(nlc | anc) : "memory");
       continue;
     }
-#endif
     auto clip = [&](uint32_t e, uint32_t c) -> uint32_t {  // bytes of chunk c past the tile's end
       const int nv = nvalid - 16 * (int)c;
       return nv >= 16 ? e : (nv <= 0 ? 0u : (e & ((1u << nv) - 1u)));
@@ -465,7 +459,7 @@ __global__ __launch_bounds__(kThreads, MODE == kScanGen ? 3 : KLF_SCAN_OCC) void
           em[k] |= bit;
           st[k] &= ~bit;
         }
-      a.segout[s].frag = nl_at_end ? 0 : 1;
+      if (!abl) a.segout[s].frag = nl_at_end ? 0 : 1;
     }
     const uint32_t cnt = (uint32_t)(__popc(em[0]) + __popc(em[1]) + __popc(em[2]) + __popc(em[3]));
     const uint32_t incl = wave_incl_scan_add(cnt, lane);
@@ -479,14 +473,15 @@ __global__ __launch_bounds__(kThreads, MODE == kScanGen ? 3 : KLF_SCAN_OCC) void
     uint32_t pool_base = 0;
     if (dense) {
       uint32_t pb = 0;
-      if (lane == 0) {
+      if (lane == 0 && !abl) {
         pb = atomicAdd(&a.counters[kCtrPool], nlines);
         if ((uint64_t)pb + nlines > a.pool_cap) atomicOr(err_flag, 1u);
       }
       pool_base = (uint32_t)__builtin_amdgcn_readlane((int)pb, 0);
     }
     const bool pool_ok = !dense || (uint64_t)pool_base + nlines <= a.pool_cap;
-    uint32_t* gslot = dense ? a.pool + pool_base : a.slots + (size_t)tile * kSlotStride;
+    uint32_t* const trec = a.slots + (size_t)tile * kRecStride;  // this tile's record region
+    uint32_t* gslot = dense ? a.pool + pool_base : trec + kRecHead;
 
     // The per-tile work on the line list, instantiated for the LDS list (normal tiles) and
     // the global pool (dense tiles).
@@ -513,13 +508,11 @@ __global__ __launch_bounds__(kThreads, MODE == kScanGen ? 3 : KLF_SCAN_OCC) void
         if (j < nlines) {
           const uint32_t off = list[j];
           bool so = false, fast = false;
-#if KLF_ABL & 1
-          fast = true;
-          so = true;
-#else
-          if (rel_lo + (int64_t)off + 31 <= seg_len)
+          if (ABL(1)) {
+            fast = so = true;
+          } else if (rel_lo + (int64_t)off + 31 <= seg_len) {
             fast = parse_fast(s_tile, off, s_month, a.since_day, a.since_sod, a.since_nsec, so);
-#endif
+          }
           list[j] = fast ? (off | ((uint32_t)make_meta(true, so, 31) << 16)) : (off | kSlotDefer);
           n_parsed += fast ? 1u : 0u;
           n_since += (fast && so) ? 1u : 0u;
@@ -602,16 +595,15 @@ __global__ __launch_bounds__(kThreads, MODE == kScanGen ? 3 : KLF_SCAN_OCC) void
       if (dense) __threadfence_block();
       wave_lds_sync();
     };
-    if (KLF_ABL & 128) {  // timing build: no line list / parse / literal
+    if (ABL(128)) {  // timing build: no line list / parse / literal
     } else if (!dense) {
       work(s_list);
-      if (KLF_ABL & 8192) {  // timing build: half the slot bytes (u16 slots); k_scatter ignores slots
-        for (uint32_t j = lane; j < nlines; j += 64) reinterpret_cast<uint16_t*>(gslot)[j] = (uint16_t)s_list[j];
-      } else if ((KLF_ABL & 32768) && ((tile / nwaves) & 3u) != 0) {  // timing build: 1 tile in 4 stores
-      } else if (!((KLF_ABL & 512) && abl_skip)) {
-        for (uint32_t j = lane + 64; j < nlines; j += 64) gslot[j] = s_list[j];
-      }
-    } else if (pool_ok) {
+      // slots past the first 60 (the record store below writes those): whole 64-word rows
+      // of the region, garbage past the last slot
+      if (!abl)
+        for (uint32_t w = 64u + (uint32_t)lane; w < kRecHead + nlines; w += 64)
+          if (w < (uint32_t)kRecStride) trec[w] = w - kRecHead < (uint32_t)kSlotStride ? s_list[w - kRecHead] : 0u;
+    } else if (pool_ok && !abl) {
       work(gslot);
     }
 
@@ -654,7 +646,7 @@ __global__ __launch_bounds__(kThreads, MODE == kScanGen ? 3 : KLF_SCAN_OCC) void
       uint32_t chit = 0;
       const uint32_t rot = ((uint32_t)lane >> 1) & 7u;
 #pragma unroll
-      for (int v = 0; v < ((KLF_ABL & 4) ? 0 : 8); ++v) {
+      for (int v = 0; v < (ABL(4) ? 0 : 8); ++v) {
         const uint32_t c = ((uint32_t)v + rot) & 7u;
         uint32_t acc = 0;
         chunk_grams(c, [&](uint32_t g, int) __attribute__((always_inline)) { acc |= hbits(g); });
@@ -675,12 +667,12 @@ __global__ __launch_bounds__(kThreads, MODE == kScanGen ? 3 : KLF_SCAN_OCC) void
           hq3 |= q == 3 ? hm : 0u;
         }
       }
-#if KLF_ABL & 8
-      any_defer |= (hq0 | hq1 | hq2 | hq3) == 0xFFFFFFFFu;  // timing build: probes only
-      hq0 = hq1 = hq2 = hq3 = 0;
-#endif
+      if (ABL(8)) {  // timing build: probes only
+        asm volatile("" ::"v"(hq0 | hq1 | hq2 | hq3));
+        hq0 = hq1 = hq2 = hq3 = 0;
+      }
       const uint32_t nh = (uint32_t)(__popc(hq0) + __popc(hq1) + __popc(hq2) + __popc(hq3));
-      if (__any(nh != 0)) {
+      if (__any(nh != 0) && !abl) {
         // tile-owned slots (u16 tile offsets, no atomics); only a tile with more than
         // kHitSlots hits spills the rest to the global list
         const uint32_t ih = wave_incl_scan_add(nh, lane);
@@ -713,26 +705,25 @@ __global__ __launch_bounds__(kThreads, MODE == kScanGen ? 3 : KLF_SCAN_OCC) void
     // on every path (see the loop entry) ----
     const uint32_t pp = wave_sum(n_parsed), qq = wave_sum(n_since), dd = wave_sum(n_defer);
     any_defer |= dd != 0;
-    {
-      const bool slot_st = !dense && !(KLF_ABL & (128 | 8192 | 32768)) && !((KLF_ABL & 512) && abl_skip);
-      const uint32_t ns = __builtin_amdgcn_readfirstlane(slot_st ? (nlines < 64u ? nlines : 64u) * 4u : 0u);
-      const __amdgpu_buffer_rsrc_t srs = __builtin_amdgcn_make_buffer_rsrc(gslot, 0, (int)ns, 0x00020000);
-      const uint32_t sv = s_list[lane];
-      __builtin_amdgcn_raw_buffer_store_b32(sv, srs, 4u * (uint32_t)lane, 0, 0);
+    {  // words 0-3 the TileStat, 4-63 the first 60 slots (garbage past the last, and all
+       // of them for a dense tile): two whole 128-B lines in one store
       const uint32_t w0 = agg, w1 = dense ? pool_base : 0u;
       const uint32_t w2 = (pp & 0xFFFFu) | (qq << 16);
       const uint32_t w3 = ((dense ? 1u : 0u) | (carry ? 2u : 0u) | (dd ? 4u : 0u)) |
                           ((uint32_t)(uint16_t)(GEN ? tile_hits : carry) << 16);  // GEN: hit slots used
-      const bool ts_st = !((KLF_ABL & 65536) && abl_skip);
-      const __amdgpu_buffer_rsrc_t trs =
-          __builtin_amdgcn_make_buffer_rsrc(a.tstat + tile, 0, ts_st ? (int)sizeof(TileStat) : 0, 0x00020000);
-      const u32x4 tv = {w0, w1, w2, w3};
-      __builtin_amdgcn_raw_buffer_store_b128(tv, trs, lane == 0 ? 0u : 0x7FFF0000u, 0, 0);
+      const uint32_t sv = s_list[lane >= kRecHead ? lane - kRecHead : 0];
+      const uint32_t v = lane == 0 ? w0 : lane == 1 ? w1 : lane == 2 ? w2 : lane == 3 ? w3 : sv;
+      // one whole line when the slots fit beside the TileStat (long-line logs: most tiles
+      // hold a line or two), else two
+      const int rb = abl ? 0 : ((dense || nlines <= 32u - kRecHead) ? 128 : 256);
+      const __amdgpu_buffer_rsrc_t rrs = __builtin_amdgcn_make_buffer_rsrc(trec, 0, rb, 0x00020000);
+      __builtin_amdgcn_raw_buffer_store_b32(v, rrs, 4u * (uint32_t)lane, 0, 0);
     }
     asm volatile("" ::: "memory");  // the next stage overwrites the LDS region read above
   }
-  if (any_defer && lane == 0) a.counters[kCtrDefer] = 1u;
-  if ((KLF_ABL & (512 | 65536)) && lane == 0) atomicAdd(&g_abl_waves, 1u);
+  if (any_defer && lane == 0 && !abl) a.counters[kCtrDefer] = 1u;
+  if (KLF_ABL != 0 && lane == 0) atomicAdd(&g_abl_waves, 1u);
+#undef ABL
 }
 
 // ---- K1e: general parse of the deferred lines (non-canonical timestamp shapes) ---------
@@ -810,7 +801,8 @@ __global__ __launch_bounds__(256) void k_fixup(RunArgs a) {
   if (!a.counters[kCtrDefer] || a.counters[2]) return;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   for (uint32_t tile = blockIdx.x * 4 + wv; tile < a.ntiles; tile += gridDim.x * 4) {
-    TileStat ts = a.tstat[tile];
+    TileStat* const trs = reinterpret_cast<TileStat*>(a.slots + (size_t)tile * kRecStride);  // k_tsum compacts later
+    TileStat ts = *trs;
     if (!(ts.flags & 4u)) continue;
     const uint32_t s = a.tile_seg[tile];
     const SegDesc sd = a.segs[s];
@@ -819,7 +811,7 @@ __global__ __launch_bounds__(256) void k_fixup(RunArgs a) {
     const bool first = rel_lo == 0, last = rel_lo + kTile >= seg_len;
     const uint32_t k0 = first ? 0 : 1, k1 = last ? ts.events : ts.events + 1;
     const uint32_t nlines = k1 > k0 ? k1 - k0 : 0;
-    uint32_t* list = (ts.flags & 1u) ? a.pool + ts.pool_base : a.slots + (size_t)tile * kSlotStride;
+    uint32_t* list = (ts.flags & 1u) ? a.pool + ts.pool_base : a.slots + (size_t)tile * kRecStride + kRecHead;
     const uint8_t* segp = a.bytes + sd.base;
     uint32_t dp = 0, dq = 0;
     for (uint32_t j = lane; j < nlines; j += 64) {
@@ -854,7 +846,7 @@ __global__ __launch_bounds__(256) void k_fixup(RunArgs a) {
     if (lane == 0) {
       ts.parsed = (uint16_t)(ts.parsed + dp);
       ts.since_ok = (uint16_t)(ts.since_ok + dq);
-      a.tstat[tile] = ts;
+      *trs = ts;
     }
   }
 }
@@ -878,10 +870,13 @@ __global__ __launch_bounds__(256) void k_tsum(RunArgs a) {
   const uint32_t t0 = blockIdx.x * (256 * R) + threadIdx.x;
   TileStat ts[R];
 #pragma unroll
-  for (int r = 0; r < R; ++r) {  // all loads in flight at once (coalesced 16-B records)
+  for (int r = 0; r < R; ++r) {  // all loads in flight at once (one 16-B record per region)
     ts[r] = TileStat{};
-    if (t0 + r * 256 < a.ntiles) ts[r] = a.tstat[t0 + r * 256];
+    if (t0 + r * 256 < a.ntiles) ts[r] = *reinterpret_cast<const TileStat*>(a.slots + (size_t)(t0 + r * 256) * kRecStride);
   }
+#pragma unroll
+  for (int r = 0; r < R; ++r)  // the compact copy every later kernel reads (coalesced)
+    if (t0 + r * 256 < a.ntiles) a.tstat[t0 + r * 256] = ts[r];
   uint64_t v = 0, p = 0, q = 0, h = 0;
 #pragma unroll
   for (int r = 0; r < R; ++r) { v += ts[r].events; p += ts[r].parsed; q += ts[r].since_ok; h += tile_hits(a, ts[r]); }
@@ -1029,7 +1024,7 @@ __global__ __launch_bounds__(256) void k_scatter(RunArgs a) {
           const uint32_t pk0 = prel == 0 ? 0 : 1;
           const uint32_t pn = pst.events + 1 > pk0 ? pst.events + 1 - pk0 : 0;  // never the stream's last tile
           if (pn == 0) continue;
-          const uint32_t* psrc = (pst.flags & 1u) ? a.pool + pst.pool_base : a.slots + (size_t)pt * kSlotStride;
+          const uint32_t* psrc = (pst.flags & 1u) ? a.pool + pst.pool_base : a.slots + (size_t)pt * kRecStride + kRecHead;
           const uint32_t v = psrc[pn - 1];
           const uint32_t mt = v >> 16;
           // a deferred line had its whole content searched by k_fixup
@@ -1066,7 +1061,7 @@ __global__ __launch_bounds__(256) void k_scatter(RunArgs a) {
           const uint32_t j = l - (lo ? s_pre[wv][lo - 1] : 0u);
           const uint32_t src = s_ent[wv][lo].src;
           const uint32_t* sp = (src & 0x80000000u) ? a.pool + (src & 0x7FFFFFFFu)
-                                                   : a.slots + (size_t)(g * kScatterGroup + lo) * kSlotStride;
+                                                   : a.slots + (size_t)(g * kScatterGroup + lo) * kRecStride + kRecHead;
           sl[u] = sp[j];
           kk[u] = lo;
           jj[u] = j;
@@ -1079,7 +1074,7 @@ __global__ __launch_bounds__(256) void k_scatter(RunArgs a) {
         const ScatterEnt& e = s_ent[wv][kk[u]];
         const uint64_t li = e.base + jj[u];
         if (li >= a.cap_lines) { atomicOr(err_flag, 1u); continue; }
-#if KLF_ABL & (8192 | 16384 | 32768)  // timing builds: slot contents ignored (no line selected downstream)
+#if KLF_ABL & 16384  // timing build: slot contents ignored (no line selected downstream)
         a.line_off[li + e.seg] = e.rel_lo;
         a.meta[li] = (uint16_t)(sl[u] & 0u);
 #else
@@ -1186,7 +1181,7 @@ __device__ void verify_hit(const RunArgs& a, uint32_t tile, uint32_t s, int32_t 
     const bool first = rel_lo == 0, last = rel_lo + kTile >= (int64_t)sd.len;
     const uint32_t k0 = first ? 0 : 1, k1 = last ? ts.events : ts.events + 1;
     const uint32_t nl = k1 > k0 ? k1 - k0 : 0;
-    const uint32_t* list = (ts.flags & 1u) ? a.pool + ts.pool_base : a.slots + (size_t)tile * kSlotStride;
+    const uint32_t* list = (ts.flags & 1u) ? a.pool + ts.pool_base : a.slots + (size_t)tile * kRecStride + kRecHead;
     int lo = 0, hi = x < 0 ? 0 : (int)nl;  // starts <= x
     while (lo < hi) {
       const int mid = (lo + hi) >> 1;
@@ -1400,7 +1395,7 @@ __global__ __launch_bounds__(256) void k_fixcount(RunArgs a) {
     const bool first = rel_lo == 0, last = rel_lo + kTile >= (int64_t)sd.len;
     const uint32_t k0 = first ? 0 : 1, k1 = last ? ts.events : ts.events + 1;
     const uint32_t nlines = k1 > k0 ? k1 - k0 : 0;
-    const uint32_t* list = (ts.flags & 1u) ? a.pool + ts.pool_base : a.slots + (size_t)tile * kSlotStride;
+    const uint32_t* list = (ts.flags & 1u) ? a.pool + ts.pool_base : a.slots + (size_t)tile * kRecStride + kRecHead;
     const uint8_t* segp = a.bytes + sd.base;
     for (uint32_t j = lane; j < nlines; j += 64) {
       const uint32_t sl = list[j];

@@ -23,7 +23,13 @@ constexpr uint32_t kMatchChunk = 8192;              // lines per k_mcount partia
 
 constexpr int kSlots = kTile / 32 + 2;  // staged line slots per tile (>= 8 KiB / 32-byte kubelet line + 1)
 constexpr uint32_t kScanSmallTiles = 1u << 20;  // tile-scan blocks of 1,024 tiles up to this many tiles (8 GiB), 4,096 above
-constexpr int kSlotStride = (kSlots + 3) & ~3;  // u32 slots per tile region in HBM (16-B aligned regions)
+constexpr int kSlotStride = (kSlots + 3) & ~3;  // u32 slots of a tile's LDS line list
+// Per-tile record region in HBM: the scan's TileStat (4 words) then the line slots, 128-B
+// aligned and written as whole 128-B lines (a 16-B record store or a slot run ending
+// inside a line is a partial-line write, read-modify-written by HBM3E: measured at ~0.3 ms
+// per 4 M tiles).  k_tsum copies the TileStats into the compact `tstat` array.
+constexpr int kRecHead = 4;
+constexpr int kRecStride = (kRecHead + kSlots + 31) & ~31;  // u32 words (1,152 B)
 
 // q-gram prefilter of general pattern sets (klf_patterns.hpp CompiledSet::qf_*)
 constexpr int kQfBucketBits = 12;                    // bitmap words = verification buckets
@@ -196,7 +202,7 @@ struct RunArgs {
   DevPatterns pats;
   // workspace (device)
   TileStat* tstat;      // [ntiles]
-  uint32_t* slots;      // [ntiles * kSlotStride] staged line slots
+  uint32_t* slots;      // [ntiles * kRecStride] per-tile records: TileStat, then staged line slots
   uint32_t* pool;       // [pool_cap] slots of dense tiles
   uint64_t pool_cap;
   uint64_t* tile_base;  // [ntiles] global line index of each tile's line 0
