@@ -598,11 +598,6 @@ __global__ __launch_bounds__(kThreads, MODE == kScanGen ? 3 : KLF_SCAN_OCC) void
     if (ABL(128)) {  // timing build: no line list / parse / literal
     } else if (!dense) {
       work(s_list);
-      // slots past the first 60 (the record store below writes those): whole 64-word rows
-      // of the region, garbage past the last slot
-      if (!abl)
-        for (uint32_t w = 64u + (uint32_t)lane; w < kRecHead + nlines; w += 64)
-          if (w < (uint32_t)kRecStride) trec[w] = w - kRecHead < (uint32_t)kSlotStride ? s_list[w - kRecHead] : 0u;
     } else if (pool_ok && !abl) {
       work(gslot);
     }
@@ -705,19 +700,22 @@ __global__ __launch_bounds__(kThreads, MODE == kScanGen ? 3 : KLF_SCAN_OCC) void
     // on every path (see the loop entry) ----
     const uint32_t pp = wave_sum(n_parsed), qq = wave_sum(n_since), dd = wave_sum(n_defer);
     any_defer |= dd != 0;
-    {  // words 0-3 the TileStat, 4-63 the first 60 slots (garbage past the last, and all
-       // of them for a dense tile): two whole 128-B lines in one store
+    {  // the record region in 16-B units, whole 128-B lines: unit 0 the TileStat, unit u
+       // slots 4u - 4 .. 4u - 1 (garbage past the last slot; a dense tile's slots are in
+       // the pool).  16 B per lane: narrower per-lane stores cost several times more per byte.
       const uint32_t w0 = agg, w1 = dense ? pool_base : 0u;
       const uint32_t w2 = (pp & 0xFFFFu) | (qq << 16);
       const uint32_t w3 = ((dense ? 1u : 0u) | (carry ? 2u : 0u) | (dd ? 4u : 0u)) |
                           ((uint32_t)(uint16_t)(GEN ? tile_hits : carry) << 16);  // GEN: hit slots used
-      const uint32_t sv = s_list[lane >= kRecHead ? lane - kRecHead : 0];
-      const uint32_t v = lane == 0 ? w0 : lane == 1 ? w1 : lane == 2 ? w2 : lane == 3 ? w3 : sv;
-      // one whole line when the slots fit beside the TileStat (long-line logs: most tiles
-      // hold a line or two), else two
-      const int rb = abl ? 0 : ((dense || nlines <= 32u - kRecHead) ? 128 : 256);
-      const __amdgpu_buffer_rsrc_t rrs = __builtin_amdgcn_make_buffer_rsrc(trec, 0, rb, 0x00020000);
-      __builtin_amdgcn_raw_buffer_store_b32(v, rrs, 4u * (uint32_t)lane, 0, 0);
+      const uint32_t nunits = abl ? 0u : (dense ? 8u : ((kRecHead + nlines + 31u) & ~31u) / 4u);
+      const __amdgpu_buffer_rsrc_t rrs = __builtin_amdgcn_make_buffer_rsrc(trec, 0, (int)(nunits * 16u), 0x00020000);
+      typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
+      for (uint32_t u = (uint32_t)lane; u < (nunits > 64u ? 128u : 64u); u += 64) {  // one or two stores
+        const uint32_t li = u ? (4u * u - 4u < (uint32_t)kSlotStride - 4u ? 4u * u - 4u : (uint32_t)kSlotStride - 4u) : 0u;
+        const uint4 sl = *reinterpret_cast<const uint4*>(s_list + li);
+        const u32x4v v = u ? u32x4v{sl.x, sl.y, sl.z, sl.w} : u32x4v{w0, w1, w2, w3};
+        __builtin_amdgcn_raw_buffer_store_b128(v, rrs, 16u * u, 0, 0);
+      }
     }
     asm volatile("" ::: "memory");  // the next stage overwrites the LDS region read above
   }
