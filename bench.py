@@ -124,16 +124,28 @@ def main():
     eng = E.Engine(local, grep=[synth.NEEDLE], hip_stream=stream.cuda_stream)
     ptr = dev.data_ptr()
 
+    step_pending = []
+
     def step():
         # per-pattern counts ride along (one literal: no extra kernel work, SPEC.md S6)
         r = eng.run_device(ptr, seg_base, [n], since=since, tail=TAIL, pattern_counts=True)
-        if world > 1:  # per-stream count records -> every rank (one all-gather, RCCL over xGMI)
+        if world > 1:  # per-stream count records -> every rank (one all-gather, RCCL over xGMI),
+            # left in flight while the next step filters; every gather is waited for before
+            # the timed region closes (finish_gathers)
             rec = dict(r.totals(), patterns=r.pattern_counts(0))
-            step.table = shard.gather_counts({rank: rec}, [n] * world, world, device=coll_dev, n_patterns=1)
+            step_pending.append(shard.gather_counts_async({rank: rec}, [n] * world, world, device=coll_dev,
+                                                          n_patterns=1))
+            if len(step_pending) > 1:
+                step_pending.pop(0).wait()
         return r
+
+    def finish_gathers():
+        while step_pending:
+            step.table = step_pending.pop(0).wait()
 
     for _ in range(args.warmup):
         step().free()
+    finish_gathers()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -150,6 +162,7 @@ def main():
             r.free()
         else:
             last = r
+    finish_gathers()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -382,13 +395,22 @@ def run_c3_sharded(args, world: int, rank: int, local: int, coll_dev) -> dict:
     eng = E.Engine(local, hip_stream=torch.cuda.current_stream().cuda_stream)
     ptr = dev.data_ptr()
 
+    pending = []
+
     def step():
         r = eng.run_device(ptr, seg_base, lens)
         recs = {sid: r.stream_counts(j) for j, sid in enumerate(mine)}
-        step.table = shard.gather_counts(recs, lens_all, world, device=coll_dev)
+        pending.append(shard.gather_counts_async(recs, lens_all, world, device=coll_dev))
+        if len(pending) > 1:
+            pending.pop(0).wait()
         return r
+
+    def finish():
+        while pending:
+            step.table = pending.pop(0).wait()
     for _ in range(args.warmup):
         step().free()
+    finish()
     torch.cuda.synchronize()
     dist.barrier()
     torch.cuda.synchronize()
@@ -396,6 +418,7 @@ def run_c3_sharded(args, world: int, rank: int, local: int, coll_dev) -> dict:
     for _ in range(args.steps):
         r = step()
         r.free()
+    finish()
     torch.cuda.synchronize()
     dist.barrier()
     dt = time.perf_counter() - t0

@@ -98,6 +98,39 @@ def gather_counts(counts: Dict[int, dict], lens: Sequence[int], world: int, devi
     return unpack_records(out.cpu().numpy(), len(lens), n_patterns)
 
 
+class PendingGather:
+    """An all-gather of count records in flight (gather_counts_async); wait() -> table."""
+
+    def __init__(self, work, out, n_streams: int, n_patterns: int, table=None):
+        self._work, self._out, self._n, self._np, self._table = work, out, n_streams, n_patterns, table
+
+    def wait(self) -> np.ndarray:
+        if self._table is None:
+            if self._work is not None:
+                self._work.wait()
+            self._table = unpack_records(self._out.cpu().numpy(), self._n, self._np)
+        return self._table
+
+
+def gather_counts_async(counts: Dict[int, dict], lens: Sequence[int], world: int, device=None,
+                        n_patterns: int = 0) -> PendingGather:
+    """gather_counts with the collective left in flight (async_op): the caller overlaps it
+    with the next batch's filter and waits later -- the bench's steps at N > 1."""
+    cap = max(len(local_streams(lens, world, r)) for r in range(world)) or 1
+    rec = pack_records(counts, cap, n_patterns)
+    if world == 1:
+        return PendingGather(None, None, len(lens), n_patterns, unpack_records(rec, len(lens), n_patterns))
+    import torch
+    import torch.distributed as dist
+
+    t = torch.from_numpy(rec)
+    if device is not None:
+        t = t.to(device, non_blocking=True)
+    out = torch.empty(world * cap, NREC + n_patterns, dtype=torch.int64, device=t.device)
+    work = dist.all_gather_into_tensor(out, t, async_op=True)
+    return PendingGather(work, out, len(lens), n_patterns)
+
+
 def run_shard(lens: Sequence[int], fetch: Callable[[int], bytes], runner, world: int, rank: int,
               device=None, allgather=None, n_patterns: int = 0):
     """Filters this rank's streams and gathers every stream's counts.

@@ -80,6 +80,13 @@ def _worker(rank, world, port, q):
         streams = _streams()
         lens = [len(s) for s in streams]
         outs, table = shard.run_shard(lens, lambda i: streams[i], _oracle_runner, world, rank, n_patterns=1)
+        # the bench's asynchronous form, two gathers in flight at once, gives the same table
+        mine = shard.local_streams(lens, world, rank)
+        res = _oracle_runner([streams[i] for i in mine])
+        counts = {sid: r[1] for sid, r in zip(mine, res)}
+        p1 = shard.gather_counts_async(counts, lens, world, n_patterns=1)
+        p2 = shard.gather_counts_async(counts, lens, world, n_patterns=1)
+        assert np.array_equal(p1.wait(), table) and np.array_equal(p2.wait(), table)
         q.put((rank, {k: v for k, v in outs.items()}, table))
     finally:
         dist.destroy_process_group()
