@@ -37,6 +37,16 @@ def stats(path):
     return rows
 
 
+def steady_us(trace_csv, kernel):
+    """Mean launch duration of `kernel` without its first launch (the warm-up the bench
+    leaves out of its timed region too)."""
+    if not Path(trace_csv).exists():
+        return None
+    d = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in csv.DictReader(open(trace_csv))
+         if short(r["Kernel_Name"]) == kernel]
+    return sum(d[1:]) / len(d[1:]) if len(d) > 1 else None
+
+
 def last_json(path):
     lines = [x for x in Path(path).read_text().splitlines() if x.startswith("{")]
     return json.loads(lines[-1])
@@ -47,12 +57,12 @@ def main():
     dst.mkdir(parents=True, exist_ok=True)
     shutil.copy(src / "bench.json", dst / "bench.json")
     shutil.copy(src / "trace" / "run_kernel_stats.csv", dst / "bench_kernel_stats.csv")
-    for c in ("c3", "c5"):
+    for c in ("c3", "c4", "c5"):
         f = src / f"trace_{c}" / "run_kernel_stats.csv"
         if f.exists():
             shutil.copy(f, dst / f"{c}_kernel_stats.csv")
     pmc = {}
-    for c in ("c2", "c3", "c5"):
+    for c in ("c2", "c3", "c4", "c5"):
         d = src / f"pmc_{c}"
         if d.exists():
             subprocess.run([sys.executable, str(ROOT / "scripts/pmc_summary.py"), str(d), "--json",
@@ -64,8 +74,8 @@ def main():
              "Made by `scripts/profile_round.sh` on one MI355X (the driver's bench command under",
              "`rocprofv3 --kernel-trace --stats`, then counter passes per config) and",
              "`scripts/collect_profiles.py`.  frac = algorithmic bytes / average launch / 8 TB/s.", "",
-             "| config | kernel | alg bytes / launch | trace avg (µs) | frac (rocprof) | frac (bench HIP events) | HBM traffic / alg |",
-             "|---|---|---|---|---|---|---|"]
+             "| config | kernel | alg bytes / launch | config-run trace avg (µs) | frac (rocprof) | bench-trace avg w/o 1st launch (µs) | frac (rocprof, steady) | frac (bench HIP events) | HBM traffic / alg |",
+             "|---|---|---|---|---|---|---|---|---|"]
     out = {}
     # C2: the headline line
     k2 = next(k for k in tr if k.startswith("k_scan<1"))
@@ -79,11 +89,15 @@ def main():
                    "write_bytes": round(p.get("write_bytes", 0)), "traffic_bytes": round(t2),
                    "correction": "FETCH_SIZE x2 (gfx950 wide streaming reads), WRITE_SIZE x1; KiB -> B",
                    "sources": [str(src / "pmc_c2")]}, open(dst / "traffic.json", "w"), indent=1)
+    st2 = steady_us(src / "trace" / "run_kernel_trace.csv", k2)
+    fs2 = st2 and alg2 / (st2 * 1e-6) / 1e9 / PEAK
     out["c2"] = {"kernel": k2, "avg_us": tr[k2]["avg_us"], "frac_rocprof": round(fr2, 4),
+                 "steady_us": st2 and round(st2, 1), "frac_rocprof_steady": fs2 and round(fs2, 4),
                  "frac_hip": b["roofline"]["frac"], "traffic_over_alg": t2 and round(t2 / alg2, 3)}
-    lines.append(f"| C2 | `{k2}` | {alg2} | {tr[k2]['avg_us']:.1f} | {fr2:.4f} | {b['roofline']['frac']} | "
+    lines.append(f"| C2 | `{k2}` | {alg2} | {tr[k2]['avg_us']:.1f} | {fr2:.4f} | "
+                 f"{'%.1f' % st2 if st2 else '—'} | {'%.4f' % fs2 if fs2 else '—'} | {b['roofline']['frac']} | "
                  f"{'%.3f' % (t2 / alg2) if t2 else '—'} |")
-    for c in ("c3", "c5"):
+    for c in ("c3", "c4", "c5"):
         f = dst / f"{c}_kernel_stats.csv"
         ex = b.get("extra", {}).get("configs", {}).get(c)
         if not f.exists() or not ex:
@@ -96,10 +110,16 @@ def main():
         if c in pmc and ks in pmc[c]:
             p = pmc[c][ks]
             tt = p.get("fetch_bytes_x2", 0) + p.get("write_bytes", 0)
+        # steady state from the bench command's own trace (the line's numbers come from it)
+        st = steady_us(src / "trace" / "run_kernel_trace.csv", ks) or \
+            steady_us(src / f"trace_{c}" / "run_kernel_trace.csv", ks)
+        fs = st and alg / (st * 1e-6) / 1e9 / PEAK
         out[c] = {"kernel": ks, "avg_us": ts[ks]["avg_us"], "frac_rocprof": round(fr, 4),
+                  "steady_us": st and round(st, 1), "frac_rocprof_steady": fs and round(fs, 4),
                   "frac_hip": ex["roofline"]["frac"], "traffic_over_alg": tt and round(tt / alg, 3),
                   "kernels": {k: round(v["avg_us"], 1) for k, v in sorted(ts.items(), key=lambda kv: -kv[1]["pct"])[:8]}}
-        lines.append(f"| {c.upper()} | `{ks}` | {alg} | {ts[ks]['avg_us']:.1f} | {fr:.4f} | {ex['roofline']['frac']} | "
+        lines.append(f"| {c.upper()} | `{ks}` | {alg} | {ts[ks]['avg_us']:.1f} | {fr:.4f} | "
+                     f"{'%.1f' % st if st else '—'} | {'%.4f' % fs if fs else '—'} | {ex['roofline']['frac']} | "
                      f"{'%.3f' % (tt / alg) if tt else '—'} |")
     lines += ["", "Per-config kernel split (trace averages, µs):", ""]
     for c, v in out.items():
