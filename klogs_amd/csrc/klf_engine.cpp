@@ -51,6 +51,29 @@ struct DevBuf {
   T* as() const { return static_cast<T*>(p); }
 };
 
+// Pinned host buffer (hipHostMalloc): per-run readbacks land here with one async DMA each
+// and a single stream sync (a pageable destination costs a staged copy and a wait per call).
+struct HostBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  hipError_t ensure(size_t bytes) {
+    if (bytes <= cap && p) return hipSuccess;
+    release();
+    const size_t want = std::max<size_t>(bytes, 4096);
+    hipError_t e = hipHostMalloc(&p, want, hipHostMallocDefault);
+    if (e == hipSuccess) cap = want;
+    else p = nullptr;
+    return e;
+  }
+  void release() {
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+  template <class T>
+  T* as() const { return static_cast<T*>(p); }
+};
+
 uint64_t align_up(uint64_t x, uint64_t a) { return (x + a - 1) / a * a; }
 
 }  // namespace
@@ -112,6 +135,7 @@ struct klf_engine {
   DevBuf d_batch, d_segs, d_tstat, d_slots, d_pool, d_tile_base, d_bsum, d_cstatus, d_counters, d_line_off,
       d_meta, d_bits, d_segout, d_wpre, d_out, d_mpart, d_trec, d_truns, d_kbase;
   uint64_t pool_cap = 1 << 20;
+  HostBuf h_rb;  // run readback: counters (64 B), then the SegOut table
   hipEvent_t ev[7] = {};
   klf::RunArgs last_args{};  // arguments of the latest completed run (klf_retail)
   uint64_t last_gen = 0;     // gen of that run's result
@@ -337,6 +361,7 @@ extern "C" void klf_close(klf_engine* e) {
     b->release();
   e->d_asm.release();
   e->d_scratch.release();
+  e->h_rb.release();
   for (DevBuf* b : {&e->d_ac_out, &e->d_ac_dict, &e->d_pcount, &e->d_pairs}) b->release();
   e->copier.reset();
   {
@@ -660,7 +685,10 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
     HIPCHK(e, e->d_meta.ensure(cap * 2 + 16), "alloc meta");
     HIPCHK(e, e->d_bits.ensure((cap / 32 + 1) * 4), "alloc bits");
     HIPCHK(e, e->d_cstatus.ensure((max_cblocks + 1) * 3 * 8), "alloc cstatus");
-    const uint64_t cmap_cap = max_cblocks + total_bytes / klf::kCopyChunk + 2;  // >= sum of ceil(bytes / chunk), >= 1 each
+    // >= sum over blocks of ceil(bytes / chunk) (>= 1 each): k_cscan's chunk keeps the
+    // output within kCopyChunksTarget chunks unless it is the largest, kCopyChunk
+    const uint64_t cmap_cap =
+        max_cblocks + std::max<uint64_t>(total_bytes / klf::kCopyChunk, klf::kCopyChunksTarget) + 2;
     HIPCHK(e, e->d_cmap.ensure(cmap_cap * 4), "alloc cmap");
     HIPCHK(e, e->d_cseg.ensure((max_cblocks + 1) * 4), "alloc cseg");
     HIPCHK(e, e->d_mpart.ensure((cap / klf::kMatchChunk + 2) * 8), "alloc mpart");
@@ -729,9 +757,14 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
     HIPCHK(e, klf::launch_pipeline(a, st, e->ev, e->num_cus), "launch");
     r->so.resize(nsegs);
     uint32_t counters[16];
-    HIPCHK(e, hipMemcpyAsync(r->so.data(), e->d_segout.p, nsegs * sizeof(SegOut), hipMemcpyDeviceToHost, st), "D2H segout");
-    HIPCHK(e, hipMemcpyAsync(counters, e->d_counters.p, sizeof(counters), hipMemcpyDeviceToHost, st), "D2H counters");
+    HIPCHK(e, e->h_rb.ensure(sizeof(counters) + nsegs * sizeof(SegOut)), "alloc readback");
+    uint8_t* rb = e->h_rb.as<uint8_t>();
+    HIPCHK(e, hipMemcpyAsync(rb, e->d_counters.p, sizeof(counters), hipMemcpyDeviceToHost, st), "D2H counters");
+    HIPCHK(e, hipMemcpyAsync(rb + sizeof(counters), e->d_segout.p, nsegs * sizeof(SegOut), hipMemcpyDeviceToHost, st),
+           "D2H segout");
     HIPCHK(e, hipStreamSynchronize(st), "sync");
+    memcpy(counters, rb, sizeof(counters));
+    memcpy(r->so.data(), rb + sizeof(counters), nsegs * sizeof(SegOut));
     e->last_segs = segs;
     if (getenv("KLF_DIAG"))
       fprintf(stderr, "[klf] hits=%u spilled=%u hits_over=%u nfa_queue=%u queue_over=%u deferred=%u\n",

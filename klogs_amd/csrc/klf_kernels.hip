@@ -1837,17 +1837,31 @@ __global__ __launch_bounds__(256) void k_cscan(RunArgs a) {
   if (a.counters[2] || a.counters[kCtrDense]) return;
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const uint32_t nb = a.counters[3];
+  __shared__ uint32_t s_lg;
   const uint32_t per = (nb + 255) / 256;
   const uint32_t i0 = t * per, i1 = i0 + per < nb ? i0 + per : nb;
+  uint64_t b = 0, c = 0, k = 0;
+  for (uint32_t i = i0; i < i1; ++i) { b += a.csum[3 * i]; c += a.csum[3 * i + 1]; }
+  const uint64_t ib = wave_incl_scan_add(b, lane), ic = wave_incl_scan_add(c, lane);
+  if (lane == 63) { s_wb[wv] = ib; s_wc[wv] = ic; }
+  __syncthreads();
+  if (t == 0) {  // this run's copy chunk (kCopyChunksTarget)
+    const uint64_t total = s_wb[0] + s_wb[1] + s_wb[2] + s_wb[3];
+    uint32_t lg = kCopyChunkMinLog2;
+    while ((1ull << lg) < kCopyChunk && (total >> lg) >= kCopyChunksTarget) ++lg;
+    s_lg = lg;
+    a.counters[kCtrChunkLog2] = lg;
+  }
+  __syncthreads();
+  const uint32_t lg = s_lg;
   // a block with no output bytes gets a chunk only when it holds a stream boundary (C2:
   // hundreds of empty blocks in the --since window, two of them with work)
   auto chunks = [&](uint64_t bytes, uint32_t i) -> uint64_t {
-    return bytes ? (bytes + kCopyChunk - 1) / kCopyChunk : ((a.cseg[i] & kCsegBoundary) ? 1 : 0);
+    return bytes ? (bytes + (1ull << lg) - 1) >> lg : ((a.cseg[i] & kCsegBoundary) ? 1 : 0);
   };
-  uint64_t b = 0, c = 0, k = 0;
-  for (uint32_t i = i0; i < i1; ++i) { b += a.csum[3 * i]; c += a.csum[3 * i + 1]; k += chunks(a.csum[3 * i], i); }
-  const uint64_t ib = wave_incl_scan_add(b, lane), ic = wave_incl_scan_add(c, lane), ik = wave_incl_scan_add(k, lane);
-  if (lane == 63) { s_wb[wv] = ib; s_wc[wv] = ic; s_wk[wv] = ik; }
+  for (uint32_t i = i0; i < i1; ++i) k += chunks(a.csum[3 * i], i);
+  const uint64_t ik = wave_incl_scan_add(k, lane);
+  if (lane == 63) s_wk[wv] = ik;
   __syncthreads();
   uint64_t pb = ib - b, pc = ic - c, pk = ik - k;
   for (int w = 0; w < wv; ++w) { pb += s_wb[w]; pc += s_wc[w]; pk += s_wk[w]; }
@@ -2020,7 +2034,9 @@ __global__ __launch_bounds__(kThreads) void k_cgather(RunArgs a) {
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   if (a.counters[2] || a.counters[kCtrDense]) return;
   const uint64_t W = a.wpre[a.nsegs];
+  __shared__ uint32_t s_mx[4];
   const uint32_t nblocks = a.counters[3], nchunks = a.counters[kCtrCopyChunks];
+  const uint64_t cs = 1ull << a.counters[kCtrChunkLog2];  // this run's copy chunk (k_cscan)
   for (uint32_t w = blockIdx.x; w < nchunks; w += gridDim.x) {
     uint32_t blk;  // the compaction block of copy chunk w (k_cscan's map; search past its end)
     if (w < a.cmap_cap) {
@@ -2056,22 +2072,45 @@ __global__ __launch_bounds__(kThreads) void k_cgather(RunArgs a) {
     }
     const uint64_t ob0 = a.csum[3 * blk];
     const uint64_t ob1 = ob0 + s_wb[0] + s_wb[1] + s_wb[2] + s_wb[3];
-    const uint64_t c0 = ob0 + (uint64_t)sub * kCopyChunk;
-    const uint64_t c1 = c0 + kCopyChunk < ob1 ? c0 + kCopyChunk : ob1;
+    const uint64_t c0 = ob0 + (uint64_t)sub * cs;
+    const uint64_t c1 = c0 + cs < ob1 ? c0 + cs : ob1;
     // chunk map: 16-B output chunk k of [c0 & ~15, c1) -> the line holding its first byte
     // of [c0, c1) (every byte of the range is in exactly one line, so every chunk gets
-    // exactly one writer); replaces a per-chunk binary search over the LDS line table
-    // (≈ 10 dependent LDS reads per 16-B chunk)
+    // exactly one writer).  Each line marks the first chunk that starts inside it, then a
+    // block max-scan fills the rest (lines ascend with their output offsets): O(1) work
+    // per thread whatever the line lengths.
     {
       const uint64_t cb0 = c0 >> 4;
+      const uint32_t nmap = c1 > c0 ? (uint32_t)(((c1 + 15) >> 4) - cb0) : 0u;
+      for (uint32_t k = (uint32_t)t; k < nmap; k += kThreads) s_map[k] = 0;
+      __syncthreads();
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int i = t * 4 + j;
         const uint64_t d = s_dst[i], e = d + s_len[i];
         const uint64_t lo = d > c0 ? d : c0, hi = e < c1 ? e : c1;
         if (lo >= hi) continue;
-        if (lo == c0) s_map[0] = (uint16_t)i;  // c0 (16-B aligned or not) lies in line i
-        for (uint64_t k = (lo + 15) >> 4; (k << 4) < hi; ++k) s_map[k - cb0] = (uint16_t)i;
+        if (lo == c0) {
+          s_map[0] = (uint16_t)i;  // c0 (16-B aligned or not) lies in line i
+        } else {
+          const uint64_t k = (lo + 15) >> 4;  // the first chunk starting inside the line
+          if ((k << 4) < hi) s_map[k - cb0] = (uint16_t)i;
+        }
+      }
+      __syncthreads();
+      const uint32_t per = (nmap + kThreads - 1) / kThreads;
+      const uint32_t m0 = (uint32_t)t * per, m1 = m0 + per < nmap ? m0 + per : nmap;
+      uint32_t mx = 0;
+      for (uint32_t k = m0; k < m1; ++k) mx = mx > s_map[k] ? mx : s_map[k];
+      const uint32_t im = wave_incl_scan_max(mx, lane);
+      if (lane == 63) s_mx[wv] = im;
+      __syncthreads();
+      uint32_t run = __shfl_up(im, 1);
+      run = lane ? run : 0u;
+      for (int k = 0; k < wv; ++k) run = run > s_mx[k] ? run : s_mx[k];
+      for (uint32_t k = m0; k < m1; ++k) {
+        run = run > s_map[k] ? run : s_map[k];
+        s_map[k] = (uint16_t)run;
       }
     }
     __syncthreads();

@@ -47,7 +47,14 @@ constexpr uint32_t kCtrCopyChunks = 11;              // counters[11]: output cop
 #ifndef KLF_COPY_CHUNK_KB
 #define KLF_COPY_CHUNK_KB 128  // measured on C3: 64 KiB 7.75 ms, 128 KiB 7.25, 256 KiB 8.39
 #endif
-constexpr uint64_t kCopyChunk = KLF_COPY_CHUNK_KB * 1024;  // output bytes per k_cgather work item
+constexpr uint64_t kCopyChunk = KLF_COPY_CHUNK_KB * 1024;  // output bytes per k_cgather work item (at most)
+// k_cscan picks the copy chunk per run: the smallest power of two >= 4 KiB (one 16-B
+// store per thread of a workgroup) that keeps the output within kCopyChunksTarget chunks,
+// up to kCopyChunk: a small output (tail-limited runs: C2, C5) is then spread over the
+// whole chip instead of a few workgroups walking 128 KiB each.
+constexpr uint32_t kCopyChunkMinLog2 = 12;
+constexpr uint32_t kCopyChunksTarget = 2048;
+constexpr uint32_t kCtrChunkLog2 = 16;               // counters[16]: log2 of this run's copy chunk
 constexpr uint32_t kCtrVerified = 10;                // counters[10]: hits k_verify walked (diagnostics)
 constexpr uint32_t kCtrDense = 14;                   // counters[14]: dense compaction (k_tkeep / k_tcopy)
 constexpr uint32_t kCtrPairsOver = 15;               // counters[15]: failed (line, pattern) pair inserts (set full)

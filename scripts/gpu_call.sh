@@ -1,5 +1,11 @@
+#!/bin/bash
+# One GPU-box call: the -m gpu suite, smoke(), then a plain bench run (each step time-limited).
+#     bash scripts/gpu_call.sh OUTDIR [bench args...]
 set -e
-O=gpurun_out/r02a; mkdir -p $O
-timeout -k 10 500 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $O/pytest_gpu.log 2>&1
+O=$1; shift
+mkdir -p $O
+timeout -k 10 500 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/pytest_gpu.log 2>&1
+tail -2 $O/pytest_gpu.log
 timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1
-echo tests done
+timeout -k 10 400 python bench.py "$@" > $O/bench.json 2> $O/bench.err
+echo "gpu_call done: $O"
