@@ -1632,7 +1632,7 @@ __device__ uint64_t select_back_bits(const uint32_t* bits, uint64_t lo, uint64_t
 // given (the bitmap only marks parsed lines), so the n-th parsed G line at/after start is
 // the window's second-to-last G line exactly when need = n + 1 (the trailing fragment is
 // then the (n+1)-th and is cut); otherwise every selected line of the window is in.
-__global__ __launch_bounds__(256) void k_tail(RunArgs a) {
+__device__ __forceinline__ void tail_body(RunArgs& a) {
   __shared__ uint32_t s_w[4];
   __shared__ uint64_t s_w64[4];
   __shared__ uint64_t s_res;
@@ -1684,7 +1684,7 @@ __global__ __launch_bounds__(256) void k_tail(RunArgs a) {
   if (t == 0) { so.win_lo = start; so.win_hi = end; }
 }
 
-__global__ __launch_bounds__(256) void k_wprefix(RunArgs a) {
+__device__ __forceinline__ void wprefix_body(RunArgs& a) {
   __shared__ uint64_t s_w64[4];
   if (a.counters[2]) return;
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
@@ -1728,6 +1728,7 @@ __global__ __launch_bounds__(256) void k_wprefix(RunArgs a) {
 // Re-tail (klf_retail): clears what k_mcount .. k_cgather accumulate into the segment
 // records, leaving the line index, the parse/since counts and the match bitmap of the run.
 __global__ __launch_bounds__(256) void k_retail_init(RunArgs a) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) a.counters[kCtrTailDone] = 0;  // k_tailw's tickets
   for (uint32_t s = blockIdx.x * 256 + threadIdx.x; s < a.nsegs; s += gridDim.x * 256) {
     SegOut& so = a.segout[s];
     so.matched = 0;
@@ -1803,7 +1804,7 @@ __device__ __forceinline__ void window_lines(const RunArgs& a, uint64_t w0, uint
 
 constexpr uint32_t kCsegBoundary = 0x80000000u;  // cseg flag: block holds a stream's first/last window line
 
-__global__ __launch_bounds__(kThreads) void k_csum(RunArgs a) {
+__device__ __forceinline__ void csum_body(RunArgs& a) {
   __shared__ uint64_t s_wb[4], s_wc[4];
   __shared__ uint32_t s_wf[4];
   if (a.counters[2] || a.counters[kCtrDense]) return;
@@ -1832,7 +1833,7 @@ __global__ __launch_bounds__(kThreads) void k_csum(RunArgs a) {
 // Exclusive prefixes of the block sums (bytes, lines) and of the copy chunks per block
 // (ceil(bytes / kCopyChunk); 0 or 1 for an empty block): long selected lines spread their copy over many
 // workgroups instead of the one that owns their 1024-line block.
-__global__ __launch_bounds__(256) void k_cscan(RunArgs a) {
+__device__ __forceinline__ void cscan_body(RunArgs& a) {
   __shared__ uint64_t s_wb[4], s_wc[4], s_wk[4];
   if (a.counters[2] || a.counters[kCtrDense]) return;
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
@@ -2025,7 +2026,7 @@ __device__ void block_gather_copy(const uint64_t* s_src, const uint64_t* s_dst, 
   }
 }
 
-__global__ __launch_bounds__(kThreads) void k_cgather(RunArgs a) {
+__device__ __forceinline__ void cgather_body(RunArgs& a) {
   __shared__ uint64_t s_src[kCompactLines];
   __shared__ uint64_t s_dst[kCompactLines];
   __shared__ uint32_t s_len[kCompactLines];
@@ -2227,9 +2228,9 @@ __device__ __forceinline__ uint32_t list_runs(const RunArgs& a, const TileLines&
 // the previous round's record stores in issue order, so a round costs one memory round
 // trip, not one per tile).
 constexpr int kTkBatch = 4;
-__global__ __launch_bounds__(256) void k_tkeep(RunArgs a, const uint32_t* __restrict__ tseg,
-                                               const SegDesc* __restrict__ segs, const TileStat* __restrict__ tstat,
-                                               const uint64_t* __restrict__ tbase, const SegOut* __restrict__ sout) {
+__device__ __forceinline__ void tkeep_body(RunArgs& a, const uint32_t* __restrict__ tseg,
+                                           const SegDesc* __restrict__ segs, const TileStat* __restrict__ tstat,
+                                           const uint64_t* __restrict__ tbase, const SegOut* __restrict__ sout) {
   if (a.counters[2] || !a.counters[kCtrDense]) return;
   const int lane = threadIdx.x & 63;
   const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -2272,7 +2273,7 @@ __global__ __launch_bounds__(256) void k_tkeep(RunArgs a, const uint32_t* __rest
 
 // Reduce-then-scan of the tiles' (kept bytes, selected lines): 256 x R tiles per block.
 template <int R>
-__global__ __launch_bounds__(256) void k_ksum(RunArgs a) {
+__device__ __forceinline__ void ksum_body(RunArgs& a) {
   __shared__ uint64_t s_w[2][4];
   if (a.counters[2] || !a.counters[kCtrDense]) return;
   const uint32_t t0 = blockIdx.x * (256 * R) + threadIdx.x;
@@ -2295,10 +2296,11 @@ __global__ __launch_bounds__(256) void k_ksum(RunArgs a) {
 }
 
 template <int R>
-__global__ __launch_bounds__(256) void k_kbase(RunArgs a) {
+__device__ __forceinline__ void kbase_body(RunArgs& a) {
   __shared__ uint64_t s_w[2][2][4];
   __shared__ uint64_t s_base[2];
   if (a.counters[2] || !a.counters[kCtrDense]) return;
+  if (blockIdx.x * (256u * R) >= a.ntiles) return;  // launched on k_cgather's grid (k_cmove)
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const uint32_t t0 = blockIdx.x * (256 * R) + t;
   {
@@ -2337,6 +2339,43 @@ __global__ __launch_bounds__(256) void k_kbase(RunArgs a) {
       if (tile + 1 == sd.tile0 + sd.ntiles) { a.segout[s].out_hi = ob + kb; a.segout[s].sel_hi = oc + kc; }
     }
   }
+}
+
+// ---- the launches after the matchers (fewer kernel boundaries: each costs ~5 us) ----------
+// k_tailw: the kubelet tail rule per stream (block per stream); the last block to finish
+// (ticket) then runs the window prefix over all streams and picks the compaction path.
+__global__ __launch_bounds__(256) void k_tailw(RunArgs a) {
+  __shared__ uint32_t s_last;
+  tail_body(a);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence();  // this block's stream records before its ticket
+    s_last = atomicAdd(&a.counters[kCtrTailDone], 1u) == gridDim.x - 1 ? 1u : 0u;
+  }
+  __syncthreads();
+  if (s_last) {
+    __threadfence();  // every block's records, seen through their tickets
+    wprefix_body(a);
+  }
+}
+// Then three launches serve either compaction path (k_wprefix's choice, counters[kCtrDense]):
+//   k_cplan   line gather: per-block selected bytes (k_csum) | tile copy: kept runs (k_tkeep)
+//   k_cmid    block prefix (k_cscan, block 0)               | tile block sums (k_ksum)
+//   k_cmove   gather copy (k_cgather)                       | tile output bases (k_kbase)
+// and k_tcopy (tile copy) last.
+__global__ __launch_bounds__(256) void k_cplan(RunArgs a, const uint32_t* __restrict__ tseg,
+                                               const SegDesc* __restrict__ segs, const TileStat* __restrict__ tstat,
+                                               const uint64_t* __restrict__ tbase, const SegOut* __restrict__ sout) {
+  if (a.counters[kCtrDense]) tkeep_body(a, tseg, segs, tstat, tbase, sout);
+  else csum_body(a);
+}
+__global__ __launch_bounds__(256) void k_cmid(RunArgs a) {
+  if (a.counters[kCtrDense]) ksum_body<16>(a);
+  else if (blockIdx.x == 0) cscan_body(a);
+}
+__global__ __launch_bounds__(256) void k_cmove(RunArgs a) {
+  if (a.counters[kCtrDense]) kbase_body<16>(a);
+  else cgather_body(a);
 }
 
 // LDS per wave: the tile (16 B of front pad, 8 KiB, 32 B of back pad: the unaligned reads of
@@ -2811,28 +2850,24 @@ static hipError_t launch_tail_stage(const RunArgs& a, hipStream_t st, hipEvent_t
     hipLaunchKernelGGL(k_mcount, dim3(g), dim3(256), 0, st, a);
     KLF_TRY(hipGetLastError());
   }
-  hipLaunchKernelGGL(k_tail, dim3(a.nsegs), dim3(256), 0, st, a);
-  KLF_TRY(hipGetLastError());
-  hipLaunchKernelGGL(k_wprefix, dim3(1), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(k_tailw, dim3(a.nsegs), dim3(256), 0, st, a);
   KLF_TRY(hipGetLastError());
   if (a.stage_times) KLF_TRY(hipEventRecord(ev[4], st));  // ~5 us of idle GPU each
-  // k_wprefix chose the path (counters[kCtrDense]); the other path's kernels exit at once
-  hipLaunchKernelGGL(k_csum, dim3(num_cus * 4), dim3(kThreads), 0, st, a);
-  KLF_TRY(hipGetLastError());
-  hipLaunchKernelGGL(k_cscan, dim3(1), dim3(256), 0, st, a);
-  KLF_TRY(hipGetLastError());
-  hipLaunchKernelGGL(k_cgather, dim3(num_cus * KLF_CG_GRID), dim3(kThreads), 0, st, a);
-  KLF_TRY(hipGetLastError());
-  if (a.compact_mode != 1) {
-    const uint32_t gk = (a.ntiles + 3) / 4, gt = (a.ntiles + 4 * kTkBatch - 1) / (4 * kTkBatch);
-    hipLaunchKernelGGL(k_tkeep, dim3(gt < (uint32_t)num_cus * 8 ? gt : num_cus * 8), dim3(256), 0, st, a,
-                       a.tile_seg, a.segs, a.tstat, a.tile_base, a.segout);
+  {
+    const uint32_t gt = (a.ntiles + 4 * kTkBatch - 1) / (4 * kTkBatch);
+    const uint32_t gp = (uint32_t)num_cus * 8;
+    hipLaunchKernelGGL(k_cplan, dim3(a.compact_mode != 1 && gt < gp ? gt : gp), dim3(256), 0, st, a, a.tile_seg,
+                       a.segs, a.tstat, a.tile_base, a.segout);
     KLF_TRY(hipGetLastError());
     const uint32_t nb = (a.ntiles + 4095) / 4096;
-    hipLaunchKernelGGL(k_ksum<16>, dim3(nb), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(k_cmid, dim3(nb), dim3(256), 0, st, a);
     KLF_TRY(hipGetLastError());
-    hipLaunchKernelGGL(k_kbase<16>, dim3(nb), dim3(256), 0, st, a);
+    const uint32_t gg = (uint32_t)num_cus * KLF_CG_GRID;
+    hipLaunchKernelGGL(k_cmove, dim3(nb > gg ? nb : gg), dim3(kThreads), 0, st, a);
     KLF_TRY(hipGetLastError());
+  }
+  if (a.compact_mode != 1) {
+    const uint32_t gk = (a.ntiles + 3) / 4;
     // persistent grid: one resident generation of blocks, so every wave's prefetch
     // pipeline runs over its whole share of tiles
     static int occ = 0;

@@ -55,6 +55,8 @@ constexpr uint64_t kCopyChunk = KLF_COPY_CHUNK_KB * 1024;  // output bytes per k
 constexpr uint32_t kCopyChunkMinLog2 = 12;
 constexpr uint32_t kCopyChunksTarget = 2048;
 constexpr uint32_t kCtrChunkLog2 = 16;               // counters[16]: log2 of this run's copy chunk
+constexpr uint32_t kCtrTicket = 17;                  // counters[17]: k_tindex block tickets
+constexpr uint32_t kCtrTailDone = 18;                // counters[18]: k_tailw blocks done
 constexpr uint32_t kCtrVerified = 10;                // counters[10]: hits k_verify walked (diagnostics)
 constexpr uint32_t kCtrDense = 14;                   // counters[14]: dense compaction (k_tkeep / k_tcopy)
 constexpr uint32_t kCtrPairsOver = 15;               // counters[15]: failed (line, pattern) pair inserts (set full)
