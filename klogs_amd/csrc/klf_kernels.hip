@@ -316,6 +316,9 @@ __global__ __launch_bounds__(kThreads, MODE == kScanGen ? 3 : KLF_SCAN_OCC) void
   __shared__ __attribute__((aligned(16))) uint32_t s_list_all[kWaves][kSlotStride];
   __shared__ __attribute__((aligned(16))) uint32_t s_lit[kMaxFusedLiteral / 4 + 1];  // literal, zero padded
   __shared__ uint32_t s_month[16];
+  // the TileStats of the wave's current tile group: LDS for the plain / literal scans (a
+  // register quad there spills), a register quad for GEN (LDS is what bounds its occupancy)
+  __shared__ uint4 s_gstat[GEN ? 1 : kWaves][kScanGroup];
   __shared__ uint32_t s_qf[GEN ? kQfWords : 1];  // q-gram bitmap of the needles
   // wv is wave-uniform; readfirstlane tells the compiler so (tile indices stay in SGPRs and
   // the descriptor reads stay scalar loads)
@@ -350,7 +353,13 @@ __global__ __launch_bounds__(kThreads, MODE == kScanGen ? 3 : KLF_SCAN_OCC) void
 #define KLF_LOAD(r) pf##r = gp[r * 64 + lane];
 #define KLF_STORE(r) l[r * 64 + lane] = pf##r;
   uint4 pfh = make_uint4(0, 0, 0, 0);
-  uint32_t tile = blockIdx.x * kWaves + wv;
+  // A wave takes groups of kScanGroup consecutive tiles (group g, g + nwaves, ...): their
+  // TileStats go out together as one whole-line store into the compact tstat array.
+  auto next_tile = [&](uint32_t x) -> uint32_t {
+    return (x % kScanGroup) == kScanGroup - 1 ? x + 1 + kScanGroup * (nwaves - 1) : x + 1;
+  };
+  uint32_t tile = (blockIdx.x * kWaves + wv) * kScanGroup;
+  uint4 stv = make_uint4(0, 0, 0, 0);  // GEN: lane k holds the group's TileStat k
   // The segment of the prefetched tile travels with it (scalar registers): a stride of
   // nwaves tiles stays inside one stream for all but the last tiles of a long stream, so
   // the dependent descriptor loads (tseg -> segs, scalar-cache misses at this stride) leave
@@ -374,7 +383,7 @@ __global__ __launch_bounds__(kThreads, MODE == kScanGen ? 3 : KLF_SCAN_OCC) void
     __builtin_amdgcn_raw_buffer_store_b32(0u, none, 0x7FFF0000u, 0, 0);
   }
   bool any_defer = false;
-  for (; tile < a.ntiles; tile += nwaves) {
+  for (; tile < a.ntiles; tile = next_tile(tile)) {
     const uint32_t s = pf_s;
     const SegDesc sd = pf_sd;
     const int64_t rel_lo = (int64_t)(tile - sd.tile0) * kTile;
@@ -389,7 +398,7 @@ __global__ __launch_bounds__(kThreads, MODE == kScanGen ? 3 : KLF_SCAN_OCC) void
       uint4* l = reinterpret_cast<uint4*>(s_tile);
       KLF_ROWS(KLF_STORE)
       if (lane < kHalo / 16) l[kTile / 16 + lane] = pfh;
-      const uint32_t nx = tile + nwaves;
+      const uint32_t nx = next_tile(tile);
       if (nx < a.ntiles) {
         if (nx - sd.tile0 >= sd.ntiles) {
           pf_s = tseg[nx];
@@ -716,6 +725,20 @@ __global__ __launch_bounds__(kThreads, MODE == kScanGen ? 3 : KLF_SCAN_OCC) void
         const u32x4v v = u ? u32x4v{sl.x, sl.y, sl.z, sl.w} : u32x4v{w0, w1, w2, w3};
         __builtin_amdgcn_raw_buffer_store_b128(v, rrs, 16u * u, 0, 0);
       }
+      // the group's TileStats, one 128-B store at its last tile (lanes past it dropped)
+      const uint32_t gk = tile % kScanGroup, g0 = tile - gk;
+      if (GEN) {
+        if ((uint32_t)lane == gk) stv = make_uint4(w0, w1, w2, w3);
+      } else {
+        if (lane == 0) s_gstat[wv][gk] = make_uint4(w0, w1, w2, w3);
+        wave_lds_sync();
+      }
+      const bool gend = gk == kScanGroup - 1 || tile + 1 >= a.ntiles;
+      const uint32_t ng = a.ntiles - g0 < kScanGroup ? a.ntiles - g0 : kScanGroup;
+      const __amdgpu_buffer_rsrc_t srs =
+          __builtin_amdgcn_make_buffer_rsrc(a.tstat + g0, 0, (gend && !abl) ? (int)(16u * ng) : 0, 0x00020000);
+      const uint4 gs = GEN ? stv : s_gstat[GEN ? 0 : wv][lane & (kScanGroup - 1)];
+      __builtin_amdgcn_raw_buffer_store_b128(u32x4v{gs.x, gs.y, gs.z, gs.w}, srs, 16u * (uint32_t)lane, 0, 0);
     }
     asm volatile("" ::: "memory");  // the next stage overwrites the LDS region read above
   }
@@ -795,177 +818,213 @@ __device__ bool general_count(const RunArgs& a, const uint8_t* p, int64_t n, uin
   return any;
 }
 
-__global__ __launch_bounds__(256) void k_fixup(RunArgs a) {
-  if (!a.counters[kCtrDefer] || a.counters[2]) return;
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  for (uint32_t tile = blockIdx.x * 4 + wv; tile < a.ntiles; tile += gridDim.x * 4) {
-    TileStat* const trs = reinterpret_cast<TileStat*>(a.slots + (size_t)tile * kRecStride);  // k_tsum compacts later
-    TileStat ts = *trs;
-    if (!(ts.flags & 4u)) continue;
-    const uint32_t s = a.tile_seg[tile];
-    const SegDesc sd = a.segs[s];
-    const int64_t rel_lo = (int64_t)(tile - sd.tile0) * kTile;
-    const int64_t seg_len = (int64_t)sd.len;
-    const bool first = rel_lo == 0, last = rel_lo + kTile >= seg_len;
-    const uint32_t k0 = first ? 0 : 1, k1 = last ? ts.events : ts.events + 1;
-    const uint32_t nlines = k1 > k0 ? k1 - k0 : 0;
-    uint32_t* list = (ts.flags & 1u) ? a.pool + ts.pool_base : a.slots + (size_t)tile * kRecStride + kRecHead;
-    const uint8_t* segp = a.bytes + sd.base;
-    uint32_t dp = 0, dq = 0;
-    for (uint32_t j = lane; j < nlines; j += 64) {
-      const uint32_t sl = list[j];
-      if (!(sl & kSlotDefer)) continue;
-      const uint32_t off = sl & kSlotOff;
-      const int64_t p0 = rel_lo + off;
-      TsResult r;
-      uint32_t plen = 0;
-      const bool ok = parse_line_prefix(GlobalBytes{segp, p0, seg_len}, r, plen);
-      const bool so = ok && !time_before(r.sec, r.nsec, a.since_sec, a.since_nsec);
-      uint32_t hit = 0;
-      const bool gen = a.grep_mode == kGrepGeneral && a.pats.qf_on;  // the scan attributed none
-      if ((a.grep_mode == kGrepLit1 || gen) && ok) {
-        const int64_t cs = p0 + plen;
-        int64_t ce;
-        if (j + 1 < nlines) {
-          ce = rel_lo + (int64_t)(list[j + 1] & kSlotOff) - 1;  // the line's '\n'
-        } else {
-          ce = cs;
-          while (ce < seg_len && segp[ce] != '\n') ++ce;
-        }
-        if (ce > cs && !gen && contains_bytes(segp + cs, ce - cs, a.lit, a.lit_len)) hit = kSlotHit;
-        if (ce > cs && gen && general_match(a.pats, segp + cs, ce - cs)) hit = kSlotHit;
+// One wave: the deferred lines of `tile` (TileStat ts) through the general parse; their
+// slots are rewritten in place and the parsed / since_ok counts the tile gains are
+// returned (wave-uniform).
+__device__ void fix_tile(const RunArgs& a, uint32_t tile, const TileStat& ts, int lane, uint32_t& add_p,
+                         uint32_t& add_q) {
+  const uint32_t s = a.tile_seg[tile];
+  const SegDesc sd = a.segs[s];
+  const int64_t rel_lo = (int64_t)(tile - sd.tile0) * kTile;
+  const int64_t seg_len = (int64_t)sd.len;
+  const bool first = rel_lo == 0, last = rel_lo + kTile >= seg_len;
+  const uint32_t k0 = first ? 0 : 1, k1 = last ? ts.events : ts.events + 1;
+  const uint32_t nlines = k1 > k0 ? k1 - k0 : 0;
+  uint32_t* list = (ts.flags & 1u) ? a.pool + ts.pool_base : a.slots + (size_t)tile * kRecStride + kRecHead;
+  const uint8_t* segp = a.bytes + sd.base;
+  uint32_t dp = 0, dq = 0;
+  for (uint32_t j = lane; j < nlines; j += 64) {
+    const uint32_t sl = list[j];
+    if (!(sl & kSlotDefer)) continue;
+    const uint32_t off = sl & kSlotOff;
+    const int64_t p0 = rel_lo + off;
+    TsResult r;
+    uint32_t plen = 0;
+    const bool ok = parse_line_prefix(GlobalBytes{segp, p0, seg_len}, r, plen);
+    const bool so = ok && !time_before(r.sec, r.nsec, a.since_sec, a.since_nsec);
+    uint32_t hit = 0;
+    const bool gen = a.grep_mode == kGrepGeneral && a.pats.qf_on;  // the scan attributed none
+    if ((a.grep_mode == kGrepLit1 || gen) && ok) {
+      const int64_t cs = p0 + plen;
+      int64_t ce;
+      if (j + 1 < nlines) {
+        ce = rel_lo + (int64_t)(list[j + 1] & kSlotOff) - 1;  // the line's '\n'
+      } else {
+        ce = cs;
+        while (ce < seg_len && segp[ce] != '\n') ++ce;
       }
-      list[j] = off | kSlotDefer | hit | ((uint32_t)make_meta(ok, so, plen) << 16);
-      dp += ok ? 1u : 0u;
-      dq += so ? 1u : 0u;
+      if (ce > cs && !gen && contains_bytes(segp + cs, ce - cs, a.lit, a.lit_len)) hit = kSlotHit;
+      if (ce > cs && gen && general_match(a.pats, segp + cs, ce - cs)) hit = kSlotHit;
     }
-    dp = wave_sum(dp);
-    dq = wave_sum(dq);
-    if (lane == 0) {
-      ts.parsed = (uint16_t)(ts.parsed + dp);
-      ts.since_ok = (uint16_t)(ts.since_ok + dq);
-      *trs = ts;
-    }
+    list[j] = off | kSlotDefer | hit | ((uint32_t)make_meta(ok, so, plen) << 16);
+    dp += ok ? 1u : 0u;
+    dq += so ? 1u : 0u;
   }
+  add_p = wave_sum(dp);
+  add_q = wave_sum(dq);
 }
 
 // ---- K1b/K1c: tile line bases (exclusive scan of TileStat.events) -------------------
-// The same pass scans the per-tile parsed / since_ok counts: a stream's counts are the
-// prefix differences at its first and last tile (no same-address atomics), and zeroes the
-// match-bitmap words whose first line falls in the block's line range (the bitmap is
-// only ever OR-ed into by the kernels after this one).
-// Tiles per block: 256 threads x R.  R = 4 up to kScanSmallTiles tiles (enough blocks to
-// fill the chip; each block sums the preceding blocks' totals itself), R = 16 above.
+// Two passes over the compact TileStats (the scan writes them 8 tiles to a 128-B line), a
+// thread owning R consecutive tiles (block: 256 R tiles):
+//   k_tindex<R, 0>  the deferred lines' general parse (fix_tile; it corrects the tiles'
+//                   counts in place), then each block's totals;
+//   k_tindex<R, 1>  the earlier blocks' totals + the block scan of events / parsed /
+//                   since_ok / prefilter hits -> tile line bases, the streams' line and
+//                   count ranges (prefix differences at their first and last tile: no
+//                   same-address atomics), the flattened hit list, and zeroed match-bitmap
+//                   words whose first line falls in the block's line range (the bitmap is
+//                   only ever OR-ed into by the kernels after this one).
 
 // TileStat.carry_off is the tile's hit-slot count with the q-gram prefilter (GEN scan)
 __device__ __forceinline__ uint32_t tile_hits(const RunArgs& a, const TileStat& ts) {
   return (a.grep_mode == kGrepGeneral && a.pats.qf_on) ? ts.carry_off : 0u;
 }
 
-template <int R>
-__global__ __launch_bounds__(256) void k_tsum(RunArgs a) {
-  __shared__ uint64_t s_w[4][4];
-  const uint32_t t0 = blockIdx.x * (256 * R) + threadIdx.x;
+template <int R, int PASS>
+__global__ __launch_bounds__(256) void k_tindex(RunArgs a) {
+  __shared__ uint32_t s_wt[4][4];
+  __shared__ uint64_t s_w64[4][4];
+  __shared__ uint64_t s_base[4];
+  __shared__ uint32_t s_ndef;
+  __shared__ uint32_t s_def[PASS == 0 ? 256 : 1];
+  __shared__ uint32_t s_fix[PASS == 0 ? 256 : 1][2];
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const uint32_t bid = blockIdx.x;
+  const uint32_t tb = bid * (256u * R) + (uint32_t)t * R;  // my first tile
   TileStat ts[R];
+  uint32_t sg[R];
 #pragma unroll
-  for (int r = 0; r < R; ++r) {  // all loads in flight at once (one 16-B record per region)
+  for (int r = 0; r < R; ++r) {
     ts[r] = TileStat{};
-    if (t0 + r * 256 < a.ntiles) ts[r] = *reinterpret_cast<const TileStat*>(a.slots + (size_t)(t0 + r * 256) * kRecStride);
+    sg[r] = 0;
+    if (tb + r < a.ntiles) {
+      ts[r] = a.tstat[tb + r];
+      sg[r] = a.tile_seg[tb + r];
+    }
   }
+  // deferred lines (non-canonical timestamp prefixes; rare): per round every thread hands
+  // its next tile that has them to the block (<= 256 per round), the waves run them
+  uint32_t dmask = 0;
 #pragma unroll
-  for (int r = 0; r < R; ++r)  // the compact copy every later kernel reads (coalesced)
-    if (t0 + r * 256 < a.ntiles) a.tstat[t0 + r * 256] = ts[r];
-  uint64_t v = 0, p = 0, q = 0, h = 0;
+  for (int r = 0; r < R; ++r)
+    if (PASS == 0 && tb + r < a.ntiles && (ts[r].flags & 4u)) dmask |= 1u << r;
+  while (PASS == 0 && __syncthreads_or(dmask != 0u)) {
+    if (t == 0) s_ndef = 0;
+    __syncthreads();
+    uint32_t slot = ~0u;
+    const uint32_t rr = dmask ? (uint32_t)__builtin_ctz(dmask) : 0u;
+    if (dmask) {
+      slot = atomicAdd(&s_ndef, 1u);  // < 256: one entry per thread and round
+      s_def[slot] = tb + rr;
+    }
+    __syncthreads();
+    const uint32_t nd = s_ndef;
+    for (uint32_t k = wv; k < nd; k += 4) {
+      const uint32_t tile = s_def[k];
+      uint32_t dp, dq;
+      fix_tile(a, tile, a.tstat[tile], lane, dp, dq);
+      if (lane == 0) { s_fix[k][0] = dp; s_fix[k][1] = dq; }
+    }
+    __syncthreads();
+    if (slot != ~0u) {
+#pragma unroll
+      for (int r = 0; r < R; ++r)
+        if ((uint32_t)r == rr) {
+          ts[r].parsed = (uint16_t)(ts[r].parsed + s_fix[slot][0]);
+          ts[r].since_ok = (uint16_t)(ts[r].since_ok + s_fix[slot][1]);
+          a.tstat[tb + r] = ts[r];  // the corrected counts for every later kernel
+        }
+      dmask &= dmask - 1u;
+    }
+  }
+  // the thread's and the block's totals (block-local: < 2^32)
+  uint32_t v = 0, p = 0, q = 0, h = 0;
 #pragma unroll
   for (int r = 0; r < R; ++r) { v += ts[r].events; p += ts[r].parsed; q += ts[r].since_ok; h += tile_hits(a, ts[r]); }
-  v = wave_sum(v);
-  p = wave_sum(p);
-  q = wave_sum(q);
-  h = wave_sum(h);
-  if ((threadIdx.x & 63) == 0) {
-    s_w[0][threadIdx.x >> 6] = v; s_w[1][threadIdx.x >> 6] = p; s_w[2][threadIdx.x >> 6] = q; s_w[3][threadIdx.x >> 6] = h;
+  const uint32_t iv = wave_incl_scan_add(v, lane), ip = wave_incl_scan_add(p, lane), iq = wave_incl_scan_add(q, lane),
+                 ih = wave_incl_scan_add(h, lane);
+  if (lane == 63) { s_wt[0][wv] = iv; s_wt[1][wv] = ip; s_wt[2][wv] = iq; s_wt[3][wv] = ih; }
+  __syncthreads();
+  uint32_t ov = iv - v, op = ip - p, oq = iq - q, oh = ih - h;
+  for (int k = 0; k < wv; ++k) { ov += s_wt[0][k]; op += s_wt[1][k]; oq += s_wt[2][k]; oh += s_wt[3][k]; }
+  if (PASS == 0) {  // the block's totals
+    if (t < 4) a.bsum[4 * (size_t)bid + t] = s_wt[t][0] + s_wt[t][1] + s_wt[t][2] + s_wt[t][3];
+    return;
+  }
+  {  // the earlier blocks' totals
+    uint64_t xv = 0, xp = 0, xq = 0, xh = 0;
+    for (uint32_t b = t; b < bid; b += 256) {
+      xv += a.bsum[4 * (size_t)b];
+      xp += a.bsum[4 * (size_t)b + 1];
+      xq += a.bsum[4 * (size_t)b + 2];
+      xh += a.bsum[4 * (size_t)b + 3];
+    }
+    xv = wave_sum(xv);
+    xp = wave_sum(xp);
+    xq = wave_sum(xq);
+    xh = wave_sum(xh);
+    if (lane == 0) { s_w64[0][wv] = xv; s_w64[1][wv] = xp; s_w64[2][wv] = xq; s_w64[3][wv] = xh; }
+    __syncthreads();
+    if (t < 4) s_base[t] = s_w64[t][0] + s_w64[t][1] + s_w64[t][2] + s_w64[t][3];
+    __syncthreads();
+  }
+  const uint32_t s_prev = tb > 0 && tb - 1 < a.ntiles ? a.tile_seg[tb - 1] : ~0u;
+  const uint32_t s_next = tb + R < a.ntiles ? a.tile_seg[tb + R] : ~0u;
+  const uint64_t blk_lo = s_base[0];
+  const uint64_t blk_hi = s_base[0] + s_wt[0][0] + s_wt[0][1] + s_wt[0][2] + s_wt[0][3];
+  const uint32_t blk_h = s_wt[3][0] + s_wt[3][1] + s_wt[3][2] + s_wt[3][3];
+  // tile bases and hit counts go through LDS so that both outputs are written coalesced
+  __shared__ uint32_t s_tbl[256 * R];   // block-local tile line base (< 2^32)
+  __shared__ uint8_t s_thit[256 * R];   // tile hit slots (<= kHitSlots)
+  __shared__ uint32_t s_hpre[256];      // inclusive prefix of the threads' hit slots
+  s_hpre[t] = oh + h;
+  uint32_t lv = ov;
+  uint64_t bv = s_base[0] + ov, bp = s_base[1] + op, bq = s_base[2] + oq;
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const uint32_t tile = tb + r;
+    s_tbl[t * R + r] = lv;
+    s_thit[t * R + r] = (uint8_t)(tile < a.ntiles ? tile_hits(a, ts[r]) : 0u);
+    if (tile < a.ntiles) {
+      const uint32_t s = sg[r];
+      const uint32_t sp = r ? sg[r - 1] : s_prev, sn = r + 1 < R ? sg[r + 1] : s_next;
+      const uint32_t nx = tile + 1 < a.ntiles ? sn : ~0u;
+      if (sp != s) { a.segout[s].line_lo = bv; a.segout[s].p_lo = bp; a.segout[s].q_lo = bq; }
+      if (nx != s) {
+        a.segout[s].line_hi = bv + ts[r].events;
+        a.segout[s].p_hi = bp + ts[r].parsed;
+        a.segout[s].q_hi = bq + ts[r].since_ok;
+      }
+    }
+    lv += ts[r].events;
+    bv += ts[r].events;
+    bp += ts[r].parsed;
+    bq += ts[r].since_ok;
   }
   __syncthreads();
-  if (threadIdx.x < 4) {
-    const int k = threadIdx.x;
-    a.bsum[4 * blockIdx.x + k] = s_w[k][0] + s_w[k][1] + s_w[k][2] + s_w[k][3];
-  }
-}
-
-// Rounds of 256 consecutive tiles (one per thread, coalesced), block scan per round.  All
-// rounds' records and tile->stream ids are loaded up front; stream boundaries are where
-// the stream id of the neighbouring tile differs (no dependent descriptor loads).  With
-// the q-gram prefilter the same scan flattens the tiles' hit slots into one list for
-// k_verify (hit slot ids tile * kHitSlots + j).
-template <int R>
-__global__ __launch_bounds__(256) void k_tbase(RunArgs a) {
-  __shared__ uint64_t s_w[2][4][4];
-  __shared__ uint64_t s_base[4];
-  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
-  const uint32_t t0 = blockIdx.x * (256 * R) + t;
-  TileStat ts[R];
-  uint32_t sg[R], sp[R], sn[R];
-#pragma unroll
-  for (int r = 0; r < R; ++r) {
-    const uint32_t tile = t0 + r * 256;
-    ts[r] = TileStat{};
-    sg[r] = sp[r] = sn[r] = 0;
-    if (tile < a.ntiles) {
-      ts[r] = a.tstat[tile];
-      sg[r] = a.tile_seg[tile];
-      sp[r] = tile > 0 ? a.tile_seg[tile - 1] : ~0u;
-      sn[r] = tile + 1 < a.ntiles ? a.tile_seg[tile + 1] : ~0u;
+  const uint32_t t0 = bid * (256u * R);
+  for (uint32_t k = (uint32_t)t; k < 256u * R; k += 256)
+    if (t0 + k < a.ntiles) a.tile_base[t0 + k] = blk_lo + s_tbl[k];
+  // the block's hit slots, in tile order: hit k -> its thread (prefix search), then tile
+  const uint64_t hb = s_base[3];
+  for (uint32_t k = (uint32_t)t; k < blk_h; k += 256) {
+    uint32_t lo = 0, hi = 255;  // the first thread whose inclusive prefix exceeds k
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (s_hpre[mid] > k) hi = mid; else lo = mid + 1;
     }
+    uint32_t j = k - (lo ? s_hpre[lo - 1] : 0u), r = 0;
+    while (j >= s_thit[lo * R + r]) j -= s_thit[lo * R + r++];
+    if (hb + k < a.hflat_cap) a.hflat[hb + k] = (t0 + lo * R + r) * kHitSlots + j;
   }
-  {  // prefix of the preceding blocks' sums
-    uint64_t v = 0, p = 0, q = 0, h = 0;
-    for (uint32_t b = t; b < blockIdx.x; b += 256) {
-      v += a.bsum[4 * b];
-      p += a.bsum[4 * b + 1];
-      q += a.bsum[4 * b + 2];
-      h += a.bsum[4 * b + 3];
-    }
-    v = wave_sum(v);
-    p = wave_sum(p);
-    q = wave_sum(q);
-    h = wave_sum(h);
-    if (lane == 0) { s_w[0][0][wv] = v; s_w[0][1][wv] = p; s_w[0][2][wv] = q; s_w[0][3][wv] = h; }
-    __syncthreads();
-    if (t < 4) s_base[t] = s_w[0][t][0] + s_w[0][t][1] + s_w[0][t][2] + s_w[0][t][3];
-    __syncthreads();
-  }
-  const uint64_t blk_lo = s_base[0];
-  uint64_t cv = s_base[0], cp = s_base[1], cq = s_base[2], ch = s_base[3];  // running bases (block-uniform)
-#pragma unroll
-  for (int r = 0; r < R; ++r) {
-    const uint32_t tile = t0 + r * 256;
-    const uint64_t v = ts[r].events, p = ts[r].parsed, q = ts[r].since_ok, h = tile_hits(a, ts[r]);
-    const uint64_t iv = wave_incl_scan_add(v, lane), ip = wave_incl_scan_add(p, lane), iq = wave_incl_scan_add(q, lane),
-                   ih = wave_incl_scan_add(h, lane);
-    const int pb = r & 1;  // double-buffered wave totals: one barrier per round
-    if (lane == 63) { s_w[pb][0][wv] = iv; s_w[pb][1][wv] = ip; s_w[pb][2][wv] = iq; s_w[pb][3][wv] = ih; }
-    __syncthreads();
-    uint64_t bv = cv + iv - v, bp = cp + ip - p, bq = cq + iq - q, bh = ch + ih - h;
-    for (int k = 0; k < wv; ++k) { bv += s_w[pb][0][k]; bp += s_w[pb][1][k]; bq += s_w[pb][2][k]; bh += s_w[pb][3][k]; }
-    cv += s_w[pb][0][0] + s_w[pb][0][1] + s_w[pb][0][2] + s_w[pb][0][3];
-    cp += s_w[pb][1][0] + s_w[pb][1][1] + s_w[pb][1][2] + s_w[pb][1][3];
-    cq += s_w[pb][2][0] + s_w[pb][2][1] + s_w[pb][2][2] + s_w[pb][2][3];
-    ch += s_w[pb][3][0] + s_w[pb][3][1] + s_w[pb][3][2] + s_w[pb][3][3];
-    if (tile < a.ntiles) {
-      a.tile_base[tile] = bv;
-      const uint32_t s = sg[r];
-      if (sp[r] != s) { a.segout[s].line_lo = bv; a.segout[s].p_lo = bp; a.segout[s].q_lo = bq; }
-      if (sn[r] != s) { a.segout[s].line_hi = bv + v; a.segout[s].p_hi = bp + p; a.segout[s].q_hi = bq + q; }
-      for (uint32_t j = 0; j < (uint32_t)h; ++j)
-        if (bh + j < a.hflat_cap) a.hflat[bh + j] = tile * kHitSlots + j;
-    }
-  }
-  if (t == 0 && blockIdx.x == gridDim.x - 1 && a.hflat) {  // the last block knows the total
-    a.counters[kCtrFlatHits] = (uint32_t)(ch < 0xFFFFFFFFull ? ch : 0xFFFFFFFFull);
-    if (ch > a.hflat_cap) atomicOr(&a.counters[kCtrHitsOver], 1u);
+  if (t == 0 && (bid + 1) * (256u * R) >= a.ntiles && a.hflat) {  // the last block knows the total
+    const uint64_t tot = hb + blk_h;
+    a.counters[kCtrFlatHits] = (uint32_t)(tot < 0xFFFFFFFFull ? tot : 0xFFFFFFFFull);
+    if (tot > a.hflat_cap) atomicOr(&a.counters[kCtrHitsOver], 1u);
   }
   if (a.grep_mode != kGrepNone) {  // bitmap words whose first line is in [blk_lo, blk_hi)
-    const uint64_t w0 = (blk_lo + 31) / 32, w1 = (cv + 31) / 32;
+    const uint64_t w0 = (blk_lo + 31) / 32, w1 = (blk_hi + 31) / 32;
     for (uint64_t w = w0 + t; w < w1 && w * 32 < a.cap_lines; w += 256) a.bits[w] = 0u;
   }
 }
@@ -1144,19 +1203,14 @@ __device__ __forceinline__ uint32_t gword(const uint8_t* p) {  // 4 bytes at any
 // x = p - k may lie before the tile: an occurrence holds no '\n', so it is then in the
 // tile's carried-in line.  Inside the tile, its line comes from the tile's own staged
 // line starts (slots, meta in the high half) instead of a search of the whole index.
-__device__ void verify_hit(const RunArgs& a, uint32_t tile, uint32_t s, int32_t p) {
-#if KLF_ABL & 16
-  if (p == 0x7FFF) atomicOr(&a.counters[13], s);  // timing build: no verification work
-  return;
-#endif
+// The bucket walk of one hit whose bucket [e0, e1) is known (the loads before it are
+// batched over several hits by k_verify).
+__device__ void verify_hit_from(const RunArgs& a, uint32_t tile, uint32_t s, const SegDesc& sd, int32_t p,
+                                uint32_t e0, uint32_t e1) {
   const DevPatterns& P = a.pats;
-  const SegDesc sd = a.segs[s];
   const uint8_t* segp = a.bytes + sd.base;
   const int64_t rel_lo = (int64_t)(tile - sd.tile0) * kTile;
-  const uint32_t g = (gword(segp + rel_lo + p) | P.qf_fold) & P.qf_mask;
-  const uint32_t b = qf_word(qf_hash(g, P.qf_w24, P.qf_k));
-  const uint32_t e1 = P.qf_head[b + 1];
-  for (uint32_t e = P.qf_head[b]; e < e1; ++e) {
+  for (uint32_t e = e0; e < e1; ++e) {
     const uint4 E = P.qf_ent[e];
     const uint32_t m = E.y & 0xFFFFu;
     const int32_t x = p - (int32_t)((E.y >> 16) & 0xFFu);
@@ -1215,15 +1269,60 @@ __device__ void verify_hit(const RunArgs& a, uint32_t tile, uint32_t s, int32_t 
   }
 }
 
-// Thread per hit: the flattened tile hit slots (k_tbase), then the spilled hits.
+__device__ void verify_hit(const RunArgs& a, uint32_t tile, uint32_t s, int32_t p) {
+  const DevPatterns& P = a.pats;
+  const SegDesc sd = a.segs[s];
+  const int64_t rel_lo = (int64_t)(tile - sd.tile0) * kTile;
+  const uint32_t g = (gword(a.bytes + sd.base + rel_lo + p) | P.qf_fold) & P.qf_mask;
+  const uint32_t b = qf_word(qf_hash(g, P.qf_w24, P.qf_k));
+  verify_hit_from(a, tile, s, sd, p, P.qf_head[b], P.qf_head[b + 1]);
+}
+
+// Thread per hit: the flattened tile hit slots (k_tindex), then the spilled hits.  The
+// chain of dependent loads before a hit's bucket walk (slot -> offset, stream ->
+// descriptor -> gram -> bucket) runs for kVerifyBatch hits at once: the kernel is bound
+// by that latency (most hits are prefilter false positives that end at the bucket).
+constexpr int kVerifyBatch = 4;
 __global__ __launch_bounds__(256) void k_verify(RunArgs a) {
   if (a.counters[2] || a.counters[kCtrHitsOver]) return;
   const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x, stride = gridDim.x * blockDim.x;
   const uint32_t nf = a.counters[kCtrFlatHits];
-  for (uint32_t i = gid; i < nf; i += stride) {
-    const uint32_t slot = a.hflat[i];
-    const uint32_t tile = slot / kHitSlots;
-    verify_hit(a, tile, a.tile_seg[tile], a.hslots[slot]);
+  const DevPatterns& P = a.pats;
+  for (uint32_t i0 = gid; i0 < nf; i0 += kVerifyBatch * stride) {
+    uint32_t tile[kVerifyBatch], sg[kVerifyBatch], e0[kVerifyBatch], e1[kVerifyBatch];
+    int32_t pp[kVerifyBatch];
+    SegDesc sd[kVerifyBatch];
+#pragma unroll
+    for (int u = 0; u < kVerifyBatch; ++u) {
+      const uint32_t i = i0 + (uint32_t)u * stride;
+      const uint32_t slot = a.hflat[i < nf ? i : i0];
+      tile[u] = slot / kHitSlots;
+      pp[u] = a.hslots[slot];
+      sg[u] = a.tile_seg[tile[u]];
+    }
+#pragma unroll
+    for (int u = 0; u < kVerifyBatch; ++u) sd[u] = a.segs[sg[u]];
+    uint32_t gg[kVerifyBatch];
+#pragma unroll
+    for (int u = 0; u < kVerifyBatch; ++u) {
+      const int64_t rel_lo = (int64_t)(tile[u] - sd[u].tile0) * kTile;
+      gg[u] = gword(a.bytes + sd[u].base + rel_lo + pp[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < kVerifyBatch; ++u) {
+      const uint32_t b = qf_word(qf_hash((gg[u] | P.qf_fold) & P.qf_mask, P.qf_w24, P.qf_k));
+      e0[u] = P.qf_head[b];
+      e1[u] = P.qf_head[b + 1];
+    }
+#pragma unroll
+    for (int u = 0; u < kVerifyBatch; ++u)
+      if (i0 + (uint32_t)u * stride < nf) {
+#if KLF_ABL & 16
+        if (pp[u] == 0x7FFF) atomicOr(&a.counters[13], sg[u]);  // timing build: no verification work
+        continue;
+#endif
+        verify_hit_from(a, tile[u], sg[u], sd[u], pp[u], e0[u], e1[u]);
+      }
   }
   const uint32_t nh = a.counters[kCtrHits] < a.qhits_cap ? a.counters[kCtrHits] : a.qhits_cap;
   for (uint32_t i = gid; i < nh; i += stride) {
@@ -2785,18 +2884,14 @@ hipError_t launch_pipeline(const RunArgs& a, hipStream_t st, hipEvent_t* ev, int
     else
       KLF_TRY((launch_scan<kScanPlain, 1>(a, st, num_cus)));
     KLF_TRY(hipEventRecord(ev[6], st));  // k_scan alone (the roofline kernel)
-    hipLaunchKernelGGL(k_fixup, dim3(num_cus * 2), dim3(256), 0, st, a);
-    KLF_TRY(hipGetLastError());
     if (a.ntiles <= kScanSmallTiles) {
-      const uint32_t nb = (a.ntiles + 1023) / 1024;
-      hipLaunchKernelGGL(k_tsum<4>, dim3(nb), dim3(256), 0, st, a);
+      hipLaunchKernelGGL((k_tindex<4, 0>), dim3((a.ntiles + 1023) / 1024), dim3(256), 0, st, a);
       KLF_TRY(hipGetLastError());
-      hipLaunchKernelGGL(k_tbase<4>, dim3(nb), dim3(256), 0, st, a);
+      hipLaunchKernelGGL((k_tindex<4, 1>), dim3((a.ntiles + 1023) / 1024), dim3(256), 0, st, a);
     } else {
-      const uint32_t nb = (a.ntiles + 4095) / 4096;
-      hipLaunchKernelGGL(k_tsum<16>, dim3(nb), dim3(256), 0, st, a);
+      hipLaunchKernelGGL((k_tindex<16, 0>), dim3((a.ntiles + 4095) / 4096), dim3(256), 0, st, a);
       KLF_TRY(hipGetLastError());
-      hipLaunchKernelGGL(k_tbase<16>, dim3(nb), dim3(256), 0, st, a);
+      hipLaunchKernelGGL((k_tindex<16, 1>), dim3((a.ntiles + 4095) / 4096), dim3(256), 0, st, a);
     }
     KLF_TRY(hipGetLastError());
     uint32_t sg = ((a.ntiles + kScatterGroup - 1) / kScatterGroup + 3) / 4;

@@ -29,6 +29,7 @@ constexpr int kSlotStride = (kSlots + 3) & ~3;  // u32 slots of a tile's LDS lin
 // inside a line is a partial-line write, read-modify-written by HBM3E: measured at ~0.3 ms
 // per 4 M tiles).  k_tsum copies the TileStats into the compact `tstat` array.
 constexpr int kRecHead = 4;
+constexpr uint32_t kScanGroup = 8;  // consecutive tiles per wave turn: 8 TileStats = one 128-B line of tstat
 constexpr int kRecStride = (kRecHead + kSlots + 31) & ~31;  // u32 words (1,152 B)
 
 // q-gram prefilter of general pattern sets (klf_patterns.hpp CompiledSet::qf_*)
@@ -55,7 +56,6 @@ constexpr uint64_t kCopyChunk = KLF_COPY_CHUNK_KB * 1024;  // output bytes per k
 constexpr uint32_t kCopyChunkMinLog2 = 12;
 constexpr uint32_t kCopyChunksTarget = 2048;
 constexpr uint32_t kCtrChunkLog2 = 16;               // counters[16]: log2 of this run's copy chunk
-constexpr uint32_t kCtrTicket = 17;                  // counters[17]: k_tindex block tickets
 constexpr uint32_t kCtrTailDone = 18;                // counters[18]: k_tailw blocks done
 constexpr uint32_t kCtrVerified = 10;                // counters[10]: hits k_verify walked (diagnostics)
 constexpr uint32_t kCtrDense = 14;                   // counters[14]: dense compaction (k_tkeep / k_tcopy)
