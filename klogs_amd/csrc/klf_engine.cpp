@@ -114,6 +114,8 @@ struct klf_engine {
   std::deque<Inflight> inflight;       // pinned chunks whose H2D may still be running
   std::vector<hipEvent_t> ev_pool;
   hipStream_t copy_stream = nullptr;   // early H2D of full chunks
+  hipStream_t aux_stream = nullptr;    // side stream of the pipeline (k_scatter beside k_verify)
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   hipEvent_t copy_done = nullptr;
   bool ran = false;                    // klf_run since the last klf_reset (stage -> ESTATE)
   std::unique_ptr<klf::CopyPool> copier;
@@ -244,6 +246,12 @@ extern "C" int klf_open(const klf_config* cfg, klf_engine** out) {
       (h = hipEventCreateWithFlags(&e->copy_done, hipEventDisableTiming)) != hipSuccess) {
     *out = e;
     return hip_err(e, h, "copy stream");
+  }
+  if ((h = hipStreamCreateWithFlags(&e->aux_stream, hipStreamNonBlocking)) != hipSuccess ||
+      (h = hipEventCreateWithFlags(&e->ev_fork, hipEventDisableTiming)) != hipSuccess ||
+      (h = hipEventCreateWithFlags(&e->ev_join, hipEventDisableTiming)) != hipSuccess) {
+    *out = e;
+    return hip_err(e, h, "side stream");
   }
   {
     int nw = 3;  // staging copy workers (+ the calling thread)
@@ -378,6 +386,10 @@ extern "C" void klf_close(klf_engine* e) {
     if (x) (void)hipEventDestroy(x);
   if (e->copy_done) (void)hipEventDestroy(e->copy_done);
   if (e->copy_stream) (void)hipStreamDestroy(e->copy_stream);
+  if (e->aux_stream) (void)hipStreamSynchronize(e->aux_stream);
+  if (e->ev_fork) (void)hipEventDestroy(e->ev_fork);
+  if (e->ev_join) (void)hipEventDestroy(e->ev_join);
+  if (e->aux_stream) (void)hipStreamDestroy(e->aux_stream);
   if (e->own_stream && e->stream) (void)hipStreamDestroy(e->stream);
   delete e;
 }
@@ -754,7 +766,7 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
     a.pcount = count ? e->d_pcount.as<uint32_t>() : nullptr;
     a.pairs = count ? e->d_pairs.as<uint64_t>() : nullptr;
     a.pairs_log2 = e->pairs_log2;
-    HIPCHK(e, klf::launch_pipeline(a, st, e->ev, e->num_cus), "launch");
+    HIPCHK(e, klf::launch_pipeline(a, st, e->ev, e->num_cus, e->aux_stream, e->ev_fork, e->ev_join), "launch");
     r->so.resize(nsegs);
     uint32_t counters[16];
     HIPCHK(e, e->h_rb.ensure(sizeof(counters) + nsegs * sizeof(SegOut)), "alloc readback");

@@ -649,12 +649,45 @@ __global__ __launch_bounds__(kThreads, MODE == kScanGen ? 3 : KLF_SCAN_OCC) void
       // fast pass: one OR-accumulated bit per chunk (no positions); most tiles stop here
       uint32_t chit = 0;
       const uint32_t rot = ((uint32_t)lane >> 1) & 7u;
+      if (QS == 4) {
+        // stride 4: a chunk's samples are its four dwords.  Two chunks per step, their
+        // eight bitmap reads issued before the first test (one LDS round trip per step,
+        // not one per probe)
 #pragma unroll
-      for (int v = 0; v < (ABL(4) ? 0 : 8); ++v) {
-        const uint32_t c = ((uint32_t)v + rot) & 7u;
-        uint32_t acc = 0;
-        chunk_grams(c, [&](uint32_t g, int) __attribute__((always_inline)) { acc |= hbits(g); });
-        chit |= (acc & 1u) << c;
+        for (int v = 0; v < (ABL(4) ? 0 : 8); v += 2) {
+          const uint32_t ca = ((uint32_t)v + rot) & 7u, cb = ((uint32_t)v + 1u + rot) & 7u;
+          const uint4 xa = *reinterpret_cast<const uint4*>(s_tile + my0 + 16u * ca);
+          const uint4 xb = *reinterpret_cast<const uint4*>(s_tile + my0 + 16u * cb);
+          const uint32_t g[8] = {xa.x, xa.y, xa.z, xa.w, xb.x, xb.y, xb.z, xb.w};
+          uint32_t h[8], w[8];
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            const uint32_t gf = g[k] | fold;
+            const uint32_t f = QK == 3 ? gf ^ __builtin_amdgcn_ubfe(gf, 13, 11) : gf;
+            h[k] = __umul24(f, 0x9E3779u) + __umul24(__builtin_amdgcn_ubfe(gf, 8, w24), 0x7F4A7Du);
+          }
+#pragma unroll
+          for (int k = 0; k < 8; ++k) w[k] = s_qf[h[k] >> (32 - kQfBucketBits)];
+          uint32_t acc_a = 0, acc_b = 0;
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            uint32_t t = (w[k] >> ((h[k] >> 15) & 31u)) & (w[k] >> ((h[k] >> 10) & 31u));
+            if (QK == 3) {
+              const uint32_t gf = g[k] | fold, f = gf ^ __builtin_amdgcn_ubfe(gf, 13, 11);
+              t &= w[k] >> ((uint32_t)(((uint64_t)(f & 0xFFFFFFu) * 0xC2B2AEu) >> 32) & 31u);
+            }
+            if (k < 4) acc_a |= t; else acc_b |= t;
+          }
+          chit |= ((acc_a & 1u) << ca) | ((acc_b & 1u) << cb);
+        }
+      } else {
+#pragma unroll
+        for (int v = 0; v < (ABL(4) ? 0 : 8); ++v) {
+          const uint32_t c = ((uint32_t)v + rot) & 7u;
+          uint32_t acc = 0;
+          chunk_grams(c, [&](uint32_t g, int) __attribute__((always_inline)) { acc |= hbits(g); });
+          chit |= (acc & 1u) << c;
+        }
       }
       // chunks with a possible hit: the sample positions (past the tile's end clipped)
       uint32_t hq0 = 0, hq1 = 0, hq2 = 0, hq3 = 0;
@@ -1240,19 +1273,33 @@ __device__ void verify_hit_from(const RunArgs& a, uint32_t tile, uint32_t s, con
       if ((int32_t)(list[mid] & kSlotOff) <= x) lo = mid + 1; else hi = mid;
     }
     const uint64_t l = a.tile_base[tile] + (lo > 0 ? k0 + (uint32_t)lo - 1 : 0);
-    uint16_t mt;
-    uint64_t ls;
+    // the line's meta and start from its slot: the tile's own, or for the line carried in
+    // from an earlier tile the last one listed by the nearest earlier tile that lists one
+    // (k_scatter may still be running: the global line index is not read here)
+    uint32_t v = 0;
+    int64_t vrel = rel_lo;
     if (lo > 0) {
-      const uint32_t v = list[lo - 1];
-      mt = (uint16_t)(v >> 16);
-      ls = (uint64_t)rel_lo + (v & kSlotOff);
+      v = list[lo - 1];
     } else {
-      mt = a.meta[l];
-      ls = a.line_off[l + s];
+      for (uint32_t pt = tile; pt > sd.tile0;) {  // the stream's first tile lists line 0
+        --pt;
+        const TileStat pst = a.tstat[pt];
+        const int64_t prel = (int64_t)(pt - sd.tile0) * kTile;
+        const uint32_t pk0 = prel == 0 ? 0u : 1u;
+        const uint32_t pn = pst.events + 1 - pk0;  // an earlier tile is never the stream's last
+        if (pn == 0) continue;
+        const uint32_t* psrc = (pst.flags & 1u) ? a.pool + pst.pool_base : a.slots + (size_t)pt * kRecStride + kRecHead;
+        v = psrc[pn - 1];
+        vrel = prel;
+        break;
+      }
     }
+    const uint16_t mt = (uint16_t)(v >> 16);
+    const uint64_t ls = (uint64_t)vrel + (v & kSlotOff);
     if (!(mt & Meta::kParsed)) continue;
     if (!(E.y & kQfRegex)) {  // literal: a match when it starts inside the content
-      const uint32_t plen = (mt >> 2) == kPlenEscape ? line_plen(a, mt, segp, ls, a.line_off[l + s + 1]) : mt >> 2;
+      // (a parsed line's first space ends its prefix: the stream end bounds the search)
+      const uint32_t plen = (mt >> 2) == kPlenEscape ? line_plen(a, mt, segp, ls, sd.len) : mt >> 2;
       if ((uint64_t)(rel_lo + x) >= ls + plen) {
         atomicOr(&a.bits[l >> 5], 1u << (l & 31));
         if (a.count_pats) count_pair(a, l, s, E.z);
@@ -2852,7 +2899,8 @@ hipError_t launch_gen(const RunArgs& a, hipStream_t st, int num_cus) {
 
 static hipError_t launch_tail_stage(const RunArgs& a, hipStream_t st, hipEvent_t* ev, int num_cus);
 
-hipError_t launch_pipeline(const RunArgs& a, hipStream_t st, hipEvent_t* ev, int num_cus) {
+hipError_t launch_pipeline(const RunArgs& a, hipStream_t st, hipEvent_t* ev, int num_cus, hipStream_t aux,
+                           hipEvent_t ev_fork, hipEvent_t ev_join) {
   hipError_t e;
 #define KLF_TRY(x) do { e = (x); if (e != hipSuccess) return e; } while (0)
   KLF_TRY(hipEventRecord(ev[0], st));
@@ -2894,15 +2942,33 @@ hipError_t launch_pipeline(const RunArgs& a, hipStream_t st, hipEvent_t* ev, int
       hipLaunchKernelGGL((k_tindex<16, 1>), dim3((a.ntiles + 4095) / 4096), dim3(256), 0, st, a);
     }
     KLF_TRY(hipGetLastError());
-    uint32_t sg = ((a.ntiles + kScatterGroup - 1) / kScatterGroup + 3) / 4;
-    if (sg > (uint32_t)num_cus * 8) sg = num_cus * 8;
-    hipLaunchKernelGGL(k_scatter, dim3(sg), dim3(256), 0, st, a);
+    KLF_TRY(hipGetLastError());
   }
-  KLF_TRY(hipGetLastError());
-  if (a.stage_times) KLF_TRY(hipEventRecord(ev[2], st));  // ~5 us of idle GPU each
+  uint32_t sg = ((a.ntiles + kScatterGroup - 1) / kScatterGroup + 3) / 4;
+  if (sg > (uint32_t)num_cus * 8) sg = num_cus * 8;
+  // With a prefiltered regex set, k_scatter (bandwidth-bound) runs on the side stream
+  // beside k_verify (latency-bound: a chain of dependent loads per hit), which reads the
+  // line slots, not the global line index; the main stream waits for it before the first
+  // kernel that reads the index.  Measured: C5 (64 regexes) -0.10 ms per step; a literal
+  // set's heavier verification (C4: 1,024 literals) contends with it instead (+0.08 ms),
+  // so literal-only sets keep the serial order.
+  const bool fork = a.grep_mode == kGrepGeneral && a.pats.qf_on && a.pats.rx_count && aux != nullptr;
+  if (fork) {
+    KLF_TRY(hipEventRecord(ev_fork, st));
+    KLF_TRY(hipStreamWaitEvent(aux, ev_fork, 0));
+    hipLaunchKernelGGL(k_scatter, dim3(sg), dim3(256), 0, aux, a);
+    KLF_TRY(hipGetLastError());
+    KLF_TRY(hipEventRecord(ev_join, aux));
+  } else {
+    hipLaunchKernelGGL(k_scatter, dim3(sg), dim3(256), 0, st, a);
+    KLF_TRY(hipGetLastError());
+  }
+  if (a.stage_times && !fork) KLF_TRY(hipEventRecord(ev[2], st));  // ~5 us of idle GPU each
   if (a.grep_mode == kGrepGeneral && a.pats.qf_on) {
     hipLaunchKernelGGL(k_verify, dim3(num_cus * 8), dim3(256), 0, st, a);
     KLF_TRY(hipGetLastError());
+    if (fork) KLF_TRY(hipStreamWaitEvent(st, ev_join, 0));
+    if (a.stage_times) KLF_TRY(hipEventRecord(ev[2], st));
     if (a.count_pats) {
       hipLaunchKernelGGL(k_fixcount, dim3(num_cus * 2), dim3(256), 0, st, a);
       KLF_TRY(hipGetLastError());

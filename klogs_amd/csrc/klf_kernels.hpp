@@ -259,7 +259,9 @@ struct RunArgs {
 // per-kernel timing: ev[0] start, ev[1] after the workspace memsets, ev[2] after the
 // scan, ev[3] after the general matcher, ev[4] after counts+tail+window prefix, ev[5]
 // after compaction.  Returns a hipError_t.
-hipError_t launch_pipeline(const RunArgs& a, hipStream_t stream, hipEvent_t* ev, int num_cus);
+// aux (may be null) with the fork / join events: a side stream for k_scatter beside k_verify.
+hipError_t launch_pipeline(const RunArgs& a, hipStream_t stream, hipEvent_t* ev, int num_cus, hipStream_t aux,
+                           hipEvent_t ev_fork, hipEvent_t ev_join);
 // Re-runs matched counts, tail and compaction of the last pipeline with a.tail changed.
 hipError_t launch_retail(const RunArgs& a, hipStream_t stream, hipEvent_t* ev, int num_cus);
 // Gram sketch (kQfHistBins u32 bins, zeroed here) of the first `sample` bytes of each
