@@ -361,6 +361,7 @@ extern "C" void klf_close(klf_engine* e) {
   if (!e) return;
   if (e->stream) (void)hipStreamSynchronize(e->stream);
   if (e->copy_stream) (void)hipStreamSynchronize(e->copy_stream);
+  if (e->aux_stream) (void)hipStreamSynchronize(e->aux_stream);
   for (DevBuf* b : {&e->d_lit, &e->d_ac_class, &e->d_ac_next, &e->d_ac_accept, &e->d_rx_class, &e->d_rx_b,
                     &e->d_rx_follow, &e->d_rx_vec, &e->d_rx_flags, &e->d_rx_pre, &e->d_qf_bitmap, &e->d_qf_head,
                     &e->d_qf_ent, &e->d_qf_nbytes, &e->d_rx_vec4, &e->d_qhits, &e->d_hslots, &e->d_hist, &e->d_hflat, &e->d_cand, &e->d_batch, &e->d_segs, &e->d_tstat,
@@ -392,6 +393,7 @@ extern "C" void klf_close(klf_engine* e) {
   if (e->aux_stream) (void)hipStreamDestroy(e->aux_stream);
   if (e->own_stream && e->stream) (void)hipStreamDestroy(e->stream);
   delete e;
+  (void)hipGetLastError();  // nothing above reports: leave no sticky error for the next engine
 }
 
 // ------------------------------------------------------------------------ staging ---
@@ -573,6 +575,17 @@ extern "C" int klf_layout(uint32_t n, const uint64_t* lens, uint64_t* seg_base, 
 
 // -------------------------------------------------------------------------- run ---
 
+// Waits for the run's readback by polling the stream: a blocking sync sleeps and wakes
+// tens of microseconds after the last copy lands (measured ~50 us between batches of a
+// capture loop), a poll returns within a microsecond or two; the calling thread has
+// nothing else to do until the results are in.
+static hipError_t wait_stream(hipStream_t st) {
+  for (;;) {
+    const hipError_t h = hipStreamQuery(st);
+    if (h != hipErrorNotReady) return h;
+  }
+}
+
 static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_streams, const uint64_t* seg_base,
                            const uint64_t* lens, const klf_filter* f, klf_result** out) {
   if (!e || !f || !out || (n_streams && (!seg_base || !lens))) return KLF_EINVAL;
@@ -705,7 +718,8 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
     HIPCHK(e, e->d_cseg.ensure((max_cblocks + 1) * 4), "alloc cseg");
     HIPCHK(e, e->d_mpart.ensure((cap / klf::kMatchChunk + 2) * 8), "alloc mpart");
     HIPCHK(e, e->d_pool.ensure(e->pool_cap * 4), "alloc pool");
-    klf::RunArgs a{};
+    klf::RunArgs a;
+    memset(static_cast<void*>(&a), 0, sizeof(a));
     a.bytes = d_bytes;
     a.segs = e->d_segs.as<SegDesc>();
     a.nsegs = nsegs;
@@ -729,7 +743,7 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
     a.lit_anchor = e->cs.literal_anchor;
     a.lit_anchor_byte = e->cs.literal.empty() ? 0u : e->cs.literal[e->cs.literal_anchor];
     a.lit_words = e->d_lit.as<uint32_t>();
-    a.pats = e->dpats;
+    memcpy(static_cast<void*>(&a.pats), &e->dpats, sizeof(a.pats));
     a.tstat = e->d_tstat.as<klf::TileStat>();
     a.slots = e->d_slots.as<uint32_t>();
     a.pool = e->d_pool.as<uint32_t>();
@@ -774,7 +788,7 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
     HIPCHK(e, hipMemcpyAsync(rb, e->d_counters.p, sizeof(counters), hipMemcpyDeviceToHost, st), "D2H counters");
     HIPCHK(e, hipMemcpyAsync(rb + sizeof(counters), e->d_segout.p, nsegs * sizeof(SegOut), hipMemcpyDeviceToHost, st),
            "D2H segout");
-    HIPCHK(e, hipStreamSynchronize(st), "sync");
+    HIPCHK(e, wait_stream(st), "sync");
     memcpy(counters, rb, sizeof(counters));
     memcpy(r->so.data(), rb + sizeof(counters), nsegs * sizeof(SegOut));
     e->last_segs = segs;
@@ -825,8 +839,12 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
     for (int k = 0; k < 4; ++k)  // scan stage, match, tail stage, compaction
       if (hipEventElapsedTime(&ms, e->ev[k + 1], e->ev[k + 2]) == hipSuccess) r->ms[k] = ms;
   if (hipEventElapsedTime(&ms, e->ev[0], e->ev[5]) == hipSuccess) r->ms[4] = ms;
-  if (hipEventElapsedTime(&ms, e->ev[0], e->ev[1]) == hipSuccess) r->ms[5] = ms;
-  if (hipEventElapsedTime(&ms, e->ev[1], e->ev[6]) == hipSuccess) r->ms[6] = ms;
+  if (f->flags & KLF_FILTER_STAGE_TIMES) {
+    if (hipEventElapsedTime(&ms, e->ev[0], e->ev[1]) == hipSuccess) r->ms[5] = ms;
+    if (hipEventElapsedTime(&ms, e->ev[1], e->ev[6]) == hipSuccess) r->ms[6] = ms;
+  } else if (hipEventElapsedTime(&ms, e->ev[0], e->ev[6]) == hipSuccess) {
+    r->ms[6] = ms;  // the scan with the run's k_init (~2 us) in front of it
+  }
   r->total_lines = r->so[nsegs - 1].line_hi;
   for (auto& s : r->so) r->total_out = std::max(r->total_out, s.out_hi);
   *out = rp.release();

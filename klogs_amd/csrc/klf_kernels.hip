@@ -2917,7 +2917,9 @@ hipError_t launch_pipeline(const RunArgs& a, hipStream_t st, hipEvent_t* ev, int
                        a.tile_seg);
     KLF_TRY(hipGetLastError());
   }
-  KLF_TRY(hipEventRecord(ev[1], st));
+  // ev[1] only with stage times: each event record idles the GPU for a few us, and the
+  // scan's own time is then taken from ev[0] (k_init in front of it: ~2 us)
+  if (a.stage_times) KLF_TRY(hipEventRecord(ev[1], st));
   {
     if (a.grep_mode == kGrepLit1)
       KLF_TRY((launch_scan<kScanLit, 1>(a, st, num_cus)));
@@ -2968,7 +2970,7 @@ hipError_t launch_pipeline(const RunArgs& a, hipStream_t st, hipEvent_t* ev, int
     hipLaunchKernelGGL(k_verify, dim3(num_cus * 8), dim3(256), 0, st, a);
     KLF_TRY(hipGetLastError());
     if (fork) KLF_TRY(hipStreamWaitEvent(st, ev_join, 0));
-    if (a.stage_times) KLF_TRY(hipEventRecord(ev[2], st));
+    if (a.stage_times && fork) KLF_TRY(hipEventRecord(ev[2], st));
     if (a.count_pats) {
       hipLaunchKernelGGL(k_fixcount, dim3(num_cus * 2), dim3(256), 0, st, a);
       KLF_TRY(hipGetLastError());
