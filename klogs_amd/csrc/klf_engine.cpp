@@ -637,7 +637,7 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
     HIPCHK(e, hipMemcpyAsync(e->d_segs.p, segs.data(), nsegs * sizeof(SegDesc), hipMemcpyHostToDevice, st),
            "H2D segs");
     HIPCHK(e, hipStreamSynchronize(st), "sync segs");
-    HIPCHK(e, e->d_tile_seg.ensure(ntiles * 4), "alloc tile_seg");
+    HIPCHK(e, e->d_tile_seg.ensure(ntiles * 4 + 16), "alloc tile_seg");  // + whole 16-B loads past the end
   }
   if (mode == klf::CompiledSet::kGeneral && e->cs.qf_on && !e->cs.qf_tuned) {
     // first batch: place the needles' sampling windows on the data's own gram statistics

@@ -927,13 +927,31 @@ __global__ __launch_bounds__(256) void k_tindex(RunArgs a) {
   const uint32_t tb = bid * (256u * R) + (uint32_t)t * R;  // my first tile
   TileStat ts[R];
   uint32_t sg[R];
+  {  // whole 16-B loads through buffer descriptors (tiles past the end read as zero): plain
+     // loads get narrowed to the fields used, four instructions per record that each touch
+     // 64 scattered lines
+    const __amdgpu_buffer_rsrc_t rt = __builtin_amdgcn_make_buffer_rsrc(a.tstat, 0, (int)(a.ntiles * 16u), 0x00020000);
+    // (tile_seg has room for whole 16-B groups past its end; entries there are never used)
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc(a.tile_seg, 0, (int)(((a.ntiles + 3u) & ~3u) * 4u), 0x00020000);
+    typedef uint32_t u32x4t __attribute__((ext_vector_type(4)));
 #pragma unroll
-  for (int r = 0; r < R; ++r) {
-    ts[r] = TileStat{};
-    sg[r] = 0;
-    if (tb + r < a.ntiles) {
-      ts[r] = a.tstat[tb + r];
-      sg[r] = a.tile_seg[tb + r];
+    for (int r = 0; r < R; ++r) {
+      const u32x4t q = __builtin_amdgcn_raw_buffer_load_b128(rt, (tb + r) * 16u, 0, 0);
+      ts[r].events = q.x;
+      ts[r].pool_base = q.y;
+      ts[r].parsed = (uint16_t)q.z;
+      ts[r].since_ok = (uint16_t)(q.z >> 16);
+      ts[r].flags = (uint16_t)q.w;
+      ts[r].carry_off = (uint16_t)(q.w >> 16);
+    }
+#pragma unroll
+    for (int r = 0; r < R; r += 4) {
+      const u32x4t q = __builtin_amdgcn_raw_buffer_load_b128(rs, (tb + r) * 4u, 0, 0);
+      sg[r] = q.x;
+      sg[r + 1] = q.y;
+      sg[r + 2] = q.z;
+      sg[r + 3] = q.w;
     }
   }
   // deferred lines (non-canonical timestamp prefixes; rare): per round every thread hands
