@@ -726,6 +726,8 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
     a.ntiles = (uint32_t)ntiles;
     a.tile_seg = e->d_tile_seg.as<uint32_t>();
     a.build_tiles = (!same_layout && attempt == 0) ? 1u : 0u;
+    // tests: KLF_DEBUG_TINDEX_WIDE=1 runs the large-batch tile index on any batch
+    a.tindex_wide = (ntiles > klf::kScanSmallTiles || getenv("KLF_DEBUG_TINDEX_WIDE")) ? 1u : 0u;
     a.since_sec = f->since.sec;
     a.since_nsec = f->since.nsec;
     {

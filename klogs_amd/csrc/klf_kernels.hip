@@ -2952,7 +2952,7 @@ hipError_t launch_pipeline(const RunArgs& a, hipStream_t st, hipEvent_t* ev, int
     else
       KLF_TRY((launch_scan<kScanPlain, 1>(a, st, num_cus)));
     KLF_TRY(hipEventRecord(ev[6], st));  // k_scan alone (the roofline kernel)
-    if (a.ntiles <= kScanSmallTiles) {
+    if (!a.tindex_wide) {
       hipLaunchKernelGGL((k_tindex<4, 0>), dim3((a.ntiles + 1023) / 1024), dim3(256), 0, st, a);
       KLF_TRY(hipGetLastError());
       hipLaunchKernelGGL((k_tindex<4, 1>), dim3((a.ntiles + 1023) / 1024), dim3(256), 0, st, a);

@@ -196,6 +196,7 @@ struct RunArgs {
   uint32_t ntiles;
   uint32_t* tile_seg;   // [ntiles] tile -> segment (filled by k_tiles when build_tiles)
   uint32_t build_tiles;
+  uint32_t tindex_wide;  // k_tindex with 4,096 tiles per block (batches above kScanSmallTiles; tests force it)
   // filter
   int64_t since_sec;
   int32_t since_nsec;
