@@ -24,7 +24,7 @@ if [ "$what" != pmc ]; then
 fi
 if [ "$what" != trace ]; then
   for c in c2 c3 c4 c5; do
-    bash scripts/pmc.sh "$out/pmc_$c" "$c" "k_scan|k_tcopy|k_tkeep|k_scatter|k_verify|k_nfa"
+    bash scripts/pmc.sh "$out/pmc_$c" "$c" "k_scan|k_tcopy|k_cplan|k_cmove|k_tindex|k_scatter|k_verify|k_nfa"
   done
 fi
 echo "profile_round done: $out"
