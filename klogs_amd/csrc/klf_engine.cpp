@@ -710,7 +710,7 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
     HIPCHK(e, e->d_meta.ensure(cap * 2 + 16), "alloc meta");
     HIPCHK(e, e->d_bits.ensure((cap / 32 + 1) * 4), "alloc bits");
     HIPCHK(e, e->d_cstatus.ensure((max_cblocks + 1) * 3 * 8), "alloc cstatus");
-    // >= sum over blocks of ceil(bytes / chunk) (>= 1 each): k_cscan's chunk keeps the
+    // >= sum over blocks of ceil(bytes / chunk) (>= 1 each): the block prefix's chunk keeps the
     // output within kCopyChunksTarget chunks unless it is the largest, kCopyChunk
     const uint64_t cmap_cap =
         max_cblocks + std::max<uint64_t>(total_bytes / klf::kCopyChunk, klf::kCopyChunksTarget) + 2;
