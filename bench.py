@@ -47,7 +47,7 @@ TAIL = 100
 
 def pmc_traffic():
     """Per-launch HBM bytes of k_scan<literal> from the newest committed rocprofv3 --pmc
-    summary (profiles/<round>/traffic.json, written by scripts/pmc_traffic.py from
+    summary (profiles/<round>/traffic.json, written by scripts/collect_profiles.py from
     FETCH_SIZE / WRITE_SIZE passes over this same command), or None."""
     files = sorted(ROOT.glob("profiles/r*/traffic.json"))
     if not files:
