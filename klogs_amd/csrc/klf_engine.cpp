@@ -8,6 +8,7 @@
 #include <algorithm>
 #include <atomic>
 #include <cerrno>
+#include <chrono>
 #include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
@@ -491,7 +492,11 @@ static int ship_chunk(klf_engine* e, klf_engine::StagedStream* s) {
   }
   hipError_t h = hipSuccess;
   if (!d) h = hipMalloc(reinterpret_cast<void**>(&d), kStageChunk);
-  if (h != hipSuccess) return hip_err(e, h, "device staging chunk");
+  if (h != hipSuccess) {  // hand the event back; the error string is shared with other stagers
+    std::lock_guard<std::mutex> g(e->mu);
+    if (ev) e->ev_pool.push_back(ev);
+    return hip_err(e, h, "device staging chunk");
+  }
   if (!ev) h = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
   if (h == hipSuccess) h = hipMemcpyAsync(d, s->cur.p, kStageChunk, hipMemcpyHostToDevice, e->copy_stream);
   if (h == hipSuccess) h = hipEventRecord(ev, e->copy_stream);
@@ -521,7 +526,10 @@ extern "C" int klf_stage(klf_engine* e, uint32_t id, const uint8_t* p, size_t n)
     dst = e->staged[id].get();  // stable: the table holds pointers, only the table moves
   }
   while (n) {
-    if (!dst->cur.p && !take_chunk(e, &dst->cur)) return set_err(e, KLF_ENOMEM, "pinned staging chunk");
+    if (!dst->cur.p && !take_chunk(e, &dst->cur)) {
+      std::lock_guard<std::mutex> g(e->mu);
+      return set_err(e, KLF_ENOMEM, "pinned staging chunk");
+    }
     const size_t k = std::min(n, kStageChunk - dst->cur.used);
     e->copier->copy(dst->cur.p + dst->cur.used, p, k);
     dst->cur.used += k;
@@ -577,12 +585,25 @@ extern "C" int klf_layout(uint32_t n, const uint64_t* lens, uint64_t* seg_base, 
 
 // Waits for the run's readback by polling the stream: a blocking sync sleeps and wakes
 // tens of microseconds after the last copy lands (measured ~50 us between batches of a
-// capture loop), a poll returns within a microsecond or two; the calling thread has
-// nothing else to do until the results are in.
-static hipError_t wait_stream(hipStream_t st) {
-  for (;;) {
+// capture loop), a poll returns within a microsecond or two.  The poll is bounded: past
+// the expected run time (`spin_us`, the batch's bytes at ~2 TB/s plus a margin) the
+// thread yields between polls for a while and then blocks, so one engine per GPU in one
+// process does not keep a host core busy per GPU through a long run, and a hung kernel
+// leaves the thread asleep in the runtime instead of spinning.
+static hipError_t wait_stream(hipStream_t st, uint64_t spin_us) {
+  const auto t0 = std::chrono::steady_clock::now();
+  for (uint32_t i = 0;; ++i) {
     const hipError_t h = hipStreamQuery(st);
     if (h != hipErrorNotReady) return h;
+    if ((i & 63) == 63) {
+      const uint64_t us = (uint64_t)std::chrono::duration_cast<std::chrono::microseconds>(
+                              std::chrono::steady_clock::now() - t0).count();
+      if (us > spin_us + 20000) return hipStreamSynchronize(st);
+      if (us > spin_us) std::this_thread::yield();
+    }
+#if defined(__x86_64__)
+    __builtin_ia32_pause();
+#endif
   }
 }
 
@@ -601,7 +622,10 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
   r->gen = ++e->gen;
   r->n_streams = n_streams;
   r->seg_of.assign(n_streams, -1);
-  const auto mode = e->cs.mode;
+  auto mode = e->cs.mode;
+  // a set with an always-pattern (also_all) filters as kAll; its other patterns are
+  // evaluated only when the run counts per pattern
+  if (e->cs.also_all && !(f->flags & KLF_FILTER_PATTERN_COUNTS)) mode = klf::CompiledSet::kAll;
   r->has_bits = mode != klf::CompiledSet::kNone;
 
   std::vector<SegDesc> segs;
@@ -623,7 +647,11 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
   }
   if (ntiles >= (1ull << 32)) return set_err(e, KLF_EINVAL, "batch too large");
   const uint32_t nsegs = (uint32_t)segs.size();
+  // asked-for per-pattern counts are reported even when every stream is empty (all zero)
+  r->counted = (f->flags & KLF_FILTER_PATTERN_COUNTS) != 0;
+  r->pcount_ok = true;  // no segment reads pcount
   if (nsegs == 0) { e->last_gen = r->gen; *out = rp.release(); return KLF_OK; }
+  r->pcount_ok = false;
   // tests: a line capacity clamped on every attempt forces the overflow error below
   uint64_t cap_clamp = ~0ull;
   if (const char* v = getenv("KLF_DEBUG_CAP_CLAMP")) cap_clamp = std::max(1L, atol(v));
@@ -740,6 +768,7 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
     }
     a.tail = f->tail;
     a.grep_mode = (uint32_t)mode;
+    a.match_all = e->cs.also_all ? 1u : 0u;
     a.lit = e->d_lit.as<uint8_t>();
     a.lit_len = (uint32_t)e->cs.literal.size();
     a.lit_anchor = e->cs.literal_anchor;
@@ -790,7 +819,7 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
     HIPCHK(e, hipMemcpyAsync(rb, e->d_counters.p, sizeof(counters), hipMemcpyDeviceToHost, st), "D2H counters");
     HIPCHK(e, hipMemcpyAsync(rb + sizeof(counters), e->d_segout.p, nsegs * sizeof(SegOut), hipMemcpyDeviceToHost, st),
            "D2H segout");
-    HIPCHK(e, wait_stream(st), "sync");
+    HIPCHK(e, wait_stream(st, 1000 + total_bytes / 2000000), "sync");
     memcpy(counters, rb, sizeof(counters));
     memcpy(r->so.data(), rb + sizeof(counters), nsegs * sizeof(SegOut));
     e->last_segs = segs;
@@ -1190,8 +1219,6 @@ extern "C" int klf_result_pattern_counts(klf_result* r, uint32_t id, uint64_t* c
   for (uint32_t u = 0; u < std::min(cap, e->n_user); ++u) {
     const int32_t m = u < cs.user_map.size() ? cs.user_map[u] : klf::CompiledSet::kCidNever;
     uint64_t v = 0;
-    if (m == klf::CompiledSet::kCidUncounted)
-      return set_err(e, KLF_EINVAL, "per-pattern counts: not counted when another pattern matches every line");
     if (s >= 0) {
       const SegOut& so = r->so[s];
       if (m == klf::CompiledSet::kCidAlways) v = so.parsed;
@@ -1305,9 +1332,12 @@ extern "C" int klf_follow_feed(klf_follow* w, uint32_t id, const uint8_t* p, siz
     return KLF_OK;
   }
   const size_t cut = (size_t)(nl - p) + 1;
-  int rc = KLF_OK;
-  if (!c->empty()) rc = klf_stage(w->e, id, reinterpret_cast<const uint8_t*>(c->data()), c->size());
-  if (!rc) rc = klf_stage(w->e, id, p, cut);
+  if (!c->empty()) {
+    const int rc = klf_stage(w->e, id, reinterpret_cast<const uint8_t*>(c->data()), c->size());
+    if (rc) return rc;
+    c->clear();  // staged: a retried feed must not stage it again
+  }
+  const int rc = klf_stage(w->e, id, p, cut);
   if (rc) return rc;
   c->assign(reinterpret_cast<const char*>(p + cut), n - cut);
   return KLF_OK;
@@ -1370,6 +1400,7 @@ extern "C" int klf_debug_match(const klf_pattern* pats, uint32_t n, const uint8_
       hit = std::search(content, content + len, cs.literal.begin(), cs.literal.end()) != content + len;
       break;
     case klf::CompiledSet::kGeneral: {
+      hit = cs.also_all;
       if (cs.ac_states) {  // run the same DFA tables the GPU runs
         uint32_t st = 0;
         for (size_t i = 0; i < len && !hit; ++i) {

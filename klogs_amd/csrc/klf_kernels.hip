@@ -1069,10 +1069,16 @@ __global__ __launch_bounds__(256) void k_tindex(RunArgs a) {
     while (j >= s_thit[lo * R + r]) j -= s_thit[lo * R + r++];
     if (hb + k < a.hflat_cap) a.hflat[hb + k] = (t0 + lo * R + r) * kHitSlots + j;
   }
-  if (t == 0 && (bid + 1) * (256u * R) >= a.ntiles && a.hflat) {  // the last block knows the total
-    const uint64_t tot = hb + blk_h;
-    a.counters[kCtrFlatHits] = (uint32_t)(tot < 0xFFFFFFFFull ? tot : 0xFFFFFFFFull);
-    if (tot > a.hflat_cap) atomicOr(&a.counters[kCtrHitsOver], 1u);
+  if (t == 0 && (bid + 1) * (256u * R) >= a.ntiles) {  // the last block knows the totals
+    // More lines than the line index holds: raised here, before any kernel that indexes
+    // by global line (k_verify runs beside k_scatter, whose own check comes too late for
+    // it; bits / meta / line_off past cap_lines are outside their allocations).
+    if (blk_hi > a.cap_lines) atomicOr(&a.counters[2], 1u);
+    if (a.hflat) {
+      const uint64_t tot = hb + blk_h;
+      a.counters[kCtrFlatHits] = (uint32_t)(tot < 0xFFFFFFFFull ? tot : 0xFFFFFFFFull);
+      if (tot > a.hflat_cap) atomicOr(&a.counters[kCtrHitsOver], 1u);
+    }
   }
   if (a.grep_mode != kGrepNone) {  // bitmap words whose first line is in [blk_lo, blk_hi)
     const uint64_t w0 = (blk_lo + 31) / 32, w1 = (blk_hi + 31) / 32;
@@ -1291,6 +1297,10 @@ __device__ void verify_hit_from(const RunArgs& a, uint32_t tile, uint32_t s, con
       if ((int32_t)(list[mid] & kSlotOff) <= x) lo = mid + 1; else hi = mid;
     }
     const uint64_t l = a.tile_base[tile] + (lo > 0 ? k0 + (uint32_t)lo - 1 : 0);
+    if (l >= a.cap_lines) {  // (k_tindex raises the overflow first; never index past the arrays)
+      atomicOr(&a.counters[2], 1u);
+      continue;
+    }
     // the line's meta and start from its slot: the tile's own, or for the line carried in
     // from an earlier tile the last one listed by the nearest earlier tile that lists one
     // (k_scatter may still be running: the global line index is not read here)
@@ -1563,6 +1573,7 @@ __global__ __launch_bounds__(256) void k_fixcount(RunArgs a) {
       const uint32_t sl = list[j];
       if (!(sl & kSlotDefer) || !(sl & kSlotHit)) continue;  // only deferred lines that matched
       const uint64_t l = a.tile_base[tile] + k0 + j;
+      if (l >= a.cap_lines) continue;  // overflowing run (counters[2]): rerun with the exact size
       const uint16_t m = a.meta[l];
       const uint64_t ls = a.line_off[l + s], le = a.line_off[l + s + 1];
       const uint64_t cs = ls + line_plen(a, m, segp, ls, le);
@@ -1650,16 +1661,20 @@ __global__ __launch_bounds__(256) void k_nfa_win(RunArgs a) {
   }
 }
 
+// Per line: kGrepAll marks every parsed line; general sets are evaluated here when the
+// prefilter is off or its lists overflowed, and with match_all (an always-pattern in the
+// set, run with per-pattern counts) every parsed line is marked after the matchers.
 __global__ __launch_bounds__(256) void k_match(RunArgs a) {
   if (a.counters[2]) return;
-  if (a.grep_mode == kGrepGeneral && a.pats.qf_on && !a.counters[kCtrQOver] && !a.counters[kCtrHitsOver])
-    return;  // prefiltered
+  const bool prefiltered =
+      a.grep_mode == kGrepGeneral && a.pats.qf_on && !a.counters[kCtrQOver] && !a.counters[kCtrHitsOver];
+  if (prefiltered && !a.match_all) return;
   const uint64_t L = a.segout[a.nsegs - 1].line_hi;
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   for (uint64_t l = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; l < L; l += stride) {
     const uint16_t m = a.meta[l];
     if (!(m & Meta::kParsed)) continue;
-    bool hit = a.grep_mode == kGrepAll;
+    bool hit = a.grep_mode == kGrepAll || (prefiltered && a.match_all);
     if (!hit) {
       const uint32_t s = find_seg_by_line(a.segout, a.nsegs, l);
       const uint8_t* segp = a.bytes + a.segs[s].base;
@@ -1675,6 +1690,7 @@ __global__ __launch_bounds__(256) void k_match(RunArgs a) {
         if (a.pats.ac_states) hit = ac_match(a.pats, p, n);
         for (uint32_t r = 0; !hit && r < a.pats.rx_count; ++r) hit = rx_match(a.pats, r, p, n);
       }
+      hit |= a.match_all != 0;
     }
     if (hit) atomicOr(&a.bits[l >> 5], 1u << (l & 31));
   }

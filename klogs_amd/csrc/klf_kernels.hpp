@@ -204,6 +204,7 @@ struct RunArgs {
   uint32_t since_sod;   // since_sec - since_day * 86400
   int64_t tail;
   uint32_t grep_mode;
+  uint32_t match_all;  // kGrepGeneral: the set also matches every content (k_match marks every parsed line)
   const uint8_t* lit;  // kGrepLit1 literal (device)
   uint32_t lit_len;
   uint32_t lit_anchor; // index of the literal's rarest byte (scan anchor)

@@ -959,14 +959,12 @@ bool compile_set(const std::vector<std::vector<uint8_t>>& pats, const std::vecto
           out.user_map[k] = CompiledSet::kCidAlways;
       }
   }
-  if (always) {
-    out.mode = CompiledSet::kAll;
-    for (auto& m : out.user_map)  // the set is not evaluated: only the always-patterns are counted
-      if (m >= 0) m = CompiledSet::kCidUncounted;
-    return true;
-  }
+  if (always && lits.empty() && rxs.empty()) { out.mode = CompiledSet::kAll; return true; }
   if (lits.empty() && rxs.empty()) { out.mode = CompiledSet::kNever; return true; }
-  if (rxs.empty() && lits.size() == 1 && lits[0].size() <= 256) {
+  // an always-pattern beside real ones: the general tables (counted per pattern), kAll's
+  // filter (also_all)
+  out.also_all = always;
+  if (!always && rxs.empty() && lits.size() == 1 && lits[0].size() <= 256) {
     out.mode = CompiledSet::kLiteral1;
     out.literal = lits[0];
     int best = 99;

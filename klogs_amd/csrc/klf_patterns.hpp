@@ -43,6 +43,10 @@ struct CompiledSet {
     kGeneral = 4,   // AC over literals and/or Glushkov regexes
   };
   Mode mode = kNone;
+  // kGeneral only: the set also holds a pattern that matches every content (an empty
+  // --grep, or a regex such as `x*`).  The filter is then kAll's (every parsed line); the
+  // other patterns are compiled so that a run with per-pattern counts can evaluate them.
+  bool also_all = false;
   std::vector<uint8_t> literal;  // kLiteral1
   uint32_t literal_anchor = 0;   // kLiteral1: index of its rarest byte in log text
 
@@ -56,7 +60,7 @@ struct CompiledSet {
   std::vector<uint32_t> ac_dict;    // [states] nearest fail-chain state with ac_out >= 0 (0 none)
 
   // per-pattern counts: compiled ids = literals (sorted, deduplicated) then regexes
-  static constexpr int32_t kCidNever = -1, kCidAlways = -2, kCidUncounted = -3;
+  static constexpr int32_t kCidNever = -1, kCidAlways = -2;
   uint32_t n_cids = 0, n_lits = 0;
   std::vector<int32_t> user_map;    // [patterns] compiled id, or kCid* for the special cases
 

@@ -9,80 +9,18 @@ client side cannot tell backlog bytes from new ones, so in follow mode the serve
 applies what is per line: the since cutoff (idempotent with the server's) and the grep
 set, prefix strip included (SPEC.md S1/S2/S5).
 
-`Follow` is the product path: a thin wrapper over the C ABI's follow session
-(klf_follow_open / feed / flush / close, include/klf.h), which carries the open lines and
-stages complete ones on the engine as they arrive.  `FollowBatch` restates the same
-carry rules in Python over any batch runner (the CPU tests drive it with the oracle).
-
-`FollowBatch` is the incremental chunked engine: `feed(stream, chunk)` carries each
-stream's open (unterminated) line across chunks; `flush()` runs ONE engine pass over the
-complete lines every stream has received since the last flush (one device batch for all
-streams: tail -1, per-line rules only), and `flush(final=True)` also closes the streams,
-emitting their last unterminated line as kubelet does at end of stream.  Concatenated
-flush outputs equal the filter of the whole stream with tail -1 (tests/test_follow.py).
+`Follow` is a thin wrapper over the C ABI's follow session (klf_follow_open / feed /
+flush / close, include/klf.h), which carries each stream's open (unterminated) line
+across reads and stages complete ones on the engine as they arrive; every flush runs ONE
+engine pass over what all streams completed since the previous flush (tail -1, per-line
+rules only), and a final flush also emits each stream's last unterminated line, as
+kubelet does at end of stream.  Concatenated flush outputs equal the filter of the whole
+stream with tail -1 (tests/test_follow.py).
 """
 from __future__ import annotations
 
 import ctypes as C
-from typing import Callable, Dict, List, Optional, Sequence, Tuple
-
-
-class FollowBatch:
-    def __init__(self, runner: Callable[[List[bytes]], List[bytes]]):
-        """runner(list of stream bytes) -> list of output bytes, tail -1 and the run's since
-        / grep (`engine_runner` over a klogs_amd.engine.Engine; the CPU tests pass the
-        oracle)."""
-        self._run = runner
-        self._carry: Dict[int, bytes] = {}
-        self._pending: Dict[int, List[bytes]] = {}
-
-    def feed(self, stream_id: int, chunk: bytes) -> None:
-        """Appends bytes read from a stream (any split: partial lines are carried)."""
-        if not chunk:
-            return
-        buf = self._carry.get(stream_id, b"") + chunk
-        cut = buf.rfind(b"\n") + 1
-        if cut:
-            self._pending.setdefault(stream_id, []).append(buf[:cut])
-        self._carry[stream_id] = buf[cut:]
-
-    def open_bytes(self, stream_id: int) -> int:
-        """Bytes of the stream's open line (received, not yet filtered)."""
-        return len(self._carry.get(stream_id, b""))
-
-    def flush(self, final: bool = False) -> Dict[int, bytes]:
-        """Filters what is complete (with final=True also the open lines, closing every
-        stream) -> {stream_id: output bytes} for the streams that had input."""
-        ids = set(self._pending)
-        if final:
-            ids |= {s for s, c in self._carry.items() if c}
-        order = sorted(ids)
-        if not order:
-            if final:
-                self._carry.clear()
-            return {}
-        data = [b"".join(self._pending.get(s, ())) + (self._carry.get(s, b"") if final else b"") for s in order]
-        outs = self._run(data)
-        self._pending.clear()
-        if final:
-            self._carry.clear()
-        return dict(zip(order, outs))
-
-
-def engine_runner(engine, since=None) -> Callable[[Sequence[bytes]], List[bytes]]:
-    """FollowBatch runner over a klogs_amd.engine.Engine: one batch run per flush."""
-    def run(streams: Sequence[bytes]) -> List[bytes]:
-        engine.reset()
-        engine.set_streams(len(streams))
-        for i, s in enumerate(streams):
-            if s:
-                engine.stage(i, s)
-        r = engine.run(since=since, tail=-1, n_streams=len(streams))
-        try:
-            return [r.stream(i).out for i in range(len(streams))]
-        finally:
-            r.free()
-    return run
+from typing import Dict, Optional, Tuple
 
 
 class Follow:
@@ -117,8 +55,10 @@ class Follow:
             i = 0
             while True:  # the result covers ids [0, max id fed]
                 p, n, c = C.c_void_p(), C.c_uint64(), E._Counts()
-                if E._lib.klf_result_stream(res._p, i, C.byref(p), C.byref(n), C.byref(c)):
+                rc = E._lib.klf_result_stream(res._p, i, C.byref(p), C.byref(n), C.byref(c))
+                if rc == E.KLF_EINVAL:  # past the last stream id of the result
                     break
+                E._check(rc, self._eng._h)  # a D2H / HIP failure is an error, not the end
                 if c.lines:
                     out[i] = C.string_at(p.value, n.value) if n.value else b""
                 i += 1

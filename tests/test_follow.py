@@ -1,10 +1,11 @@
-"""Follow mode (klogs_amd/follow.py): chunked feeding with carried partial lines equals
+"""Follow mode (klogs_amd/follow.py; tests/follow_batch.py restates its carry rules): chunked feeding with carried partial lines equals
 the filter of the whole stream with tail -1 (C oracle on the CPU; the engine on the GPU)."""
 import random
 
 import pytest
 
 import c_oracle as co
+from follow_batch import FollowBatch, engine_runner
 from klogs_amd import follow, synth
 
 SINCE = (synth.T0 + 1200, 0)
@@ -25,7 +26,7 @@ def _oracle_runner(streams):
 
 def _drive(runner, streams, seed, fb=None):
     rng = random.Random(seed)
-    fb = fb or follow.FollowBatch(runner)
+    fb = fb or FollowBatch(runner)
     pos = [0] * len(streams)
     got = [b""] * len(streams)
     while any(p < len(s) for p, s in zip(pos, streams)):
@@ -51,7 +52,7 @@ def test_follow_equals_whole_stream(seed):
 
 
 def test_follow_carry_and_empty_flush():
-    fb = follow.FollowBatch(_oracle_runner)
+    fb = FollowBatch(_oracle_runner)
     assert fb.flush() == {} and fb.flush(final=True) == {}
     fb.feed(3, b"2024-10-22T00:59:00Z pod a")
     assert fb.open_bytes(3) == len(b"2024-10-22T00:59:00Z pod a") and fb.flush() == {}
@@ -115,5 +116,5 @@ def test_follow_engine_runner(gpu):
     from klogs_amd import engine as E
     streams = _streams()
     with E.Engine(0, grep=GREP) as eng:
-        got = _drive(follow.engine_runner(eng, since=SINCE), streams, 11)
+        got = _drive(engine_runner(eng, since=SINCE), streams, 11)
     assert got == _oracle_runner(streams)

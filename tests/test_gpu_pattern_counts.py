@@ -82,8 +82,39 @@ def test_always_pattern(gpu):
     d = synth.generate(synth.ADVERSARIAL, 5, 0, 2000, permille=40)
     got, cnt = check([d], grep=[b""], match=[rb"x*"])
     assert got[0] == [cnt[0]["parsed"]] * 2
-    with pytest.raises(E.KlfError):  # an empty --grep beside real patterns: the set is not evaluated
-        run_counts([d], grep=[b"", b"pod"])
+
+
+@pytest.mark.parametrize("grep,match", [([b"", b"pod"], []), ([b"", b"pod", b"ready"], [rb"took \d+ms"]),
+                                        ([b"pod"], [rb"x*"]), ([b""], [rb"(?i)ERR_\w+"])])
+def test_always_pattern_beside_others(gpu, grep, match):
+    """`--grep ""` (bytes.Contains(x, "") is true) next to real patterns: every parsed line
+    is selected, and each other pattern still gets its own count; same output as the
+    always-set without counts."""
+    d = synth.generate(synth.ADVERSARIAL, 5, 0, 3000, permille=40)
+    t = synth.generate(synth.TEXT, 6, 0, 200_000)
+    got, cnt = check([d, t, b""], grep, match)
+    for i in range(2):
+        assert cnt[i]["matched"] == cnt[i]["parsed"]
+    always = [k for k, p in enumerate(list(grep) + list(match)) if p in (b"", rb"x*")]
+    assert all(got[0][k] == cnt[0]["parsed"] for k in always)
+    with E.Engine(0, grep=grep, match=match) as eng:  # the same selection without counts
+        for i, s in enumerate([d, t]):
+            eng.stage(i, s)
+        r = eng.run(since=(synth.T0 + 1800, 0), tail=40, n_streams=2)
+        plain = [r.stream(i).out for i in range(2)]
+        r.free()
+    with E.Engine(0, grep=[b""]) as eng:
+        for i, s in enumerate([d, t]):
+            eng.stage(i, s)
+        r = eng.run(since=(synth.T0 + 1800, 0), tail=40, n_streams=2)
+        assert [r.stream(i).out for i in range(2)] == plain
+        r.free()
+
+
+def test_counts_on_all_empty_batch(gpu):
+    """Per-pattern counts asked for on a batch whose streams are all empty: zeros."""
+    got, cnt = run_counts([b"", b""], grep=[b"pod", b"ready"], match=[rb"took \d+ms"])
+    assert got == [[0, 0, 0], [0, 0, 0]]
 
 
 def test_counts_need_the_flag(gpu):
