@@ -515,6 +515,67 @@ def cpu_extra(name: str, kind: int, pats: dict, permille: int, since, tail: int)
     return res
 
 
+def verify_large(name, sizes, lens, kind, permille, pats, since, tail, r) -> dict:
+    """Checks the last timed run of C4 / C5 against the oracles (after the timed region):
+    C4 in full with the C oracle (Aho-Corasick over the 1,024 literals, one host thread per
+    stream): every stream's output bytes, counts and match bitmap.  C5: every stream's
+    lines / parsed / since_ok with the C oracle (no patterns), and its tail window with the
+    Python oracle (the 64 regexes through Python `re`, forked workers): the stream's
+    shortest suffix holding the last tail + 2 matching lines gives the whole stream's
+    output (SPEC.md S4), and the suffix's match bitmap equals the run's over those lines.
+    The whole-stream match decisions of C5 are checked at 9 GiB by tests/test_gpu_large.py."""
+    from concurrent.futures import ThreadPoolExecutor
+    sys.path.insert(0, str(ROOT / "oracle"))
+    sys.path.insert(0, str(ROOT / "tests"))
+    import big_check as bc
+    import c_oracle as co
+    t = time.perf_counter()
+    got = [(r.stream(i), r.match_bits(i)) for i in range(len(lens))]
+    hosts = []
+    for i, (sz, n) in enumerate(zip(sizes, lens)):
+        h = np.empty(n + 1, dtype=np.uint8)
+        synth.generate_into(h, kind, 42, i, sz, permille=permille)
+        hosts.append(h[:n])
+    sn = since if since is not None else co.GO_ZERO_TIME
+    threads = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", "16") or 16)))
+    bad = []
+    if name == "c4":
+        grep = pats["grep"]
+        with ThreadPoolExecutor(min(threads, len(hosts))) as ex:
+            refs = list(ex.map(lambda h: co.filter_stream(h, sn, tail, grep, want_lines=False), hosts))
+        for i, (out, _, bits, c) in enumerate(refs):
+            so, gbits = got[i]
+            if so.out != out or gbits != bits or any(so.counts[k] != c[k] for k in c):
+                bad.append(i)
+        scope = "every stream in full: output bytes, all counts, match bitmap (C oracle, Aho-Corasick)"
+    else:
+        with ThreadPoolExecutor(min(threads, len(hosts))) as ex:
+            base = list(ex.map(lambda h: co.filter_stream(h, sn, tail, [], want_lines=False, want_bits=False,
+                                                          grep_active=False)[3], hosts))
+        starts, firsts = [], []
+        for i, h in enumerate(hosts):
+            ls = np.concatenate([np.zeros(1, np.int64), np.flatnonzero(h[:-1] == 10) + 1])
+            gb = bc.unpack_bits(got[i][1], len(ls))
+            a = bc.tail_suffix(h, ls, gb, tail)
+            starts.append(a)
+            firsts.append(int(np.searchsorted(ls, a)))
+            if any(got[i][0].counts[k] != base[i][k] for k in ("lines", "parsed", "since_ok")):
+                bad.append(i)
+        refs = bc.py_filter_suffixes(hosts, starts, sn, tail, match=pats["match"])
+        for i, (out, sel, matched, nl, mbits) in enumerate(refs):
+            so, gbits = got[i]
+            L = so.counts["lines"]
+            window = bc.unpack_bits(gbits, L)[firsts[i]:]
+            if (so.out != out or so.counts["selected"] != sel or matched < tail + 2 or nl != len(window)
+                    or not np.array_equal(bc.unpack_bits(mbits, nl), window)):
+                bad.append(i)
+        scope = ("every stream: lines/parsed/since_ok in full (C oracle); output bytes, selected count and the "
+                 "match bitmap over the tail window (the shortest suffix holding the last tail+2 matching "
+                 "lines) with the Python oracle; whole-stream match decisions: tests/test_gpu_large.py (9 GiB)")
+    return {"ok": not bad, "streams": len(lens), "failed_streams": sorted(set(bad)), "scope": scope,
+            "s": round(time.perf_counter() - t, 1)}
+
+
 def run_extra(name: str, args, local: int, now: int) -> dict:
     sizes, kind, pats, permille, desc = extra_streams(name, args.extra_bytes)
     t = time.time()
@@ -578,10 +639,19 @@ def run_extra(name: str, args, local: int, now: int) -> dict:
         write["verified_vs_c_oracle"] = bool(verified)
     if wdir is not None:
         wdir.cleanup()
+    vlarge = None
+    if name in ("c4", "c5") and not args.no_verify:
+        del dev  # the checks regenerate the streams on the host
+        torch.cuda.empty_cache()
+        dev = None
+        vlarge = verify_large(name, sizes, lens, kind, permille, pats, since, tail, last)
     tot = last.totals()
-    staged = eng.run_device(ptr, seg_base, lens, since=since, tail=tail, stage_times=True)
-    stage = staged.timing()
-    staged.free()
+    if dev is not None:
+        staged = eng.run_device(ptr, seg_base, lens, since=since, tail=tail, stage_times=True)
+        stage = staged.timing()
+        staged.free()
+    else:  # the batch was dropped for the checks: the stage split of the timed runs' last
+        stage = last.timing()
     n = sum(lens)
     scan_s = float(np.mean(scan_ms)) / 1e3
     dev_s = float(np.mean(total_ms)) / 1e3
@@ -602,6 +672,9 @@ def run_extra(name: str, args, local: int, now: int) -> dict:
         out["cpu_baseline"] = cpu_extra(name, kind, pats, permille, since, tail)
     if verified is not None:
         out["verified_vs_c_oracle"] = bool(verified)
+    if vlarge is not None:
+        out["verified_vs_oracle"] = vlarge.pop("ok")
+        out["verify"] = vlarge
     if write is not None:
         out["write_path"] = write
     last.free()

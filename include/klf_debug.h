@@ -19,10 +19,19 @@ int klf_debug_compile(const klf_pattern* pats, uint32_t n, uint32_t* mode, char*
 int klf_debug_match(const klf_pattern* pats, uint32_t n, const uint8_t* content, size_t len, int* match);
 /* The prefiltered path of general sets on one content, as the scan runs it: q-gram
  * samples at positions = phase (mod stride), bitmap + bucket verification, literal hits
- * final, regex factor hits -> Glushkov NFA.  info (nullable) = {prefilter on, q, stride,
- * needles}; when the prefilter is off *match is the full matcher's answer. */
+ * final, regex factor hits -> Glushkov NFA; anchored short needles at every position
+ * holding the anchor byte.  info (nullable, 5 words) = {prefilter on, q, stride, needles,
+ * 0x100 | anchor byte (0: no anchor)}; when the prefilter is off *match is the full
+ * matcher's answer. */
 int klf_debug_prefilter(const klf_pattern* pats, uint32_t n, const uint8_t* content, size_t len,
                         uint32_t phase, int* match, uint32_t* info);
+
+/* The prefilter's layout chosen on the statistics of `sample` (the host twin of the first
+ * batch's k_gramhist; slen 0: the compile-time layout), then its work over `data`:
+ * out[8] = {stride, q, K, 0x100 | anchor byte (0: none), probes, bitmap hits, anchor hits,
+ * verified needle occurrences}; layout (cap bytes) gets the layout's description. */
+int klf_debug_prefilter_hits(const klf_pattern* pats, uint32_t n, const uint8_t* sample, size_t slen,
+                             const uint8_t* data, size_t dlen, uint64_t* out, char* layout, size_t cap);
 
 /* The required factor set of one regex (SPEC.md S5) as the prefilter uses it: the
  * strings '\0'-separated into buf (cap bytes), *pre = bound on the distance from a match's

@@ -127,7 +127,8 @@ struct klf_engine {
   uint32_t n_user = 0;                 // patterns as given to klf_open
   // device pattern tables
   DevBuf d_lit, d_ac_class, d_ac_next, d_ac_accept, d_rx_class, d_rx_b, d_rx_follow, d_rx_vec, d_rx_flags, d_rx_pre;
-  DevBuf d_qf_bitmap, d_qf_head, d_qf_ent, d_qf_nbytes, d_cand, d_rx_vec4, d_qhits, d_hslots, d_hist, d_hflat;
+  DevBuf d_qf_bitmap, d_qf_head, d_qf_ent, d_qf_nbytes, d_cand, d_rx_vec4, d_qhits, d_hslots, d_hist, d_hflat, d_qf_anc;
+  HostBuf h_hist;  // gram / byte statistics of the first batch (pinned readback)
   uint32_t cand_cap = 1u << 22;  // NFA candidate queue (32 MiB); overflow -> k_match
   uint64_t hits_cap_max = 1u << 26;  // prefilter hit list (512 MiB at most); overflow -> k_match
   klf::DevPatterns dpats;
@@ -198,6 +199,42 @@ static hipError_t upload(DevBuf& b, const std::vector<T>& v, hipStream_t st) {
   h = hipMemcpyAsync(b.p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice, st);
   if (h != hipSuccess) return h;
   return hipStreamSynchronize(st);
+}
+
+// The prefilter tables that the layout choice (place_needles) rewrites: bitmap, buckets,
+// anchor pre-checks, and the scalar layout fields of the device pattern set.
+static hipError_t upload_prefilter(klf_engine* e) {
+  const auto& cs = e->cs;
+  hipStream_t st = e->stream;
+  hipError_t h;
+  std::vector<uint32_t> anc = cs.qf_anc_pre;
+  if (anc.empty()) anc.assign(2, 0u);
+  if ((h = upload(e->d_qf_bitmap, cs.qf_bitmap, st)) != hipSuccess || (h = upload(e->d_qf_head, cs.qf_head, st)) != hipSuccess ||
+      (h = upload(e->d_qf_ent, cs.qf_ent, st)) != hipSuccess || (h = upload(e->d_qf_anc, anc, st)) != hipSuccess ||
+      (h = upload(e->d_qf_nbytes, cs.qf_nbytes, st)) != hipSuccess)
+    return h;
+  klf::DevPatterns& P = e->dpats;
+  if (cs.rx_count) {  // the chosen needle set's match-start bounds (k_nfa_win / k_nfa split)
+    std::vector<uint32_t> pre = cs.rx_pre;
+    if (pre.empty()) pre.assign(cs.rx_count, klf::kRxPreUnbounded);
+    if ((h = upload(e->d_rx_pre, pre, st)) != hipSuccess) return h;
+    P.rx_pre = e->d_rx_pre.as<uint32_t>();
+    P.rx_unbounded = (uint32_t)std::count(pre.begin(), pre.end(), klf::kRxPreUnbounded);
+  }
+  P.qf_stride = cs.qf_stride;
+  P.qf_mask = cs.qf_mask;
+  P.qf_w24 = cs.qf_q == 4 ? 24u : 0u;
+  P.qf_k = cs.qf_k;
+  P.qf_bitmap = e->d_qf_bitmap.as<uint32_t>();
+  P.qf_head = e->d_qf_head.as<uint32_t>();
+  P.qf_ent = e->d_qf_ent.as<uint4>();
+  P.qf_nbytes = e->d_qf_nbytes.as<uint32_t>();
+  P.qf_anc_on = cs.qf_anc_on ? 1u : 0u;
+  P.qf_anc_byte = cs.qf_anc_byte * 0x01010101u;
+  P.qf_anc_fold = cs.qf_anc_fold;
+  P.qf_anc_n = (uint32_t)(cs.qf_anc_pre.size() / 2);
+  P.qf_anc_pre = e->d_qf_anc.as<uint32_t>();
+  return hipSuccess;
 }
 
 extern "C" int klf_open(const klf_config* cfg, klf_engine** out) {
@@ -326,23 +363,12 @@ extern "C" int klf_open(const klf_config* cfg, klf_engine** out) {
       P.rx_maxpos = std::max<uint32_t>(1, cs.rx_maxpos);
     }
     if (cs.qf_on) {
-      if ((h = upload(e->d_qf_bitmap, cs.qf_bitmap, st)) != hipSuccess ||
-          (h = upload(e->d_qf_head, cs.qf_head, st)) != hipSuccess ||
-          (h = upload(e->d_qf_ent, cs.qf_ent, st)) != hipSuccess ||
-          (h = upload(e->d_qf_nbytes, cs.qf_nbytes, st)) != hipSuccess) {
+      if ((h = upload_prefilter(e)) != hipSuccess) {
         *out = e;
         return hip_err(e, h, "upload prefilter tables");
       }
       P.qf_on = 1;
-      P.qf_stride = cs.qf_stride;
       P.qf_fold = cs.qf_fold;
-      P.qf_mask = cs.qf_mask;
-      P.qf_w24 = cs.qf_q == 4 ? 24u : 0u;
-      P.qf_k = cs.qf_k;
-      P.qf_bitmap = e->d_qf_bitmap.as<uint32_t>();
-      P.qf_head = e->d_qf_head.as<uint32_t>();
-      P.qf_ent = e->d_qf_ent.as<uint4>();
-      P.qf_nbytes = e->d_qf_nbytes.as<uint32_t>();
     }
   }
   if (const char* cc = getenv("KLF_CAND_CAP"))  // tests: force the queue-overflow fallback
@@ -365,13 +391,14 @@ extern "C" void klf_close(klf_engine* e) {
   if (e->aux_stream) (void)hipStreamSynchronize(e->aux_stream);
   for (DevBuf* b : {&e->d_lit, &e->d_ac_class, &e->d_ac_next, &e->d_ac_accept, &e->d_rx_class, &e->d_rx_b,
                     &e->d_rx_follow, &e->d_rx_vec, &e->d_rx_flags, &e->d_rx_pre, &e->d_qf_bitmap, &e->d_qf_head,
-                    &e->d_qf_ent, &e->d_qf_nbytes, &e->d_rx_vec4, &e->d_qhits, &e->d_hslots, &e->d_hist, &e->d_hflat, &e->d_cand, &e->d_batch, &e->d_segs, &e->d_tstat,
+                    &e->d_qf_ent, &e->d_qf_nbytes, &e->d_qf_anc, &e->d_rx_vec4, &e->d_qhits, &e->d_hslots, &e->d_hist, &e->d_hflat, &e->d_cand, &e->d_batch, &e->d_segs, &e->d_tstat,
                     &e->d_slots, &e->d_pool, &e->d_tile_base, &e->d_bsum, &e->d_cstatus, &e->d_counters, &e->d_cmap, &e->d_cseg,
                     &e->d_line_off, &e->d_meta, &e->d_bits, &e->d_segout, &e->d_wpre, &e->d_out, &e->d_tile_seg, &e->d_mpart, &e->d_trec, &e->d_truns, &e->d_kbase})
     b->release();
   e->d_asm.release();
   e->d_scratch.release();
   e->h_rb.release();
+  e->h_hist.release();
   for (DevBuf* b : {&e->d_ac_out, &e->d_ac_dict, &e->d_pcount, &e->d_pairs}) b->release();
   e->copier.reset();
   {
@@ -672,26 +699,27 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
     e->cs.qf_tuned = true;
     const char* tune = getenv("KLF_QF_TUNE");
     if (!tune || strcmp(tune, "0") != 0) {
-      std::vector<uint32_t> hist(klf::kQfHistBins);
-      HIPCHK(e, e->d_hist.ensure(klf::kQfHistBins * 4), "alloc hist");
-      HIPCHK(e, klf::launch_gramhist(d_bytes, e->d_segs.as<SegDesc>(), nsegs, 1u << 20, e->cs.qf_fold, e->cs.qf_mask,
+      const size_t nh = klf::kGramHistWords;
+      HIPCHK(e, e->d_hist.ensure(nh * 4), "alloc hist");
+      HIPCHK(e, e->h_hist.ensure(nh * 4), "alloc hist readback");
+      HIPCHK(e, klf::launch_gramhist(d_bytes, e->d_segs.as<SegDesc>(), nsegs, klf::kGramHistSample, e->cs.qf_fold,
                                      e->d_hist.as<uint32_t>(), st), "gram histogram");
-      HIPCHK(e, hipMemcpyAsync(hist.data(), e->d_hist.p, hist.size() * 4, hipMemcpyDeviceToHost, st), "D2H hist");
+      HIPCHK(e, hipMemcpyAsync(e->h_hist.p, e->d_hist.p, nh * 4, hipMemcpyDeviceToHost, st), "D2H hist");
       HIPCHK(e, hipStreamSynchronize(st), "sync hist");
-      if (getenv("KLF_DIAG")) {
-        uint64_t tot = 0, nz = 0, mx = 0;
-        for (uint32_t v : hist) { tot += v; nz += v != 0; mx = std::max<uint64_t>(mx, v); }
-        fprintf(stderr, "[klf] gram histogram: %llu grams, %llu bins used, max bin %llu\n", (unsigned long long)tot,
-                (unsigned long long)nz, (unsigned long long)mx);
+      const uint32_t* hv = e->h_hist.as<uint32_t>();
+      klf::DataStats ds;
+      ds.gram3.assign(hv, hv + klf::kQfHistBins);
+      ds.gram4.assign(hv + klf::kQfHistBins, hv + 2 * klf::kQfHistBins);
+      ds.bytes.assign(256, 0);
+      for (int c = 0; c < 256; ++c) {
+        ds.bytes[c] = hv[2 * klf::kQfHistBins + c];
+        ds.nbytes += ds.bytes[c];
       }
-      klf::place_needles(e->cs, &hist);
-      HIPCHK(e, upload(e->d_qf_bitmap, e->cs.qf_bitmap, st), "upload bitmap");
-      HIPCHK(e, upload(e->d_qf_head, e->cs.qf_head, st), "upload buckets");
-      HIPCHK(e, upload(e->d_qf_ent, e->cs.qf_ent, st), "upload entries");
-      e->dpats.qf_k = e->cs.qf_k;
-      e->dpats.qf_bitmap = e->d_qf_bitmap.as<uint32_t>();
-      e->dpats.qf_head = e->d_qf_head.as<uint32_t>();
-      e->dpats.qf_ent = e->d_qf_ent.as<uint4>();
+      klf::place_needles(e->cs, &ds);
+      if (getenv("KLF_DIAG"))
+        fprintf(stderr, "[klf] prefilter layout from %llu sampled bytes: %s\n", (unsigned long long)ds.nbytes,
+                e->cs.qf_layout.c_str());
+      HIPCHK(e, upload_prefilter(e), "upload prefilter tables");
     }
   }
   HIPCHK(e, e->d_tstat.ensure(ntiles * sizeof(klf::TileStat)), "alloc tstat");
@@ -1448,9 +1476,42 @@ extern "C" int klf_debug_prefilter(const klf_pattern* pats, uint32_t n, const ui
     info[1] = cs.qf_q;
     info[2] = cs.qf_stride;
     info[3] = cs.qf_needles;
+    info[4] = cs.qf_anc_on ? 0x100u | cs.qf_anc_byte : 0u;
   }
   if (cs.mode != klf::CompiledSet::kGeneral || !cs.qf_on) return klf_debug_match(pats, n, content, len, match);
   *match = klf::prefilter_match(cs, content, len, phase) ? 1 : 0;
+  return KLF_OK;
+}
+
+extern "C" int klf_debug_prefilter_hits(const klf_pattern* pats, uint32_t n, const uint8_t* sample, size_t slen,
+                                        const uint8_t* data, size_t dlen, uint64_t* out, char* layout, size_t cap) {
+  if ((n && !pats) || (slen && !sample) || (dlen && !data) || !out) return KLF_EINVAL;
+  std::vector<std::vector<uint8_t>> ps;
+  std::vector<uint32_t> kinds;
+  for (uint32_t i = 0; i < n; ++i) {
+    ps.emplace_back(pats[i].bytes, pats[i].bytes + pats[i].len);
+    kinds.push_back(pats[i].kind);
+  }
+  klf::CompiledSet cs;
+  std::string err;
+  int code = KLF_OK;
+  if (!klf::compile_set(ps, kinds, cs, err, code)) return code;
+  if (cs.mode != klf::CompiledSet::kGeneral || !cs.qf_on) return KLF_EINVAL;
+  if (slen) {
+    klf::DataStats st;
+    klf::data_stats(sample, slen, cs.qf_fold, st);
+    klf::place_needles(cs, &st);
+  }
+  const klf::PrefilterHits h = klf::prefilter_hits(cs, data, dlen);
+  out[0] = cs.qf_stride;
+  out[1] = cs.qf_q;
+  out[2] = cs.qf_k;
+  out[3] = cs.qf_anc_on ? 0x100u | cs.qf_anc_byte : 0u;
+  out[4] = h.probes;
+  out[5] = h.bitmap_hits;
+  out[6] = h.anchor_hits;
+  out[7] = h.verified;
+  if (layout && cap) { strncpy(layout, cs.qf_layout.c_str(), cap - 1); layout[cap - 1] = 0; }
   return KLF_OK;
 }
 

@@ -15,6 +15,9 @@
 // Go time.Parse(RFC3339Nano) / bytes.Contains / regexp.Match).
 #include <hip/hip_runtime.h>
 
+#include <cstdio>
+#include <cstdlib>
+
 #include "klf_kernels.hpp"
 #include "klf_ts.hpp"
 
@@ -212,6 +215,30 @@ __constant__ uint32_t c_month[16] = {0,
                                      243 | (30u << 16), 273 | (31u << 16), 304 | (30u << 16), 334 | (31u << 16),
                                      0, 0, 0};
 
+// v_mul_hi_u32_u24: bits 32..47 of the product of the low 24 bits of a and b (no intrinsic;
+// the 64-bit C++ form only lowers to it when a is known to fit in 24 bits)
+__device__ __forceinline__ uint32_t mul_hi_u24(uint32_t a, uint32_t b) {
+  uint32_t r;
+  asm("v_mul_hi_u32_u24 %0, %1, %2" : "=v"(r) : "s"(b), "v"(a));
+  return r;
+}
+// v_mul_u32_u24 / v_bfe_u32 as single instructions: __umul24 keeps an explicit 24-bit mask
+// in front of the multiply, and a bfe feeding an xor is split into shift + and
+__device__ __forceinline__ uint32_t mul_u24(uint32_t a, uint32_t b) {
+  uint32_t r;
+  asm("v_mul_u32_u24 %0, %1, %2" : "=v"(r) : "s"(b), "v"(a));
+  return r;
+}
+__device__ __forceinline__ uint32_t mad_u24(uint32_t a, uint32_t b, uint32_t c) {
+  uint32_t r;
+  asm("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(r) : "v"(a), "s"(b), "v"(c));
+  return r;
+}
+__device__ __forceinline__ uint32_t bfe_u32(uint32_t a, uint32_t off, uint32_t width) {
+  uint32_t r;
+  asm("v_bfe_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "n"(off), "n"(width));
+  return r;
+}
 // v_mad_u32_u24: a * b + c for a, b < 2^24 (low 32 bits of the product)
 __device__ __forceinline__ uint32_t mad24(uint32_t a, uint32_t b, uint32_t c) { return __umul24(a, b) + c; }
 
@@ -305,11 +332,15 @@ constexpr int kScanPlain = 0, kScanLit = 1, kScanGen = 2;
 // The tile descriptors come in as separate __restrict__ const parameters so that their
 // (wave-uniform) reads compile to scalar loads: a vector load of them would be ordered
 // behind the in-flight prefetch by vmcnt and stall every tile on the next tile's bytes.
-template <int MODE, int QS, int QK>
+// General sets: QS sampling stride, QK bits per gram, QQ gram bytes (3 or 4), QA (stride 8
+// only) the short needles' anchor test (DevPatterns::qf_anc_*).
+template <int MODE, int QS, int QK, int QQ = 4, bool QA = false>
 __global__ __launch_bounds__(kThreads, MODE == kScanGen ? 3 : KLF_SCAN_OCC) void k_scan(RunArgs a, const uint32_t* __restrict__ tseg,
                                                                const SegDesc* __restrict__ segs) {
   constexpr bool LIT = MODE == kScanLit;
   constexpr bool GEN = MODE == kScanGen;
+  constexpr bool ANC = GEN && QA;
+  static_assert(QQ == 3 || QQ == 4, "3- or 4-byte grams");
   constexpr int kWaves = kThreads / 64;
   constexpr int kRows = kTile / 1024;  // 1 KiB rows: 16 B per lane per row
   __shared__ __attribute__((aligned(16))) uint8_t s_tile_all[kWaves][kTile + kHalo];
@@ -416,7 +447,11 @@ __global__ __launch_bounds__(kThreads, MODE == kScanGen ? 3 : KLF_SCAN_OCC) void
     const uint32_t my0 = (uint32_t)lane * kLaneBytes;
     const int nvalid_s = tile_len - (int)my0;
     const int nvalid = nvalid_s <= 0 ? 0 : (nvalid_s >= kLaneBytes ? kLaneBytes : nvalid_s);
-    const uint32_t pat = a.lit_anchor_byte * 0x01010101u;
+    // the byte of the anchor test: the fused literal's rarest byte, or the short needles'
+    // anchor (loose short needles: bytes tested OR 0x20)
+    const uint32_t pat = ANC ? a.pats.qf_anc_byte : a.lit_anchor_byte * 0x01010101u;
+    const uint32_t afold = ANC ? a.pats.qf_anc_fold : 0u;
+    auto or4 = [](const uint4& x, uint32_t f) { return make_uint4(x.x | f, x.y | f, x.z | f, x.w | f); };
     uint32_t nlc = 0, anc = 0;
     {
       const uint32_t rot = ((uint32_t)lane >> 1) & 7u;
@@ -429,6 +464,7 @@ __global__ __launch_bounds__(kThreads, MODE == kScanGen ? 3 : KLF_SCAN_OCC) void
         const uint32_t c = ((uint32_t)v + rot) & 7u;
         nlc |= any_eq16(xs[v], 0x0A0A0A0Au) ? (1u << c) : 0u;
         if (LIT && !ABL(2)) anc |= any_eq16(xs[v], pat) ? (1u << c) : 0u;
+        if (ANC) anc |= any_eq16(afold ? or4(xs[v], afold) : xs[v], pat) ? (1u << c) : 0u;
       }
       if (nvalid < kLaneBytes) {
         const uint32_t vm = (1u << ((nvalid + 15) >> 4)) - 1u;
@@ -620,17 +656,33 @@ __global__ __launch_bounds__(kThreads, MODE == kScanGen ? 3 : KLF_SCAN_OCC) void
     // the scan keeps no verification code, and the latency-bound bucket walks run with
     // the whole GPU's parallelism.
     if (GEN) {
-      const uint32_t fold = a.pats.qf_fold, w24 = a.pats.qf_w24;
+      const uint32_t fold = a.pats.qf_fold;
       const uint32_t* s32 = reinterpret_cast<const uint32_t*>(s_tile);
-      // bit 0 of the result: gram g has all K bits of its bitmap word set (qf_hash / qf_bits)
-      auto hbits = [&](uint32_t g) __attribute__((always_inline)) -> uint32_t {
+      // bit 0 of the result: gram g has all K bits of its bitmap word set (qf_f / qf_hash /
+      // qf_bits): the multiplies, the word read, and the bit positions as byte / word selects
+      // or low bits of the products (SDWA operands of the shifts)
+      struct Probe {
+        uint32_t h, p, m;
+      };
+      // (the 24-bit multiplies ignore bits 24..31 of f: no mask)
+      auto probe = [&](uint32_t g) __attribute__((always_inline)) -> Probe {
         const uint32_t gf = g | fold;
-        const uint32_t f = QK == 3 ? gf ^ __builtin_amdgcn_ubfe(gf, 13, 11) : gf;  // qf_fold3 (bits >= 24 unused)
-        const uint32_t h = __umul24(f, 0x9E3779u) + __umul24(__builtin_amdgcn_ubfe(gf, 8, w24), 0x7F4A7Du);
-        const uint32_t w = s_qf[h >> (32 - kQfBucketBits)];
-        uint32_t t = (w >> ((h >> 15) & 31u)) & (w >> ((h >> 10) & 31u));
-        if (QK == 3) t &= w >> ((uint32_t)(((uint64_t)(f & 0xFFFFFFu) * 0xC2B2AEu) >> 32) & 31u);
+        const uint32_t f = QK == 3 ? gf ^ bfe_u32(gf, 13, 11) : gf;
+        Probe r;
+        r.h = mul_u24(f, 0x9E3779u);
+        if (QQ == 4) r.h = mad_u24(gf >> 8, 0x7F4A7Du, r.h);  // + bytes 1..3 * C2
+        r.p = mul_hi_u24(f, 0xC2B2AEu);
+        r.m = mul_u24(f, 0x5BD1E9u);
+        return r;
+      };
+      auto test = [&](uint32_t w, const Probe& r) __attribute__((always_inline)) -> uint32_t {
+        uint32_t t = (w >> ((r.m >> 24) & 31u)) & (w >> (r.p & 31u));
+        if (QK == 3) t &= w >> ((r.h >> 16) & 31u);
         return t;
+      };
+      auto hbits = [&](uint32_t g) __attribute__((always_inline)) -> uint32_t {
+        const Probe r = probe(g);
+        return test(s_qf[r.h >> (32 - kQfBucketBits)], r);
       };
       // the samples of chunk c (16 B) -> their grams, in order (QS = 8: dwords 0 and 2)
       auto chunk_grams = [&](uint32_t c, auto&& f) __attribute__((always_inline)) {
@@ -659,23 +711,16 @@ __global__ __launch_bounds__(kThreads, MODE == kScanGen ? 3 : KLF_SCAN_OCC) void
           const uint4 xa = *reinterpret_cast<const uint4*>(s_tile + my0 + 16u * ca);
           const uint4 xb = *reinterpret_cast<const uint4*>(s_tile + my0 + 16u * cb);
           const uint32_t g[8] = {xa.x, xa.y, xa.z, xa.w, xb.x, xb.y, xb.z, xb.w};
-          uint32_t h[8], w[8];
+          Probe r[8];
+          uint32_t w[8];
 #pragma unroll
-          for (int k = 0; k < 8; ++k) {
-            const uint32_t gf = g[k] | fold;
-            const uint32_t f = QK == 3 ? gf ^ __builtin_amdgcn_ubfe(gf, 13, 11) : gf;
-            h[k] = __umul24(f, 0x9E3779u) + __umul24(__builtin_amdgcn_ubfe(gf, 8, w24), 0x7F4A7Du);
-          }
+          for (int k = 0; k < 8; ++k) r[k] = probe(g[k]);
 #pragma unroll
-          for (int k = 0; k < 8; ++k) w[k] = s_qf[h[k] >> (32 - kQfBucketBits)];
+          for (int k = 0; k < 8; ++k) w[k] = s_qf[r[k].h >> (32 - kQfBucketBits)];
           uint32_t acc_a = 0, acc_b = 0;
 #pragma unroll
           for (int k = 0; k < 8; ++k) {
-            uint32_t t = (w[k] >> ((h[k] >> 15) & 31u)) & (w[k] >> ((h[k] >> 10) & 31u));
-            if (QK == 3) {
-              const uint32_t gf = g[k] | fold, f = gf ^ __builtin_amdgcn_ubfe(gf, 13, 11);
-              t &= w[k] >> ((uint32_t)(((uint64_t)(f & 0xFFFFFFu) * 0xC2B2AEu) >> 32) & 31u);
-            }
+            const uint32_t t = test(w[k], r[k]);
             if (k < 4) acc_a |= t; else acc_b |= t;
           }
           chit |= ((acc_a & 1u) << ca) | ((acc_b & 1u) << cb);
@@ -702,6 +747,29 @@ __global__ __launch_bounds__(kThreads, MODE == kScanGen ? 3 : KLF_SCAN_OCC) void
           hq1 |= q == 1 ? hm : 0u;
           hq2 |= q == 2 ? hm : 0u;
           hq3 |= q == 3 ? hm : 0u;
+        }
+      }
+      // short needles: every anchor byte whose dword passes a pre-check is a hit (its
+      // bucket entries name the anchor's offset in the needle); anchors are rare
+      if (ANC && __any(anc != 0)) {
+        const uint32_t npre = a.pats.qf_anc_n;
+        for (uint32_t cm = anc; cm; cm &= cm - 1u) {
+          const uint32_t c = (uint32_t)__builtin_ctz(cm);
+          const uint4 x = *reinterpret_cast<const uint4*>(s_tile + my0 + 16u * c);
+          uint32_t am = 0;
+          for (uint32_t e = clip(eq_mask16(afold ? or4(x, afold) : x, pat), c); e; e &= e - 1u) {
+            const uint32_t pos = my0 + 16u * c + (uint32_t)__builtin_ctz(e);
+            const uint32_t w = __builtin_amdgcn_alignbyte(s32[(pos >> 2) + 1], s32[pos >> 2], pos & 3u) | fold;
+            bool ok = false;
+            for (uint32_t j = 0; j < npre; ++j) ok |= (w & a.pats.qf_anc_pre[2 * j + 1]) == a.pats.qf_anc_pre[2 * j];
+            am |= ok ? 1u << (pos & 15u) : 0u;
+          }
+          am <<= (c & 1u) * 16u;
+          const uint32_t q = c >> 1;
+          hq0 |= q == 0 ? am : 0u;
+          hq1 |= q == 1 ? am : 0u;
+          hq2 |= q == 2 ? am : 0u;
+          hq3 |= q == 3 ? am : 0u;
         }
       }
       if (ABL(8)) {  // timing build: probes only
@@ -2811,10 +2879,15 @@ __global__ __launch_bounds__(256) void k_tcopy(RunArgs a, const uint4* __restric
 #undef KLF_TC_STORE
 }
 
-// Gram statistics for the prefilter's window choice: every byte position of a sample of
-// the batch into a count-min sketch (two rows, global atomics; one-off, first batch).
+// Data statistics for the prefilter's layout and window choice (one-off, first batch):
+// every byte position of a sample of the batch into the 3-gram and 4-gram count-min
+// sketches (two rows each, global atomics) and the byte histogram (LDS per block, one
+// global add per bin and block).
 __global__ __launch_bounds__(256) void k_gramhist(const uint8_t* bytes, const SegDesc* segs, uint32_t nsegs,
-                                                  uint64_t sample, uint32_t fold, uint32_t qmask, uint32_t* hist) {
+                                                  uint64_t sample, uint32_t fold, uint32_t* hist) {
+  __shared__ uint32_t s_b[256];
+  s_b[threadIdx.x] = 0;
+  __syncthreads();
   const uint32_t nseg = nsegs < 16 ? nsegs : 16;
   const uint32_t step = nsegs / nseg;
   const uint64_t per = sample / 4;  // dwords per segment sample
@@ -2826,11 +2899,17 @@ __global__ __launch_bounds__(256) void k_gramhist(const uint8_t* bytes, const Se
     const uint32_t w0 = p[0], w1 = p[1];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      const uint32_t g = ((k ? __builtin_amdgcn_alignbyte(w1, w0, k) : w0) | fold) & qmask;
-      atomicAdd(&hist[qf_hist_bin0(g)], 1u);
-      atomicAdd(&hist[qf_hist_bin1(g)], 1u);
+      const uint32_t g = (k ? __builtin_amdgcn_alignbyte(w1, w0, k) : w0) | fold;
+      const uint32_t g3 = g & 0xFFFFFFu;
+      atomicAdd(&hist[qf_hist_bin0(g3)], 1u);
+      atomicAdd(&hist[qf_hist_bin1(g3)], 1u);
+      atomicAdd(&hist[kQfHistBins + qf_hist_bin0(g)], 1u);
+      atomicAdd(&hist[kQfHistBins + qf_hist_bin1(g)], 1u);
+      atomicAdd(&s_b[(w0 >> (8 * k)) & 0xFFu], 1u);
     }
   }
+  __syncthreads();
+  if (s_b[threadIdx.x]) atomicAdd(&hist[2 * kQfHistBins + threadIdx.x], s_b[threadIdx.x]);
 }
 
 // Capture assembly: block b copies 1 MiB of piece b / kAsmBlocks (pieces are 64 MiB
@@ -2903,10 +2982,13 @@ hipError_t clear_timeline() {
 }
 
 hipError_t launch_gramhist(const uint8_t* bytes, const SegDesc* segs, uint32_t nsegs, uint64_t sample, uint32_t fold,
-                           uint32_t qmask, uint32_t* hist, hipStream_t st) {
-  hipError_t e = hipMemsetAsync(hist, 0, kQfHistBins * 4, st);
+                           uint32_t* hist, hipStream_t st) {
+  hipError_t e = hipMemsetAsync(hist, 0, kGramHistWords * 4, st);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k_gramhist, dim3(1024), dim3(256), 0, st, bytes, segs, nsegs, sample, fold, qmask, hist);
+  const uint32_t nseg = nsegs < 16 ? nsegs : 16;
+  const uint64_t threads = nseg * (sample / 4);
+  const uint32_t grid = (uint32_t)((threads + 255) / 256 < 1024 ? (threads + 255) / 256 : 1024);
+  hipLaunchKernelGGL(k_gramhist, dim3(grid ? grid : 1), dim3(256), 0, st, bytes, segs, nsegs, sample, fold, hist);
   return hipGetLastError();
 }
 
@@ -2914,21 +2996,31 @@ size_t nfa_lds_bytes(const DevPatterns& P) {
   return 8ull * P.rx_count * (P.rx_classes + P.rx_maxpos + 4) + 256;
 }
 
-template <int MODE, int QS, int QK = 3>
+template <int MODE, int QS, int QK = 3, int QQ = 4, bool QA = false>
 hipError_t launch_scan(const RunArgs& a, hipStream_t st, int num_cus) {
   static int occ = 0;  // queried once per variant: the host query delays the launch
   if (occ == 0) {
-    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_scan<MODE, QS, QK>, kThreads, 0);
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_scan<MODE, QS, QK, QQ, QA>, kThreads, 0);
     occ = occ < 1 ? 1 : (occ > 8 ? 8 : occ);
+    if (getenv("KLF_DIAG"))
+      fprintf(stderr, "[klf] k_scan<%d,%d,%d,%d,%d>: %d blocks per CU\n", MODE, QS, QK, QQ, (int)QA, occ);
   }
   uint32_t grid = (uint32_t)(num_cus * occ);
   if (grid > a.ntiles) grid = a.ntiles;
-  hipLaunchKernelGGL((k_scan<MODE, QS, QK>), dim3(grid), dim3(kThreads), 0, st, a, a.tile_seg, a.segs);
+  hipLaunchKernelGGL((k_scan<MODE, QS, QK, QQ, QA>), dim3(grid), dim3(kThreads), 0, st, a, a.tile_seg, a.segs);
   return hipGetLastError();
+}
+template <int QS, int QQ>
+hipError_t launch_gen_q(const RunArgs& a, hipStream_t st, int num_cus) {
+  if (QS == 8 && a.pats.qf_anc_on)  // short needles anchored (only beside stride-8 probes)
+    return a.pats.qf_k == 2 ? launch_scan<kScanGen, QS, 2, QQ, true>(a, st, num_cus)
+                            : launch_scan<kScanGen, QS, 3, QQ, true>(a, st, num_cus);
+  return a.pats.qf_k == 2 ? launch_scan<kScanGen, QS, 2, QQ>(a, st, num_cus)
+                          : launch_scan<kScanGen, QS, 3, QQ>(a, st, num_cus);
 }
 template <int QS>
 hipError_t launch_gen(const RunArgs& a, hipStream_t st, int num_cus) {
-  return a.pats.qf_k == 2 ? launch_scan<kScanGen, QS, 2>(a, st, num_cus) : launch_scan<kScanGen, QS, 3>(a, st, num_cus);
+  return a.pats.qf_w24 ? launch_gen_q<QS, 4>(a, st, num_cus) : launch_gen_q<QS, 3>(a, st, num_cus);
 }
 
 static hipError_t launch_tail_stage(const RunArgs& a, hipStream_t st, hipEvent_t* ev, int num_cus);

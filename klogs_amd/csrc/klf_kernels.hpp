@@ -62,46 +62,47 @@ constexpr uint32_t kCtrDense = 14;                   // counters[14]: dense comp
 constexpr uint32_t kCtrPairsOver = 15;               // counters[15]: failed (line, pattern) pair inserts (set full)
 constexpr uint32_t kQfRegex = 1u << 24;              // entry flags: regex factor (else literal)
 constexpr uint32_t kQfLoose = 1u << 25;              //   compare OR 0x20 per byte
+constexpr uint32_t kQfAnchored = 1u << 26;           //   a short needle reached through its anchor (no bitmap bits)
 constexpr size_t kNfaMaxLds = 64 * 1024;            // k_nfa stages its tables in LDS up to this
 constexpr uint32_t kCarryBias = 256;
 constexpr uint32_t kRxPreNone = 0xFFFFFFFFu;         // rx_pre: no bound (= klf_patterns.hpp kRxPreUnbounded)                 // TileStat.carry_off = hit offset + 1 + bias
-// Blocked Bloom filter, one 32-bit bitmap word per probe.  The gram is folded to 24 bits
-// (byte 3 xor-ed into bits 11..18) so that both hashes are full-rate 24-bit multiplies:
-// word = top 12 bits of the low product (also the verification bucket), three bits inside
-// the word from the low and the high product.
-__host__ __device__ inline uint32_t qf_fold24(uint32_t g) { return (g ^ (g >> 13)) & 0xFFFFFFu; }
-__host__ __device__ inline uint32_t qf_h1(uint32_t g) { return qf_fold24(g) * 0x9E3779u; }
-__host__ __device__ inline uint32_t qf_h2(uint32_t g) {
-  return (uint32_t)(((uint64_t)qf_fold24(g) * 0xC2B2AEu) >> 32);  // v_mul_hi_u32_u24
-}
-// Gram statistics of the window choice: a count-min sketch, 2 rows of 2^16 bins
-constexpr int kQfHistBits = 16;
-constexpr uint32_t kQfHistBins = 2u << kQfHistBits;
-__host__ __device__ inline uint32_t qf_hist_bin0(uint32_t g) { return qf_h1(g) >> (32 - kQfHistBits); }
-__host__ __device__ inline uint32_t qf_hist_bin1(uint32_t g) {
-  return (1u << kQfHistBits) + ((g * 0x85EBCA77u) >> (32 - kQfHistBits));
-}
-// The scan's probe (k_scan<gen>): the gram's bytes 0..2 (for K = 3 folded, f = x ^ x >> 13,
-// so that the bit positions see all of them: measured offline on the C4 set, 1.7 false
-// hits per 8 KiB tile folded against 9.9 unfolded; the K = 2 sets are small and do as
-// well without) and, for 4-byte grams, bytes 1..3 (v_bfe extracts them, width 0 for
-// 3-byte grams, so no mask is applied), hashed with two full-rate 24-bit
-// multiply(-add)s; a blocked Bloom word (top 12 bits = also the verification bucket)
-// with K = 2 bits at hash bits 15..19 / 10..14, or K = 3 with a third from the high half
-// of f's product.  ~11 (K = 2) / 15 (K = 3) VALU per probe (the previous design: ~19).
-__host__ __device__ inline uint32_t qf_fold3(uint32_t g, uint32_t k) {
-  return (k == 3 ? g ^ ((g & 0xFFFFFFu) >> 13) : g) & 0xFFFFFFu;
+// Blocked Bloom filter, one 32-bit bitmap word per probe, K = 2 or 3 bits per gram.  The
+// multiplies see f = bytes 0..2 of the gram (K = 3: folded, f ^ f >> 13, so that byte 2
+// reaches the low product bits too):
+//   h    = f * C1 (+ bytes 1..3 * C2 for 4-byte grams): 24-bit multiply(-add)s, low 32
+//          bits; word = h >> 20, also the verification bucket;
+//   p    = the high half of f * C3 (v_mul_hi_u32_u24), m = f * C4;
+//   bits = K = 2: m bits 24..28, p bits 0..4; K = 3: p bits 0..4, h bits 16..20, m bits 24..28.
+// The scan takes every bit position as a byte / word select of a product (SDWA operands of
+// the shifts) or its low bits, so a probe costs about 10 VALU (K = 2) / 13 (K = 3); the
+// previous design cost ~14 / ~18.  Measured on the C4 / C5 sets and data (host emulation,
+// tools in tests/test_prefilter.py): 0.9 / 0.01 bitmap hits per 8 KiB tile (before: 2.2 /
+// 0.017).
+__host__ __device__ inline uint32_t qf_f(uint32_t g, uint32_t k) {
+  const uint32_t g24 = g & 0xFFFFFFu;
+  return k == 3 ? g24 ^ (g24 >> 13) : g24;
 }
 __host__ __device__ inline uint32_t qf_hash(uint32_t g, uint32_t w24, uint32_t k) {  // w24 = 24 (q = 4) or 0 (q = 3)
   const uint32_t hi = w24 ? (g >> 8) & 0xFFFFFFu : 0u;
-  return qf_fold3(g, k) * 0x9E3779u + hi * 0x7F4A7Du;
-}
-__host__ __device__ inline uint32_t qf_hash3(uint32_t g) {  // the third bit (K = 3)
-  return (uint32_t)(((uint64_t)qf_fold3(g, 3) * 0xC2B2AEu) >> 32);  // v_mul_hi_u32_u24
+  return qf_f(g, k) * 0x9E3779u + hi * 0x7F4A7Du;
 }
 __host__ __device__ inline uint32_t qf_word(uint32_t h) { return h >> (32 - kQfBucketBits); }
 __host__ __device__ inline uint32_t qf_bits(uint32_t g, uint32_t h, uint32_t k) {
-  return (1u << ((h >> 15) & 31u)) | (1u << ((h >> 10) & 31u)) | (k == 3 ? 1u << (qf_hash3(g) & 31u) : 0u);
+  const uint32_t f = qf_f(g, k);
+  const uint32_t p = (uint32_t)(((uint64_t)f * 0xC2B2AEu) >> 32), m = f * 0x5BD1E9u;
+  const uint32_t b = (1u << ((m >> 24) & 31u)) | (1u << (p & 31u));
+  return k == 3 ? b | (1u << ((h >> 16) & 31u)) : b;
+}
+// Gram statistics of the window choice: a count-min sketch, 2 rows of 2^16 bins, for the
+// 3-byte and for the 4-byte grams, then a byte histogram (k_gramhist)
+constexpr int kQfHistBits = 16;
+constexpr uint32_t kQfHistBins = 2u << kQfHistBits;
+constexpr uint32_t kGramHistWords = 2 * kQfHistBins + 256;
+constexpr uint64_t kGramHistSample = 64u << 10;  // bytes sampled per segment (<= 16 segments)
+__host__ __device__ inline uint32_t qf_h1(uint32_t g) { return (g ^ (g >> 13)) * 0x9E3779B1u; }
+__host__ __device__ inline uint32_t qf_hist_bin0(uint32_t g) { return qf_h1(g) >> (32 - kQfHistBits); }
+__host__ __device__ inline uint32_t qf_hist_bin1(uint32_t g) {
+  return (1u << kQfHistBits) + ((g * 0x85EBCA77u) >> (32 - kQfHistBits));
 }
 constexpr uint32_t kQfK2MaxGrams = 1536;  // up to this many sampled grams K = 2 bits, else 3
 
@@ -186,6 +187,9 @@ struct DevPatterns {  // device copies of CompiledSet tables (kGrepGeneral)
   const uint32_t* qf_head = nullptr;
   const uint4* qf_ent = nullptr;
   const uint32_t* qf_nbytes = nullptr;
+  // short needles anchored on a rare byte (klf_patterns.hpp CompiledSet::qf_anc_*)
+  uint32_t qf_anc_on = 0, qf_anc_byte = 0, qf_anc_fold = 0, qf_anc_n = 0;  // anc_byte replicated x4
+  const uint32_t* qf_anc_pre = nullptr;  // [qf_anc_n] {want, mask}
 };
 
 struct RunArgs {
@@ -266,10 +270,11 @@ hipError_t launch_pipeline(const RunArgs& a, hipStream_t stream, hipEvent_t* ev,
                            hipEvent_t ev_fork, hipEvent_t ev_join);
 // Re-runs matched counts, tail and compaction of the last pipeline with a.tail changed.
 hipError_t launch_retail(const RunArgs& a, hipStream_t stream, hipEvent_t* ev, int num_cus);
-// Gram sketch (kQfHistBins u32 bins, zeroed here) of the first `sample` bytes of each
-// of up to 16 segments, every position, grams folded / masked like the prefilter's.
+// Data statistics (kGramHistWords u32, zeroed here) of the first `sample` bytes of each of
+// up to 16 segments, every position: 3-gram and 4-gram sketches (folded like the
+// prefilter's grams), byte counts.
 hipError_t launch_gramhist(const uint8_t* bytes, const SegDesc* segs, uint32_t nsegs, uint64_t sample, uint32_t fold,
-                           uint32_t qmask, uint32_t* hist, hipStream_t stream);
+                           uint32_t* hist, hipStream_t stream);
 // Staged capture (klf_run): device chunks of the early H2D -> their places in the batch.
 struct AsmPiece {
   const uint8_t* src;  // device chunk (16-B aligned)

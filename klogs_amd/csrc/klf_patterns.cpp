@@ -4,8 +4,11 @@
 
 #include <algorithm>
 #include <bitset>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
+#include <set>
 #include <queue>
 
 #include "../../include/klf.h"
@@ -771,8 +774,10 @@ bool regex_factors(const uint8_t* pat, size_t n, std::vector<std::string>& alts,
   return true;
 }
 
-void build_prefilter(const std::vector<std::vector<uint8_t>>& lits, const std::vector<std::vector<std::string>>& rx_fac,
-                     const std::vector<bool>& rx_loose, CompiledSet& out);
+void build_prefilter(const std::vector<std::vector<uint8_t>>& lits,
+                     const std::vector<std::vector<std::vector<std::string>>>& fac_v,
+                     const std::vector<std::vector<bool>>& loose_v, const std::vector<std::vector<uint32_t>>& pre_v,
+                     CompiledSet& out);
 
 bool compile_regex(const uint8_t* pat, size_t n, GlushkovTables& out, std::string& err,
                    int& err_code) {
@@ -906,30 +911,47 @@ bool compile_set(const std::vector<std::vector<uint8_t>>& pats, const std::vecto
     err_code = KLF_ETOOBIG;
     return false;
   }
-  {  // second pass: the sampling stride follows the shortest needle of the first pass; keep
-     // it, and per regex prefer factor sets with a bounded match-start window (rx_pre)
+  // Second pass: two factor choices per regex for the layout to pick from (place_needles,
+  // with the data's statistics at the first batch).  [0]: the sampling stride follows the
+  // shortest needle of the first pass; keep it, and per regex prefer factor sets with a
+  // bounded match-start window (rx_pre).  [1]: prefer sets of >= 10 bytes (stride 8), the
+  // shorter needles left then being anchored on a rare byte when they share one.
+  std::vector<std::vector<std::vector<std::string>>> fac_v;
+  std::vector<std::vector<bool>> loose_v;
+  std::vector<std::vector<uint32_t>> pre_v;
+  {
     size_t g = SIZE_MAX;
     for (auto& l : lits) g = std::min(g, l.size());
     for (auto& f : rx_fac)
       for (auto& x : f) g = std::min(g, x.size());
-    const size_t want = g >= 10 ? 10 : g >= 6 ? 6 : g >= 4 ? 4 : 3;  // = build_prefilter's stride rule
-    for (size_t r = 0; r < rx_fac.size(); ++r) {
-      if (rx_fac[r].empty()) continue;
-      std::vector<std::string> alts;
-      bool loose = false;
-      uint32_t pre = kRxPreUnbounded;
-      const size_t k = rx_src[r];
-      if (!regex_factors(pats[k].data(), pats[k].size(), alts, loose, &pre, want)) continue;
-      drop_nl(alts);
-      size_t m = SIZE_MAX;
-      for (auto& x : alts) m = std::min(m, x.size());
-      if (alts.empty() || m < want) continue;
-      rx_fac[r] = alts;
-      rx_loose[r] = loose;
-      rx_pre[r] = pre;
+    const size_t want0 = g >= 10 ? 10 : g >= 6 ? 6 : g >= 4 ? 4 : 3;  // = the stride rule
+    for (size_t want : {want0, (size_t)10}) {
+      auto fac = rx_fac;
+      auto lo = rx_loose;
+      auto pr = rx_pre;
+      for (size_t r = 0; r < fac.size(); ++r) {
+        if (fac[r].empty()) continue;
+        std::vector<std::string> alts;
+        bool loose = false;
+        uint32_t pre = kRxPreUnbounded;
+        const size_t k = rx_src[r];
+        if (!regex_factors(pats[k].data(), pats[k].size(), alts, loose, &pre, want)) continue;
+        drop_nl(alts);
+        size_t m = SIZE_MAX;
+        for (auto& x : alts) m = std::min(m, x.size());
+        if (alts.empty() || m < want) continue;
+        fac[r] = alts;
+        lo[r] = loose;
+        pr[r] = pre;
+      }
+      if (!fac_v.empty() && fac == fac_v[0]) break;  // nothing longer to prefer
+      fac_v.push_back(fac);
+      loose_v.push_back(lo);
+      pre_v.push_back(pr);
+      if (want0 == 10) break;
     }
   }
-  out.rx_pre = rx_pre;
+  out.rx_pre = pre_v[0];
   // dedupe literals
   std::sort(lits.begin(), lits.end());
   lits.erase(std::unique(lits.begin(), lits.end()), lits.end());
@@ -1079,7 +1101,7 @@ bool compile_set(const std::vector<std::vector<uint8_t>>& pats, const std::vecto
       out.rx_flags.push_back((rxs[r].accept_at_start ? 1u : 0u) | (rxs[r].accept_empty ? 2u : 0u));
     }
   }
-  build_prefilter(lits, rx_fac, rx_loose, out);
+  build_prefilter(lits, fac_v, loose_v, pre_v, out);
   return true;
 }
 
@@ -1088,58 +1110,252 @@ bool compile_set(const std::vector<std::vector<uint8_t>>& pats, const std::vecto
 // without any factor (e.g. `\d+`): those need a look at every line anyway.
 //
 // Each needle is sampled through a window of q + S - 1 of its bytes (any substring of a
-// literal / factor occurs wherever the needle does); place_needles picks the windows.
-void build_prefilter(const std::vector<std::vector<uint8_t>>& lits, const std::vector<std::vector<std::string>>& rx_fac,
-                     const std::vector<bool>& rx_loose, CompiledSet& out) {
-  struct Needle {
-    std::string s;
-    uint32_t flags, rx;
-  };
-  std::vector<Needle> nd;
-  for (size_t i = 0; i < lits.size(); ++i) nd.push_back({std::string(lits[i].begin(), lits[i].end()), 0u, (uint32_t)i});
-  for (size_t r = 0; r < rx_fac.size(); ++r) {
-    if (rx_fac[r].empty()) { out.qf_why = "regex " + std::to_string(r) + " has no required literal factor"; return; }
-    for (auto& f : rx_fac[r]) nd.push_back({f, kQfRegex | (rx_loose[r] ? kQfLoose : 0u), (uint32_t)r});
-  }
-  if (nd.empty()) { out.qf_why = "no needles"; return; }
-  if (nd.size() > (1u << 24)) { out.qf_why = "too many needles"; return; }
-  size_t minlen = SIZE_MAX;
+// literal / factor occurs wherever the needle does); place_needles picks the layout, the
+// needle set (one per factor choice, fac_v) and the windows.
+void build_prefilter(const std::vector<std::vector<uint8_t>>& lits,
+                     const std::vector<std::vector<std::vector<std::string>>>& fac_v,
+                     const std::vector<std::vector<bool>>& loose_v, const std::vector<std::vector<uint32_t>>& pre_v,
+                     CompiledSet& out) {
+  out.qf_variants.clear();
   bool loose = false;
-  for (auto& n : nd) {
-    minlen = std::min(minlen, n.s.size());
-    loose |= (n.flags & kQfLoose) != 0;
+  for (size_t v = 0; v < fac_v.size(); ++v) {
+    CompiledSet::NeedleSet ns;
+    for (size_t i = 0; i < lits.size(); ++i) {
+      ns.s.push_back(std::string(lits[i].begin(), lits[i].end()));
+      ns.flags.push_back(0u);
+      ns.rx.push_back((uint32_t)i);
+    }
+    const auto& rx_fac = fac_v[v];
+    for (size_t r = 0; r < rx_fac.size(); ++r) {
+      if (rx_fac[r].empty()) { out.qf_why = "regex " + std::to_string(r) + " has no required literal factor"; return; }
+      for (auto& f : rx_fac[r]) {
+        ns.s.push_back(f);
+        ns.flags.push_back(kQfRegex | (loose_v[v][r] ? kQfLoose : 0u));
+        ns.rx.push_back((uint32_t)r);
+        loose |= loose_v[v][r];
+      }
+    }
+    if (ns.s.empty()) { out.qf_why = "no needles"; return; }
+    if (ns.s.size() > (1u << 24)) { out.qf_why = "too many needles"; return; }
+    size_t minlen = SIZE_MAX;
+    for (auto& x : ns.s) minlen = std::min(minlen, x.size());
+    if (minlen < kQfMinNeedle) {
+      if (v == 0) { out.qf_why = "a needle is shorter than 3 bytes"; return; }
+      break;
+    }
+    ns.rx_pre = pre_v[v];
+    out.qf_variants.push_back(std::move(ns));
   }
-  if (minlen < kQfMinNeedle) { out.qf_why = "a needle is shorter than 3 bytes"; return; }
-  // the widest sampling stride that keeps grams of >= 3 bytes (each probe costs ~18 VALU
-  // in the scan, so S = 8 halves the probe work of S = 4), then the longest gram that
-  // stride allows
-  const size_t sw = std::min<size_t>(8, minlen - 2);
-  const uint32_t S = sw >= 8 ? 8 : (sw >= 4 ? 4 : (sw >= 2 ? 2 : 1));
-  const uint32_t q = (uint32_t)std::min<size_t>(4, minlen - S + 1);
-  out.qf_q = q;
-  out.qf_stride = S;
-  out.qf_fold = loose ? 0x20202020u : 0u;
-  out.qf_mask = q == 4 ? ~0u : ((1u << (8 * q)) - 1u);
-  out.qf_needle.clear();
-  out.qf_nflags.clear();
-  out.qf_nrx.clear();
-  for (auto& n : nd) {
-    out.qf_needle.push_back(n.s);
-    out.qf_nflags.push_back(n.flags);
-    out.qf_nrx.push_back(n.rx);
-  }
-  out.qf_needles = (uint32_t)nd.size();
+  out.qf_fold = loose ? 0x20202020u : 0u;  // grams of every variant fold alike
   out.qf_on = true;
   place_needles(out, nullptr);
 }
 
-// Window choice + tables.  Each needle is sampled through q + S - 1 of its bytes: the
-// window whose S grams are the least frequent -- in the gram histogram of the data when
-// one is given (k_gramhist count-min sketch over a sample of the first batch), else by
-// a byte-class estimate -- with a small penalty for grams other needles already sample
-// (bucket length).  Every gram sets three bits of one bitmap word (blocked Bloom, k = 3).
-void place_needles(CompiledSet& out, const std::vector<uint32_t>* hist) {
+namespace {
+
+// The widest sampling stride whose windows (q + S - 1 bytes, grams of q >= 3 bytes) fit
+// every needle of length >= minlen (each probe costs ~12-17 VALU in the scan, so S = 8
+// halves the probe work of S = 4), then the longest gram that stride allows.
+void stride_rule(size_t minlen, uint32_t& S, uint32_t& q) {
+  const size_t sw = std::min<size_t>(8, minlen - 2);
+  S = sw >= 8 ? 8 : (sw >= 4 ? 4 : (sw >= 2 ? 2 : 1));
+  q = (uint32_t)std::min<size_t>(4, minlen - S + 1);
+}
+
+// Estimated share of data positions holding byte c (anchors of short needles): the sample's
+// byte histogram, else the byte-class guess of log text.
+double byte_share(uint32_t c, uint32_t fold, const DataStats* st) {
+  if (st && st->nbytes) {
+    uint64_t n = st->bytes[c];
+    if (fold && (c & 0x20u)) n += st->bytes[c & ~0x20u];  // loose: both cases
+    return (double)n / (double)st->nbytes;
+  }
+  uint8_t b = (uint8_t)c;
+  if (b >= 'a' && b <= 'z') return 1.0 / 20;
+  if (b == ' ' || (b >= '0' && b <= '9')) return 1.0 / 20;
+  if (b && strchr("\":,=./{}-TZ", b)) return 1.0 / 60;
+  return 1.0 / 2000;
+}
+
+// Picks the layout: all needles probed at the stride of the shortest, or (when that
+// stride is below 8 and the needles shorter than 10 bytes share a rare byte) the long
+// needles probed at stride 8 and the short ones anchored.
+void choose_layout(CompiledSet& out, const DataStats* st, bool allow_anchor) {
+  const auto& nd = out.qf_needle;
+  const size_t n = nd.size();
+  size_t minlen = SIZE_MAX, minlong = SIZE_MAX;
+  for (auto& x : nd) {
+    minlen = std::min(minlen, x.size());
+    if (x.size() >= 10) minlong = std::min(minlong, x.size());
+  }
+  uint32_t S, q;
+  stride_rule(minlen, S, q);
+  out.qf_anc_on = false;
+  out.qf_anc_pre.clear();
+  out.qf_nshort.assign(n, 0);
+  out.qf_nanc.assign(n, 0);
+  out.qf_layout = "all probed, S=" + std::to_string(S) + " q=" + std::to_string(q);
+  const char* env = getenv("KLF_QF_ANCHOR");  // tests / ablation: 0 never anchors
+  if (allow_anchor && S < 8 && minlong != SIZE_MAX && !(env && !strcmp(env, "0"))) {
+    uint32_t Sl, ql;
+    stride_rule(minlong, Sl, ql);
+    uint32_t afold = 0;
+    for (size_t i = 0; i < n; ++i)
+      if (nd[i].size() < 10 && (out.qf_nflags[i] & kQfLoose)) afold = 0x20202020u;
+    // candidate anchors: a byte every short needle holds at an offset <= len - q (the
+    // bucket's gram at the anchor lies inside the needle); 3-byte grams when no byte
+    // qualifies for 4-byte ones
+    // more common than 1 in 256 bytes: not worth it (tests: KLF_QF_ANCHOR=force takes any)
+    const double limit = (env && !strcmp(env, "force")) ? 2.0 : 1.0 / 256;
+    double best = limit;
+    int best_c = -1;
+    for (uint32_t qq = ql; qq >= 3 && best_c < 0; --qq) {
+      for (uint32_t c = 0; c < 256; ++c) {
+        if (c == '\n') continue;
+        if (afold && ((c | 0x20u) != c)) continue;  // stored loose bytes carry bit 5
+        bool ok = true;
+        for (size_t i = 0; i < n && ok; ++i) {
+          if (nd[i].size() >= 10) continue;
+          const size_t lim = nd[i].size() - qq;
+          const size_t pos = nd[i].find((char)c);
+          ok = pos != std::string::npos && pos <= lim;
+        }
+        if (!ok) continue;
+        const double sh = byte_share(c, afold, st);
+        if (sh < best) { best = sh; best_c = (int)c; }
+      }
+      if (best_c >= 0) ql = qq;
+    }
+    if (best_c >= 0) {
+      std::vector<std::pair<uint32_t, uint32_t>> pre;
+      for (size_t i = 0; i < n; ++i) {
+        if (nd[i].size() >= 10) continue;
+        const uint32_t a = (uint32_t)nd[i].find((char)best_c);
+        const uint32_t m = (uint32_t)std::min<size_t>(4, nd[i].size() - a);
+        uint32_t w = 0;
+        for (uint32_t b = 0; b < m; ++b) w |= (uint32_t)(uint8_t)nd[i][a + b] << (8 * b);
+        const uint32_t mask = m == 4 ? ~0u : (1u << (8 * m)) - 1u;
+        pre.push_back({(w | out.qf_fold) & mask, mask});
+        out.qf_nshort[i] = 1;
+        out.qf_nanc[i] = a;
+      }
+      std::sort(pre.begin(), pre.end());
+      pre.erase(std::unique(pre.begin(), pre.end()), pre.end());
+      if (pre.size() <= kQfAncPreMax) {
+        S = Sl;
+        q = ql;
+        out.qf_anc_on = true;
+        out.qf_anc_share = best;
+        out.qf_anc_byte = (uint32_t)best_c;
+        out.qf_anc_fold = afold;
+        for (auto& x : pre) {
+          out.qf_anc_pre.push_back(x.first);
+          out.qf_anc_pre.push_back(x.second);
+        }
+        char buf[160];
+        snprintf(buf, sizeof buf, "long needles probed S=%u q=%u; short ones anchored at 0x%02x (share %.2e, %zu pre-checks)",
+                 S, q, (unsigned)best_c, best, pre.size());
+        out.qf_layout = buf;
+      } else {
+        out.qf_nshort.assign(n, 0);
+      }
+    }
+  }
+  out.qf_q = q;
+  out.qf_stride = S;
+  out.qf_mask = q == 4 ? ~0u : ((1u << (8 * q)) - 1u);
+}
+
+// Estimated scan work per 8 KiB tile of a placed layout on the sample's statistics, in
+// VALU-instruction units of one wave: the probes (~11 each, a lane per 128 B), the anchor
+// test, and every hit (bitmap or anchor: the exact pass in the scan, the recording, the
+// verification) at ~40.  Hits per tile = samples per tile x the summed data share of the
+// sampled grams, plus the anchors whose dword passes a pre-check.
+double layout_cost(const CompiledSet& c, const DataStats& st) {
+  const double nb = st.nbytes ? (double)st.nbytes : 1.0;
+  const std::vector<uint32_t>& sk = c.qf_q == 3 ? st.gram3 : st.gram4;
+  auto share = [&](const std::vector<uint32_t>& h, uint32_t g) {
+    return std::min(h[qf_hist_bin0(g)], h[qf_hist_bin1(g)]) / nb;
+  };
+  std::set<uint32_t> grams;
+  for (size_t e = 0; e + 3 < c.qf_ent.size(); e += 4) {  // the probed grams, read back from the needles
+    if (c.qf_ent[e + 1] & kQfAnchored) continue;
+    const uint32_t off = c.qf_ent[e], len = c.qf_ent[e + 1] & 0xFFFFu, k = (c.qf_ent[e + 1] >> 16) & 0xFFu;
+    const uint8_t* nb8 = reinterpret_cast<const uint8_t*>(c.qf_nbytes.data() + off);
+    uint32_t g = 0;
+    for (uint32_t b = 0; b < c.qf_q && k + b < len; ++b) g |= (uint32_t)nb8[k + b] << (8 * b);
+    grams.insert((g | c.qf_fold) & c.qf_mask);
+  }
+  double hit_share = 0;  // probed grams (the anchored ones only reach a bucket through an anchor)
+  for (uint32_t g : grams) hit_share += share(sk, g);
+  const double samples = 8192.0 / c.qf_stride;
+  double hits = samples * std::min(1.0, hit_share);
+  double cost = 11.0 * samples / 64.0;
+  if (c.qf_anc_on) {
+    cost += 60.0;
+    double pass = 0;
+    for (size_t j = 0; j + 1 < c.qf_anc_pre.size(); j += 2)
+      pass += c.qf_anc_pre[j + 1] == ~0u ? share(st.gram4, c.qf_anc_pre[j]) : share(st.gram3, c.qf_anc_pre[j] & 0xFFFFFFu);
+    hits += 8192.0 * std::min(1.0, pass);
+  }
+  return cost + 40.0 * hits;
+}
+
+void place_tables(CompiledSet& out, const DataStats* st);
+
+}  // namespace
+
+// The layout: each needle set (factor choice) with every needle probed, and, where short
+// needles can be anchored, with the long ones probed at stride 8.  With the data's
+// statistics the cheapest by layout_cost wins; without them (klf_open, before any batch)
+// the widest stride, then the rarest anchor.
+void place_needles(CompiledSet& out, const DataStats* st) {
+  CompiledSet best;
+  double best_cost = 0;
+  bool have = false;
+  for (uint32_t v = 0; v < out.qf_variants.size(); ++v)
+    for (int anchored = 0; anchored < 2; ++anchored) {
+      CompiledSet c = out;
+      const auto& ns = c.qf_variants[v];
+      c.qf_variant = v;
+      c.qf_needle = ns.s;
+      c.qf_nflags = ns.flags;
+      c.qf_nrx = ns.rx;
+      c.qf_needles = (uint32_t)ns.s.size();
+      c.rx_pre = ns.rx_pre;
+      choose_layout(c, st, anchored != 0);
+      if (anchored && !c.qf_anc_on) continue;  // nothing to anchor: same as the probed layout
+      place_tables(c, st);
+      double cost;
+      if (st && st->nbytes) {
+        cost = layout_cost(c, *st);
+      } else {  // no statistics: stride first (8 is ~2x cheaper than 4), then the anchor's share
+        cost = 1e6 / c.qf_stride + (c.qf_anc_on ? c.qf_anc_share * 1e3 : 0.0);
+      }
+      char buf[64];
+      snprintf(buf, sizeof buf, " [est %.0f VALU/tile]", cost);
+      c.qf_layout += buf;
+      if (!have || cost < best_cost) {
+        best = std::move(c);
+        best_cost = cost;
+        have = true;
+      }
+    }
+  out = std::move(best);
+}
+
+namespace {
+
+// Window choice + tables.  Each probed needle is sampled through q + S - 1 of its bytes:
+// the window whose S grams are the least frequent -- in the gram sketch of the data when
+// one is given (k_gramhist count-min sketch over a sample of the first batch), else by a
+// byte-class estimate -- with a small penalty for grams other needles already sample
+// (bucket length).  Every probed gram sets K bits of one bitmap word (blocked Bloom); an
+// anchored needle has one bucket entry, at its anchor's gram, and no bitmap bits.
+void place_tables(CompiledSet& out, const DataStats* st) {
   const uint32_t q = out.qf_q, S = out.qf_stride;
+  const std::vector<uint32_t>* hist = st ? (q == 3 ? &st->gram3 : &st->gram4) : nullptr;
+  if (hist && hist->size() < kQfHistBins) hist = nullptr;
   const bool loose = out.qf_fold != 0;
   out.qf_bitmap.assign(kQfWords, 0u);
   out.qf_head.clear();
@@ -1159,10 +1375,17 @@ void place_needles(CompiledSet& out, const std::vector<uint32_t>* hist) {
   std::map<uint32_t, int> used;  // gram -> needles sampling it so far
   std::vector<std::vector<uint32_t>> buckets(kQfWords);
   const size_t n = out.qf_needle.size();
-  out.qf_k = n * S <= kQfK2MaxGrams ? 2u : 3u;  // few grams: two bits per gram keep the false hits rare
+  size_t nprobed = 0;
+  for (size_t i = 0; i < n; ++i) nprobed += out.qf_nshort[i] ? 0 : 1;
+  out.qf_k = nprobed * S <= kQfK2MaxGrams ? 2u : 3u;  // few grams: two bits per gram keep the false hits rare
   const uint32_t w24 = q == 4 ? 24u : 0u;
   for (uint32_t i = 0; i < n; ++i) {
     const std::string& s = out.qf_needle[i];
+    if (out.qf_nshort[i]) {  // anchored: the bucket of the gram at the anchor
+      const uint32_t k = out.qf_nanc[i], g = gram_at(s, k);
+      buckets[qf_word(qf_hash(g, w24, out.qf_k))].push_back(i << 8 | k);
+      continue;
+    }
     const uint32_t amax = (uint32_t)std::min<size_t>(s.size() - (q + S - 1), 255 - (S - 1));
     uint32_t best_a = 0;
     uint64_t best = UINT64_MAX;
@@ -1207,12 +1430,70 @@ void place_needles(CompiledSet& out, const std::vector<uint32_t>* hist) {
     for (uint32_t v : buckets[b]) {
       const uint32_t i = v >> 8;
       out.qf_ent.push_back(noff[i]);
-      out.qf_ent.push_back((uint32_t)out.qf_needle[i].size() | (v & 0xFFu) << 16 | out.qf_nflags[i]);
+      out.qf_ent.push_back((uint32_t)out.qf_needle[i].size() | (v & 0xFFu) << 16 | out.qf_nflags[i] |
+                           (out.qf_nshort[i] ? kQfAnchored : 0u));
       out.qf_ent.push_back(out.qf_nrx[i]);
       out.qf_ent.push_back(out.qf_nbytes[noff[i]]);  // first dword: the pre-check
     }
   }
   out.qf_head[buckets.size()] = (uint32_t)(out.qf_ent.size() / 4);
+}
+
+}  // namespace
+
+void data_stats(const uint8_t* p, size_t n, uint32_t fold, DataStats& st) {
+  st.gram3.assign(kQfHistBins, 0u);
+  st.gram4.assign(kQfHistBins, 0u);
+  st.bytes.assign(256, 0u);
+  st.nbytes = 0;
+  for (size_t i = 0; i + 4 <= n; ++i) {
+    uint32_t g = 0;
+    for (int b = 0; b < 4; ++b) g |= (uint32_t)p[i + b] << (8 * b);
+    g |= fold;
+    const uint32_t g3 = g & 0xFFFFFFu;
+    st.gram3[qf_hist_bin0(g3)]++;
+    st.gram3[qf_hist_bin1(g3)]++;
+    st.gram4[qf_hist_bin0(g)]++;
+    st.gram4[qf_hist_bin1(g)]++;
+    st.bytes[p[i]]++;
+    st.nbytes++;
+  }
+}
+
+PrefilterHits prefilter_hits(const CompiledSet& cs, const uint8_t* s, size_t n) {
+  PrefilterHits r;
+  const uint32_t S = cs.qf_stride, w24 = cs.qf_q == 4 ? 24u : 0u;
+  for (size_t p = 0; p < n; ++p) {
+    uint32_t g = 0;
+    for (uint32_t b = 0; b < 4; ++b) g |= (uint32_t)(p + b < n ? s[p + b] : 0) << (8 * b);
+    bool hit = false;
+    if (p % S == 0) {
+      ++r.probes;
+      const uint32_t gq = (g | cs.qf_fold) & cs.qf_mask;
+      const uint32_t h = qf_hash(gq, w24, cs.qf_k), bits = qf_bits(gq, h, cs.qf_k);
+      hit = (cs.qf_bitmap[qf_word(h)] & bits) == bits;
+      r.bitmap_hits += hit;
+    }
+    if (!hit && cs.qf_anc_on && ((uint32_t)s[p] | (cs.qf_anc_fold & 0xFFu)) == cs.qf_anc_byte) {
+      for (size_t j = 0; j + 1 < cs.qf_anc_pre.size() && !hit; j += 2)
+        hit = ((g | cs.qf_fold) & cs.qf_anc_pre[j + 1]) == cs.qf_anc_pre[j];
+      r.anchor_hits += hit;
+    }
+    if (!hit) continue;
+    const uint32_t b = qf_word(qf_hash((g | cs.qf_fold) & cs.qf_mask, w24, cs.qf_k));
+    for (uint32_t e = cs.qf_head[b]; e < cs.qf_head[b + 1]; ++e) {
+      const uint32_t* E = cs.qf_ent.data() + 4 * (size_t)e;
+      const uint32_t m = E[1] & 0xFFFFu, k = (E[1] >> 16) & 0xFFu;
+      const int64_t x = (int64_t)p - (int64_t)k;
+      if (x < 0 || (uint64_t)x + m > n) continue;
+      const uint8_t* nb = reinterpret_cast<const uint8_t*>(cs.qf_nbytes.data() + E[0]);
+      const uint8_t lm = (E[1] & kQfLoose) ? 0x20 : 0;
+      bool eq = true;
+      for (uint32_t j = 0; j < m && eq; ++j) eq = (uint8_t)(s[x + j] | lm) == nb[j];
+      r.verified += eq;
+    }
+  }
+  return r;
 }
 
 bool nfa_window(const CompiledSet& cs, uint32_t r, const uint8_t* s, size_t n, size_t x) {
@@ -1237,14 +1518,24 @@ bool prefilter_match(const CompiledSet& cs, const uint8_t* s, size_t n, uint32_t
   // Any window of S consecutive positions holds a sample, and every needle's chosen
   // window is q + S - 1 long, so each occurrence spans one sample with its gram inside
   // the window (the scan's tiles own their samples; the occurrence may start before).
+  // Anchored short needles: every position holding the anchor byte whose dword passes a
+  // pre-check is a hit too (the scan's anchor test), walked through the same buckets.
   const uint32_t S = cs.qf_stride;
-  for (size_t p = phase % S; p < n; p += S) {
+  for (size_t p = 0; p < n; ++p) {
     uint32_t g = 0;
     for (uint32_t b = 0; b < 4; ++b) g |= (uint32_t)(p + b < n ? s[p + b] : 0) << (8 * b);
+    bool hit = false;
+    if (p % S == phase % S) {
+      const uint32_t gq = (g | cs.qf_fold) & cs.qf_mask;
+      const uint32_t h = qf_hash(gq, cs.qf_q == 4 ? 24u : 0u, cs.qf_k), bits = qf_bits(gq, h, cs.qf_k);
+      hit = (cs.qf_bitmap[qf_word(h)] & bits) == bits;
+    }
+    if (!hit && cs.qf_anc_on && ((uint32_t)s[p] | (cs.qf_anc_fold & 0xFFu)) == cs.qf_anc_byte)
+      for (size_t j = 0; j + 1 < cs.qf_anc_pre.size() && !hit; j += 2)
+        hit = ((g | cs.qf_fold) & cs.qf_anc_pre[j + 1]) == cs.qf_anc_pre[j];
+    if (!hit) continue;
     g = (g | cs.qf_fold) & cs.qf_mask;
-    const uint32_t h = qf_hash(g, cs.qf_q == 4 ? 24u : 0u, cs.qf_k), bits = qf_bits(g, h, cs.qf_k);
-    if ((cs.qf_bitmap[qf_word(h)] & bits) != bits) continue;
-    const uint32_t b = qf_word(h);
+    const uint32_t b = qf_word(qf_hash(g, cs.qf_q == 4 ? 24u : 0u, cs.qf_k));
     for (uint32_t e = cs.qf_head[b]; e < cs.qf_head[b + 1]; ++e) {
       const uint32_t* E = cs.qf_ent.data() + 4 * (size_t)e;
       const uint32_t m = E[1] & 0xFFFFu, k = (E[1] >> 16) & 0xFFu;

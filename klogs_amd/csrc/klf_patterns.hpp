@@ -96,7 +96,41 @@ struct CompiledSet {
   std::vector<uint32_t> qf_nflags, qf_nrx;
   bool qf_tuned = false;               // windows placed from the data's gram histogram
   std::string qf_why;                // why the prefilter is off (diagnostics)
+  // Short needles: a needle shorter than the window q + S - 1 of the stride the others
+  // allow (S = 8 needs 10 bytes at q = 3) is not sampled by the probes.  When every short
+  // needle holds one byte that is rare in the data (the anchor), the scan tests each 16-B
+  // chunk for that byte (one SWAR any-test, like the newline test), pre-checks the dword at
+  // each anchor against the short needles' bytes there, and records the passing anchors as
+  // hits; their bucket entries (k = the anchor's offset in the needle) sit beside the
+  // probed ones, so k_verify walks both alike.  Off: every needle is probed (stride by the
+  // shortest needle).
+  bool qf_anc_on = false;
+  uint32_t qf_anc_byte = 0;          // the anchor byte (loose short needles: compared OR 0x20)
+  uint32_t qf_anc_fold = 0;          // 0x20202020 when a short needle is loose
+  double qf_anc_share = 0;           // the anchor's estimated share of data bytes
+  std::vector<uint32_t> qf_anc_pre;  // {want, mask} pairs: (dword at the anchor | qf_fold) & mask == want
+  std::vector<uint8_t> qf_nshort;    // [needles] 1: anchored (not probed)
+  std::vector<uint32_t> qf_nanc;     // [needles] offset of the anchor byte in a short needle
+  std::string qf_layout;             // diagnostics: the chosen layout
+  // The needle sets the layout picks from (one per factor choice of the regexes: [0] the
+  // shortest needle's stride kept, [1] factors of >= 10 bytes preferred); the chosen one
+  // is copied into qf_needle / qf_nflags / qf_nrx and its bounds into rx_pre.
+  struct NeedleSet {
+    std::vector<std::string> s;
+    std::vector<uint32_t> flags, rx, rx_pre;
+  };
+  std::vector<NeedleSet> qf_variants;
+  uint32_t qf_variant = 0;
 };
+
+// Statistics of a data sample (k_gramhist, first batch): count-min sketches of the 3- and
+// 4-byte grams (kQfHistBins bins each, needles' fold applied) and the byte histogram.
+struct DataStats {
+  std::vector<uint32_t> gram3, gram4;
+  std::vector<uint64_t> bytes;  // [256]
+  uint64_t nbytes = 0;          // positions counted in `bytes`
+};
+constexpr uint32_t kQfAncPreMax = 8;  // distinct short-needle pre-check dwords
 
 // Required literal factors of one regex (Go syntax, SPEC.md S5): every match contains
 // one of `alts`; `loose` when some byte is an ASCII case pair ((?i)), then every byte is
@@ -108,10 +142,21 @@ constexpr uint32_t kRxPreUnbounded = 0xFFFFFFFFu;
 bool regex_factors(const uint8_t* pat, size_t n, std::vector<std::string>& alts, bool& loose,
                    uint32_t* pre = nullptr, size_t want = SIZE_MAX);
 
-// (Re)places every needle's sampling window and rebuilds the bitmap and buckets; hist =
-// gram count-min sketch of a data sample (kQfHistBins bins) or null for the byte-class
-// estimate.
-void place_needles(CompiledSet& cs, const std::vector<uint32_t>* hist);
+// Host twin of k_gramhist over one sample (tests / diagnostics): every position's 3- and
+// 4-gram (OR fold) into the sketches, every byte into the histogram.
+void data_stats(const uint8_t* p, size_t n, uint32_t fold, DataStats& st);
+
+// Diagnostics of the prefiltered scan over `data` with the current layout: sampled
+// positions, bitmap hits, anchor hits (pre-check passed), verified needle occurrences.
+struct PrefilterHits {
+  uint64_t probes = 0, bitmap_hits = 0, anchor_hits = 0, verified = 0;
+};
+PrefilterHits prefilter_hits(const CompiledSet& cs, const uint8_t* data, size_t n);
+
+// (Re)chooses the prefilter layout (stride, gram length, short-needle anchor) and places
+// every needle's sampling window, rebuilding the bitmap and buckets; st = statistics of a
+// data sample (the first batch) or null for the byte-class estimates.
+void place_needles(CompiledSet& cs, const DataStats* st);
 
 // Regex r over content s[0, n) restricted to matches holding the factor occurrence that
 // starts at x: starts in [x - rx_pre[r], x], then no new start (the GPU's k_nfa).

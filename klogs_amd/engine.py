@@ -105,6 +105,8 @@ SIGNATURES = {
                                     C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]),
     "klf_debug_prefilter": (C.c_int, [C.POINTER(_Pattern), C.c_uint32, C.c_void_p, C.c_size_t, C.c_uint32,
                                       C.POINTER(C.c_int), C.POINTER(C.c_uint32)]),
+    "klf_debug_prefilter_hits": (C.c_int, [C.POINTER(_Pattern), C.c_uint32, C.c_void_p, C.c_size_t, C.c_void_p,
+                                           C.c_size_t, C.POINTER(C.c_uint64), C.c_char_p, C.c_size_t]),
 }
 
 
@@ -203,13 +205,28 @@ def debug_match(content: bytes, grep=(), match=()) -> bool:
 
 
 def debug_prefilter(content: bytes, grep=(), match=(), phase: int = 0):
-    """(match, {on, q, stride, needles}) of the prefiltered general matcher on the host."""
+    """(match, {on, q, stride, needles, anchor}) of the prefiltered general matcher on the host
+    (anchor: the short needles' anchor byte, None when every needle is probed)."""
     arr, n, keep = _patterns(grep, match)
     m = C.c_int()
-    info = (C.c_uint32 * 4)()
+    info = (C.c_uint32 * 5)()
     buf = C.create_string_buffer(content, len(content) or 1)
     _check(_lib.klf_debug_prefilter(arr, n, buf, len(content), phase, C.byref(m), info))
-    return bool(m.value), dict(on=bool(info[0]), q=info[1], stride=info[2], needles=info[3])
+    return bool(m.value), dict(on=bool(info[0]), q=info[1], stride=info[2], needles=info[3],
+                               anchor=(info[4] & 0xFF) if info[4] else None)
+
+
+def debug_prefilter_hits(sample: bytes, data: bytes, grep=(), match=()):
+    """The prefilter layout chosen on `sample`'s statistics and its work over `data` (host):
+    {stride, q, k, anchor, probes, bitmap_hits, anchor_hits, verified, layout}."""
+    arr, n, keep = _patterns(grep, match)
+    out = (C.c_uint64 * 8)()
+    lay = C.create_string_buffer(256)
+    sb = C.create_string_buffer(sample, len(sample) or 1)
+    db = C.create_string_buffer(data, len(data) or 1)
+    _check(_lib.klf_debug_prefilter_hits(arr, n, sb, len(sample), db, len(data), out, lay, 256))
+    return dict(stride=out[0], q=out[1], k=out[2], anchor=(out[3] & 0xFF) if out[3] else None, probes=out[4],
+                bitmap_hits=out[5], anchor_hits=out[6], verified=out[7], layout=lay.value.decode())
 
 
 def debug_factors(pattern: bytes, want: int = 0):

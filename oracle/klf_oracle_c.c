@@ -11,7 +11,8 @@
  *   - read loop:     kubelet pkg/kubelet/kuberuntime/logs/logs.go ReadLogs (limitedNum
  *                    decremented per parsed line, unparseable lines skipped uncounted)
  *                    + logWriter.write (drop ts.Before(since));
- *   - grep:          Go bytes.Contains via memmem over the content without its '\n'.
+ *   - grep:          Go bytes.Contains via memmem over the content without its '\n'
+ *                    (sets of more than 8 literals: an Aho-Corasick DFA, same answer).
  * Regex patterns are checked by the Python oracle only (Python `re`), see SPEC.md S5.
  */
 #define _GNU_SOURCE
@@ -142,13 +143,87 @@ static uint64_t find_tail_start(const uint8_t* buf, uint64_t size, int64_t n) {
   return left;
 }
 
-static int content_matches(const uint8_t* c, size_t cn, uint32_t n_lit, const uint8_t* const* lits,
-                           const uint64_t* lens) {
-  if (cn && c[cn - 1] == '\n') --cn;
-  for (uint32_t k = 0; k < n_lit; ++k) {
-    if (lens[k] == 0) return 1;
-    if (lens[k] <= cn && memmem(c, cn, lits[k], lens[k])) return 1;
+/* Large literal sets (C4: 1,024 literals): OR of bytes.Contains through a textbook
+ * Aho-Corasick automaton (goto trie, BFS failure links, completed into a 256-way DFA; a
+ * state accepts when some literal ends there or on its failure chain), one table step per
+ * content byte instead of one memmem per literal.  Small sets keep memmem. */
+typedef struct {
+  int32_t* next;  /* [states * nc]: byte classes (the literals' bytes, one class each; the rest 0) */
+  uint8_t* acc;   /* [states] */
+  int32_t n, nc;
+  uint8_t cls[256];
+} ko_ac;
+
+static void ac_free(ko_ac* a) {
+  free(a->next);
+  free(a->acc);
+  a->next = NULL;
+  a->acc = NULL;
+}
+
+static int ac_build(ko_ac* a, uint32_t n_lit, const uint8_t* const* lits, const uint64_t* lens) {
+  uint64_t cap = 1;
+  for (uint32_t k = 0; k < n_lit; ++k) cap += lens[k];
+  memset(a->cls, 0, sizeof a->cls);
+  a->nc = 1;
+  for (uint32_t k = 0; k < n_lit; ++k)
+    for (uint64_t j = 0; j < lens[k]; ++j)
+      if (!a->cls[lits[k][j]]) a->cls[lits[k][j]] = (uint8_t)a->nc++;
+  const int NC = a->nc;  /* <= 256: class 0 = bytes in no literal */
+  a->next = (int32_t*)malloc(cap * NC * sizeof(int32_t));
+  a->acc = (uint8_t*)calloc(cap, 1);
+  int32_t* fail = (int32_t*)malloc(cap * sizeof(int32_t));
+  int32_t* queue = (int32_t*)malloc(cap * sizeof(int32_t));
+  if (!a->next || !a->acc || !fail || !queue) { free(fail); free(queue); ac_free(a); return -1; }
+  for (uint64_t i = 0; i < cap * NC; ++i) a->next[i] = -1;
+  a->n = 1;
+  for (uint32_t k = 0; k < n_lit; ++k) {  /* goto trie */
+    int32_t st = 0;
+    for (uint64_t j = 0; j < lens[k]; ++j) {
+      int32_t* t = &a->next[(uint64_t)st * NC + a->cls[lits[k][j]]];
+      if (*t < 0) *t = a->n++;
+      st = *t;
+    }
+    a->acc[st] = 1;
   }
+  uint64_t qh = 0, qt = 0;  /* BFS: root's missing edges loop to the root */
+  for (int c = 0; c < NC; ++c) {
+    int32_t* t = &a->next[c];
+    if (*t < 0 || c == 0) { *t = 0; continue; }
+    fail[*t] = 0;
+    queue[qt++] = *t;
+  }
+  while (qh < qt) {
+    const int32_t u = queue[qh++];
+    a->acc[u] |= a->acc[fail[u]];
+    for (int c = 0; c < NC; ++c) {
+      int32_t* t = &a->next[(uint64_t)u * NC + c];
+      const int32_t via_fail = a->next[(uint64_t)fail[u] * NC + c];
+      if (*t < 0) { *t = via_fail; continue; }
+      fail[*t] = via_fail;
+      queue[qt++] = *t;
+    }
+  }
+  free(fail);
+  free(queue);
+  return 0;
+}
+
+static int content_matches(const uint8_t* c, size_t cn, uint32_t n_lit, const uint8_t* const* lits,
+                           const uint64_t* lens, const ko_ac* ac) {
+  if (cn && c[cn - 1] == '\n') --cn;
+  for (uint32_t k = 0; k < n_lit; ++k)
+    if (lens[k] == 0) return 1;
+  if (ac && ac->next) {
+    int32_t st = 0;
+    for (size_t i = 0; i < cn; ++i) {
+      st = ac->next[(uint64_t)st * ac->nc + ac->cls[c[i]]];
+      if (ac->acc[st]) return 1;
+    }
+    return 0;
+  }
+  for (uint32_t k = 0; k < n_lit; ++k)
+    if (lens[k] <= cn && memmem(c, cn, lits[k], lens[k])) return 1;
   return 0;
 }
 
@@ -160,6 +235,9 @@ int64_t ko_filter(const uint8_t* data, uint64_t n, int64_t since_sec, int32_t si
                   uint64_t* line_off, uint64_t line_cap, uint8_t* match_bits, ko_counts* cnt) {
   ko_counts c;
   memset(&c, 0, sizeof(c));
+  ko_ac ac;
+  memset(&ac, 0, sizeof ac);
+  if (grep_active && n_lit > 8 && ac_build(&ac, n_lit, lits, lit_lens) != 0) return -1;
   /* pass 1: lines, counts, G */
   uint8_t* gfile = NULL;
   uint64_t glen = 0, gcap = 0;
@@ -179,14 +257,14 @@ int64_t ko_filter(const uint8_t* data, uint64_t n, int64_t since_sec, int32_t si
       if (!before(s, ns, since_sec, since_nsec)) c.since_ok++;
     }
     if (grep_active) {
-      const int hit = ok && content_matches(data + pos + plen, end - pos - plen, n_lit, lits, lit_lens);
+      const int hit = ok && content_matches(data + pos + plen, end - pos - plen, n_lit, lits, lit_lens, &ac);
       if (hit) {
         if (match_bits) match_bits[li >> 3] |= (uint8_t)(1u << (li & 7));
         c.matched++;
         if (glen + (end - pos) > gcap) {
           gcap = (gcap + (end - pos)) * 2;
           uint8_t* g2 = (uint8_t*)realloc(gfile, gcap);
-          if (!g2) { free(gfile); return -1; }
+          if (!g2) { free(gfile); ac_free(&ac); return -1; }
           gfile = g2;
         }
         memcpy(gfile + glen, data + pos, end - pos);
@@ -227,6 +305,7 @@ int64_t ko_filter(const uint8_t* data, uint64_t n, int64_t since_sec, int32_t si
     p = end;
   }
   free(gfile);
+  ac_free(&ac);
   c.out_bytes = o;
   if (cnt) *cnt = c;
   return (int64_t)o;

@@ -1,0 +1,113 @@
+"""Parity helpers for batches of many GiB -- TEST INFRASTRUCTURE ONLY (tests/ and
+bench.py's verification leg; the product never imports it).
+
+* `py_line_table`: the Python oracle's per-line decisions (klf_oracle.parse_line, since,
+  Pattern.matches on the content -- SPEC.md S2/S3/S5) over a large stream, in a pool of
+  forked workers over line-aligned slices (Python `re` holds the GIL, so threads would not
+  help).  The workers only read the parent's bytes and never touch the GPU.
+* `tail_suffix`: the shortest line-aligned suffix of a stream that holds more than `n`
+  newline-terminated G lines (kubelet's tail over G then starts inside it, so any oracle
+  run on the suffix gives the whole stream's output: SPEC.md S4).
+"""
+from __future__ import annotations
+
+import multiprocessing as mp
+from typing import Sequence, Tuple
+
+import numpy as np
+
+import klf_oracle as po
+
+_DATA = None
+_PATS = None
+_SINCE = None
+
+
+def _chunk(ab: Tuple[int, int]):
+    a, b = ab
+    buf = bytes(_DATA[a:b])
+    hit, parsed, since_ok = [], 0, 0
+    for s, e in po.split_lines(buf):
+        p = po.parse_line(buf[s:e])
+        if p is None:
+            hit.append(False)
+            continue
+        parsed += 1
+        if not po.time_before(p[0], _SINCE):
+            since_ok += 1
+        c = po.content_for_match(p[1])
+        hit.append(any(pt.matches(c) for pt in _PATS))
+    return np.array(hit, dtype=bool), parsed, since_ok
+
+
+def line_cuts(data: np.ndarray, parts: int) -> list:
+    """Offsets 0 = c0 < c1 < ... < ck = len(data), each ci > 0 just past a '\\n'."""
+    n = len(data)
+    cuts = [0]
+    for k in range(1, parts):
+        lo = max(cuts[-1], k * n // parts)
+        nl = np.flatnonzero(data[lo:lo + (4 << 20)] == 10)
+        if nl.size and lo + int(nl[0]) + 1 < n:
+            cuts.append(lo + int(nl[0]) + 1)
+    cuts.append(n)
+    return sorted(set(cuts))
+
+
+def py_line_table(data: np.ndarray, since, grep: Sequence[bytes] = (), match: Sequence[bytes] = (),
+                  procs: int = 12):
+    """(match bool[lines], parsed, since_ok) of one stream by the Python oracle.  procs <=
+    12: a forked worker inherits the parent's GPU handles, and the box allows 16 processes
+    on the card."""
+    global _DATA, _PATS, _SINCE
+    _DATA, _PATS, _SINCE = data, po.compile_patterns(grep, match), since
+    cuts = line_cuts(data, procs * 6)
+    try:
+        with mp.get_context("fork").Pool(procs) as pool:
+            parts = pool.map(_chunk, list(zip(cuts, cuts[1:])), chunksize=1)
+    finally:
+        _DATA = None
+    hit = np.concatenate([p[0] for p in parts]) if parts else np.zeros(0, dtype=bool)
+    return hit, sum(p[1] for p in parts), sum(p[2] for p in parts)
+
+
+def tail_suffix(data: np.ndarray, line_starts: np.ndarray, gbits: np.ndarray, n: int) -> int:
+    """Start offset of the shortest suffix holding more than n + 1 G lines (G = gbits over
+    the stream's lines, line_starts[i] = start of line i); 0 when the stream has fewer."""
+    g = np.flatnonzero(gbits)
+    if g.size <= n + 2:
+        return 0
+    return int(line_starts[g[-(n + 3)]])
+
+
+def unpack_bits(b: bytes, n: int) -> np.ndarray:
+    """LSB-first packed bits (klf_result_match_bits) -> bool[n]."""
+    return np.unpackbits(np.frombuffer(b, np.uint8), bitorder="little")[:n].astype(bool)
+
+
+_HOSTS = None
+_ARGS = None
+
+
+def _suffix_job(job):
+    i, a = job
+    since, tail, pats = _ARGS
+    ref = po.filter_stream(bytes(_HOSTS[i][a:]), since, tail, pats)
+    return ref.out, ref.n_selected, ref.n_matched, ref.n_lines, ref.match_bits
+
+
+def py_filter_suffixes(hosts, starts, since, tail: int, grep=(), match=(), procs: int = 12):
+    """The Python oracle's filter_stream on hosts[i][starts[i]:] for every i, in a pool of
+    forked workers (each reads the parent's arrays; nothing large is pickled).  Returns
+    [(out, selected, matched, lines, match_bits)] in order."""
+    global _HOSTS, _ARGS
+    _HOSTS, _ARGS = hosts, (since, tail, po.compile_patterns(grep, match))
+    jobs = sorted(range(len(hosts)), key=lambda i: len(hosts[i]) - starts[i], reverse=True)  # longest first
+    try:
+        with mp.get_context("fork").Pool(min(procs, len(hosts))) as pool:
+            res = pool.map(_suffix_job, [(i, starts[i]) for i in jobs], chunksize=1)
+    finally:
+        _HOSTS = None
+    out = [None] * len(hosts)
+    for i, r in zip(jobs, res):
+        out[i] = r
+    return out

@@ -176,6 +176,42 @@ def test_c5_regex_set_long_json(gpu, since, tail):
     check_against_py(streams, since, tail, match=rx)
 
 
+def _with_inserts(data: bytes, parts, seed: int, every: int) -> bytes:
+    """`data` with one of `parts` inserted after every `every`-th line's timestamp prefix."""
+    rng = random.Random(seed)
+    lines = data.split(b"\n")
+    for i in range(0, len(lines), every):
+        ln = lines[i]
+        if len(ln) > 31:
+            k = rng.randint(31, len(ln))
+            lines[i] = ln[:k] + rng.choice(parts) + ln[k:]
+    return b"\n".join(lines)
+
+
+ANC_PARTS = [b"tx-0123abcd-commit5", b"tx-0123abc-commit5", b"-commit", b"tx--commit1", b"user3_id=u12345 login",
+             b"a-b", b"K_EY=value", b"k_ey=", b"AB_CD7", b"ab_cd", b"x_y_z", b"deadline exceeded after 3s"]
+
+
+@pytest.mark.parametrize("which", ["c5", "loose"])
+@pytest.mark.parametrize("since,tail", [(None, -1), ((synth.T0 + 1800, 0), 30)])
+def test_anchored_short_needles(gpu, monkeypatch, which, since, tail):
+    """Short needles anchored on one byte beside stride-8 probes (forced, so that every
+    data shape runs it): the C5 set (`-commitN` on '-') and a loose set (anchor '_' tested
+    OR 0x20), over JSON / text / adversarial streams with the needles and look-alikes
+    inserted, tile-crossing ones included."""
+    monkeypatch.setenv("KLF_QF_ANCHOR", "force")
+    if which == "c5":
+        grep, match = [], synth.c5_regexes()
+    else:
+        grep, match = [b"longer needle here"], [rb"(?i)k_ey=\w+", rb"(?i)ab_cd\d", rb"(?i)x_y_z", rb"deadline exceeded after \d+s"]
+    info = E.debug_prefilter(b"", grep=grep, match=match)[1]
+    assert info["stride"] == 8 and info["anchor"] is not None, info
+    streams = [_with_inserts(synth.generate(synth.LONGJSON, 7, 0, 1_500_000, permille=20), ANC_PARTS, 1, 3),
+               _with_inserts(synth.generate(synth.TEXT, 8, 0, 600_000), ANC_PARTS, 2, 5),
+               synth.generate(synth.ADVERSARIAL, 9, 0, 3000, permille=40), b""]
+    check_against_py(streams, since, tail, grep, match)
+
+
 GEN_SETS = [
     ([synth.NEEDLE, b"volume", b"x" * 80], [rb"(?i)took \d+ms", rb"status=(200|5\d\d)"]),
     ([b"pod", b"ready"], []),

@@ -212,3 +212,39 @@ def test_golden_c_oracle(case):
     assert lo.tolist() == np.load(GOLDEN / case["expect_lines"]).tolist()
     if grep:
         assert bits.hex() == case["expect_bits"]
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_c_oracle_aho_corasick_equals_memmem(seed):
+    """Sets of more than 8 literals go through the C oracle's Aho-Corasick DFA; the same set
+    split into groups of <= 8 (memmem) must give the same match bits, OR-ed."""
+    import numpy as np
+    rng = random.Random(seed)
+    lits = rng.sample(synth.c4_literals(1024), 200) + [b"pod", b"took 1", b"=0h"]  # overlapping / common ones too
+    d = synth.generate(synth.MIXED, 40 + seed, 0, 1_500_000, permille=40)
+    whole = co.filter_stream(d, co.GO_ZERO_TIME, 30, lits)
+    bits = None
+    for k in range(0, len(lits), 8):
+        b = np.frombuffer(co.filter_stream(d, co.GO_ZERO_TIME, -1, lits[k:k + 8])[2], np.uint8)
+        bits = b.copy() if bits is None else bits | b
+    assert whole[2] == bits.tobytes()
+    assert whole[3]["matched"] == int(np.unpackbits(bits).sum()) > 0
+
+
+def test_big_check_helpers_equal_the_whole_stream_oracle():
+    """tests/big_check.py (the >8 GiB parity checks): the forked per-line table equals
+    filter_stream's counts and bits, and the oracle on the tail suffix gives the whole
+    stream's output."""
+    import big_check as bc
+    rx = synth.c5_regexes()
+    d = synth.generate(synth.LONGJSON, 21, 0, 1_200_000, permille=300)
+    arr = np.frombuffer(d, np.uint8)
+    since = (synth.T0 + 1800, 0)
+    pats = po.compile_patterns(match=rx)
+    ref = po.filter_stream(d, since, 5, pats)
+    hit, parsed, since_ok = bc.py_line_table(arr, since, match=rx, procs=4)
+    assert (hit.size, parsed, since_ok, int(hit.sum())) == (ref.n_lines, ref.n_parsed, ref.n_since, ref.n_matched)
+    assert np.array_equal(bc.unpack_bits(ref.match_bits, ref.n_lines), hit)
+    starts = np.array(ref.line_off, dtype=np.uint64)
+    a = bc.tail_suffix(arr, starts, hit, 5)
+    assert a > 0 and po.filter_stream(d[a:], since, 5, pats).out == ref.out

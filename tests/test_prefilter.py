@@ -113,6 +113,49 @@ def test_gram_and_stride_choice(grep, match, q, stride):
     assert info["on"] and (info["q"], info["stride"]) == (q, stride), info
 
 
+def test_short_needles_anchored():
+    """Needles shorter than the stride-8 window (10 bytes) that share a rare byte ('_'):
+    anchored at it, the rest probed at stride 8; the decision still equals the full
+    matcher's on contents that hold the needles, their look-alikes and the anchor alone."""
+    rng = random.Random(11)
+    grep = [b"ab_cd1", b"xy_z9", b"q_rst", b"0123456789AB", b"longer needle here"]
+    match = [rb"tx=[0-9]{3}_end\d", rb"(?i)deadline exceeded after \d+s"]
+    _, info = E.debug_prefilter(b"", grep=grep, match=match)
+    assert info["on"] and info["stride"] == 8 and info["anchor"] == ord("_"), info
+    extra = [b"ab_cd1", b"xy_z9", b"q_rst", b"ab_cd", b"y_z9", b"_rst", b"0123456789AB", b"tx=123_end4",
+             b"tx=12_end4", b"_end7", b"DEADLINE exceeded after 5s", b"longer needle here", b"___", b"_"]
+    contents = []
+    for _ in range(400):
+        s = _text(rng, rng.randint(0, 50))
+        for _ in range(rng.randint(0, 3)):
+            k = rng.randint(0, len(s))
+            s = s[:k] + rng.choice(extra) + s[k:]
+        contents.append(s)
+    _check(grep, match, contents + extra)
+
+
+def test_c5_set_anchored(monkeypatch):
+    """The C5 regex set with its short factor family (`-commitN`, 8 bytes) anchored on
+    '-' (forced: without data statistics '-' counts as common): stride 8, equal decisions
+    on C5-shaped content."""
+    monkeypatch.setenv("KLF_QF_ANCHOR", "force")
+    rx = synth.c5_regexes()
+    _, info = E.debug_prefilter(b"", match=rx)
+    assert info["on"] and info["stride"] == 8 and info["q"] == 3 and info["anchor"] == ord("-"), info
+    rng = random.Random(12)
+    parts = [b"tx-0123abcd-commit5", b"tx-0123abc-commit5", b"-commit", b"tx--commit1", b"user3_id=u12345 login",
+             b"status=503 path=/api/v3/x", b"PANIC: foo error in mod3", b"shard2 deadline exceeded after 1.5s",
+             b"GET /v2/items/7 404", b"conn reset by peer3", b"OOMkilled for pid5=9", b"2024-10-22", b"a-b-c"]
+    contents = []
+    for _ in range(300):
+        s = _text(rng, rng.randint(0, 60))
+        for _ in range(rng.randint(0, 3)):
+            k = rng.randint(0, len(s))
+            s = s[:k] + rng.choice(parts) + s[k:]
+        contents.append(s)
+    _check([], rx, contents + parts)
+
+
 def test_c4_c5_sets_are_prefiltered():
     lits = synth.c4_literals(1024)
     assert len(lits) == 1024 and min(map(len, lits)) >= 6 and max(map(len, lits)) <= 24
