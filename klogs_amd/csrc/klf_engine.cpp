@@ -136,6 +136,7 @@ struct klf_engine {
   std::vector<SegDesc> last_segs;  // tile_seg cache key
   DevBuf d_tile_seg;
   DevBuf d_cmap, d_cseg;
+  DevBuf d_fstate;  // fused compaction turn records
   DevBuf d_batch, d_segs, d_tstat, d_slots, d_pool, d_tile_base, d_bsum, d_cstatus, d_counters, d_line_off,
       d_meta, d_bits, d_segout, d_wpre, d_out, d_mpart, d_trec, d_truns, d_kbase;
   uint64_t pool_cap = 1 << 20;
@@ -393,7 +394,7 @@ extern "C" void klf_close(klf_engine* e) {
                     &e->d_rx_follow, &e->d_rx_vec, &e->d_rx_flags, &e->d_rx_pre, &e->d_qf_bitmap, &e->d_qf_head,
                     &e->d_qf_ent, &e->d_qf_nbytes, &e->d_qf_anc, &e->d_rx_vec4, &e->d_qhits, &e->d_hslots, &e->d_hist, &e->d_hflat, &e->d_cand, &e->d_batch, &e->d_segs, &e->d_tstat,
                     &e->d_slots, &e->d_pool, &e->d_tile_base, &e->d_bsum, &e->d_cstatus, &e->d_counters, &e->d_cmap, &e->d_cseg,
-                    &e->d_line_off, &e->d_meta, &e->d_bits, &e->d_segout, &e->d_wpre, &e->d_out, &e->d_tile_seg, &e->d_mpart, &e->d_trec, &e->d_truns, &e->d_kbase})
+                    &e->d_fstate, &e->d_line_off, &e->d_meta, &e->d_bits, &e->d_segout, &e->d_wpre, &e->d_out, &e->d_tile_seg, &e->d_mpart, &e->d_trec, &e->d_truns, &e->d_kbase})
     b->release();
   e->d_asm.release();
   e->d_scratch.release();
@@ -735,6 +736,12 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
   HIPCHK(e, e->d_kbase.ensure(ntiles * 16), "alloc kbase");
   uint32_t compact_mode = 0;  // tests: force either compaction path
   if (const char* v = getenv("KLF_COMPACT")) compact_mode = !strcmp(v, "sparse") ? 1u : !strcmp(v, "dense") ? 2u : 0u;
+  // Fused compaction: every line is decided where it starts (--tail -1, no patterns), so
+  // the scan copies the output itself (one read of the input).  Off when a compaction
+  // path is forced (tests), with KLF_FUSE=0, or past the 1 TiB output offsets it records.
+  bool fused = mode == klf::CompiledSet::kNone && f->tail == -1 && compact_mode == 0 && total_bytes < (1ull << 40);
+  if (const char* v = getenv("KLF_FUSE")) fused = fused && strcmp(v, "0") != 0;
+  if (fused) HIPCHK(e, e->d_fstate.ensure(((ntiles + 3) / 4) * 8 + 16), "alloc fused turns");
   const bool need_cand = mode == klf::CompiledSet::kGeneral && e->cs.qf_on && e->cs.rx_count;
   if (need_cand) HIPCHK(e, e->d_cand.ensure((size_t)e->cand_cap * 16), "alloc cand");
   const bool need_hits = mode == klf::CompiledSet::kGeneral && e->cs.qf_on;
@@ -835,13 +842,15 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
     a.truns = e->d_truns.as<uint32_t>();
     a.kbase = e->d_kbase.as<uint64_t>();
     a.compact_mode = compact_mode;
+    a.fused = fused ? 1u : 0u;
+    a.fstate = fused ? e->d_fstate.as<uint64_t>() : nullptr;
     a.count_pats = count ? 1u : 0u;
     a.pcount = count ? e->d_pcount.as<uint32_t>() : nullptr;
     a.pairs = count ? e->d_pairs.as<uint64_t>() : nullptr;
     a.pairs_log2 = e->pairs_log2;
     HIPCHK(e, klf::launch_pipeline(a, st, e->ev, e->num_cus, e->aux_stream, e->ev_fork, e->ev_join), "launch");
     r->so.resize(nsegs);
-    uint32_t counters[16];
+    uint32_t counters[32];
     HIPCHK(e, e->h_rb.ensure(sizeof(counters) + nsegs * sizeof(SegOut)), "alloc readback");
     uint8_t* rb = e->h_rb.as<uint8_t>();
     HIPCHK(e, hipMemcpyAsync(rb, e->d_counters.p, sizeof(counters), hipMemcpyDeviceToHost, st), "D2H counters");
@@ -855,6 +864,11 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
       fprintf(stderr, "[klf] hits=%u spilled=%u hits_over=%u nfa_queue=%u queue_over=%u deferred=%u\n",
               counters[klf::kCtrVerified], counters[klf::kCtrHits], counters[klf::kCtrHitsOver],
               counters[klf::kCtrQueue], counters[klf::kCtrQOver], counters[5]);
+    if (fused && counters[klf::kCtrFuseBailHost]) {  // the fused scan met a case it leaves to the two passes
+      if (getenv("KLF_DIAG")) fprintf(stderr, "[klf] fused compaction bailed (%u): rerun unfused\n", counters[klf::kCtrFuseBailHost]);
+      fused = false;
+      continue;
+    }
     overflow = (counters[2] & 1u) != 0;
     if (overflow) {  // more lines (or dense-tile slots) than estimated: rerun with exact sizes
       if (line_reruns++) break;
@@ -936,6 +950,7 @@ extern "C" int klf_retail(klf_engine* e, klf_result* prev, int64_t tail, klf_res
   if (nsegs) {
     klf::RunArgs a = e->last_args;
     a.tail = tail;
+    a.fused = 0;  // re-tail: the two-pass compaction over the line index
     a.stage_times = 0;
     hipStream_t st = e->stream;
     hipError_t h = klf::launch_retail(a, st, e->ev, e->num_cus);
