@@ -2246,7 +2246,7 @@ __global__ __launch_bounds__(256) void k_init(RunArgs a) {
 struct WinLines {
   uint64_t src[4];
   uint32_t len[4], seg[4];
-  bool first[4], last[4];
+  bool first[4], last[4], sel[4];  // sel: selected (a fragment's content may be empty)
   uint64_t bytes;
   uint32_t nsel;
 };
@@ -2270,7 +2270,7 @@ __device__ __forceinline__ void window_lines(const RunArgs& a, uint64_t w0, uint
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const uint64_t wj = w0 + j;
-    r.len[j] = 0; r.src[j] = 0; r.first[j] = r.last[j] = false; r.seg[j] = s;
+    r.len[j] = 0; r.src[j] = 0; r.first[j] = r.last[j] = r.sel[j] = false; r.seg[j] = s;
     if (wj >= W) continue;
     while (wj >= a.wpre[s + 1]) ++s;
     r.seg[j] = s;
@@ -2279,6 +2279,7 @@ __device__ __forceinline__ void window_lines(const RunArgs& a, uint64_t w0, uint
     const uint64_t l = a.segout[s].win_lo + (wj - a.wpre[s]);
     const uint16_t m = a.meta[l];
     const bool sel = (m & Meta::kParsed) && (m & Meta::kSince) && gbit(a, l);
+    r.sel[j] = sel;
     if (sel) {
       const uint8_t* segp = a.bytes + a.segs[s].base;
       const uint64_t ls = a.line_off[l + s], le = a.line_off[l + s + 1];
@@ -2557,7 +2558,7 @@ __device__ __forceinline__ void cgather_body(RunArgs& a) {
       s_dst[i] = ob;
       s_len[i] = r.len[j];
       ob += r.len[j];
-      oc += r.len[j] ? 1 : 0;
+      oc += r.sel[j] ? 1 : 0;  // = k_csum's count (an empty fragment is still a line out)
       if (sub == 0 && r.last[j]) { a.segout[r.seg[j]].out_hi = ob; a.segout[r.seg[j]].sel_hi = oc; }
     }
     const uint64_t ob0 = a.csum[3 * blk];

@@ -33,6 +33,16 @@ def test_forced_paths_text_json(gpu, compact, since, tail, grep):
     check_against_c(streams, since, tail, grep)
 
 
+@pytest.mark.parametrize("tail", [-1, 0, 1, 3])
+def test_empty_content_fragment(gpu, compact, tail):
+    """A stream ending in a parsed fragment whose content is empty ("<ts> "): kubelet emits
+    it (no bytes) and it counts as a selected line, on both paths (and fused)."""
+    base = synth.generate(synth.TEXT, 44, 0, 30_000)
+    streams = [base + b"2024-10-22T00:59:59.5Z ", b"2024-10-22T00:00:01Z ", base + b"2024-10-22T00:59:59.5Z x\n"]
+    check_against_c(streams, None, tail, [])
+    check_against_c(streams, None, tail, [b""])
+
+
 @pytest.mark.parametrize("seed", range(3))
 def test_forced_paths_adversarial(gpu, compact, seed):
     """Unparseable lines, odd prefixes, CRLF, fragments, empty contents."""

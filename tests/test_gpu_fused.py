@@ -38,8 +38,16 @@ def check(streams, since=None, monkeypatch=None):
             assert got[i][1][k] == c[k], (i, k, got[i][1], c)
     if monkeypatch is not None:  # the two-pass compaction agrees
         monkeypatch.setenv("KLF_FUSE", "0")
-        assert run(streams, since) == got
+        two = run(streams, since)
         monkeypatch.delenv("KLF_FUSE")
+        for i in range(len(streams)):
+            if two[i][1] != got[i][1]:
+                raise AssertionError(f"stream {i}: counts fused {got[i][1]} two-pass {two[i][1]}")
+            if two[i][0] != got[i][0]:
+                a, b = two[i][0], got[i][0]
+                k = next((j for j in range(min(len(a), len(b))) if a[j] != b[j]), min(len(a), len(b)))
+                raise AssertionError(f"stream {i}: output fused {len(b)} B two-pass {len(a)} B, first diff at {k}: "
+                                     f"{b[max(0, k - 20):k + 20]!r} vs {a[max(0, k - 20):k + 20]!r}")
     return got
 
 
