@@ -32,15 +32,19 @@ using klf::SegOut;
 
 namespace {
 
+// time spent growing device buffers (KLF_DIAG: the first run's allocation share)
+static std::atomic<uint64_t> g_alloc_ns{0};
 struct DevBuf {
   void* p = nullptr;
   size_t cap = 0;
   hipError_t ensure(size_t bytes) {
     if (bytes <= cap && p) return hipSuccess;
+    const auto t0 = std::chrono::steady_clock::now();
     if (p) { (void)hipFree(p); p = nullptr; cap = 0; }
     size_t want = std::max<size_t>(bytes, 256);
     hipError_t e = hipMalloc(&p, want);
     if (e == hipSuccess) cap = want;
+    g_alloc_ns += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
     return e;
   }
   void release() {
@@ -635,6 +639,31 @@ static hipError_t wait_stream(hipStream_t st, uint64_t spin_us) {
   }
 }
 
+// Output bigger than the buffer (counters[kCtrOutShort], from k_cmove / k_tcopy, which
+// skipped the copies that would not fit but still wrote every stream's output range): grow
+// the buffer to the run's output and rerun the tail stage over the line index and bitmap
+// still in HBM (k_mcount .. k_tcopy, tens of us), then read the stream records back.
+static hipError_t grow_out_retail(klf_engine* e, klf::RunArgs& a, std::vector<SegOut>& so) {
+  for (int k = 0; k < 2; ++k) {
+    uint64_t need = 0;
+    for (auto& s : so) need = std::max(need, s.out_hi);
+    hipError_t h = e->d_out.ensure(need + 64);
+    if (h != hipSuccess) return h;
+    a.out = e->d_out.as<uint8_t>();
+    a.out_cap = e->d_out.cap;
+    a.fused = 0;
+    if ((h = klf::launch_retail(a, e->stream, e->ev, e->num_cus)) != hipSuccess) return h;
+    uint32_t* rb = static_cast<uint32_t*>(e->h_rb.p);  // counters, then the stream records
+    if ((h = hipMemcpyAsync(rb, e->d_counters.p, 32 * 4, hipMemcpyDeviceToHost, e->stream)) != hipSuccess) return h;
+    if ((h = hipMemcpyAsync(so.data(), e->d_segout.p, so.size() * sizeof(SegOut), hipMemcpyDeviceToHost,
+                            e->stream)) != hipSuccess)
+      return h;
+    if ((h = hipStreamSynchronize(e->stream)) != hipSuccess) return h;
+    if (!rb[klf::kCtrOutShort]) return hipSuccess;
+  }
+  return hipErrorOutOfMemory;  // the ranges did not settle (cannot happen: they do not depend on the buffer)
+}
+
 static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_streams, const uint64_t* seg_base,
                            const uint64_t* lens, const klf_filter* f, klf_result** out) {
   if (!e || !f || !out || (n_streams && (!seg_base || !lens))) return KLF_EINVAL;
@@ -642,6 +671,9 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
   if (f->since.nsec < 0 || f->since.nsec >= 1000000000) return set_err(e, KLF_EINVAL, "since.nsec out of range");
   if (reinterpret_cast<uintptr_t>(d_bytes) % 16) return set_err(e, KLF_EINVAL, "device bytes must be 16-B aligned");
   *out = nullptr;
+  const auto t_run0 = std::chrono::steady_clock::now();
+  const uint64_t alloc0 = g_alloc_ns.load();
+  uint64_t tune_ns = 0;
   HIPCHK(e, hipSetDevice(e->device), "hipSetDevice");
   std::unique_ptr<klf_result> rp(new (std::nothrow) klf_result());  // freed on every error return
   klf_result* r = rp.get();
@@ -698,6 +730,7 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
   if (mode == klf::CompiledSet::kGeneral && e->cs.qf_on && !e->cs.qf_tuned) {
     // first batch: place the needles' sampling windows on the data's own gram statistics
     e->cs.qf_tuned = true;
+    const auto t_tune0 = std::chrono::steady_clock::now();
     const char* tune = getenv("KLF_QF_TUNE");
     if (!tune || strcmp(tune, "0") != 0) {
       const size_t nh = klf::kGramHistWords;
@@ -711,6 +744,8 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
       klf::DataStats ds;
       ds.gram3.assign(hv, hv + klf::kQfHistBins);
       ds.gram4.assign(hv + klf::kQfHistBins, hv + 2 * klf::kQfHistBins);
+      for (auto& c : ds.gram3) c *= klf::kGramHistStride;  // grams were counted at every 4th position
+      for (auto& c : ds.gram4) c *= klf::kGramHistStride;
       ds.bytes.assign(256, 0);
       for (int c = 0; c < 256; ++c) {
         ds.bytes[c] = hv[2 * klf::kQfHistBins + c];
@@ -722,6 +757,7 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
                 e->cs.qf_layout.c_str());
       HIPCHK(e, upload_prefilter(e), "upload prefilter tables");
     }
+    tune_ns = (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t_tune0).count();
   }
   HIPCHK(e, e->d_tstat.ensure(ntiles * sizeof(klf::TileStat)), "alloc tstat");
   HIPCHK(e, e->d_slots.ensure(ntiles * klf::kRecStride * 4), "alloc slots");
@@ -730,18 +766,28 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
   HIPCHK(e, e->d_counters.ensure(klf::kNumCounters * 4), "alloc counters");
   HIPCHK(e, e->d_segout.ensure(nsegs * sizeof(SegOut)), "alloc segout");
   HIPCHK(e, e->d_wpre.ensure((nsegs + 1) * 8), "alloc wpre");
-  HIPCHK(e, e->d_out.ensure(total_bytes + 64), "alloc out");
   HIPCHK(e, e->d_trec.ensure(ntiles * sizeof(klf::TRec)), "alloc trec");
   HIPCHK(e, e->d_truns.ensure(ntiles * klf::kRunSlots * 4), "alloc truns");
   HIPCHK(e, e->d_kbase.ensure(ntiles * 16), "alloc kbase");
   uint32_t compact_mode = 0;  // tests: force either compaction path
   if (const char* v = getenv("KLF_COMPACT")) compact_mode = !strcmp(v, "sparse") ? 1u : !strcmp(v, "dense") ? 2u : 0u;
-  // Fused compaction: every line is decided where it starts (--tail -1, no patterns), so
-  // the scan copies the output itself (one read of the input).  Off when a compaction
-  // path is forced (tests), with KLF_FUSE=0, or past the 1 TiB output offsets it records.
-  bool fused = mode == klf::CompiledSet::kNone && f->tail == -1 && compact_mode == 0 && total_bytes < (1ull << 40);
-  if (const char* v = getenv("KLF_FUSE")) fused = fused && strcmp(v, "0") != 0;
+  // Fused compaction (opt-in, KLF_FUSE=1): every line is decided where it starts (--tail -1,
+  // no patterns), so the scan can copy the output itself and read the input once.  Not the
+  // default: on MI355X the decoupled look-back it needs per workgroup turn waits on
+  // cross-XCD loads of several us under full HBM load, and the turn tiles it holds in LDS
+  // leave no room to overlap them (C3: 5.2-10 ms fused vs 5.9 ms two-pass; DESIGN.md
+  // section 4).  Off when a compaction path is forced (tests) or past 1 TiB of output.
+  bool fused = false;
+  if (const char* v = getenv("KLF_FUSE"))
+    fused = strcmp(v, "0") != 0 && mode == klf::CompiledSet::kNone && f->tail == -1 && compact_mode == 0 &&
+            total_bytes < (1ull << 40);
   if (fused) HIPCHK(e, e->d_fstate.ensure(((ntiles + 3) / 4) * 8 + 16), "alloc fused turns");
+  // The output buffer: sized for the whole input up front when the run keeps about as much
+  // as it reads (no --tail limit: C3-like; the fused scan writes it as it goes), else grown
+  // on demand -- the compaction skips a copy that would not fit, the host grows the buffer
+  // to the run's output and reruns the tail stage (first runs only: the buffer is kept).
+  // A --tail run then never maps an input-sized buffer (34 GB for C4 / C5).
+  if (fused || f->tail < 0) HIPCHK(e, e->d_out.ensure(total_bytes + 64), "alloc out");
   const bool need_cand = mode == klf::CompiledSet::kGeneral && e->cs.qf_on && e->cs.rx_count;
   if (need_cand) HIPCHK(e, e->d_cand.ensure((size_t)e->cand_cap * 16), "alloc cand");
   const bool need_hits = mode == klf::CompiledSet::kGeneral && e->cs.qf_on;
@@ -829,6 +875,7 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
     a.segout = e->d_segout.as<SegOut>();
     a.wpre = e->d_wpre.as<uint64_t>();
     a.out = e->d_out.as<uint8_t>();
+    a.out_cap = e->d_out.p ? e->d_out.cap : 0;
     a.max_cblocks = (uint32_t)max_cblocks;
     a.stage_times = (f->flags & KLF_FILTER_STAGE_TIMES) ? 1u : 0u;
     a.cand = need_cand ? e->d_cand.as<uint64_t>() : nullptr;
@@ -864,6 +911,10 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
       fprintf(stderr, "[klf] hits=%u spilled=%u hits_over=%u nfa_queue=%u queue_over=%u deferred=%u\n",
               counters[klf::kCtrVerified], counters[klf::kCtrHits], counters[klf::kCtrHitsOver],
               counters[klf::kCtrQueue], counters[klf::kCtrQOver], counters[5]);
+    if (fused && getenv("KLF_DIAG") && counters[29])
+      fprintf(stderr, "[klf] fused turns: %u workgroups, Kcycles per workgroup: scan %.1f look-back %.1f copy %.1f; rounds %u spins %u\n",
+              counters[29], (double)counters[24] / counters[29], (double)counters[25] / counters[29],
+              (double)counters[26] / counters[29], counters[27], counters[28]);
     if (fused && counters[klf::kCtrFuseBailHost]) {  // the fused scan met a case it leaves to the two passes
       if (getenv("KLF_DIAG")) fprintf(stderr, "[klf] fused compaction bailed (%u): rerun unfused\n", counters[klf::kCtrFuseBailHost]);
       fused = false;
@@ -886,6 +937,10 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
       e->pairs_log2 = lg;
       continue;
     }
+    if (counters[klf::kCtrOutShort]) {  // the output did not fit: grow, rerun the tail stage
+      HIPCHK(e, grow_out_retail(e, a, r->so), "grow output");
+      if (getenv("KLF_DIAG")) fprintf(stderr, "[klf] output buffer grown to %zu B\n", e->d_out.cap);
+    }
     e->last_args = a;
     e->last_gen = r->gen;
     break;
@@ -894,6 +949,11 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
     r->pcount.resize((size_t)nsegs * e->cs.n_cids);
     HIPCHK(e, hipMemcpy(r->pcount.data(), e->d_pcount.p, r->pcount.size() * 4, hipMemcpyDeviceToHost), "D2H pcount");
     r->pcount_ok = true;
+  }
+  if (getenv("KLF_DIAG")) {
+    const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t_run0).count();
+    fprintf(stderr, "[klf] run %.1f us: allocations %.1f us, first-batch tuning %.1f us\n", us,
+            (g_alloc_ns.load() - alloc0) / 1e3, tune_ns / 1e3);
   }
   if (overflow)  // the exact rerun overflowed too: never hand out the aborted run's records
     return set_err(e, KLF_ENOMEM, "line index / dense-tile pool overflow after the exact rerun");
@@ -954,8 +1014,13 @@ extern "C" int klf_retail(klf_engine* e, klf_result* prev, int64_t tail, klf_res
     a.stage_times = 0;
     hipStream_t st = e->stream;
     hipError_t h = klf::launch_retail(a, st, e->ev, e->num_cus);
+    uint32_t short_out = 0;
     if (h == hipSuccess) h = hipMemcpyAsync(r->so.data(), e->d_segout.p, nsegs * sizeof(SegOut), hipMemcpyDeviceToHost, st);
+    if (h == hipSuccess) h = hipMemcpyAsync(e->h_rb.p, e->d_counters.p, 32 * 4, hipMemcpyDeviceToHost, st);
     if (h == hipSuccess) h = hipStreamSynchronize(st);
+    if (h == hipSuccess) short_out = static_cast<uint32_t*>(e->h_rb.p)[klf::kCtrOutShort];
+    if (h == hipSuccess && short_out) h = grow_out_retail(e, a, r->so);  // a larger window than the buffer holds
+    if (h == hipSuccess) e->last_args = a;
     if (h != hipSuccess) { delete r; return hip_err(e, h, "klf_retail"); }
     float ms;
     if (hipEventElapsedTime(&ms, e->ev[0], e->ev[5]) == hipSuccess) r->ms[4] = ms;

@@ -393,6 +393,12 @@ __device__ __forceinline__ bool parse_fast(const uint8_t* lds, uint32_t o, const
 #ifndef KLF_ABL
 #define KLF_ABL 0
 #endif
+#ifndef KLF_FSTATIC
+#define KLF_FSTATIC 0  // timing builds: fused turns assigned round-robin instead of claimed
+#endif
+#ifndef KLF_FDIAG
+#define KLF_FDIAG 0  // timing builds: per-phase cycle sums of the fused scan (counters[24..29])
+#endif
 #ifndef KLF_CG_NT
 #define KLF_CG_NT 0
 #endif
@@ -490,9 +496,14 @@ __global__ __launch_bounds__(kThreads, (MODE == kScanGen || FUSE) ? 3 : KLF_SCAN
   uint32_t cur = 0, nxt = 0;
   if constexpr (FUSE) {
     if (t == 0) {
+#if KLF_FSTATIC
+      s_fagg[0] = blockIdx.x;
+      s_fagg[1] = blockIdx.x + gridDim.x;
+#else
       const uint32_t c0 = atomicAdd(&a.counters[kCtrTurn], 1u);
       s_fagg[0] = c0;
       s_fagg[1] = atomicAdd(&a.counters[kCtrTurn], 1u);
+#endif
     }
     __syncthreads();
     cur = __builtin_amdgcn_readfirstlane((uint32_t)s_fagg[0]);
@@ -524,8 +535,15 @@ __global__ __launch_bounds__(kThreads, (MODE == kScanGen || FUSE) ? 3 : KLF_SCAN
     __builtin_amdgcn_raw_buffer_store_b32(0u, none, 0x7FFF0000u, 0, 0);
   }
   bool any_defer = false;
+#if KLF_FDIAG
+  uint64_t fd_scan = 0, fd_look = 0, fd_copy = 0, fd_t0 = 0;
+  uint32_t fd_rounds = 0, fd_spins = 0;
+#endif
   for (;; tile = FUSE ? tile : next_tile(tile)) {  // (fused: the turn section moves on)
     if (FUSE ? cur >= nturns : tile >= a.ntiles) break;
+#if KLF_FDIAG
+    fd_t0 = __builtin_readcyclecounter();
+#endif
     // fused: the turn's aggregate of this tile (identity for a wave past the last tile)
     FAgg fa{0u, 0u, -1, false, false};
     bool f_ok = false;  // the line list can be read back for the copy
@@ -802,12 +820,12 @@ __global__ __launch_bounds__(kThreads, (MODE == kScanGen || FUSE) ? 3 : KLF_SCAN
         Probe r;
         r.h = mul_u24(f, 0x9E3779u);
         if (QQ == 4) r.h = mad_u24(gf >> 8, 0x7F4A7Du, r.h);  // + bytes 1..3 * C2
-        r.p = mul_hi_u24(f, 0xC2B2AEu);
+        r.p = QK == 3 ? mul_hi_u24(f, 0xC2B2AEu) : 0u;  // K = 2: both bits from m (qf_bits)
         r.m = mul_u24(f, 0x5BD1E9u);
         return r;
       };
       auto test = [&](uint32_t w, const Probe& r) __attribute__((always_inline)) -> uint32_t {
-        uint32_t t = (w >> ((r.m >> 24) & 31u)) & (w >> (r.p & 31u));
+        uint32_t t = (w >> ((r.m >> 24) & 31u)) & (w >> (QK == 3 ? (r.p & 31u) : ((r.m >> 16) & 31u)));
         if (QK == 3) t &= w >> ((r.h >> 16) & 31u);
         return t;
       };
@@ -1011,41 +1029,93 @@ __global__ __launch_bounds__(kThreads, (MODE == kScanGen || FUSE) ? 3 : KLF_SCAN
       // ---- the turn: combine the four tiles, publish, look back, copy ----
       if (lane == 0) s_fagg[wv] = f_pack_a(fa);
       __syncthreads();
-      if (wv == 0 && lane == 0) {
+#if KLF_FDIAG
+      const uint64_t fd_t1 = __builtin_readcyclecounter();
+      fd_scan += fd_t1 - fd_t0;
+#endif
+      if (wv == 0) {
+        // the look-back by one wave: lane i reads turn hi - i, one round of loads covers 64
+        // turns.  (Measured on C3: a 512-turn window read by the whole workgroup made each
+        // round ~3x slower for half the rounds; one thread walking a turn per load, 2x
+        // slower.)
         FAgg ta = f_unpack_a(s_fagg[0]);
         for (int k = 1; k < kWaves; ++k) ta = f_combine(ta, f_unpack_a(s_fagg[k]));
         FPre p{0ull, -1, false};
         if (cur > 0) {
-          __hip_atomic_store(&a.fstate[cur], f_pack_a(ta), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          FAgg acc{0u, 0u, -1, false, false};  // the aggregates between the prefix found and this turn
-          uint32_t q = cur - 1;
+          if (lane == 0) __hip_atomic_store(&a.fstate[cur], f_pack_a(ta), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          FAgg acc{0u, 0u, -1, false, false};  // the aggregates between the window and this turn
+          int64_t hi = (int64_t)cur - 1;
+          const uint64_t p0 = f_pack_p(FPre{0ull, -1, false});  // before turn 0: nothing out
           for (uint32_t spins = 0;;) {
-            const uint64_t v = __hip_atomic_load(&a.fstate[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const int64_t q = hi - lane;
+            const uint64_t v = q >= 0 ? __hip_atomic_load(&a.fstate[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : p0;
             const uint32_t st = (uint32_t)(v >> 62);
-            if (st == 2u) { p = f_apply(f_unpack_p(v), acc); break; }
-            if (st == 1u) {
-              acc = f_combine(f_unpack_a(v), acc);
-              if (q == 0) { p = f_apply(p, acc); break; }  // (turn 0 publishes its prefix at once)
-              --q;
+            const uint64_t m2 = __ballot(st == 2u), m0 = __ballot(st == 0u);
+            const uint32_t pl = m2 ? (uint32_t)__builtin_ctzll(m2) : 64u;  // nearest prefix
+            const uint64_t below = pl >= 64u ? ~0ull : ((1ull << pl) - 1ull);
+            if (m0 & below) {  // a turn in between has not published: read the window again
+              if (++spins > (1u << 18)) {  // a turn never published: fail the run, never hang
+                if (lane == 0) atomicOr(&a.counters[kCtrFuseBail], 2u);
+                p = f_apply(p, acc);
+                break;
+              }
+#if KLF_FDIAG
+              ++fd_spins;
+#endif
+              __builtin_amdgcn_s_sleep(1);
               continue;
             }
-            if (++spins > (1u << 22)) {  // a turn never published: fail the run, never hang
-              atomicOr(&a.counters[kCtrFuseBail], 2u);
-              p = f_apply(p, acc);
+#if KLF_FDIAG
+            ++fd_rounds;
+#endif
+            // lanes [0, pl) in time order (lane pl - 1 earliest): a reduction toward lane 0
+            FAgg x = (uint32_t)lane < pl ? f_unpack_a(v) : FAgg{0u, 0u, -1, false, false};
+#pragma unroll
+            for (int d = 1; d < 64; d <<= 1) {
+              FAgg y;
+              y.bytes = (uint32_t)__shfl_down((int)x.bytes, d, 64);
+              y.span = (uint32_t)__shfl_down((int)x.span, d, 64);
+              y.crel = __shfl_down(x.crel, d, 64);
+              const int fl = __shfl_down((x.has ? 1 : 0) | (x.sel ? 2 : 0), d, 64);
+              y.has = fl & 1;
+              y.sel = (fl & 2) != 0;
+              if (lane + d < 64) x = f_combine(y, x);
+            }
+            FAgg w;
+            w.bytes = (uint32_t)__builtin_amdgcn_readfirstlane((int)x.bytes);
+            w.span = (uint32_t)__builtin_amdgcn_readfirstlane((int)x.span);
+            w.crel = __builtin_amdgcn_readfirstlane(x.crel);
+            w.has = __builtin_amdgcn_readfirstlane(x.has ? 1 : 0) != 0;
+            w.sel = __builtin_amdgcn_readfirstlane(x.sel ? 1 : 0) != 0;
+            acc = f_combine(w, acc);
+            if (pl < 64u) {
+              const uint64_t pv = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), (int)pl) << 32) |
+                                  (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, (int)pl);
+              p = f_apply(f_unpack_p(pv), acc);
               break;
             }
-            __builtin_amdgcn_s_sleep(1);
+            hi -= 64;
           }
         }
-        FPre pk = p;
-        for (int k = 0; k < kWaves; ++k) {
-          s_fpre[k] = pk;
-          pk = f_apply(pk, f_unpack_a(s_fagg[k]));
+        if (lane == 0) {
+          FPre pk = p;
+          for (int k = 0; k < kWaves; ++k) {
+            s_fpre[k] = pk;
+            pk = f_apply(pk, f_unpack_a(s_fagg[k]));
+          }
+          __hip_atomic_store(&a.fstate[cur], f_pack_p(pk), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#if KLF_FSTATIC
+          s_fturn = nxt + gridDim.x;
+#else
+          s_fturn = atomicAdd(&a.counters[kCtrTurn], 1u);
+#endif
         }
-        __hip_atomic_store(&a.fstate[cur], f_pack_p(pk), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        s_fturn = atomicAdd(&a.counters[kCtrTurn], 1u);
       }
       __syncthreads();
+#if KLF_FDIAG
+      const uint64_t fd_t2 = __builtin_readcyclecounter();
+      fd_look += fd_t2 - fd_t1;
+#endif
       if (tile < a.ntiles && f_ok) {  // the kept runs: the carried-in line's, then the lines'
         const FPre pin = s_fpre[wv];
         uint32_t* runs = s_frun[wv];
@@ -1079,8 +1149,21 @@ __global__ __launch_bounds__(kThreads, (MODE == kScanGen || FUSE) ? 3 : KLF_SCAN
       cur = nxt;
       nxt = __builtin_amdgcn_readfirstlane(s_fturn);
       tile = cur * kWaves + wv;
+#if KLF_FDIAG
+      fd_copy += __builtin_readcyclecounter() - fd_t2;
+#endif
     }
   }
+#if KLF_FDIAG
+  if (FUSE && lane == 0 && wv == 0) {  // cycles summed over workgroups (wave 0), in 2^10 units
+    atomicAdd(&a.counters[24], (uint32_t)(fd_scan >> 10));
+    atomicAdd(&a.counters[25], (uint32_t)(fd_look >> 10));
+    atomicAdd(&a.counters[26], (uint32_t)(fd_copy >> 10));
+    atomicAdd(&a.counters[27], fd_rounds);
+    atomicAdd(&a.counters[28], fd_spins);
+    atomicAdd(&a.counters[29], 1u);
+  }
+#endif
   if (any_defer && lane == 0 && !abl) a.counters[kCtrDefer] = 1u;
   if (KLF_ABL != 0 && lane == 0) atomicAdd(&g_abl_waves, 1u);
 #undef ABL
@@ -2215,7 +2298,10 @@ __device__ __forceinline__ void wprefix_body(RunArgs& a) {
 // Re-tail (klf_retail): clears what k_mcount .. k_cgather accumulate into the segment
 // records, leaving the line index, the parse/since counts and the match bitmap of the run.
 __global__ __launch_bounds__(256) void k_retail_init(RunArgs a) {
-  if (blockIdx.x == 0 && threadIdx.x == 0) a.counters[kCtrTailDone] = 0;  // k_tailw's tickets
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    a.counters[kCtrTailDone] = 0;  // k_tailw's tickets
+    a.counters[kCtrOutShort] = 0;
+  }
   for (uint32_t s = blockIdx.x * 256 + threadIdx.x; s < a.nsegs; s += gridDim.x * 256) {
     SegOut& so = a.segout[s];
     so.matched = 0;
@@ -2605,6 +2691,10 @@ __device__ __forceinline__ void cgather_body(RunArgs& a) {
       }
     }
     __syncthreads();
+    if (c1 + 16 > a.out_cap) {  // the buffer is too small: the host grows it and reruns
+      if (t == 0) atomicOr(&a.counters[kCtrOutShort], 1u);
+      continue;
+    }
     if (!(KLF_ABL & 1024)) block_gather_copy(s_src, s_dst, s_len, s_map, c0, c1, a.bytes, a.out);
   }
 }
@@ -3121,6 +3211,10 @@ __global__ __launch_bounds__(256) void k_tcopy(RunArgs a, const uint4* __restric
       nr = list_runs(a, g, a.segout[g.s].win_lo, a.segout[g.s].win_hi, s_run, kTcRuns, lane, &kept, &nsel);
     }
     if (KLF_TC_ABL & 2) continue;
+    if (obase + cr.kept + 16 > a.out_cap) {  // the buffer is too small: the host grows it and reruns
+      if (lane == 0) atomicOr(&a.counters[kCtrOutShort], 1u);
+      continue;
+    }
     copy_tile_runs(s_buf, s_run, s_map, nr, cr.kept, obase, a.out, lane);
     asm volatile("" ::: "memory");  // the next tile rewrites the wave's LDS
   }
@@ -3130,10 +3224,10 @@ __global__ __launch_bounds__(256) void k_tcopy(RunArgs a, const uint4* __restric
 #undef KLF_TC_STORE
 }
 
-// Data statistics for the prefilter's layout and window choice (one-off, first batch):
-// every byte position of a sample of the batch into the 3-gram and 4-gram count-min
-// sketches (two rows each, global atomics) and the byte histogram (LDS per block, one
-// global add per bin and block).
+// Data statistics for the prefilter's layout and window choice (one-off, first batch): the
+// grams at every 4th byte position of a sample of the batch into the 3-gram and 4-gram
+// count-min sketches (two rows each, global atomics: they bound the pass) and every byte
+// into the histogram (LDS per block, one global add per bin and block).
 __global__ __launch_bounds__(256) void k_gramhist(const uint8_t* bytes, const SegDesc* segs, uint32_t nsegs,
                                                   uint64_t sample, uint32_t fold, uint32_t* hist) {
   __shared__ uint32_t s_b[256];
@@ -3147,17 +3241,15 @@ __global__ __launch_bounds__(256) void k_gramhist(const uint8_t* bytes, const Se
     const uint64_t o = (w % per) * 4;
     if (o + 8 > sd.len) continue;
     const uint32_t* p = reinterpret_cast<const uint32_t*>(bytes + sd.base + o);
-    const uint32_t w0 = p[0], w1 = p[1];
+    const uint32_t w0 = p[0];
+    static_assert(kGramHistStride == 4, "one gram per dword");
+    const uint32_t g = w0 | fold, g3 = g & 0xFFFFFFu;  // (the host scales the counts by 4)
+    atomicAdd(&hist[qf_hist_bin0(g3)], 1u);
+    atomicAdd(&hist[qf_hist_bin1(g3)], 1u);
+    atomicAdd(&hist[kQfHistBins + qf_hist_bin0(g)], 1u);
+    atomicAdd(&hist[kQfHistBins + qf_hist_bin1(g)], 1u);
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const uint32_t g = (k ? __builtin_amdgcn_alignbyte(w1, w0, k) : w0) | fold;
-      const uint32_t g3 = g & 0xFFFFFFu;
-      atomicAdd(&hist[qf_hist_bin0(g3)], 1u);
-      atomicAdd(&hist[qf_hist_bin1(g3)], 1u);
-      atomicAdd(&hist[kQfHistBins + qf_hist_bin0(g)], 1u);
-      atomicAdd(&hist[kQfHistBins + qf_hist_bin1(g)], 1u);
-      atomicAdd(&s_b[(w0 >> (8 * k)) & 0xFFu], 1u);
-    }
+    for (int k = 0; k < 4; ++k) atomicAdd(&s_b[(w0 >> (8 * k)) & 0xFFu], 1u);
   }
   __syncthreads();
   if (s_b[threadIdx.x]) atomicAdd(&hist[2 * kQfHistBins + threadIdx.x], s_b[threadIdx.x]);

@@ -60,6 +60,7 @@ constexpr uint32_t kCtrTailDone = 18;                // counters[18]: k_tailw bl
 constexpr uint32_t kCtrFuseBailHost = 21;            // counters[21]: the fused scan bailed (= klf_kernels.hip kCtrFuseBail)
 constexpr uint32_t kCtrVerified = 10;                // counters[10]: hits k_verify walked (diagnostics)
 constexpr uint32_t kCtrDense = 14;                   // counters[14]: dense compaction (k_tkeep / k_tcopy)
+constexpr uint32_t kCtrOutShort = 22;                // counters[22]: the output did not fit out_cap
 constexpr uint32_t kCtrPairsOver = 15;               // counters[15]: failed (line, pattern) pair inserts (set full)
 constexpr uint32_t kQfRegex = 1u << 24;              // entry flags: regex factor (else literal)
 constexpr uint32_t kQfLoose = 1u << 25;              //   compare OR 0x20 per byte
@@ -72,8 +73,10 @@ constexpr uint32_t kRxPreNone = 0xFFFFFFFFu;         // rx_pre: no bound (= klf_
 // reaches the low product bits too):
 //   h    = f * C1 (+ bytes 1..3 * C2 for 4-byte grams): 24-bit multiply(-add)s, low 32
 //          bits; word = h >> 20, also the verification bucket;
-//   p    = the high half of f * C3 (v_mul_hi_u32_u24), m = f * C4;
-//   bits = K = 2: m bits 24..28, p bits 0..4; K = 3: p bits 0..4, h bits 16..20, m bits 24..28.
+//   m    = f * C4, p = the high half of f * C3 (v_mul_hi_u32_u24, K = 3 only);
+//   bits = K = 2: m bits 24..28 and 16..20 (no third multiply: the C5 set's hits on C5 data
+//          74 vs 70 per 32 MiB); K = 3: p bits 0..4, h bits 16..20, m bits 24..28 (m bits
+//          16..20 in place of p: 11x the C4 hits).
 // The scan takes every bit position as a byte / word select of a product (SDWA operands of
 // the shifts) or its low bits, so a probe costs about 10 VALU (K = 2) / 13 (K = 3); the
 // previous design cost ~14 / ~18.  Measured on the C4 / C5 sets and data (host emulation,
@@ -90,9 +93,10 @@ __host__ __device__ inline uint32_t qf_hash(uint32_t g, uint32_t w24, uint32_t k
 __host__ __device__ inline uint32_t qf_word(uint32_t h) { return h >> (32 - kQfBucketBits); }
 __host__ __device__ inline uint32_t qf_bits(uint32_t g, uint32_t h, uint32_t k) {
   const uint32_t f = qf_f(g, k);
-  const uint32_t p = (uint32_t)(((uint64_t)f * 0xC2B2AEu) >> 32), m = f * 0x5BD1E9u;
-  const uint32_t b = (1u << ((m >> 24) & 31u)) | (1u << (p & 31u));
-  return k == 3 ? b | (1u << ((h >> 16) & 31u)) : b;
+  const uint32_t m = f * 0x5BD1E9u;
+  if (k != 3) return (1u << ((m >> 24) & 31u)) | (1u << ((m >> 16) & 31u));
+  const uint32_t p = (uint32_t)(((uint64_t)f * 0xC2B2AEu) >> 32);
+  return (1u << ((m >> 24) & 31u)) | (1u << (p & 31u)) | (1u << ((h >> 16) & 31u));
 }
 // Gram statistics of the window choice: a count-min sketch, 2 rows of 2^16 bins, for the
 // 3-byte and for the 4-byte grams, then a byte histogram (k_gramhist)
@@ -100,6 +104,9 @@ constexpr int kQfHistBits = 16;
 constexpr uint32_t kQfHistBins = 2u << kQfHistBits;
 constexpr uint32_t kGramHistWords = 2 * kQfHistBins + 256;
 constexpr uint64_t kGramHistSample = 64u << 10;  // bytes sampled per segment (<= 16 segments)
+// grams counted at every kGramHistStride-th position of the sample (the host scales the
+// counts back): a quarter of the global atomics, which bound the one-off pass
+constexpr uint32_t kGramHistStride = 4;
 __host__ __device__ inline uint32_t qf_h1(uint32_t g) { return (g ^ (g >> 13)) * 0x9E3779B1u; }
 __host__ __device__ inline uint32_t qf_hist_bin0(uint32_t g) { return qf_h1(g) >> (32 - kQfHistBits); }
 __host__ __device__ inline uint32_t qf_hist_bin1(uint32_t g) {
@@ -237,7 +244,9 @@ struct RunArgs {
   uint64_t cap_lines;
   SegOut* segout;       // [nsegs]
   uint64_t* wpre;       // [nsegs + 1] exclusive prefix of window sizes
-  uint8_t* out;         // output bytes (capacity >= total input)
+  uint8_t* out;         // output bytes
+  uint64_t out_cap;     // bytes of `out`: a copy that would pass it is skipped and flagged
+                        // (counters[kCtrOutShort]); the host grows the buffer and reruns the tail stage
   uint32_t max_cblocks; // compaction block capacity
   uint32_t stage_times; // record the inner stage events (ev[2..4])
   uint64_t* cand;       // [2 * cand_cap] NFA candidates: {global line index | regex << 40,

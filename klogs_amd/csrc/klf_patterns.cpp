@@ -9,6 +9,7 @@
 #include <cstring>
 #include <map>
 #include <set>
+#include <unordered_map>
 #include <queue>
 
 #include "../../include/klf.h"
@@ -1310,6 +1311,18 @@ void place_tables(CompiledSet& out, const DataStats* st);
 // statistics the cheapest by layout_cost wins; without them (klf_open, before any batch)
 // the widest stride, then the rarest anchor.
 void place_needles(CompiledSet& out, const DataStats* st) {
+  // the matcher tables play no part in the layout: kept aside while the candidates are
+  // copied (a 1,024-literal set's AC automaton is megabytes per copy)
+  std::vector<uint32_t> ac_next, ac_dict;
+  std::vector<uint8_t> ac_accept;
+  std::vector<int32_t> ac_out;
+  std::vector<uint64_t> rx_b, rx_follow;
+  ac_next.swap(out.ac_next);
+  ac_dict.swap(out.ac_dict);
+  ac_accept.swap(out.ac_accept);
+  ac_out.swap(out.ac_out);
+  rx_b.swap(out.rx_b);
+  rx_follow.swap(out.rx_follow);
   CompiledSet best;
   double best_cost = 0;
   bool have = false;
@@ -1335,6 +1348,7 @@ void place_needles(CompiledSet& out, const DataStats* st) {
       char buf[64];
       snprintf(buf, sizeof buf, " [est %.0f VALU/tile]", cost);
       c.qf_layout += buf;
+      if (getenv("KLF_DIAG")) fprintf(stderr, "[klf] layout candidate (variant %u): %s\n", v, c.qf_layout.c_str());
       if (!have || cost < best_cost) {
         best = std::move(c);
         best_cost = cost;
@@ -1342,6 +1356,12 @@ void place_needles(CompiledSet& out, const DataStats* st) {
       }
     }
   out = std::move(best);
+  out.ac_next.swap(ac_next);
+  out.ac_dict.swap(ac_dict);
+  out.ac_accept.swap(ac_accept);
+  out.ac_out.swap(ac_out);
+  out.rx_b.swap(rx_b);
+  out.rx_follow.swap(rx_follow);
 }
 
 namespace {
@@ -1372,7 +1392,8 @@ void place_tables(CompiledSet& out, const DataStats* st) {
     if (strchr("\":,=./{}-TZ", c) && c) return 3;                                  // JSON / timestamp punctuation
     return 1;  // upper case, '_', other punctuation, control and high bytes
   };
-  std::map<uint32_t, int> used;  // gram -> needles sampling it so far
+  std::unordered_map<uint32_t, int> used;  // gram -> needles sampling it so far
+  used.reserve(out.qf_needle.size() * S * 2);
   std::vector<std::vector<uint32_t>> buckets(kQfWords);
   const size_t n = out.qf_needle.size();
   size_t nprobed = 0;
@@ -1447,16 +1468,17 @@ void data_stats(const uint8_t* p, size_t n, uint32_t fold, DataStats& st) {
   st.bytes.assign(256, 0u);
   st.nbytes = 0;
   for (size_t i = 0; i + 4 <= n; ++i) {
+    st.bytes[p[i]]++;
+    st.nbytes++;
+    if (i % kGramHistStride) continue;  // grams at every 4th position, counted 4 times (k_gramhist)
     uint32_t g = 0;
     for (int b = 0; b < 4; ++b) g |= (uint32_t)p[i + b] << (8 * b);
     g |= fold;
     const uint32_t g3 = g & 0xFFFFFFu;
-    st.gram3[qf_hist_bin0(g3)]++;
-    st.gram3[qf_hist_bin1(g3)]++;
-    st.gram4[qf_hist_bin0(g)]++;
-    st.gram4[qf_hist_bin1(g)]++;
-    st.bytes[p[i]]++;
-    st.nbytes++;
+    st.gram3[qf_hist_bin0(g3)] += kGramHistStride;
+    st.gram3[qf_hist_bin1(g3)] += kGramHistStride;
+    st.gram4[qf_hist_bin0(g)] += kGramHistStride;
+    st.gram4[qf_hist_bin1(g)] += kGramHistStride;
   }
 }
 

@@ -1,0 +1,15 @@
+#!/bin/bash
+# GPU suite, cold-run diagnostics of C4/C5, then the default bench
+set -e
+cd "$(dirname "$0")/.."
+out=$1; mkdir -p $out
+export TMPDIR=/tmp
+timeout -k 10 500 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $out/pytest_gpu.log 2>&1
+tail -1 $out/pytest_gpu.log
+for c in c5 c4; do
+  KLF_DIAG=1 timeout -k 10 240 python3 scripts/run_config.py $c --steps 2 > $out/diag_$c.json 2> $out/diag_$c.err
+  grep -E "run [0-9.]+ us|grown" $out/diag_$c.err | head -4
+  python3 -c "import json; d=json.load(open('$out/diag_$c.json')); print('$c', d['roofline']['avg_launch_ms'], d['device_ms_per_step'], d.get('cold'))"
+done
+timeout -k 10 400 python bench.py > $out/bench.json 2> $out/bench.err
+echo done

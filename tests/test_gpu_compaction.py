@@ -157,3 +157,27 @@ def test_c3_full_per_gpu_batch(gpu):
     with ThreadPoolExecutor(8) as ex:
         bad = [i for i, ok in ex.map(check, range(n_streams)) if not ok]
     assert not bad, f"streams differ from the oracle: {bad[:10]}"
+
+
+@pytest.mark.parametrize("tails", [(100, -1, 10**9), (0, 5, -1), (10**9, 3, -1)])
+def test_output_buffer_grown_on_demand(gpu, compact, tails):
+    """A --tail run sizes the output buffer to its output (the copy that would not fit is
+    skipped, the buffer grown, the tail stage rerun); a fresh engine's first run and a
+    re-tail to a larger window (klf_retail) both take that path, bit-exact."""
+    streams = [synth.generate(synth.TEXT, 61, i, 400_000 + 50_000 * i) for i in range(5)]
+    with E.Engine(0, grep=[]) as eng:
+        eng.set_streams(len(streams))
+        for i, s in enumerate(streams):
+            eng.stage(i, s)
+        r = eng.run(tail=tails[0], n_streams=len(streams))
+        for k, tail in enumerate(tails):
+            if k:
+                r2 = r.retail(tail)
+                r.free()
+                r = r2
+            for i, s in enumerate(streams):
+                out, _, _, c = co.filter_stream(s, co.GO_ZERO_TIME, tail, [], want_lines=False, want_bits=False)
+                g = r.stream(i)
+                assert g.out == out, (tail, i, len(g.out), len(out))
+                assert g.counts["selected"] == c["selected"], (tail, i)
+        r.free()

@@ -1,6 +1,7 @@
 """The fused compaction (k_scan<plain, fused>: --tail -1 without patterns, the copy done by
-the scan through a look-back over workgroup turns) against the C oracle and against the
-two-pass compaction (KLF_FUSE=0) on the same batches: tiles whose carried-in line starts
+the scan through a look-back over workgroup turns; opt-in with KLF_FUSE=1, which every test
+here sets) against the C oracle and against the two-pass compaction (the default) on the
+same batches: tiles whose carried-in line starts
 many tiles back, prefixes that straddle tile boundaries, non-canonical timestamps parsed in
 the scan, unparseable lines, dense tiles, fragments, streams shorter than a turn, and the
 since cutoff.  Anchor: the per-stream output of writeLogToDisk (cmd/root.go:359-374) under
@@ -15,6 +16,11 @@ from klogs_amd import engine as E
 from klogs_amd import synth
 
 pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(autouse=True)
+def fused_on(monkeypatch):
+    monkeypatch.setenv("KLF_FUSE", "1")
 
 
 def run(streams, since=None, tail=-1):
@@ -39,7 +45,7 @@ def check(streams, since=None, monkeypatch=None):
     if monkeypatch is not None:  # the two-pass compaction agrees
         monkeypatch.setenv("KLF_FUSE", "0")
         two = run(streams, since)
-        monkeypatch.delenv("KLF_FUSE")
+        monkeypatch.setenv("KLF_FUSE", "1")
         for i in range(len(streams)):
             if two[i][1] != got[i][1]:
                 raise AssertionError(f"stream {i}: counts fused {got[i][1]} two-pass {two[i][1]}")
