@@ -1181,7 +1181,7 @@ double byte_share(uint32_t c, uint32_t fold, const DataStats* st) {
 // Picks the layout: all needles probed at the stride of the shortest, or (when that
 // stride is below 8 and the needles shorter than 10 bytes share a rare byte) the long
 // needles probed at stride 8 and the short ones anchored.
-void choose_layout(CompiledSet& out, const DataStats* st, bool allow_anchor) {
+void choose_layout(CompiledSet& out, const DataStats* st, bool allow_anchor, uint32_t qmax = 4) {
   const auto& nd = out.qf_needle;
   const size_t n = nd.size();
   size_t minlen = SIZE_MAX, minlong = SIZE_MAX;
@@ -1191,6 +1191,7 @@ void choose_layout(CompiledSet& out, const DataStats* st, bool allow_anchor) {
   }
   uint32_t S, q;
   stride_rule(minlen, S, q);
+  q = std::min(q, qmax);
   out.qf_anc_on = false;
   out.qf_anc_pre.clear();
   out.qf_nshort.assign(n, 0);
@@ -1200,6 +1201,7 @@ void choose_layout(CompiledSet& out, const DataStats* st, bool allow_anchor) {
   if (allow_anchor && S < 8 && minlong != SIZE_MAX && !(env && !strcmp(env, "0"))) {
     uint32_t Sl, ql;
     stride_rule(minlong, Sl, ql);
+    ql = std::min(ql, qmax);
     uint32_t afold = 0;
     for (size_t i = 0; i < n; ++i)
       if (nd[i].size() < 10 && (out.qf_nflags[i] & kQfLoose)) afold = 0x20202020u;
@@ -1291,7 +1293,10 @@ double layout_cost(const CompiledSet& c, const DataStats& st) {
   for (uint32_t g : grams) hit_share += share(sk, g);
   const double samples = 8192.0 / c.qf_stride;
   double hits = samples * std::min(1.0, hit_share);
-  double cost = 11.0 * samples / 64.0;
+  // VALU per probe (scan ISA): ~8 for a 3-byte gram with two bits, + 2 for the fourth byte
+  // (shift + multiply-add), + 3 for the third bit (folded gram, mul_hi, shift)
+  const double per_probe = 8.0 + (c.qf_q == 4 ? 2.0 : 0.0) + (c.qf_k == 3 ? 3.0 : 0.0);
+  double cost = per_probe * samples / 64.0;
   if (c.qf_anc_on) {
     cost += 60.0;
     double pass = 0;
@@ -1327,7 +1332,12 @@ void place_needles(CompiledSet& out, const DataStats* st) {
   double best_cost = 0;
   bool have = false;
   for (uint32_t v = 0; v < out.qf_variants.size(); ++v)
-    for (int anchored = 0; anchored < 2; ++anchored) {
+    for (int cand = 0; cand < 4; ++cand) {
+      const int anchored = cand & 1;
+      const uint32_t qmax = cand < 2 ? 4u : 3u;  // 3-byte grams: a cheaper probe, more hits
+      if (qmax == 3 && !(st && st->nbytes)) continue;  // (only the data can say whether they pay)
+      if (const char* qv = getenv("KLF_QF_QMAX"))  // ablation: one gram length at the data's layout
+        if (st && st->nbytes && (uint32_t)atoi(qv) != qmax) continue;
       CompiledSet c = out;
       const auto& ns = c.qf_variants[v];
       c.qf_variant = v;
@@ -1336,7 +1346,7 @@ void place_needles(CompiledSet& out, const DataStats* st) {
       c.qf_nrx = ns.rx;
       c.qf_needles = (uint32_t)ns.s.size();
       c.rx_pre = ns.rx_pre;
-      choose_layout(c, st, anchored != 0);
+      choose_layout(c, st, anchored != 0, qmax);
       if (anchored && !c.qf_anc_on) continue;  // nothing to anchor: same as the probed layout
       place_tables(c, st);
       double cost;
@@ -1355,7 +1365,7 @@ void place_needles(CompiledSet& out, const DataStats* st) {
         have = true;
       }
     }
-  out = std::move(best);
+  if (have) out = std::move(best);  // (every candidate skipped: the layout stays as it was)
   out.ac_next.swap(ac_next);
   out.ac_dict.swap(ac_dict);
   out.ac_accept.swap(ac_accept);
