@@ -811,8 +811,9 @@ __global__ __launch_bounds__(kThreads, (MODE == kScanGen || FUSE) ? 3 : KLF_SCAN
       // qf_bits): the multiplies, the word read, and the bit positions as byte / word selects
       // or low bits of the products (SDWA operands of the shifts)
       struct Probe {
-        uint32_t h, p, m;
+        uint32_t h, p, m, a;  // a: byte offset of the bitmap word in LDS (qf_bucket * 4)
       };
+      constexpr bool kMidIdx = QQ == 3 && QK == 2;  // word from h bits 18..29 (qf_bucket)
       // (the 24-bit multiplies ignore bits 24..31 of f: no mask)
       auto probe = [&](uint32_t g) __attribute__((always_inline)) -> Probe {
         const uint32_t gf = g | fold;
@@ -822,7 +823,11 @@ __global__ __launch_bounds__(kThreads, (MODE == kScanGen || FUSE) ? 3 : KLF_SCAN
         if (QQ == 4) r.h = mad_u24(gf >> 8, 0x7F4A7Du, r.h);  // + bytes 1..3 * C2
         r.p = QK == 3 ? mul_hi_u24(f, 0xC2B2AEu) : 0u;  // K = 2: both bits from m (qf_bits)
         r.m = mul_u24(f, 0x5BD1E9u);
+        r.a = kMidIdx ? ((r.h >> 16) & ((kQfWords - 1u) << 2)) : ((r.h >> (32 - kQfBucketBits)) << 2);
         return r;
+      };
+      auto word = [&](const Probe& r) __attribute__((always_inline)) -> uint32_t {
+        return *reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(s_qf) + r.a);
       };
       auto test = [&](uint32_t w, const Probe& r) __attribute__((always_inline)) -> uint32_t {
         uint32_t t = (w >> ((r.m >> 24) & 31u)) & (w >> (QK == 3 ? (r.p & 31u) : ((r.m >> 16) & 31u)));
@@ -831,7 +836,7 @@ __global__ __launch_bounds__(kThreads, (MODE == kScanGen || FUSE) ? 3 : KLF_SCAN
       };
       auto hbits = [&](uint32_t g) __attribute__((always_inline)) -> uint32_t {
         const Probe r = probe(g);
-        return test(s_qf[r.h >> (32 - kQfBucketBits)], r);
+        return test(word(r), r);
       };
       // the samples of chunk c (16 B) -> their grams, in order (QS = 8: dwords 0 and 2)
       auto chunk_grams = [&](uint32_t c, auto&& f) __attribute__((always_inline)) {
@@ -865,7 +870,7 @@ __global__ __launch_bounds__(kThreads, (MODE == kScanGen || FUSE) ? 3 : KLF_SCAN
 #pragma unroll
           for (int k = 0; k < 8; ++k) r[k] = probe(g[k]);
 #pragma unroll
-          for (int k = 0; k < 8; ++k) w[k] = s_qf[r[k].h >> (32 - kQfBucketBits)];
+          for (int k = 0; k < 8; ++k) w[k] = word(r[k]);
           uint32_t acc_a = 0, acc_b = 0;
 #pragma unroll
           for (int k = 0; k < 8; ++k) {
@@ -1738,7 +1743,7 @@ __device__ void verify_hit(const RunArgs& a, uint32_t tile, uint32_t s, int32_t 
   const SegDesc sd = a.segs[s];
   const int64_t rel_lo = (int64_t)(tile - sd.tile0) * kTile;
   const uint32_t g = (gword(a.bytes + sd.base + rel_lo + p) | P.qf_fold) & P.qf_mask;
-  const uint32_t b = qf_word(qf_hash(g, P.qf_w24, P.qf_k));
+  const uint32_t b = qf_bucket(g, P.qf_w24, P.qf_k);
   verify_hit_from(a, tile, s, sd, p, P.qf_head[b], P.qf_head[b + 1]);
 }
 
@@ -1774,7 +1779,7 @@ __global__ __launch_bounds__(256) void k_verify(RunArgs a) {
     }
 #pragma unroll
     for (int u = 0; u < kVerifyBatch; ++u) {
-      const uint32_t b = qf_word(qf_hash((gg[u] | P.qf_fold) & P.qf_mask, P.qf_w24, P.qf_k));
+      const uint32_t b = qf_bucket((gg[u] | P.qf_fold) & P.qf_mask, P.qf_w24, P.qf_k);
       e0[u] = P.qf_head[b];
       e1[u] = P.qf_head[b + 1];
     }

@@ -91,6 +91,15 @@ __host__ __device__ inline uint32_t qf_hash(uint32_t g, uint32_t w24, uint32_t k
   return qf_f(g, k) * 0x9E3779u + hi * 0x7F4A7Du;
 }
 __host__ __device__ inline uint32_t qf_word(uint32_t h) { return h >> (32 - kQfBucketBits); }
+// The bitmap word (= verification bucket) of gram g: h's top 12 bits, or for 3-byte grams
+// with two bits (no bit position taken from h) bits 18..29, whose LDS byte offset
+// (h >> 16) & 0x3FFC is one SDWA AND -- a VALU fewer per probe; the C5 set's bitmap hits
+// on C5 data are unchanged (96 per 32 MiB either way).  (Bits 34..45 of a second product,
+// v_mul_hi_u32_u24: 54x the hits -- a product's top bits follow the gram's top byte.)
+__host__ __device__ inline uint32_t qf_bucket(uint32_t g, uint32_t w24, uint32_t k) {
+  if (w24 == 0 && k == 2) return (qf_hash(g, w24, k) >> 18) & (kQfWords - 1u);
+  return qf_word(qf_hash(g, w24, k));
+}
 __host__ __device__ inline uint32_t qf_bits(uint32_t g, uint32_t h, uint32_t k) {
   const uint32_t f = qf_f(g, k);
   const uint32_t m = f * 0x5BD1E9u;

@@ -1414,7 +1414,7 @@ void place_tables(CompiledSet& out, const DataStats* st) {
     const std::string& s = out.qf_needle[i];
     if (out.qf_nshort[i]) {  // anchored: the bucket of the gram at the anchor
       const uint32_t k = out.qf_nanc[i], g = gram_at(s, k);
-      buckets[qf_word(qf_hash(g, w24, out.qf_k))].push_back(i << 8 | k);
+      buckets[qf_bucket(g, w24, out.qf_k)].push_back(i << 8 | k);
       continue;
     }
     const uint32_t amax = (uint32_t)std::min<size_t>(s.size() - (q + S - 1), 255 - (S - 1));
@@ -1441,8 +1441,9 @@ void place_tables(CompiledSet& out, const DataStats* st) {
       const uint32_t k = best_a + j, g = gram_at(s, k);
       used[g]++;
       const uint32_t h = qf_hash(g, w24, out.qf_k);
-      out.qf_bitmap[qf_word(h)] |= qf_bits(g, h, out.qf_k);
-      buckets[qf_word(h)].push_back(i << 8 | k);
+      const uint32_t bw = qf_bucket(g, w24, out.qf_k);
+      out.qf_bitmap[bw] |= qf_bits(g, h, out.qf_k);
+      buckets[bw].push_back(i << 8 | k);
     }
   }
   // needle bytes (loose needles are already stored OR 0x20), then 16-B entries per bucket
@@ -1503,7 +1504,7 @@ PrefilterHits prefilter_hits(const CompiledSet& cs, const uint8_t* s, size_t n) 
       ++r.probes;
       const uint32_t gq = (g | cs.qf_fold) & cs.qf_mask;
       const uint32_t h = qf_hash(gq, w24, cs.qf_k), bits = qf_bits(gq, h, cs.qf_k);
-      hit = (cs.qf_bitmap[qf_word(h)] & bits) == bits;
+      hit = (cs.qf_bitmap[qf_bucket(gq, w24, cs.qf_k)] & bits) == bits;
       r.bitmap_hits += hit;
     }
     if (!hit && cs.qf_anc_on && ((uint32_t)s[p] | (cs.qf_anc_fold & 0xFFu)) == cs.qf_anc_byte) {
@@ -1512,7 +1513,7 @@ PrefilterHits prefilter_hits(const CompiledSet& cs, const uint8_t* s, size_t n) 
       r.anchor_hits += hit;
     }
     if (!hit) continue;
-    const uint32_t b = qf_word(qf_hash((g | cs.qf_fold) & cs.qf_mask, w24, cs.qf_k));
+    const uint32_t b = qf_bucket((g | cs.qf_fold) & cs.qf_mask, w24, cs.qf_k);
     for (uint32_t e = cs.qf_head[b]; e < cs.qf_head[b + 1]; ++e) {
       const uint32_t* E = cs.qf_ent.data() + 4 * (size_t)e;
       const uint32_t m = E[1] & 0xFFFFu, k = (E[1] >> 16) & 0xFFu;
@@ -1560,14 +1561,14 @@ bool prefilter_match(const CompiledSet& cs, const uint8_t* s, size_t n, uint32_t
     if (p % S == phase % S) {
       const uint32_t gq = (g | cs.qf_fold) & cs.qf_mask;
       const uint32_t h = qf_hash(gq, cs.qf_q == 4 ? 24u : 0u, cs.qf_k), bits = qf_bits(gq, h, cs.qf_k);
-      hit = (cs.qf_bitmap[qf_word(h)] & bits) == bits;
+      hit = (cs.qf_bitmap[qf_bucket(gq, cs.qf_q == 4 ? 24u : 0u, cs.qf_k)] & bits) == bits;
     }
     if (!hit && cs.qf_anc_on && ((uint32_t)s[p] | (cs.qf_anc_fold & 0xFFu)) == cs.qf_anc_byte)
       for (size_t j = 0; j + 1 < cs.qf_anc_pre.size() && !hit; j += 2)
         hit = ((g | cs.qf_fold) & cs.qf_anc_pre[j + 1]) == cs.qf_anc_pre[j];
     if (!hit) continue;
     g = (g | cs.qf_fold) & cs.qf_mask;
-    const uint32_t b = qf_word(qf_hash(g, cs.qf_q == 4 ? 24u : 0u, cs.qf_k));
+    const uint32_t b = qf_bucket(g, cs.qf_q == 4 ? 24u : 0u, cs.qf_k);
     for (uint32_t e = cs.qf_head[b]; e < cs.qf_head[b + 1]; ++e) {
       const uint32_t* E = cs.qf_ent.data() + 4 * (size_t)e;
       const uint32_t m = E[1] & 0xFFFFu, k = (E[1] >> 16) & 0xFFu;
