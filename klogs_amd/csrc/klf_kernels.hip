@@ -322,6 +322,14 @@ __device__ __forceinline__ uint32_t bfe_u32(uint32_t a, uint32_t off, uint32_t w
   asm("v_bfe_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "n"(off), "n"(width));
   return r;
 }
+// w >> ((h >> 8) & 31) in one instruction (the shift amount as an SDWA byte select; the
+// compiler emits a separate shift for it)
+__device__ __forceinline__ uint32_t shr_byte1(uint32_t w, uint32_t h) {
+  uint32_t r;
+  asm("v_lshrrev_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_1 src1_sel:DWORD"
+      : "=v"(r) : "v"(h), "v"(w));
+  return r;
+}
 // v_mad_u32_u24: a * b + c for a, b < 2^24 (low 32 bits of the product)
 __device__ __forceinline__ uint32_t mad24(uint32_t a, uint32_t b, uint32_t c) { return __umul24(a, b) + c; }
 
@@ -821,8 +829,8 @@ __global__ __launch_bounds__(kThreads, (MODE == kScanGen || FUSE) ? 3 : KLF_SCAN
         Probe r;
         r.h = mul_u24(f, 0x9E3779u);
         if (QQ == 4) r.h = mad_u24(gf >> 8, 0x7F4A7Du, r.h);  // + bytes 1..3 * C2
-        r.p = QK == 3 ? mul_hi_u24(f, 0xC2B2AEu) : 0u;  // K = 2: both bits from m (qf_bits)
-        r.m = mul_u24(f, 0x5BD1E9u);
+        r.p = QK == 3 ? mul_hi_u24(f, 0xC2B2AEu) : 0u;  // K = 2: both bits from h (qf_bits)
+        r.m = QK == 3 ? mul_u24(f, 0x5BD1E9u) : 0u;
         r.a = kMidIdx ? ((r.h >> 16) & ((kQfWords - 1u) << 2)) : ((r.h >> (32 - kQfBucketBits)) << 2);
         return r;
       };
@@ -830,7 +838,8 @@ __global__ __launch_bounds__(kThreads, (MODE == kScanGen || FUSE) ? 3 : KLF_SCAN
         return *reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(s_qf) + r.a);
       };
       auto test = [&](uint32_t w, const Probe& r) __attribute__((always_inline)) -> uint32_t {
-        uint32_t t = (w >> ((r.m >> 24) & 31u)) & (w >> (QK == 3 ? (r.p & 31u) : ((r.m >> 16) & 31u)));
+        uint32_t t = QK == 3 ? (w >> ((r.m >> 24) & 31u)) & (w >> (r.p & 31u))
+                             : shr_byte1(w, r.h) & (w >> ((r.h >> 16) & 31u));
         if (QK == 3) t &= w >> ((r.h >> 16) & 31u);
         return t;
       };

@@ -73,10 +73,10 @@ constexpr uint32_t kRxPreNone = 0xFFFFFFFFu;         // rx_pre: no bound (= klf_
 // reaches the low product bits too):
 //   h    = f * C1 (+ bytes 1..3 * C2 for 4-byte grams): 24-bit multiply(-add)s, low 32
 //          bits; word = h >> 20, also the verification bucket;
-//   m    = f * C4, p = the high half of f * C3 (v_mul_hi_u32_u24, K = 3 only);
-//   bits = K = 2: m bits 24..28 and 16..20 (no third multiply: the C5 set's hits on C5 data
-//          74 vs 70 per 32 MiB); K = 3: p bits 0..4, h bits 16..20, m bits 24..28 (m bits
-//          16..20 in place of p: 11x the C4 hits).
+//   m    = f * C4, p = the high half of f * C3 (v_mul_hi_u32_u24) (K = 3 only);
+//   bits = K = 2: h bits 8..12 and 16..20 (byte selects of h: no second multiply; the C5
+//          set's hits on C5 data 115 vs 96 per 32 MiB with m's bytes); K = 3: p bits 0..4,
+//          h bits 16..20, m bits 24..28 (m bits 16..20 in place of p: 11x the C4 hits).
 // The scan takes every bit position as a byte / word select of a product (SDWA operands of
 // the shifts) or its low bits, so a probe costs about 10 VALU (K = 2) / 13 (K = 3); the
 // previous design cost ~14 / ~18.  Measured on the C4 / C5 sets and data (host emulation,
@@ -103,7 +103,7 @@ __host__ __device__ inline uint32_t qf_bucket(uint32_t g, uint32_t w24, uint32_t
 __host__ __device__ inline uint32_t qf_bits(uint32_t g, uint32_t h, uint32_t k) {
   const uint32_t f = qf_f(g, k);
   const uint32_t m = f * 0x5BD1E9u;
-  if (k != 3) return (1u << ((m >> 24) & 31u)) | (1u << ((m >> 16) & 31u));
+  if (k != 3) return (1u << ((h >> 8) & 31u)) | (1u << ((h >> 16) & 31u));
   const uint32_t p = (uint32_t)(((uint64_t)f * 0xC2B2AEu) >> 32);
   return (1u << ((m >> 24) & 31u)) | (1u << (p & 31u)) | (1u << ((h >> 16) & 31u));
 }

@@ -1293,9 +1293,10 @@ double layout_cost(const CompiledSet& c, const DataStats& st) {
   for (uint32_t g : grams) hit_share += share(sk, g);
   const double samples = 8192.0 / c.qf_stride;
   double hits = samples * std::min(1.0, hit_share);
-  // VALU per probe (scan ISA): ~8 for a 3-byte gram with two bits, + 2 for the fourth byte
-  // (shift + multiply-add), + 3 for the third bit (folded gram, mul_hi, shift)
-  const double per_probe = 8.0 + (c.qf_q == 4 ? 2.0 : 0.0) + (c.qf_k == 3 ? 3.0 : 0.0);
+  // VALU per probe (the scan's ISA, its unrolled fast pass / 32 probes): 6.9 for a 3-byte
+  // gram with two bits (fold, multiply, word offset, two shifts, and / or), 9.9 with the
+  // fourth byte, 13.4 for 3 bits (folded gram, two more multiplies, a shift)
+  const double per_probe = 7.0 + (c.qf_q == 4 ? 3.0 : 0.0) + (c.qf_k == 3 ? 6.5 : 0.0);
   double cost = per_probe * samples / 64.0;
   if (c.qf_anc_on) {
     cost += 60.0;
