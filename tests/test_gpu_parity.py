@@ -326,3 +326,41 @@ def test_staging_across_pinned_chunks(gpu):
                 assert so.out == want, (rep, i)
                 assert so.counts["lines"] == wc["lines"] and so.counts["selected"] == wc["selected"]
             r.free()
+
+
+def test_short_lines_regex_set_first_attempt_overflows(gpu):
+    """Lines averaging under 32 B overflow the first attempt's line capacity (estimated at
+    one line per 32 B).  With a regex set k_verify runs beside k_scatter (side stream), so
+    the overflow must be raised before either indexes the match bitmap by line (the r03a
+    fault: k_verify wrote bits[] past cap_lines); a fresh engine per case, so every run
+    starts from the estimate.  Output equal to the Python oracle."""
+    rng = random.Random(17)
+    parts = []
+    for i in range(60000):
+        k = rng.random()
+        parts.append(b"\n" if k < 0.55 else b"x\n" if k < 0.7 else
+                     b"2024-10-22T00:00:%02dZ %s\n" % (i % 60, rng.choice([b"pod x", b"took 7ms", b"q"])))
+    d = b"".join(parts)
+    assert len(d) / d.count(b"\n") < 32
+    for grep, match in [([b"pod x"], [rb"took \d+ms"]), ([], [rb"took \d+ms", rb"(?i)POD"])]:
+        check_against_py([d, d[:9000], b""], None, -1, grep, match)
+        check_against_py([d], (synth.T0 + 30, 0), 25, grep, match)
+
+
+def test_clamped_capacity_with_regex_set_fails_cleanly(gpu, monkeypatch):
+    """A line capacity clamped on every attempt (KLF_DEBUG_CAP_CLAMP) with a regex set:
+    the run fails with KLF_ENOMEM, nothing past the arrays is touched, and the engine
+    stays usable (advisor r02)."""
+    d = synth.generate(synth.TEXT, 8, 0, 300_000)
+    rx = [rb"pod=\d+", rb"(?i)TIMEOUT \w+", rb"took \d+ms"]
+    monkeypatch.setenv("KLF_DEBUG_CAP_CLAMP", "40")
+    with E.Engine(0, match=rx) as eng:
+        eng.stage(0, d)
+        with pytest.raises(E.KlfError) as ei:
+            eng.run(n_streams=1)
+        assert ei.value.code == E.KLF_ENOMEM
+        monkeypatch.delenv("KLF_DEBUG_CAP_CLAMP")
+        r = eng.run(n_streams=1)
+        ref = po.filter_stream(d, GZ, -1, po.compile_patterns([], rx))
+        assert r.stream(0).out == ref.out
+        r.free()
