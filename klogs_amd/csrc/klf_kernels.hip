@@ -237,7 +237,7 @@ __device__ __forceinline__ FAgg f_unpack_a(uint64_t v) {
 __device__ __forceinline__ uint64_t f_pack_p(const FPre& p) {
   return (2ull << 62) | (p.off & 0xFFFFFFFFFFull) | ((uint64_t)p.sel << 40) | ((uint64_t)(uint16_t)(int16_t)p.crel << 41);
 }
-__device__ __forceinline__ void copy_tile_runs(const uint8_t* s_buf, uint32_t* s_run, uint32_t* s_map, uint32_t nr,
+__device__ __forceinline__ void copy_tile_runs(const uint8_t* s_buf, uint32_t* s_run, uint16_t* s_map, uint32_t nr,
                                                uint32_t kept, uint64_t obase, uint8_t* out, int lane);
 __device__ __forceinline__ FPre f_unpack_p(uint64_t v) {
   FPre p;
@@ -448,7 +448,7 @@ __global__ __launch_bounds__(kThreads, (MODE == kScanGen || FUSE) ? 3 : KLF_SCAN
   // fused copy: per wave the tile's kept runs and chunk map; per workgroup the turn's tile
   // aggregates, the waves' entering prefixes, the next claimed turn
   __shared__ uint32_t s_frun[FUSE ? kWaves : 1][FUSE ? kTcRuns : 1];
-  __shared__ __attribute__((aligned(16))) uint32_t s_fmap[FUSE ? kWaves : 1][FUSE ? kTcChunks : 1];
+  __shared__ __attribute__((aligned(16))) uint16_t s_fmap[FUSE ? kWaves : 1][FUSE ? kTcChunks : 1];
   __shared__ uint64_t s_fagg[FUSE ? kWaves : 1];
   __shared__ FPre s_fpre[FUSE ? kWaves : 1];
   __shared__ uint32_t s_fturn;
@@ -2982,44 +2982,46 @@ __global__ __launch_bounds__(256) void k_cmove(RunArgs a) {
 // scratch.  Every 16-B output chunk holding only this tile's bytes is built from <= 2 runs
 // (five dword LDS reads + v_alignbyte each, branch-free blend) and stored once; the two
 // edge chunks shared with the neighbouring tiles are stored bytewise in one instruction.
-__device__ __forceinline__ void copy_tile_runs(const uint8_t* s_buf, uint32_t* s_run, uint32_t* s_map, uint32_t nr,
+__device__ __forceinline__ void copy_tile_runs(const uint8_t* s_buf, uint32_t* s_run, uint16_t* s_map, uint32_t nr,
                                                uint32_t kept, uint64_t obase, uint8_t* out, int lane) {
   const uint32_t* s32 = reinterpret_cast<const uint32_t*>(s_buf - 16);  // dword k = s_buf[4k - 16]
   const uint32_t o15 = (uint32_t)(obase & 15u);
   const uint32_t nch = (uint32_t)(((obase + kept + 15) >> 4) - (obase >> 4));
   // chunk c covers output [16 * (obase / 16 + c), +16); its first byte inside this tile's
-  // output, x0(c) = (c ? 16c - o15 : 0), lies in exactly one run.  The map: run k marks
-  // the first chunk whose x0 is at or past its start (LDS max: several short runs may
-  // mark one chunk; the last of them holds x0), then a running max over the chunks.
+  // output, x0(c) = (c ? 16c - o15 : 0), lies in exactly one run.  The map (u16): run k
+  // marks the first chunk whose x0 is at or past its start; several short runs may mark
+  // one chunk, and as the runs ascend the last of them (the one holding x0) is the one
+  // whose successor marks a later chunk: it alone stores (no LDS atomics).  Then a
+  // running max over the chunks.
     // two sentinel runs past the last (start = kept) spare the bounds checks below
     if (lane < 2) s_run[nr + lane] = kept << 16;
-    for (uint32_t c = 8 * (uint32_t)lane; c < nch; c += 512) {
-      *reinterpret_cast<uint4*>(&s_map[c]) = make_uint4(0, 0, 0, 0);
-      *reinterpret_cast<uint4*>(&s_map[c + 4]) = make_uint4(0, 0, 0, 0);
-    }
+    for (uint32_t c = 8 * (uint32_t)lane; c < nch; c += 512) *reinterpret_cast<uint4*>(&s_map[c]) = make_uint4(0, 0, 0, 0);
     wave_lds_sync();
+    auto mark = [&](uint32_t d) { return d ? (d + o15 + 15) >> 4 : 0u; };
     for (uint32_t k = lane; k < nr; k += 64) {
-      const uint32_t d = s_run[k] >> 16;
-      const uint32_t c = d ? (d + o15 + 15) >> 4 : 0u;
-      if (c < nch) atomicMax(&s_map[c], k);
+      const uint32_t c = mark(s_run[k] >> 16);
+      // (the sentinel run nr marks chunk nch exactly: a chunk it shares is past the output)
+      if (c < nch && mark(s_run[k + 1] >> 16) != c) s_map[c] = (uint16_t)k;
     }
     wave_lds_sync();
-    // running max: 8 consecutive entries per lane, one wave scan of the lanes' maxima
+    // running max: 8 consecutive entries per lane (one 16-B LDS access), one wave scan of
+    // the lanes' maxima
     for (uint32_t c0 = 0, carry = 0; c0 < nch; c0 += 512) {
       const uint32_t c = c0 + 8 * (uint32_t)lane;
-      uint4 p = *reinterpret_cast<const uint4*>(&s_map[c]), q = *reinterpret_cast<const uint4*>(&s_map[c + 4]);
+      const uint4 pk = *reinterpret_cast<const uint4*>(&s_map[c]);
+      uint32_t v[8] = {pk.x & 0xFFFFu, pk.x >> 16, pk.y & 0xFFFFu, pk.y >> 16,
+                       pk.z & 0xFFFFu, pk.z >> 16, pk.w & 0xFFFFu, pk.w >> 16};
       auto mx = [](uint32_t x, uint32_t y) { return x > y ? x : y; };
-      p.y = mx(p.y, p.x); p.z = mx(p.z, p.y); p.w = mx(p.w, p.z);
-      q.x = mx(q.x, p.w); q.y = mx(q.y, q.x); q.z = mx(q.z, q.y); q.w = mx(q.w, q.z);
-      const uint32_t incl = mx(wave_incl_scan_max(q.w, lane), carry);
+#pragma unroll
+      for (int q = 1; q < 8; ++q) v[q] = mx(v[q], v[q - 1]);
+      const uint32_t incl = mx(wave_incl_scan_max(v[7], lane), carry);
       uint32_t pre = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)incl, 0x138, 0xF, 0xF, false);  // wave_shr:1
       pre = mx(lane ? pre : 0u, carry);
-      p.x = mx(p.x, pre); p.y = mx(p.y, pre); p.z = mx(p.z, pre); p.w = mx(p.w, pre);
-      q.x = mx(q.x, pre); q.y = mx(q.y, pre); q.z = mx(q.z, pre); q.w = mx(q.w, pre);
-      if (c < nch) {
-        *reinterpret_cast<uint4*>(&s_map[c]) = p;
-        *reinterpret_cast<uint4*>(&s_map[c + 4]) = q;
-      }
+#pragma unroll
+      for (int q = 0; q < 8; ++q) v[q] = mx(v[q], pre);
+      if (c < nch)
+        *reinterpret_cast<uint4*>(&s_map[c]) =
+            make_uint4(v[0] | (v[1] << 16), v[2] | (v[3] << 16), v[4] | (v[5] << 16), v[6] | (v[7] << 16));
       carry = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
     }
     wave_lds_sync();
@@ -3134,18 +3136,25 @@ __device__ __forceinline__ void copy_tile_runs(const uint8_t* s_buf, uint32_t* s
 // a piece start up to 15 B before its chunk and end up to 20 B after it), the kept runs
 // (a selected line carries a >= 20-B prefix, so at most kTile / 20 + 2 runs), and the
 // chunk -> first run map.
-__global__ __launch_bounds__(256) void k_tcopy(RunArgs a, const uint4* __restrict__ trec,
+// Workgroups of kTcWaves waves (no workgroup barrier: each wave owns its tiles and LDS).
+// Measured on C3 (same box): 4-wave workgroups, 12 waves per CU, 5.52 ms per step;
+// 2-wave (14 per CU) 5.70, 1-wave (14 per CU) 5.73 -- more copy waves per CU slow it.
+#ifndef KLF_TC_WAVES
+#define KLF_TC_WAVES 4
+#endif
+constexpr int kTcWaves = KLF_TC_WAVES;
+__global__ __launch_bounds__(64 * kTcWaves) void k_tcopy(RunArgs a, const uint4* __restrict__ trec,
                                                const uint64_t* __restrict__ kbase, const uint32_t* __restrict__ truns) {
-  __shared__ __attribute__((aligned(16))) uint8_t s_buf_all[4][kTile + 48];
-  __shared__ uint32_t s_run_all[4][kTcRuns];
-  __shared__ __attribute__((aligned(16))) uint32_t s_map_all[4][kTcChunks];
+  __shared__ __attribute__((aligned(16))) uint8_t s_buf_all[kTcWaves][kTile + 48];
+  __shared__ uint32_t s_run_all[kTcWaves][kTcRuns];
+  __shared__ __attribute__((aligned(16))) uint16_t s_map_all[kTcWaves][kTcChunks];
   if (a.counters[2] || !a.counters[kCtrDense]) return;
   const int lane = threadIdx.x & 63;
   const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   uint8_t* s_buf = s_buf_all[wv] + 16;
   uint32_t* s_run = s_run_all[wv];
-  uint32_t* s_map = s_map_all[wv];
-  const uint32_t stride = gridDim.x * 4;
+  uint16_t* s_map = s_map_all[wv];
+  const uint32_t stride = gridDim.x * kTcWaves;
   // software pipeline: tile t's bytes and runs are in registers while tile t - stride is
   // copied; the records run one tile further ahead
   // (named registers: an array here is put on the scratch stack)
@@ -3174,7 +3183,7 @@ __global__ __launch_bounds__(256) void k_tcopy(RunArgs a, const uint4* __restric
       rw1 = (uint32_t)lane + 64 < r.nruns ? rp[lane + 64] : 0u;
     }
   };
-  uint32_t tile = blockIdx.x * 4 + wv;
+  uint32_t tile = blockIdx.x * kTcWaves + wv;
   TRec rec{}, nrec{};
   uint64_t ob = 0, nob = 0;
   if (tile < a.ntiles) {
@@ -3521,16 +3530,17 @@ static hipError_t launch_tail_stage(const RunArgs& a, hipStream_t st, hipEvent_t
     KLF_TRY(hipGetLastError());
   }
   if (a.compact_mode != 1) {
-    const uint32_t gk = (a.ntiles + 3) / 4;
+    const uint32_t gk = (a.ntiles + kTcWaves - 1) / kTcWaves;
     // persistent grid: one resident generation of blocks, so every wave's prefetch
     // pipeline runs over its whole share of tiles
     static int occ = 0;
     if (occ == 0) {
-      (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_tcopy, 256, 0);
-      occ = occ < 1 ? 1 : (occ > 8 ? 8 : occ);
+      (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_tcopy, 64 * kTcWaves, 0);
+      occ = occ < 1 ? 1 : (occ > 32 ? 32 : occ);
+      if (getenv("KLF_DIAG")) fprintf(stderr, "[klf] k_tcopy: %d blocks of %d waves per CU\n", occ, kTcWaves);
     }
     const uint32_t gc = (uint32_t)num_cus * (uint32_t)occ;
-    hipLaunchKernelGGL(k_tcopy, dim3(gk < gc ? gk : gc), dim3(256), 0, st, a,
+    hipLaunchKernelGGL(k_tcopy, dim3(gk < gc ? gk : gc), dim3(64 * kTcWaves), 0, st, a,
                        reinterpret_cast<const uint4*>(a.trec), a.kbase, a.truns);
     KLF_TRY(hipGetLastError());
   }
