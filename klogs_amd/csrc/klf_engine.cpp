@@ -44,7 +44,10 @@ struct DevBuf {
     size_t want = std::max<size_t>(bytes, 256);
     hipError_t e = hipMalloc(&p, want);
     if (e == hipSuccess) cap = want;
-    g_alloc_ns += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
+    const uint64_t ns = (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
+    g_alloc_ns += ns;
+    static const bool diag = getenv("KLF_DIAG_ALLOC") != nullptr;
+    if (diag) fprintf(stderr, "[klf] alloc %zu B: %.1f us\n", want, ns / 1e3);
     return e;
   }
   void release() {
@@ -144,7 +147,14 @@ struct klf_engine {
   DevBuf d_batch, d_segs, d_tstat, d_slots, d_pool, d_tile_base, d_bsum, d_cstatus, d_counters, d_line_off,
       d_meta, d_bits, d_segout, d_wpre, d_out, d_mpart, d_trec, d_truns, d_kbase;
   uint64_t pool_cap = 1 << 20;
+  // lines per input byte of the last run (0: no run yet): sizes the line arrays of the next
+  // runs (the first run sizes them from its own tile index, between two launch phases)
+  double line_density = 0.0;
+  bool dense_tail_seen = false;  // a --tail run took the dense compaction (keep its run table)
   HostBuf h_rb;  // run readback: counters (64 B), then the SegOut table
+  HostBuf h_stage;  // pinned staging of the prefilter tables (upload_prefilter)
+  hipEvent_t stage_ev = nullptr;  // the staged copies have drained
+  bool stage_ev_pending = false;
   hipEvent_t ev[7] = {};
   klf::RunArgs last_args{};  // arguments of the latest completed run (klf_retail)
   uint64_t last_gen = 0;     // gen of that run's result
@@ -205,6 +215,28 @@ static hipError_t upload(DevBuf& b, const std::vector<T>& v, hipStream_t st) {
   if (h != hipSuccess) return h;
   return hipStreamSynchronize(st);
 }
+// Several tables through one pinned staging buffer: async copies in stream order, no sync
+// (the staging buffer is rewritten only after the stream has drained it: the next
+// staged upload waits for the previous one's event)
+struct StagedUpload {
+  HostBuf& stage;
+  hipStream_t st;
+  hipEvent_t done;
+  size_t off = 0;
+  std::vector<std::pair<DevBuf*, std::pair<size_t, size_t>>> items;  // (buffer, (offset, bytes))
+  template <class T>
+  hipError_t add(DevBuf& b, const std::vector<T>& v) {
+    hipError_t h = b.ensure(std::max<size_t>(v.size() * sizeof(T), 16));
+    if (h != hipSuccess) return h;
+    items.push_back({&b, {off, v.size() * sizeof(T)}});
+    off += (v.size() * sizeof(T) + 255) & ~(size_t)255;
+    return hipSuccess;
+  }
+  template <class T>
+  void fill(size_t k, const std::vector<T>& v) {
+    if (!v.empty()) memcpy(stage.as<uint8_t>() + items[k].second.first, v.data(), v.size() * sizeof(T));
+  }
+};
 
 // The prefilter tables that the layout choice (place_needles) rewrites: bitmap, buckets,
 // anchor pre-checks, and the scalar layout fields of the device pattern set.
@@ -214,15 +246,31 @@ static hipError_t upload_prefilter(klf_engine* e) {
   hipError_t h;
   std::vector<uint32_t> anc = cs.qf_anc_pre;
   if (anc.empty()) anc.assign(2, 0u);
-  if ((h = upload(e->d_qf_bitmap, cs.qf_bitmap, st)) != hipSuccess || (h = upload(e->d_qf_head, cs.qf_head, st)) != hipSuccess ||
-      (h = upload(e->d_qf_ent, cs.qf_ent, st)) != hipSuccess || (h = upload(e->d_qf_anc, anc, st)) != hipSuccess ||
-      (h = upload(e->d_qf_nbytes, cs.qf_nbytes, st)) != hipSuccess)
+  std::vector<uint32_t> pre = cs.rx_pre;  // the chosen needle set's match-start bounds
+  if (pre.empty()) pre.assign(std::max<uint32_t>(cs.rx_count, 1u), klf::kRxPreUnbounded);
+  // one pinned staging buffer, six async copies, no host sync (first-run latency)
+  if (e->stage_ev_pending && (h = hipEventSynchronize(e->stage_ev)) != hipSuccess) return h;
+  StagedUpload u{e->h_stage, st, e->stage_ev};
+  if ((h = u.add(e->d_qf_bitmap, cs.qf_bitmap)) != hipSuccess || (h = u.add(e->d_qf_head, cs.qf_head)) != hipSuccess ||
+      (h = u.add(e->d_qf_ent, cs.qf_ent)) != hipSuccess || (h = u.add(e->d_qf_anc, anc)) != hipSuccess ||
+      (h = u.add(e->d_qf_nbytes, cs.qf_nbytes)) != hipSuccess || (h = u.add(e->d_rx_pre, pre)) != hipSuccess)
     return h;
+  if ((h = e->h_stage.ensure(u.off + 256)) != hipSuccess) return h;
+  u.fill(0, cs.qf_bitmap);
+  u.fill(1, cs.qf_head);
+  u.fill(2, cs.qf_ent);
+  u.fill(3, anc);
+  u.fill(4, cs.qf_nbytes);
+  u.fill(5, pre);
+  for (auto& it : u.items)
+    if (it.second.second &&
+        (h = hipMemcpyAsync(it.first->p, e->h_stage.as<uint8_t>() + it.second.first, it.second.second,
+                            hipMemcpyHostToDevice, st)) != hipSuccess)
+      return h;
+  if ((h = hipEventRecord(e->stage_ev, st)) != hipSuccess) return h;
+  e->stage_ev_pending = true;
   klf::DevPatterns& P = e->dpats;
-  if (cs.rx_count) {  // the chosen needle set's match-start bounds (k_nfa_win / k_nfa split)
-    std::vector<uint32_t> pre = cs.rx_pre;
-    if (pre.empty()) pre.assign(cs.rx_count, klf::kRxPreUnbounded);
-    if ((h = upload(e->d_rx_pre, pre, st)) != hipSuccess) return h;
+  if (cs.rx_count) {  // (k_nfa_win / k_nfa split)
     P.rx_pre = e->d_rx_pre.as<uint32_t>();
     P.rx_unbounded = (uint32_t)std::count(pre.begin(), pre.end(), klf::kRxPreUnbounded);
   }
@@ -292,7 +340,8 @@ extern "C" int klf_open(const klf_config* cfg, klf_engine** out) {
   }
   if ((h = hipStreamCreateWithFlags(&e->aux_stream, hipStreamNonBlocking)) != hipSuccess ||
       (h = hipEventCreateWithFlags(&e->ev_fork, hipEventDisableTiming)) != hipSuccess ||
-      (h = hipEventCreateWithFlags(&e->ev_join, hipEventDisableTiming)) != hipSuccess) {
+      (h = hipEventCreateWithFlags(&e->ev_join, hipEventDisableTiming)) != hipSuccess ||
+      (h = hipEventCreateWithFlags(&e->stage_ev, hipEventDisableTiming)) != hipSuccess) {
     *out = e;
     return hip_err(e, h, "side stream");
   }
@@ -404,6 +453,7 @@ extern "C" void klf_close(klf_engine* e) {
   e->d_scratch.release();
   e->h_rb.release();
   e->h_hist.release();
+  e->h_stage.release();
   for (DevBuf* b : {&e->d_ac_out, &e->d_ac_dict, &e->d_pcount, &e->d_pairs}) b->release();
   e->copier.reset();
   {
@@ -423,6 +473,7 @@ extern "C" void klf_close(klf_engine* e) {
   if (e->aux_stream) (void)hipStreamSynchronize(e->aux_stream);
   if (e->ev_fork) (void)hipEventDestroy(e->ev_fork);
   if (e->ev_join) (void)hipEventDestroy(e->ev_join);
+  if (e->stage_ev) (void)hipEventDestroy(e->stage_ev);
   if (e->aux_stream) (void)hipStreamDestroy(e->aux_stream);
   if (e->own_stream && e->stream) (void)hipStreamDestroy(e->stream);
   delete e;
@@ -707,6 +758,12 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
   }
   if (ntiles >= (1ull << 32)) return set_err(e, KLF_EINVAL, "batch too large");
   const uint32_t nsegs = (uint32_t)segs.size();
+  // the line arrays: from the last run's line density (+25 %) once there is one, else the
+  // 32-B estimate above (1 G lines for 32 GiB: gigabytes of line index for a first run)
+  auto learned_cap = [&]() {
+    return (uint64_t)(e->line_density * (double)total_bytes * 1.25) + 2ull * nsegs + 4096;
+  };
+  if (e->line_density > 0.0) cap = std::min<uint64_t>(cap, learned_cap());
   // asked-for per-pattern counts are reported even when every stream is empty (all zero)
   r->counted = (f->flags & KLF_FILTER_PATTERN_COUNTS) != 0;
   r->pcount_ok = true;  // no segment reads pcount
@@ -740,6 +797,7 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
                                      e->d_hist.as<uint32_t>(), st), "gram histogram");
       HIPCHK(e, hipMemcpyAsync(e->h_hist.p, e->d_hist.p, nh * 4, hipMemcpyDeviceToHost, st), "D2H hist");
       HIPCHK(e, hipStreamSynchronize(st), "sync hist");
+      const auto t_hist = std::chrono::steady_clock::now();
       const uint32_t* hv = e->h_hist.as<uint32_t>();
       klf::DataStats ds;
       ds.gram3.assign(hv, hv + klf::kQfHistBins);
@@ -752,10 +810,16 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
         ds.nbytes += ds.bytes[c];
       }
       klf::place_needles(e->cs, &ds);
+      const auto t_place = std::chrono::steady_clock::now();
       if (getenv("KLF_DIAG"))
         fprintf(stderr, "[klf] prefilter layout from %llu sampled bytes: %s\n", (unsigned long long)ds.nbytes,
                 e->cs.qf_layout.c_str());
       HIPCHK(e, upload_prefilter(e), "upload prefilter tables");
+      if (getenv("KLF_DIAG"))
+        fprintf(stderr, "[klf] first-batch tuning: statistics %.1f us, layout %.1f us, uploads %.1f us\n",
+                std::chrono::duration<double, std::micro>(t_hist - t_tune0).count(),
+                std::chrono::duration<double, std::micro>(t_place - t_hist).count(),
+                std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t_place).count());
     }
     tune_ns = (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t_tune0).count();
   }
@@ -767,7 +831,11 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
   HIPCHK(e, e->d_segout.ensure(nsegs * sizeof(SegOut)), "alloc segout");
   HIPCHK(e, e->d_wpre.ensure((nsegs + 1) * 8), "alloc wpre");
   HIPCHK(e, e->d_trec.ensure(ntiles * sizeof(klf::TRec)), "alloc trec");
-  HIPCHK(e, e->d_truns.ensure(ntiles * klf::kRunSlots * 4), "alloc truns");
+  // the dense compaction's per-tile run table (512 B per tile: 2.1 GB for 32 GiB) only for
+  // runs without a --tail limit or after a --tail run took the dense path (k_tcopy lists
+  // the runs itself without it)
+  const bool want_truns = f->tail < 0 || e->dense_tail_seen;
+  if (want_truns) HIPCHK(e, e->d_truns.ensure(ntiles * klf::kRunSlots * 4), "alloc truns");
   HIPCHK(e, e->d_kbase.ensure(ntiles * 16), "alloc kbase");
   uint32_t compact_mode = 0;  // tests: force either compaction path
   if (const char* v = getenv("KLF_COMPACT")) compact_mode = !strcmp(v, "sparse") ? 1u : !strcmp(v, "dense") ? 2u : 0u;
@@ -808,24 +876,42 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
   r->counted = (f->flags & KLF_FILTER_PATTERN_COUNTS) != 0;
   bool overflow = false, pairs_over = false;
   for (int attempt = 0, line_reruns = 0, pair_reruns = 0; attempt < 4; ++attempt) {
-    const uint64_t max_cblocks = cap / klf::kCompactLines + 2;
     if (count) {
       HIPCHK(e, e->d_pcount.ensure((size_t)nsegs * e->cs.n_cids * 4), "alloc pcount");
       HIPCHK(e, e->d_pairs.ensure((size_t)8 << e->pairs_log2), "alloc pairs");
       HIPCHK(e, hipMemsetAsync(e->d_pcount.p, 0, (size_t)nsegs * e->cs.n_cids * 4, st), "zero pcount");
       HIPCHK(e, hipMemsetAsync(e->d_pairs.p, 0, (size_t)8 << e->pairs_log2, st), "zero pairs");
     }
-    HIPCHK(e, e->d_line_off.ensure((cap + nsegs + 1) * 8), "alloc line_off");
-    HIPCHK(e, e->d_meta.ensure(cap * 2 + 16), "alloc meta");
-    HIPCHK(e, e->d_bits.ensure((cap / 32 + 1) * 4), "alloc bits");
-    HIPCHK(e, e->d_cstatus.ensure((max_cblocks + 1) * 3 * 8), "alloc cstatus");
-    // >= sum over blocks of ceil(bytes / chunk) (>= 1 each): the block prefix's chunk keeps the
-    // output within kCopyChunksTarget chunks unless it is the largest, kCopyChunk
-    const uint64_t cmap_cap =
-        max_cblocks + std::max<uint64_t>(total_bytes / klf::kCopyChunk, klf::kCopyChunksTarget) + 2;
-    HIPCHK(e, e->d_cmap.ensure(cmap_cap * 4), "alloc cmap");
-    HIPCHK(e, e->d_cseg.ensure((max_cblocks + 1) * 4), "alloc cseg");
-    HIPCHK(e, e->d_mpart.ensure((cap / klf::kMatchChunk + 2) * 8), "alloc mpart");
+    // An engine's first run sizes its line arrays from its own line count: the pipeline
+    // runs up to the tile index, the count is read back, the arrays are allocated, the
+    // rest follows (one extra sync, first runs only).
+    const bool two_phase = attempt == 0 && e->line_density == 0.0 && !getenv("KLF_ONE_PHASE");
+    // the arrays indexed by global line (and the compaction's per-block tables)
+    auto alloc_lines = [&](klf::RunArgs& x, uint64_t c) -> hipError_t {
+      const uint64_t mcb = c / klf::kCompactLines + 2;
+      // >= sum over blocks of ceil(bytes / chunk) (>= 1 each): the block prefix's chunk keeps
+      // the output within kCopyChunksTarget chunks unless it is the largest, kCopyChunk
+      const uint64_t cmc = mcb + std::max<uint64_t>(total_bytes / klf::kCopyChunk, klf::kCopyChunksTarget) + 2;
+      hipError_t h;
+      if ((h = e->d_line_off.ensure((c + nsegs + 1) * 8)) != hipSuccess) return h;
+      if ((h = e->d_meta.ensure(c * 2 + 16)) != hipSuccess) return h;
+      if ((h = e->d_bits.ensure((c / 32 + 1) * 4)) != hipSuccess) return h;
+      if ((h = e->d_cstatus.ensure((mcb + 1) * 3 * 8)) != hipSuccess) return h;
+      if ((h = e->d_cmap.ensure(cmc * 4)) != hipSuccess) return h;
+      if ((h = e->d_cseg.ensure((mcb + 1) * 4)) != hipSuccess) return h;
+      if ((h = e->d_mpart.ensure((c / klf::kMatchChunk + 2) * 8)) != hipSuccess) return h;
+      x.line_off = e->d_line_off.as<uint64_t>();
+      x.meta = e->d_meta.as<uint16_t>();
+      x.bits = e->d_bits.as<uint32_t>();
+      x.csum = e->d_cstatus.as<uint64_t>();
+      x.cmap = e->d_cmap.as<uint32_t>();
+      x.cmap_cap = cmc;
+      x.cseg = e->d_cseg.as<uint32_t>();
+      x.mpart = e->d_mpart.as<uint64_t>();
+      x.cap_lines = c;
+      x.max_cblocks = (uint32_t)mcb;
+      return hipSuccess;
+    };
     HIPCHK(e, e->d_pool.ensure(e->pool_cap * 4), "alloc pool");
     klf::RunArgs a;
     memset(static_cast<void*>(&a), 0, sizeof(a));
@@ -862,21 +948,11 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
     a.pool_cap = e->pool_cap;
     a.tile_base = e->d_tile_base.as<uint64_t>();
     a.bsum = e->d_bsum.as<uint64_t>();
-    a.mpart = e->d_mpart.as<uint64_t>();
-    a.csum = e->d_cstatus.as<uint64_t>();
-    a.cmap = e->d_cmap.as<uint32_t>();
-    a.cmap_cap = cmap_cap;
-    a.cseg = e->d_cseg.as<uint32_t>();
     a.counters = e->d_counters.as<uint32_t>();
-    a.line_off = e->d_line_off.as<uint64_t>();
-    a.meta = e->d_meta.as<uint16_t>();
-    a.bits = e->d_bits.as<uint32_t>();
-    a.cap_lines = cap;
     a.segout = e->d_segout.as<SegOut>();
     a.wpre = e->d_wpre.as<uint64_t>();
     a.out = e->d_out.as<uint8_t>();
     a.out_cap = e->d_out.p ? e->d_out.cap : 0;
-    a.max_cblocks = (uint32_t)max_cblocks;
     a.stage_times = (f->flags & KLF_FILTER_STAGE_TIMES) ? 1u : 0u;
     a.cand = need_cand ? e->d_cand.as<uint64_t>() : nullptr;
     a.cand_cap = need_cand ? e->cand_cap : 0;
@@ -886,7 +962,7 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
     a.hflat_cap = need_hits ? hflat_cap : 0;
     a.qhits_cap = need_hits ? qhits_cap : 0;
     a.trec = e->d_trec.as<klf::TRec>();
-    a.truns = e->d_truns.as<uint32_t>();
+    a.truns = want_truns ? e->d_truns.as<uint32_t>() : nullptr;
     a.kbase = e->d_kbase.as<uint64_t>();
     a.compact_mode = compact_mode;
     a.fused = fused ? 1u : 0u;
@@ -895,10 +971,36 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
     a.pcount = count ? e->d_pcount.as<uint32_t>() : nullptr;
     a.pairs = count ? e->d_pairs.as<uint64_t>() : nullptr;
     a.pairs_log2 = e->pairs_log2;
-    HIPCHK(e, klf::launch_pipeline(a, st, e->ev, e->num_cus, e->aux_stream, e->ev_fork, e->ev_join), "launch");
     r->so.resize(nsegs);
     uint32_t counters[32];
     HIPCHK(e, e->h_rb.ensure(sizeof(counters) + nsegs * sizeof(SegOut)), "alloc readback");
+    if (two_phase) {
+      a.cap_lines = 1ull << 40;  // phase 1 indexes no line array (k_tindex: no overflow, no bitmap)
+      HIPCHK(e, klf::launch_pipeline(a, st, e->ev, e->num_cus, e->aux_stream, e->ev_fork, e->ev_join, 1), "launch");
+      uint8_t* rb1 = e->h_rb.as<uint8_t>();
+      HIPCHK(e, hipMemcpyAsync(rb1, e->d_counters.p, sizeof(counters), hipMemcpyDeviceToHost, st), "D2H counters");
+      HIPCHK(e, hipMemcpyAsync(rb1 + sizeof(counters), e->d_segout.p, nsegs * sizeof(SegOut), hipMemcpyDeviceToHost, st),
+             "D2H segout");
+      HIPCHK(e, hipStreamSynchronize(st), "sync phase 1");
+      memcpy(counters, rb1, sizeof(counters));
+      memcpy(r->so.data(), rb1 + sizeof(counters), nsegs * sizeof(SegOut));
+      if (counters[2]) {  // the dense-tile pool overflowed: a whole rerun (as below)
+        e->pool_cap = std::max<uint64_t>(e->pool_cap, (uint64_t)counters[klf::kCtrPool] + 1024);
+        e->line_density = (double)(r->so[nsegs - 1].line_hi + 1) / (double)total_bytes;
+        cap = std::min<uint64_t>(cap, r->so[nsegs - 1].line_hi + 2);
+        continue;
+      }
+      // the same margin later runs size by (their line density estimate), so that they fit
+      e->line_density = (double)(r->so[nsegs - 1].line_hi + 1) / (double)total_bytes;
+      cap = std::min<uint64_t>(std::min<uint64_t>(cap, learned_cap()), cap_clamp);
+      HIPCHK(e, alloc_lines(a, cap), "alloc line arrays");
+      if (a.grep_mode != klf::CompiledSet::kNone)  // (phase 1's k_tindex zeroes it otherwise)
+        HIPCHK(e, hipMemsetAsync(a.bits, 0, (cap / 32 + 1) * 4, st), "zero bits");
+      HIPCHK(e, klf::launch_pipeline(a, st, e->ev, e->num_cus, e->aux_stream, e->ev_fork, e->ev_join, 2), "launch");
+    } else {
+      HIPCHK(e, alloc_lines(a, cap), "alloc line arrays");
+      HIPCHK(e, klf::launch_pipeline(a, st, e->ev, e->num_cus, e->aux_stream, e->ev_fork, e->ev_join), "launch");
+    }
     uint8_t* rb = e->h_rb.as<uint8_t>();
     HIPCHK(e, hipMemcpyAsync(rb, e->d_counters.p, sizeof(counters), hipMemcpyDeviceToHost, st), "D2H counters");
     HIPCHK(e, hipMemcpyAsync(rb + sizeof(counters), e->d_segout.p, nsegs * sizeof(SegOut), hipMemcpyDeviceToHost, st),
@@ -943,6 +1045,8 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
     }
     e->last_args = a;
     e->last_gen = r->gen;
+    e->line_density = (double)(r->so[nsegs - 1].line_hi + 1) / (double)total_bytes;
+    if (f->tail >= 0 && counters[klf::kCtrDense]) e->dense_tail_seen = true;
     break;
   }
   if (count && !overflow && !pairs_over) {

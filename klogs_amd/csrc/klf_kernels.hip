@@ -1483,7 +1483,7 @@ __global__ __launch_bounds__(256) void k_tindex(RunArgs a) {
       if (tot > a.hflat_cap) atomicOr(&a.counters[kCtrHitsOver], 1u);
     }
   }
-  if (a.grep_mode != kGrepNone) {  // bitmap words whose first line is in [blk_lo, blk_hi)
+  if (a.grep_mode != kGrepNone && a.bits) {  // bitmap words whose first line is in [blk_lo, blk_hi)
     const uint64_t w0 = (blk_lo + 31) / 32, w1 = (blk_hi + 31) / 32;
     for (uint64_t w = w0 + t; w < w1 && w * 32 < a.cap_lines; w += 256) a.bits[w] = 0u;
   }
@@ -2851,13 +2851,14 @@ __device__ __forceinline__ void tkeep_body(RunArgs& a, const uint32_t* __restric
       if (tile >= a.ntiles) break;
       const uint64_t wlo = sout[g[u].s].win_lo, whi = sout[g[u].s].win_hi;
       uint32_t kept, nsel;
-      const uint32_t nr = list_runs(a, g[u], wlo, whi, a.truns + (size_t)tile * kRunSlots, kRunSlots, lane, &kept,
-                                    &nsel, &pre[u]);
+      // (no run table, a.truns null: --tail runs do not map one; k_tcopy lists the runs again)
+      const uint32_t nr = list_runs(a, g[u], wlo, whi, a.truns ? a.truns + (size_t)tile * kRunSlots : nullptr,
+                                    a.truns ? (uint32_t)kRunSlots : 0u, lane, &kept, &nsel, &pre[u]);
       if (lane == 0) {
         TRec rec;
         rec.src = g[u].sd.base + (uint64_t)g[u].rel_lo;
         rec.kept = kept;
-        rec.nruns = nr <= (uint32_t)kRunSlots ? (uint16_t)nr : kRunsRecompute;
+        rec.nruns = (a.truns && nr <= (uint32_t)kRunSlots) ? (uint16_t)nr : kRunsRecompute;
         rec.nsel = (uint16_t)nsel;
         a.trec[tile] = rec;
       }
@@ -3394,11 +3395,12 @@ hipError_t launch_gen(const RunArgs& a, hipStream_t st, int num_cus) {
 static hipError_t launch_tail_stage(const RunArgs& a, hipStream_t st, hipEvent_t* ev, int num_cus);
 
 hipError_t launch_pipeline(const RunArgs& a0, hipStream_t st, hipEvent_t* ev, int num_cus, hipStream_t aux,
-                           hipEvent_t ev_fork, hipEvent_t ev_join) {
+                           hipEvent_t ev_fork, hipEvent_t ev_join, int phase) {
   RunArgs a = a0;
   if (KLF_ABL != 0) a.fused = 0;  // timing builds ablate the scan: the two-pass compaction
   hipError_t e;
 #define KLF_TRY(x) do { e = (x); if (e != hipSuccess) return e; } while (0)
+  if (phase != 2) {
   KLF_TRY(hipEventRecord(ev[0], st));
   {
     const uint32_t nw = a.nsegs * (uint32_t)(sizeof(SegOut) / 8);
@@ -3445,6 +3447,8 @@ hipError_t launch_pipeline(const RunArgs& a0, hipStream_t st, hipEvent_t* ev, in
     KLF_TRY(hipGetLastError());
     KLF_TRY(hipGetLastError());
   }
+  if (phase == 1) return hipSuccess;
+  }  // phase != 2
   uint32_t sg = ((a.ntiles + kScatterGroup - 1) / kScatterGroup + 3) / 4;
   if (sg > (uint32_t)num_cus * 8) sg = num_cus * 8;
   // With a prefiltered regex set, k_scatter (bandwidth-bound) runs on the side stream
