@@ -1665,8 +1665,31 @@ __device__ __forceinline__ uint32_t gword(const uint8_t* p) {  // 4 bytes at any
 // line starts (slots, meta in the high half) instead of a search of the whole index.
 // The bucket walk of one hit whose bucket [e0, e1) is known (the loads before it are
 // batched over several hits by k_verify).
+// NFA candidates of one wave, staged in LDS and appended to the global queue with one
+// atomic per wave at the end (k_verify): one counter that every candidate of the run
+// incremented serialized them at the memory side (C5: ~67 K candidates).
+constexpr uint32_t kVerifyQ = 256;  // candidates staged per wave (more: pushed directly)
+struct VerifyQ {
+  uint32_t* n;        // LDS: staged count
+  uint64_t (*buf)[2];  // LDS: [kVerifyQ] {line | regex << 40, occurrence}
+};
+__device__ __forceinline__ void push_candidate(const RunArgs& a, const VerifyQ& q, uint64_t key, uint64_t x) {
+  const uint32_t k = atomicAdd(q.n, 1u);  // (LDS)
+  if (k < kVerifyQ) {
+    q.buf[k][0] = key;
+    q.buf[k][1] = x;
+    return;
+  }
+  const uint32_t qi = atomicAdd(&a.counters[kCtrQueue], 1u);
+  if (qi < a.cand_cap) {
+    a.cand[2 * (size_t)qi] = key;
+    a.cand[2 * (size_t)qi + 1] = x;
+  } else {
+    atomicOr(&a.counters[kCtrQOver], 1u);
+  }
+}
 __device__ void verify_hit_from(const RunArgs& a, uint32_t tile, uint32_t s, const SegDesc& sd, int32_t p,
-                                uint32_t e0, uint32_t e1) {
+                                uint32_t e0, uint32_t e1, const VerifyQ& vq) {
   const DevPatterns& P = a.pats;
   const uint8_t* segp = a.bytes + sd.base;
   const int64_t rel_lo = (int64_t)(tile - sd.tile0) * kTile;
@@ -1738,22 +1761,17 @@ __device__ void verify_hit_from(const RunArgs& a, uint32_t tile, uint32_t s, con
       continue;
     }
     if (!a.count_pats && ((a.bits[l >> 5] >> (l & 31)) & 1u)) continue;  // counting: every regex decides
-    const uint32_t qi = atomicAdd(&a.counters[kCtrQueue], 1u);
-    if (qi < a.cand_cap) {
-      a.cand[2 * (size_t)qi] = l | ((uint64_t)E.z << 40);
-      a.cand[2 * (size_t)qi + 1] = (uint64_t)(rel_lo + x);  // the occurrence (stream offset)
-    }
-    else atomicOr(&a.counters[kCtrQOver], 1u);
+    push_candidate(a, vq, l | ((uint64_t)E.z << 40), (uint64_t)(rel_lo + x));  // (the occurrence: stream offset)
   }
 }
 
-__device__ void verify_hit(const RunArgs& a, uint32_t tile, uint32_t s, int32_t p) {
+__device__ void verify_hit(const RunArgs& a, uint32_t tile, uint32_t s, int32_t p, const VerifyQ& vq) {
   const DevPatterns& P = a.pats;
   const SegDesc sd = a.segs[s];
   const int64_t rel_lo = (int64_t)(tile - sd.tile0) * kTile;
   const uint32_t g = (gword(a.bytes + sd.base + rel_lo + p) | P.qf_fold) & P.qf_mask;
   const uint32_t b = qf_bucket(g, P.qf_w24, P.qf_k);
-  verify_hit_from(a, tile, s, sd, p, P.qf_head[b], P.qf_head[b + 1]);
+  verify_hit_from(a, tile, s, sd, p, P.qf_head[b], P.qf_head[b + 1], vq);
 }
 
 // Thread per hit: the flattened tile hit slots (k_tindex), then the spilled hits.  The
@@ -1762,7 +1780,13 @@ __device__ void verify_hit(const RunArgs& a, uint32_t tile, uint32_t s, int32_t 
 // by that latency (most hits are prefilter false positives that end at the bucket).
 constexpr int kVerifyBatch = 4;
 __global__ __launch_bounds__(256) void k_verify(RunArgs a) {
+  __shared__ uint32_t s_qn[4];
+  __shared__ uint64_t s_qbuf[4][kVerifyQ][2];
   if (a.counters[2] || a.counters[kCtrHitsOver]) return;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  if (lane == 0) s_qn[wv] = 0;
+  wave_lds_sync();
+  const VerifyQ vq{&s_qn[wv], s_qbuf[wv]};
   const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x, stride = gridDim.x * blockDim.x;
   const uint32_t nf = a.counters[kCtrFlatHits];
   const DevPatterns& P = a.pats;
@@ -1799,7 +1823,7 @@ __global__ __launch_bounds__(256) void k_verify(RunArgs a) {
         if (pp[u] == 0x7FFF) atomicOr(&a.counters[13], sg[u]);  // timing build: no verification work
         continue;
 #endif
-        verify_hit_from(a, tile[u], sg[u], sd[u], pp[u], e0[u], e1[u]);
+        verify_hit_from(a, tile[u], sg[u], sd[u], pp[u], e0[u], e1[u], vq);
       }
   }
   const uint32_t nh = a.counters[kCtrHits] < a.qhits_cap ? a.counters[kCtrHits] : a.qhits_cap;
@@ -1812,9 +1836,25 @@ __global__ __launch_bounds__(256) void k_verify(RunArgs a) {
     }
     const uint64_t rel = pos - a.segs[lo].base;
     const uint32_t tile = a.segs[lo].tile0 + (uint32_t)(rel / kTile);
-    verify_hit(a, tile, lo, (int32_t)(rel % kTile));
+    verify_hit(a, tile, lo, (int32_t)(rel % kTile), vq);
   }
   if (gid == 0) a.counters[kCtrVerified] = nf + nh;
+  // the wave's staged candidates: one queue reservation, then coalesced stores
+  wave_lds_sync();
+  const uint32_t nq = s_qn[wv] < kVerifyQ ? s_qn[wv] : kVerifyQ;
+  if (nq) {
+    uint32_t base = 0;
+    if (lane == 0) base = atomicAdd(&a.counters[kCtrQueue], nq);
+    base = (uint32_t)__builtin_amdgcn_readfirstlane((int)base);
+    for (uint32_t k = (uint32_t)lane; k < nq; k += 64) {
+      if ((uint64_t)base + k < a.cand_cap) {
+        a.cand[2 * ((size_t)base + k)] = s_qbuf[wv][k][0];
+        a.cand[2 * ((size_t)base + k) + 1] = s_qbuf[wv][k][1];
+      } else {
+        atomicOr(&a.counters[kCtrQOver], 1u);
+      }
+    }
+  }
 }
 
 // K2b: the prefiltered regex stage.  One lane per queued (batch offset, regex) candidate:
