@@ -3490,7 +3490,10 @@ hipError_t launch_pipeline(const RunArgs& a0, hipStream_t st, hipEvent_t* ev, in
   if (phase == 1) return hipSuccess;
   }  // phase != 2
   uint32_t sg = ((a.ntiles + kScatterGroup - 1) / kScatterGroup + 3) / 4;
-  if (sg > (uint32_t)num_cus * 8) sg = num_cus * 8;
+#ifndef KLF_SCATTER_GRID
+#define KLF_SCATTER_GRID 8  // k_scatter workgroups per CU at most
+#endif
+  if (sg > (uint32_t)num_cus * KLF_SCATTER_GRID) sg = num_cus * KLF_SCATTER_GRID;
   // With a prefiltered regex set, k_scatter (bandwidth-bound) runs on the side stream
   // beside k_verify (latency-bound: a chain of dependent loads per hit), which reads the
   // line slots, not the global line index; the main stream waits for it before the first
