@@ -856,6 +856,11 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
   // to the run's output and reruns the tail stage (first runs only: the buffer is kept).
   // A --tail run then never maps an input-sized buffer (34 GB for C4 / C5).
   if (fused || f->tail < 0) HIPCHK(e, e->d_out.ensure(total_bytes + 64), "alloc out");
+  else if (!e->d_out.p) {  // a first --tail run: room for a typical tail window (no rerun to grow)
+    uint64_t first = 64ull << 20;
+    if (const char* v = getenv("KLF_DEBUG_OUT_INIT")) first = (uint64_t)std::max(1L, atol(v));  // tests: force growth
+    HIPCHK(e, e->d_out.ensure(std::min<uint64_t>(total_bytes + 64, first)), "alloc out");
+  }
   const bool need_cand = mode == klf::CompiledSet::kGeneral && e->cs.qf_on && e->cs.rx_count;
   if (need_cand) HIPCHK(e, e->d_cand.ensure((size_t)e->cand_cap * 16), "alloc cand");
   const bool need_hits = mode == klf::CompiledSet::kGeneral && e->cs.qf_on;

@@ -160,10 +160,12 @@ def test_c3_full_per_gpu_batch(gpu):
 
 
 @pytest.mark.parametrize("tails", [(100, -1, 10**9), (0, 5, -1), (10**9, 3, -1)])
-def test_output_buffer_grown_on_demand(gpu, compact, tails):
+def test_output_buffer_grown_on_demand(gpu, compact, tails, monkeypatch):
     """A --tail run sizes the output buffer to its output (the copy that would not fit is
-    skipped, the buffer grown, the tail stage rerun); a fresh engine's first run and a
-    re-tail to a larger window (klf_retail) both take that path, bit-exact."""
+    skipped, the buffer grown, the tail stage rerun); a fresh engine's first run (its
+    initial buffer forced down to 4 KiB) and a re-tail to a larger window (klf_retail) both
+    take that path, bit-exact."""
+    monkeypatch.setenv("KLF_DEBUG_OUT_INIT", "4096")
     streams = [synth.generate(synth.TEXT, 61, i, 400_000 + 50_000 * i) for i in range(5)]
     with E.Engine(0, grep=[]) as eng:
         eng.set_streams(len(streams))
