@@ -420,7 +420,10 @@ __device__ __forceinline__ bool parse_fast(const uint8_t* lds, uint32_t o, const
 #define KLF_COPY_U 1
 #endif
 #ifndef KLF_SCAN_OCC
-#define KLF_SCAN_OCC 4
+// plain / literal scans: waves per SIMD the launch bounds ask for.  3 leaves the compiler
+// up to 168 VGPRs: C3's plain scan 1.84 -> 1.67 ms, C2's literal scan unchanged within the
+// box spread (0.90-0.94 ms either way), 5: no better (same box, scripts/r3_check15.sh)
+#define KLF_SCAN_OCC 3
 #endif
 // Scan variants: no patterns, the fused single literal, general sets through the fused
 // q-gram prefilter (QS = sampling stride).
