@@ -82,7 +82,8 @@ def main():
     ap.add_argument("--no-write", action="store_true", help="skip C3's file write path")
     ap.add_argument("--no-capture", action="store_true", help="skip the host-staged capture-path timing")
     ap.add_argument("--capture-piece", type=int, default=4 << 20, help="klf_stage piece size of the capture path")
-    ap.add_argument("--extra-configs", default="c3,c4,c5", help="N=1 only: comma list of c3,c4,c5 ('' = none)")
+    ap.add_argument("--extra-configs", default="c1,c3,c4,c5",
+                    help="comma list of c1,c3,c4,c5 ('' = none); at N > 1: c3 and c5 run sharded")
     ap.add_argument("--extra-bytes", type=int, default=32 << 30, help="total bytes of each extra config")
     args = ap.parse_args()
 
@@ -189,7 +190,7 @@ def main():
     log(f"[rank {rank}] timed {args.steps} steps: {dt / args.steps * 1e3:.3f} ms/step")
     cold = cold_run(local, dict(grep=[synth.NEEDLE]), ptr, seg_base, [n], since, TAIL) if world == 1 else None
     verified = None
-    if rank == 0 and not args.no_verify and world == 1:
+    if not args.no_verify:  # every rank: its own stream in full against the C oracle
         sys.path.insert(0, str(ROOT / "oracle"))
         import c_oracle as co
         so = last.stream(0)
@@ -200,6 +201,10 @@ def main():
         verified = ref_out == so.out and ref_c["selected"] == tot["selected"] and ref_c["lines"] == lines
         lo = last.lines(0)
         verified = bool(verified and lo.shape[0] == lines + 1 and int(lo[-1]) == n)
+        if world > 1:  # every rank's verdict (MIN)
+            vt = torch.tensor([int(verified)], dtype=torch.int64, device=coll_dev)
+            dist.all_reduce(vt, op=dist.ReduceOp.MIN)
+            verified = bool(vt.item())
     records_ok = None
     if world > 1:  # the gathered table: every rank's row equals what that rank computed
         mine = step.table[rank].tolist()
@@ -314,9 +319,11 @@ def main():
         for name in [x for x in args.extra_configs.split(",") if x]:
             res["extra"]["configs"][name] = run_extra(name, args, local, now)
             torch.cuda.empty_cache()
-    if world > 1 and "c3" in args.extra_configs.split(","):
-        res["extra"]["configs"] = {"c3_sharded": run_c3_sharded(args, world, rank, local, coll_dev)}
-        torch.cuda.empty_cache()
+    if world > 1:
+        res["extra"]["configs"] = {}
+        for name in [x for x in args.extra_configs.split(",") if x in ("c3", "c5")]:
+            res["extra"]["configs"][name + "_sharded"] = run_sharded(name, args, world, rank, local, coll_dev, now)
+            torch.cuda.empty_cache()
     if rank == 0:
         print(json.dumps(res), flush=True)
     if world > 1:
@@ -376,13 +383,36 @@ def cpu_variants(host: np.ndarray, since) -> dict:
     }
 
 
-def run_c3_sharded(args, world: int, rank: int, local: int, coll_dev) -> dict:
-    """BASELINE config 3 across ranks: 128 x 64 MiB TEXT streams per rank
-    (the per-GPU share at 8 GPUs; weak scaling at fewer), LPT-assigned (shard.assign), each
-    rank one device batch of its streams, then the one all-gather of per-stream count
-    records.  value = all ranks' bytes / max-over-ranks time."""
-    size, per = 64 << 20, 128
-    lens_all = [synth.size(synth.TEXT, 42, i, size) for i in range(per * world)]
+def sharded_table(name: str, world: int):
+    """(stream sizes, kind, patterns, permille, since_tail, description) of config `name`
+    at N ranks, weak scaling: each rank's share is the config's per-GPU workload.
+      c3: 128 x 64 MiB TEXT streams per rank (256 pods x 4 containers over 8 GPUs), -l only;
+      c5: 8 x N pods with 1-2 init containers + 2 containers (-i stream table, getPodLogs
+          order), 32 GiB per rank of 1-32 KiB JSON lines, 64 --match regexes, since + tail."""
+    if name == "c3":
+        return [64 << 20] * (128 * world), synth.TEXT, {}, 10, "-l", \
+            "C3 at N GPUs: 128 x 64 MiB TEXT streams per GPU, LPT-sharded, -l only (every line out)"
+    from klogs_amd import host as H
+    pods = [(f"synthetic-{p}", [f"init-{k}" for k in range(1 + p % 2)], ["app", "sidecar"]) for p in range(8 * world)]
+    table = H.stream_table(pods, init=True)  # getPodLogs order with -i (cmd/root.go:240-262)
+    w = [1 if is_init else 4 for _, _, is_init in table]
+    per_rank = 32 << 30
+    sizes = [per_rank * world * x // sum(w) for x in w]
+    return sizes, synth.LONGJSON, dict(match=synth.c5_regexes()), 5, "since+tail", \
+        (f"C5 at N GPUs: {len(table)} streams (8 pods per GPU, 1-2 init containers + 2 containers each, -i), "
+         "32 GiB per GPU of 1-32 KiB JSON lines, 64 --match regexes, --since 5m --tail 100, LPT-sharded")
+
+
+def run_sharded(name: str, args, world: int, rank: int, local: int, coll_dev, now: int) -> dict:
+    """BASELINE config 3 or 5 across ranks: the stream table LPT-assigned
+    (shard.assign), each rank one device batch of its own streams, then the one all-gather
+    of per-stream count records (+ per-pattern counts for C5) per step over RCCL.  value =
+    all ranks' bytes / max-over-ranks time.  After the timed region every rank checks its
+    own rows of the gathered table and verifies its first and last stream in full against
+    the C oracle (C5: the glibc-regex leg, ko_filter_rx); the flags are all-reduced (MIN)."""
+    sizes, kind, pats, permille, mode, desc = sharded_table(name, world)
+    since, tail = ((None, -1) if mode == "-l" else ((now - SINCE_S, 0), TAIL))
+    lens_all = [synth.size(kind, 42, i, sz, permille=permille) for i, sz in enumerate(sizes)]
     mine = shard.local_streams(lens_all, world, rank)
     lens = [lens_all[i] for i in mine]
     seg_base, total = E.layout(lens)
@@ -390,19 +420,29 @@ def run_c3_sharded(args, world: int, rank: int, local: int, coll_dev) -> dict:
     h = np.empty(max(lens) + 1, dtype=np.uint8)
     t = time.time()
     for j, i in enumerate(mine):
-        synth.generate_into(h, synth.TEXT, 42, i, size)
+        synth.generate_into(h, kind, 42, i, sizes[i], permille=permille)
         dev[int(seg_base[j]):int(seg_base[j]) + lens[j]].copy_(torch.from_numpy(h[:lens[j]]))
     torch.cuda.synchronize()
-    log(f"[rank {rank}] c3 share: {len(mine)} streams, {sum(lens)} B in {time.time() - t:.1f}s")
-    eng = E.Engine(local, hip_stream=torch.cuda.current_stream().cuda_stream)
+    del h
+    log(f"[rank {rank}] {name} share: {len(mine)} streams, {sum(lens)} B in {time.time() - t:.1f}s")
+    eng = E.Engine(local, hip_stream=torch.cuda.current_stream().cuda_stream, **pats)
     ptr = dev.data_ptr()
+    npat = len(pats.get("match", [])) + len(pats.get("grep", []))
 
     pending = []
 
+    def records(r):
+        recs = {}
+        for j, sid in enumerate(mine):
+            c = r.stream_counts(j)
+            if npat:
+                c = dict(c, patterns=r.pattern_counts(j))
+            recs[sid] = c
+        return recs
+
     def step():
-        r = eng.run_device(ptr, seg_base, lens)
-        recs = {sid: r.stream_counts(j) for j, sid in enumerate(mine)}
-        pending.append(shard.gather_counts_async(recs, lens_all, world, device=coll_dev))
+        r = eng.run_device(ptr, seg_base, lens, since=since, tail=tail, pattern_counts=bool(npat))
+        pending.append(shard.gather_counts_async(records(r), lens_all, world, device=coll_dev, n_patterns=npat))
         if len(pending) > 1:
             pending.pop(0).wait()
         return r
@@ -417,9 +457,13 @@ def run_c3_sharded(args, world: int, rank: int, local: int, coll_dev) -> dict:
     dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    last = None
+    for i in range(args.steps):
         r = step()
-        r.free()
+        if i + 1 < args.steps:
+            r.free()
+        else:
+            last = r
     finish()
     torch.cuda.synchronize()
     dist.barrier()
@@ -428,18 +472,54 @@ def run_c3_sharded(args, world: int, rank: int, local: int, coll_dev) -> dict:
     dist.all_reduce(tt, op=dist.ReduceOp.MAX)
     dt = float(tt.item())
     # every rank's own rows of the gathered table equal its own counts; totals add up
-    r = eng.run_device(ptr, seg_base, lens)
-    ok = all(step.table[sid].tolist() == [r.stream_counts(j)[k] for k in shard.RECORD_FIELDS[1:]]
-             for j, sid in enumerate(mine))
-    ok = ok and int(step.table[:, 0].sum()) > 0 and int(step.table[:, 5].sum()) > 0
-    r.free()
+    mine_rec = records(last)
+    fields = shard.RECORD_FIELDS[1:]
+    rec_ok = all(step.table[sid].tolist() == [mine_rec[sid][k] for k in fields] + list(mine_rec[sid].get("patterns", []))
+                 for sid in mine)
+    rec_ok = rec_ok and int(step.table[:, 0].sum()) > 0 and int(step.table[:, 5].sum()) > 0
+    ver = None
+    if not args.no_verify:  # the rank's first and last stream in full vs the C oracle
+        sys.path.insert(0, str(ROOT / "oracle"))
+        import c_oracle as co
+        rs = co.RegexSet(pats["match"]) if "match" in pats else None
+        sn = since if since is not None else co.GO_ZERO_TIME
+        got = {j: (last.stream(j), last.match_bits(j) if npat else None) for j in sorted({0, len(mine) - 1})}
+        del dev
+        torch.cuda.empty_cache()
+        dev = None
+
+        def check(j):
+            i = mine[j]
+            hh = np.empty(lens[j] + 1, dtype=np.uint8)
+            synth.generate_into(hh, kind, 42, i, sizes[i], permille=permille)
+            if rs is not None:
+                out, _, bits, c = co.filter_stream_rx(hh[:lens[j]], sn, tail, rs, want_lines=False)
+            else:
+                out, _, bits, c = co.filter_stream(hh[:lens[j]], sn, tail, [], want_lines=False, want_bits=False)
+            so, gb = got[j]
+            return so.out == out and all(so.counts[k] == c[k] for k in c) and (gb is None or gb == bits)
+        from concurrent.futures import ThreadPoolExecutor
+        tv = time.perf_counter()
+        with ThreadPoolExecutor(len(got)) as ex:
+            ver = all(ex.map(check, list(got)))
+        log(f"[rank {rank}] {name} verified={ver} ({time.perf_counter() - tv:.1f}s)")
+    flags = torch.tensor([int(rec_ok), -1 if ver is None else int(ver)], dtype=torch.int64, device=coll_dev)
+    dist.all_reduce(flags, op=dist.ReduceOp.MIN)
+    last.free()
     eng.close()
     del dev
-    return {"workload": "C3 at N GPUs: 128 x 64 MiB TEXT streams per GPU, LPT-sharded, -l only (every line out), "
-                        "one all-gather of per-stream count records per step",
-            "streams": per * world, "bytes": int(sum(lens_all)),
-            "value_GBps": round(sum(lens_all) * args.steps / dt / 1e9, 1),
-            "ms_per_step": round(dt / args.steps * 1e3, 3), "records_consistent": bool(ok)}
+    out = {"workload": desc, "streams": len(lens_all), "bytes": int(sum(lens_all)),
+           "value_GBps": round(sum(lens_all) * args.steps / dt / 1e9, 1),
+           "ms_per_step": round(dt / args.steps * 1e3, 3),
+           "records_consistent": bool(flags[0].item()),
+           "collective": f"one all-gather per step of {len(lens_all)} x {shard.NREC + npat} int64 records "
+                         f"({'RCCL' if coll_dev != 'cpu' else 'gloo'})"}
+    if ver is not None:
+        out["verified_vs_oracle"] = bool(flags[1].item() == 1)
+        out["verify_scope"] = ("on every rank: its first and last stream in full (output bytes, all counts"
+                               + (", match bitmap" if npat else "") + ") against "
+                               + ("the C oracle's glibc-regex leg (ko_filter_rx)" if npat else "the C oracle"))
+    return out
 
 
 def extra_streams(name: str, total: int):
@@ -448,6 +528,9 @@ def extra_streams(name: str, total: int):
     if name == "c2":  # the headline workload, for scripts/run_config.py
         return [STREAM_BYTES], synth.JSON, dict(grep=[synth.NEEDLE]), 10, \
             "C2: one 4 GiB JSON log stream, --since 5m --tail 100 --grep " + synth.NEEDLE.decode()
+    if name == "c1":  # the reference's own CPU-runnable case (BASELINE configs[0])
+        return [64 << 20], synth.TEXT, {}, 10, \
+            "C1: one 64 MiB stream (lognormal line lengths, median 96 B), --since 5m --tail 100"
     if name == "c3":  # one GPU's share of C3 at 8 GPUs (fixed size: --extra-bytes is for C4/C5)
         n = 128
         return [64 << 20] * n, synth.TEXT, {}, 10, \
@@ -472,21 +555,32 @@ def extra_streams(name: str, total: int):
 
 
 def cpu_extra(name: str, kind: int, pats: dict, permille: int, since, tail: int) -> dict:
-    """CPU reference points for configs 3-5 (rank 0, N = 1; bounded, a few seconds each) on
-    samples of the same generator and shape: the C restatement (literal paths) on 1 and on
-    T host threads (one stream per thread, as the reference runs one goroutine per stream),
-    and for the regex set the Python restatement (one core: Python `re` holds the GIL)."""
+    """CPU reference points for configs 1 and 3-5 (rank 0, N = 1; bounded, a few seconds
+    each) on samples of the same generator and shape: the C restatement on 1 and on T host
+    threads (one stream per thread, as the reference runs one goroutine per stream).  Literal
+    paths: oracle/klf_oracle_c.c ko_filter (memmem / Aho-Corasick).  The regex set (C5):
+    ko_filter_rx, glibc POSIX ERE translated from the Go subset (oracle/posix_re.py) behind an
+    Aho-Corasick pass over each pattern's required literal, first checked against the Python
+    oracle on one sample stream; the Python oracle's own rate (one core, Python `re`) beside it.
+    C1 is one 64 MiB stream: one core only."""
     from concurrent.futures import ThreadPoolExecutor
     sys.path.insert(0, str(ROOT / "oracle"))
     import c_oracle as co
     threads = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", "16") or 16)))
-    sample = {"c3": 64 << 20, "c4": 2 << 20, "c5": 2 << 20}[name]
-    streams = [synth.generate(kind, 7, i, sample, permille=permille) for i in range(threads)]
+    sample = {"c1": 64 << 20, "c3": 64 << 20, "c4": 2 << 20, "c5": 8 << 20}[name]
+    nstreams = 1 if name == "c1" else threads
+    streams = [synth.generate(kind, 7, i, sample, permille=permille) for i in range(nstreams)]
     grep = pats.get("grep", [])
     sn = since if since is not None else co.GO_ZERO_TIME
 
-    def one(b):
-        return co.filter_stream(b, sn, tail, grep, want_lines=False, want_bits=False)
+    if name == "c5":
+        rs = co.RegexSet(pats["match"])
+
+        def one(b):
+            return co.filter_stream_rx(b, sn, tail, rs, want_lines=False, want_bits=False)
+    else:
+        def one(b):
+            return co.filter_stream(b, sn, tail, grep, want_lines=False, want_bits=False)
 
     def timed(f, budget):
         n, t = 0, 0.0
@@ -496,24 +590,32 @@ def cpu_extra(name: str, kind: int, pats: dict, permille: int, since, tail: int)
             t += time.perf_counter() - t0
             n += 1
         return n, t
+    what = {"c5": "oracle/klf_oracle_c.c ko_filter_rx (glibc regexec behind the required-literal Aho-Corasick pass)"}
+    impl = what.get(name, "oracle/klf_oracle_c.c")
     res = {}
-    if name == "c5":
+    if name == "c5":  # the C leg decides every line as the Python oracle does (one sample stream)
         from oracle import klf_oracle as ko
         cp = ko.compile_patterns(match=pats["match"])
-        n, t = timed(lambda: ko.filter_stream(streams[0], sn, tail, cp), 3.0)
-        res["port_1_core"] = {"value": round(sample * n / t / 1e9, 4), "unit": "GB/s", "cores": 1,
-                              "kind": "port", "sample": f"{n} passes over one {sample >> 20} MiB stream of the "
-                                                        f"C5 generator, oracle/klf_oracle.py (Python re), {t:.1f} s"}
-        return res
+        probe = streams[0][:2 << 20]
+        probe = probe[:probe.rfind(b"\n") + 1]
+        ref = ko.filter_stream(probe, sn, tail, cp)
+        got = co.filter_stream_rx(probe, sn, tail, rs, want_lines=False)
+        res["c_leg_equals_python_oracle"] = bool(got[0] == ref.out and got[2] == ref.match_bits)
+        n, t = timed(lambda: ko.filter_stream(probe, sn, tail, cp), 3.0)
+        res["python_1_core"] = {"value": round(len(probe) * n / t / 1e9, 4), "unit": "GB/s", "cores": 1,
+                                "kind": "port", "sample": f"{n} passes over {len(probe)} B of the C5 generator, "
+                                                          f"oracle/klf_oracle.py (Python re), {t:.1f} s"}
     n, t = timed(lambda: one(streams[0]), 3.0)
     res["port_1_core"] = {"value": round(sample * n / t / 1e9, 4), "unit": "GB/s", "cores": 1, "kind": "port",
                           "sample": f"{n} passes over one {sample >> 20} MiB stream of the {name.upper()} generator, "
-                                    f"oracle/klf_oracle_c.c, {t:.1f} s"}
-    with ThreadPoolExecutor(threads) as ex:
-        n, t = timed(lambda: list(ex.map(one, streams)), 3.0)
-    res["port_threads"] = {"value": round(sample * threads * n / t / 1e9, 4), "unit": "GB/s", "cores": threads,
-                           "kind": "port", "sample": f"{n} passes over {threads} streams of {sample >> 20} MiB, "
-                                                     f"one host thread per stream, {t:.1f} s"}
+                                    f"{impl}, {t:.1f} s"}
+    if nstreams > 1:
+        with ThreadPoolExecutor(threads) as ex:
+            n, t = timed(lambda: list(ex.map(one, streams)), 3.0)
+        res["port_threads"] = {"value": round(sample * threads * n / t / 1e9, 4), "unit": "GB/s",
+                               "cores": threads, "kind": "port",
+                               "sample": f"{n} passes over {threads} streams of {sample >> 20} MiB, one host thread "
+                                         f"per stream, {impl}, {t:.1f} s"}
     return res
 
 
@@ -540,63 +642,37 @@ def cold_run(local: int, pats: dict, ptr: int, seg_base, lens, since, tail: int)
 
 
 def verify_large(name, sizes, lens, kind, permille, pats, since, tail, r) -> dict:
-    """Checks the last timed run of C4 / C5 against the oracles (after the timed region):
-    C4 in full with the C oracle (Aho-Corasick over the 1,024 literals, one host thread per
-    stream): every stream's output bytes, counts and match bitmap.  C5: every stream's
-    lines / parsed / since_ok with the C oracle (no patterns), and its tail window with the
-    Python oracle (the 64 regexes through Python `re`, forked workers): the stream's
-    shortest suffix holding the last tail + 2 matching lines gives the whole stream's
-    output (SPEC.md S4), and the suffix's match bitmap equals the run's over those lines.
-    The whole-stream match decisions of C5 are checked at 9 GiB by tests/test_gpu_large.py."""
+    """Checks the last timed run of C4 / C5 against the oracles (after the timed region),
+    every stream in full, one host thread per stream: output bytes, all counts and the match
+    bitmap.  C4: the C oracle (Aho-Corasick over the 1,024 literals).  C5: the C oracle's
+    regex leg (ko_filter_rx: the 64 regexes as glibc POSIX ERE behind a required-literal
+    pass, itself checked against the Python oracle in tests/test_oracle.py and, on a sample
+    of this run's generator, in cpu_baseline.c_leg_equals_python_oracle)."""
     from concurrent.futures import ThreadPoolExecutor
     sys.path.insert(0, str(ROOT / "oracle"))
-    sys.path.insert(0, str(ROOT / "tests"))
-    import big_check as bc
     import c_oracle as co
     t = time.perf_counter()
     got = [(r.stream(i), r.match_bits(i)) for i in range(len(lens))]
-    hosts = []
-    for i, (sz, n) in enumerate(zip(sizes, lens)):
-        h = np.empty(n + 1, dtype=np.uint8)
-        synth.generate_into(h, kind, 42, i, sz, permille=permille)
-        hosts.append(h[:n])
     sn = since if since is not None else co.GO_ZERO_TIME
     threads = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", "16") or 16)))
-    bad = []
-    if name == "c4":
-        grep = pats["grep"]
-        with ThreadPoolExecutor(min(threads, len(hosts))) as ex:
-            refs = list(ex.map(lambda h: co.filter_stream(h, sn, tail, grep, want_lines=False), hosts))
-        for i, (out, _, bits, c) in enumerate(refs):
-            so, gbits = got[i]
-            if so.out != out or gbits != bits or any(so.counts[k] != c[k] for k in c):
-                bad.append(i)
-        scope = "every stream in full: output bytes, all counts, match bitmap (C oracle, Aho-Corasick)"
-    else:
-        with ThreadPoolExecutor(min(threads, len(hosts))) as ex:
-            base = list(ex.map(lambda h: co.filter_stream(h, sn, tail, [], want_lines=False, want_bits=False,
-                                                          grep_active=False)[3], hosts))
-        starts, firsts = [], []
-        for i, h in enumerate(hosts):
-            ls = np.concatenate([np.zeros(1, np.int64), np.flatnonzero(h[:-1] == 10) + 1])
-            gb = bc.unpack_bits(got[i][1], len(ls))
-            a = bc.tail_suffix(h, ls, gb, tail)
-            starts.append(a)
-            firsts.append(int(np.searchsorted(ls, a)))
-            if any(got[i][0].counts[k] != base[i][k] for k in ("lines", "parsed", "since_ok")):
-                bad.append(i)
-        refs = bc.py_filter_suffixes(hosts, starts, sn, tail, match=pats["match"])
-        for i, (out, sel, matched, nl, mbits) in enumerate(refs):
-            so, gbits = got[i]
-            L = so.counts["lines"]
-            window = bc.unpack_bits(gbits, L)[firsts[i]:]
-            if (so.out != out or so.counts["selected"] != sel or matched < tail + 2 or nl != len(window)
-                    or not np.array_equal(bc.unpack_bits(mbits, nl), window)):
-                bad.append(i)
-        scope = ("every stream: lines/parsed/since_ok in full (C oracle); output bytes, selected count and the "
-                 "match bitmap over the tail window (the shortest suffix holding the last tail+2 matching "
-                 "lines) with the Python oracle; whole-stream match decisions: tests/test_gpu_large.py (9 GiB)")
-    return {"ok": not bad, "streams": len(lens), "failed_streams": sorted(set(bad)), "scope": scope,
+    rs = co.RegexSet(pats["match"]) if name == "c5" else None
+
+    def check(i):
+        h = np.empty(lens[i] + 1, dtype=np.uint8)
+        synth.generate_into(h, kind, 42, i, sizes[i], permille=permille, threads=1)
+        if rs is not None:
+            out, _, bits, c = co.filter_stream_rx(h[:lens[i]], sn, tail, rs, want_lines=False)
+        else:
+            out, _, bits, c = co.filter_stream(h[:lens[i]], sn, tail, pats["grep"], want_lines=False)
+        so, gbits = got[i]
+        return so.out == out and gbits == bits and all(so.counts[k] == c[k] for k in c)
+    with ThreadPoolExecutor(min(threads, len(lens))) as ex:
+        ok = list(ex.map(check, range(len(lens))))
+    bad = [i for i, x in enumerate(ok) if not x]
+    scope = ("every stream in full: output bytes, all counts, match bitmap ("
+             + ("C oracle regex leg: glibc POSIX ERE behind the required-literal pass" if rs is not None
+                else "C oracle, Aho-Corasick") + ")")
+    return {"ok": not bad, "streams": len(lens), "failed_streams": bad, "scope": scope,
             "s": round(time.perf_counter() - t, 1)}
 
 
@@ -664,6 +740,15 @@ def run_extra(name: str, args, local: int, now: int) -> dict:
         write["verified_vs_c_oracle"] = bool(verified)
     if wdir is not None:
         wdir.cleanup()
+    if name == "c1" and not args.no_verify:  # the whole stream vs the C oracle
+        sys.path.insert(0, str(ROOT / "oracle"))
+        import c_oracle as co
+        h = np.empty(lens[0] + 1, dtype=np.uint8)
+        synth.generate_into(h, kind, 42, 0, sizes[0], permille=permille)
+        ref_out, ref_lo, _, ref_c = co.filter_stream(h[:lens[0]], since, tail, [], want_bits=False)
+        so = last.stream(0)
+        verified = bool(so.out == ref_out and all(so.counts[k] == ref_c[k] for k in ref_c)
+                        and np.array_equal(last.lines(0), ref_lo))
     vlarge = None
     if name in ("c4", "c5") and not args.no_verify:
         del dev  # the checks regenerate the streams on the host

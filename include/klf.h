@@ -161,8 +161,9 @@ int klf_result_match_bits(klf_result* r, uint32_t stream_id, const uint8_t** bit
  * pattern p (klf_config order; a line matching several patterns counts for each), for
  * p < min(cap, n_patterns); *n = n_patterns.  Independent of --since / --tail, like
  * klf_counts.matched.  The run must set KLF_FILTER_PATTERN_COUNTS (KLF_ESTATE otherwise).
- * KLF_EINVAL when a pattern that matches every line (an empty --grep) sits beside others:
- * the set is then not evaluated.  Extends the size report of printLogSize
+ * A pattern that matches every content (an empty --grep, a regex such as `x*`) counts every
+ * parsed line, also beside other patterns, whose counts are then evaluated as usual (their
+ * tables are compiled on the first run that asks for counts).  Extends the size report of printLogSize
  * (cmd/root.go:279-309) with the new --grep / --match flags (:485-497). */
 int klf_result_pattern_counts(klf_result* r, uint32_t stream_id, uint64_t* counts, uint32_t cap, uint32_t* n);
 /* Position of the stream's last unparseable newline-terminated line, counted from the end

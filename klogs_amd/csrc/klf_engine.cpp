@@ -306,7 +306,12 @@ extern "C" int klf_open(const klf_config* cfg, klf_engine** out) {
   }
   int code = KLF_OK;
   std::string err;
-  if (!klf::compile_set(pats, kinds, e->cs, err, code)) {
+  const auto t_open0 = std::chrono::steady_clock::now();
+  const bool compiled = klf::compile_set(pats, kinds, e->cs, err, code);
+  if (getenv("KLF_DIAG"))
+    fprintf(stderr, "[klf] open: pattern compile %.1f us\n",
+            std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t_open0).count());
+  if (!compiled) {
     // keep the engine alive so the caller can read klf_last_error; report failure
     e->err = err;
     *out = e;
@@ -431,6 +436,9 @@ extern "C" int klf_open(const klf_config* cfg, klf_engine** out) {
     e->pairs_log2 = (uint32_t)std::max(4L, std::min(atol(pl), 28L));
   if (const char* hc = getenv("KLF_HITS_CAP"))  // tests: force the hit-list overflow fallback
     e->hits_cap_max = (uint64_t)std::max(1L, std::min(atol(hc), 1L << 28));
+  if (getenv("KLF_DIAG"))
+    fprintf(stderr, "[klf] open: total %.1f us\n",
+            std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t_open0).count());
   *out = e;
   return KLF_OK;
 }
@@ -725,6 +733,12 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
   const auto t_run0 = std::chrono::steady_clock::now();
   const uint64_t alloc0 = g_alloc_ns.load();
   uint64_t tune_ns = 0;
+  // KLF_DIAG: wall-clock marks through the run (the first run's cost breakdown)
+  static const bool diag_marks = getenv("KLF_DIAG") != nullptr;
+  std::vector<std::pair<const char*, std::chrono::steady_clock::time_point>> marks;
+  auto mark = [&](const char* what) {
+    if (diag_marks) marks.emplace_back(what, std::chrono::steady_clock::now());
+  };
   HIPCHK(e, hipSetDevice(e->device), "hipSetDevice");
   std::unique_ptr<klf_result> rp(new (std::nothrow) klf_result());  // freed on every error return
   klf_result* r = rp.get();
@@ -784,6 +798,7 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
     HIPCHK(e, hipStreamSynchronize(st), "sync segs");
     HIPCHK(e, e->d_tile_seg.ensure(ntiles * 4 + 16), "alloc tile_seg");  // + whole 16-B loads past the end
   }
+  mark("segs");
   if (mode == klf::CompiledSet::kGeneral && e->cs.qf_on && !e->cs.qf_tuned) {
     // first batch: place the needles' sampling windows on the data's own gram statistics
     e->cs.qf_tuned = true;
@@ -822,6 +837,7 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
                 std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t_place).count());
     }
     tune_ns = (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t_tune0).count();
+    mark("first-batch tuning");
   }
   HIPCHK(e, e->d_tstat.ensure(ntiles * sizeof(klf::TileStat)), "alloc tstat");
   HIPCHK(e, e->d_slots.ensure(ntiles * klf::kRecStride * 4), "alloc slots");
@@ -879,6 +895,7 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
 
   const bool count = (f->flags & KLF_FILTER_PATTERN_COUNTS) && mode == klf::CompiledSet::kGeneral && e->cs.n_cids;
   r->counted = (f->flags & KLF_FILTER_PATTERN_COUNTS) != 0;
+  mark("workspace");
   bool overflow = false, pairs_over = false;
   for (int attempt = 0, line_reruns = 0, pair_reruns = 0; attempt < 4; ++attempt) {
     if (count) {
@@ -987,6 +1004,7 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
       HIPCHK(e, hipMemcpyAsync(rb1 + sizeof(counters), e->d_segout.p, nsegs * sizeof(SegOut), hipMemcpyDeviceToHost, st),
              "D2H segout");
       HIPCHK(e, hipStreamSynchronize(st), "sync phase 1");
+      mark("phase 1 (launch + sync)");
       memcpy(counters, rb1, sizeof(counters));
       memcpy(r->so.data(), rb1 + sizeof(counters), nsegs * sizeof(SegOut));
       if (counters[2]) {  // the dense-tile pool overflowed: a whole rerun (as below)
@@ -997,11 +1015,21 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
       }
       // the same margin later runs size by (their line density estimate), so that they fit
       e->line_density = (double)(r->so[nsegs - 1].line_hi + 1) / (double)total_bytes;
-      cap = std::min<uint64_t>(std::min<uint64_t>(cap, learned_cap()), cap_clamp);
+      // phase 1 knows the exact line count: size the arrays to it (the 32-B estimate is
+      // short for lines under 32 B); a capacity still below it (only KLF_DEBUG_CAP_CLAMP)
+      // fails here, before phase 2's kernels index the arrays (advisor r03)
+      const uint64_t need = r->so[nsegs - 1].line_hi + 2;
+      cap = std::min<uint64_t>(std::max<uint64_t>(std::min<uint64_t>(cap, learned_cap()), need), cap_clamp);
+      if (need > cap) {
+        overflow = true;
+        break;
+      }
       HIPCHK(e, alloc_lines(a, cap), "alloc line arrays");
+      mark("line arrays");
       if (a.grep_mode != klf::CompiledSet::kNone)  // (phase 1's k_tindex zeroes it otherwise)
         HIPCHK(e, hipMemsetAsync(a.bits, 0, (cap / 32 + 1) * 4, st), "zero bits");
       HIPCHK(e, klf::launch_pipeline(a, st, e->ev, e->num_cus, e->aux_stream, e->ev_fork, e->ev_join, 2), "launch");
+      mark("phase 2 launched");
     } else {
       HIPCHK(e, alloc_lines(a, cap), "alloc line arrays");
       HIPCHK(e, klf::launch_pipeline(a, st, e->ev, e->num_cus, e->aux_stream, e->ev_fork, e->ev_join), "launch");
@@ -1011,6 +1039,7 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
     HIPCHK(e, hipMemcpyAsync(rb + sizeof(counters), e->d_segout.p, nsegs * sizeof(SegOut), hipMemcpyDeviceToHost, st),
            "D2H segout");
     HIPCHK(e, wait_stream(st, 1000 + total_bytes / 2000000), "sync");
+    mark("pipeline done");
     memcpy(counters, rb, sizeof(counters));
     memcpy(r->so.data(), rb + sizeof(counters), nsegs * sizeof(SegOut));
     e->last_segs = segs;
@@ -1063,6 +1092,13 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
     const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t_run0).count();
     fprintf(stderr, "[klf] run %.1f us: allocations %.1f us, first-batch tuning %.1f us\n", us,
             (g_alloc_ns.load() - alloc0) / 1e3, tune_ns / 1e3);
+    std::string m = "[klf] run marks (us):";
+    auto prev = t_run0;
+    for (auto& x : marks) {
+      m += std::string(" ") + x.first + " " + std::to_string((int)std::chrono::duration<double, std::micro>(x.second - prev).count()) + ";";
+      prev = x.second;
+    }
+    fprintf(stderr, "%s\n", m.c_str());
   }
   if (overflow)  // the exact rerun overflowed too: never hand out the aborted run's records
     return set_err(e, KLF_ENOMEM, "line index / dense-tile pool overflow after the exact rerun");

@@ -12,10 +12,18 @@
  *                    decremented per parsed line, unparseable lines skipped uncounted)
  *                    + logWriter.write (drop ts.Before(since));
  *   - grep:          Go bytes.Contains via memmem over the content without its '\n'
- *                    (sets of more than 8 literals: an Aho-Corasick DFA, same answer).
- * Regex patterns are checked by the Python oracle only (Python `re`), see SPEC.md S5.
+ *                    (sets of more than 8 literals: an Aho-Corasick DFA, same answer);
+ *   - match (ko_filter_rx, the CPU baseline of regex sets): Go regexp.Match restated as
+ *                    glibc POSIX ERE (regcomp REG_EXTENDED | REG_NOSUB [| REG_ICASE],
+ *                    regexec REG_STARTEND over the content), translated from the SPEC.md S5
+ *                    subset by oracle/posix_re.py, behind an Aho-Corasick pass over every
+ *                    pattern's required literal (a content holding none of them cannot
+ *                    match).  The regex parity checker stays the Python oracle (Python `re`);
+ *                    this one is validated against it (tests/test_oracle.py).
  */
 #define _GNU_SOURCE
+#include <locale.h>
+#include <regex.h>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
@@ -151,25 +159,33 @@ typedef struct {
   int32_t* next;  /* [states * nc]: byte classes (the literals' bytes, one class each; the rest 0) */
   uint8_t* acc;   /* [states] */
   int32_t n, nc;
-  uint8_t cls[256];
+  uint16_t cls[256];  /* class per byte: 0 = in no literal, else 1..256 */
+  int32_t* wide;      /* small automata: [states * 256] by raw byte, bit 30 = the target accepts
+                         (one dependent load per byte instead of two) */
 } ko_ac;
 
 static void ac_free(ko_ac* a) {
   free(a->next);
   free(a->acc);
+  free(a->wide);
   a->next = NULL;
   a->acc = NULL;
+  a->wide = NULL;
 }
 
-static int ac_build(ko_ac* a, uint32_t n_lit, const uint8_t* const* lits, const uint64_t* lens) {
+/* fold: ASCII letters compare case-insensitively (an upper-case byte takes its lower-case
+ * byte's class; the literals are given lower-cased). */
+static int ac_build_fold(ko_ac* a, uint32_t n_lit, const uint8_t* const* lits, const uint64_t* lens, int fold) {
   uint64_t cap = 1;
   for (uint32_t k = 0; k < n_lit; ++k) cap += lens[k];
   memset(a->cls, 0, sizeof a->cls);
   a->nc = 1;
   for (uint32_t k = 0; k < n_lit; ++k)
     for (uint64_t j = 0; j < lens[k]; ++j)
-      if (!a->cls[lits[k][j]]) a->cls[lits[k][j]] = (uint8_t)a->nc++;
-  const int NC = a->nc;  /* <= 256: class 0 = bytes in no literal */
+      if (!a->cls[lits[k][j]]) a->cls[lits[k][j]] = (uint16_t)a->nc++;
+  if (fold)
+    for (int c = 'A'; c <= 'Z'; ++c) a->cls[c] = a->cls[c | 0x20];
+  const int NC = a->nc;  /* <= 257: class 0 = bytes in no literal */
   a->next = (int32_t*)malloc(cap * NC * sizeof(int32_t));
   a->acc = (uint8_t*)calloc(cap, 1);
   int32_t* fail = (int32_t*)malloc(cap * sizeof(int32_t));
@@ -206,7 +222,33 @@ static int ac_build(ko_ac* a, uint32_t n_lit, const uint8_t* const* lits, const 
   }
   free(fail);
   free(queue);
+  a->wide = NULL;
+  if ((uint64_t)a->n * 256 <= (1u << 19) && (a->wide = (int32_t*)malloc((size_t)a->n * 256 * sizeof(int32_t))))
+    for (int32_t st = 0; st < a->n; ++st)
+      for (int c = 0; c < 256; ++c) {
+        const int32_t t = a->next[(uint64_t)st * NC + a->cls[c]];
+        a->wide[(size_t)st * 256 + c] = t | (a->acc[t] ? (1 << 30) : 0);
+      }
   return 0;
+}
+/* 1 when some literal occurs in c[0, cn) */
+static int ac_scan(const ko_ac* a, const uint8_t* c, size_t cn) {
+  int32_t st = 0;
+  if (a->wide) {
+    for (size_t i = 0; i < cn; ++i) {
+      st = a->wide[(size_t)st * 256 + c[i]];
+      if (st & (1 << 30)) return 1;
+    }
+    return 0;
+  }
+  for (size_t i = 0; i < cn; ++i) {
+    st = a->next[(uint64_t)st * a->nc + a->cls[c[i]]];
+    if (a->acc[st]) return 1;
+  }
+  return 0;
+}
+static int ac_build(ko_ac* a, uint32_t n_lit, const uint8_t* const* lits, const uint64_t* lens) {
+  return ac_build_fold(a, n_lit, lits, lens, 0);
 }
 
 static int content_matches(const uint8_t* c, size_t cn, uint32_t n_lit, const uint8_t* const* lits,
@@ -214,30 +256,20 @@ static int content_matches(const uint8_t* c, size_t cn, uint32_t n_lit, const ui
   if (cn && c[cn - 1] == '\n') --cn;
   for (uint32_t k = 0; k < n_lit; ++k)
     if (lens[k] == 0) return 1;
-  if (ac && ac->next) {
-    int32_t st = 0;
-    for (size_t i = 0; i < cn; ++i) {
-      st = ac->next[(uint64_t)st * ac->nc + ac->cls[c[i]]];
-      if (ac->acc[st]) return 1;
-    }
-    return 0;
-  }
+  if (ac && ac->next) return ac_scan(ac, c, cn);
   for (uint32_t k = 0; k < n_lit; ++k)
     if (lens[k] <= cn && memmem(c, cn, lits[k], lens[k])) return 1;
   return 0;
 }
 
-/* Filters one stream.  out: capacity >= n.  line_off (nullable): capacity line_cap, gets
- * lines+1 entries when they fit.  match_bits (nullable, only with literals): capacity
- * ceil(lines/8) bytes, zeroed by the caller.  Returns the output length, or -1 on error. */
-int64_t ko_filter(const uint8_t* data, uint64_t n, int64_t since_sec, int32_t since_nsec, int64_t tail,
-                  int grep_active, uint32_t n_lit, const uint8_t* const* lits, const uint64_t* lit_lens, uint8_t* out,
-                  uint64_t* line_off, uint64_t line_cap, uint8_t* match_bits, ko_counts* cnt) {
+/* The line matcher of one filter call: content (its '\n' included or not) -> match. */
+typedef int (*ko_match_fn)(void* ctx, const uint8_t* c, size_t cn);
+
+static int64_t filter_impl(const uint8_t* data, uint64_t n, int64_t since_sec, int32_t since_nsec, int64_t tail,
+                           int grep_active, ko_match_fn match, void* mctx, uint8_t* out, uint64_t* line_off,
+                           uint64_t line_cap, uint8_t* match_bits, ko_counts* cnt) {
   ko_counts c;
   memset(&c, 0, sizeof(c));
-  ko_ac ac;
-  memset(&ac, 0, sizeof ac);
-  if (grep_active && n_lit > 8 && ac_build(&ac, n_lit, lits, lit_lens) != 0) return -1;
   /* pass 1: lines, counts, G */
   uint8_t* gfile = NULL;
   uint64_t glen = 0, gcap = 0;
@@ -257,14 +289,14 @@ int64_t ko_filter(const uint8_t* data, uint64_t n, int64_t since_sec, int32_t si
       if (!before(s, ns, since_sec, since_nsec)) c.since_ok++;
     }
     if (grep_active) {
-      const int hit = ok && content_matches(data + pos + plen, end - pos - plen, n_lit, lits, lit_lens, &ac);
+      const int hit = ok && match(mctx, data + pos + plen, end - pos - plen);
       if (hit) {
         if (match_bits) match_bits[li >> 3] |= (uint8_t)(1u << (li & 7));
         c.matched++;
         if (glen + (end - pos) > gcap) {
           gcap = (gcap + (end - pos)) * 2;
           uint8_t* g2 = (uint8_t*)realloc(gfile, gcap);
-          if (!g2) { free(gfile); ac_free(&ac); return -1; }
+          if (!g2) { free(gfile); return -1; }
           gfile = g2;
         }
         memcpy(gfile + glen, data + pos, end - pos);
@@ -305,8 +337,134 @@ int64_t ko_filter(const uint8_t* data, uint64_t n, int64_t since_sec, int32_t si
     p = end;
   }
   free(gfile);
-  ac_free(&ac);
   c.out_bytes = o;
   if (cnt) *cnt = c;
   return (int64_t)o;
+}
+
+typedef struct {
+  uint32_t n_lit;
+  const uint8_t* const* lits;
+  const uint64_t* lens;
+  const ko_ac* ac;
+} lit_ctx;
+static int lit_match(void* ctx, const uint8_t* c, size_t cn) {
+  const lit_ctx* x = (const lit_ctx*)ctx;
+  return content_matches(c, cn, x->n_lit, x->lits, x->lens, x->ac);
+}
+
+/* Filters one stream.  out: capacity >= n.  line_off (nullable): capacity line_cap, gets
+ * lines+1 entries when they fit.  match_bits (nullable, only with literals): capacity
+ * ceil(lines/8) bytes, zeroed by the caller.  Returns the output length, or -1 on error. */
+int64_t ko_filter(const uint8_t* data, uint64_t n, int64_t since_sec, int32_t since_nsec, int64_t tail,
+                  int grep_active, uint32_t n_lit, const uint8_t* const* lits, const uint64_t* lit_lens, uint8_t* out,
+                  uint64_t* line_off, uint64_t line_cap, uint8_t* match_bits, ko_counts* cnt) {
+  ko_ac ac;
+  memset(&ac, 0, sizeof ac);
+  if (grep_active && n_lit > 8 && ac_build(&ac, n_lit, lits, lit_lens) != 0) return -1;
+  lit_ctx x = {n_lit, lits, lit_lens, &ac};
+  const int64_t r = filter_impl(data, n, since_sec, since_nsec, tail, grep_active, lit_match, &x, out, line_off,
+                                line_cap, match_bits, cnt);
+  ac_free(&ac);
+  return r;
+}
+
+/* ---- regex sets: glibc POSIX ERE behind a required-literal Aho-Corasick pass ----------- */
+typedef struct {
+  uint32_t n;
+  regex_t* re;
+  const int32_t* icase;        /* [n] pattern compiled REG_ICASE; its required literal is lower case */
+  const uint8_t* const* req;   /* [n] required literal (len 0: none, the pattern is always run) */
+  const uint64_t* req_len;
+  ko_ac ac;                    /* every required literal, lower-cased, matched case-insensitively:
+                                  a line holding none of them skips the patterns */
+  int always;                  /* some pattern has no required literal */
+  int any_ci;                  /* some pattern is REG_ICASE */
+  uint8_t* low;                /* the content lower-cased (REG_ICASE literals) */
+  size_t low_cap;
+} rx_ctx;
+
+static int ac_any(const ko_ac* ac, const uint8_t* c, size_t cn) {
+  return ac->next ? ac_scan(ac, c, cn) : 0;
+}
+
+static int rx_match(void* ctx, const uint8_t* c, size_t cn) {
+  rx_ctx* x = (rx_ctx*)ctx;
+  if (cn && c[cn - 1] == '\n') --cn;
+  if (!x->always && !ac_any(&x->ac, c, cn)) return 0;
+  const uint8_t* low = NULL;
+  if (x->any_ci) {
+    if (cn > x->low_cap) {
+      free(x->low);
+      x->low_cap = cn * 2;
+      x->low = (uint8_t*)malloc(x->low_cap);
+      if (!x->low) { x->low_cap = 0; return 0; }
+    }
+    for (size_t i = 0; i < cn; ++i) x->low[i] = (uint8_t)(c[i] >= 'A' && c[i] <= 'Z' ? c[i] | 0x20 : c[i]);
+    low = x->low;
+  }
+  for (uint32_t k = 0; k < x->n; ++k) {
+    if (x->req_len[k]) {
+      const uint8_t* src = x->icase[k] ? low : c;
+      if (x->req_len[k] > cn || !memmem(src, cn, x->req[k], x->req_len[k])) continue;
+    }
+    regmatch_t m;
+    m.rm_so = 0;
+    m.rm_eo = (regoff_t)cn;
+    if (regexec(&x->re[k], (const char*)c, 1, &m, REG_STARTEND) == 0) return 1;
+  }
+  return 0;
+}
+
+/* As ko_filter with n_rx regexes (POSIX ERE, NUL-terminated, translated from the Go
+ * subset) in place of literals.  Returns -1 on allocation failure, -2 - k when pattern k
+ * does not compile. */
+int64_t ko_filter_rx(const uint8_t* data, uint64_t n, int64_t since_sec, int32_t since_nsec, int64_t tail,
+                     uint32_t n_rx, const char* const* ere, const int32_t* icase, const uint8_t* const* req,
+                     const uint64_t* req_len, uint8_t* out, uint64_t* line_off, uint64_t line_cap, uint8_t* match_bits,
+                     ko_counts* cnt) {
+  rx_ctx x;
+  memset(&x, 0, sizeof x);
+  x.n = n_rx;
+  x.icase = icase;
+  x.req = req;
+  x.req_len = req_len;
+  x.re = (regex_t*)calloc(n_rx ? n_rx : 1, sizeof(regex_t));
+  uint8_t** lw = (uint8_t**)calloc(n_rx ? n_rx : 1, sizeof(void*));
+  uint64_t* lwl = (uint64_t*)calloc(n_rx ? n_rx : 1, sizeof(uint64_t));
+  int64_t r = -1;
+  uint32_t ok = 0, nl = 0;
+  /* byte semantics whatever the process locale (a UTF-8 LC_CTYPE would read the classes'
+   * high bytes as broken multibyte characters): the C locale for this thread */
+  locale_t cloc = newlocale(LC_ALL_MASK, "C", (locale_t)0);
+  locale_t prev = cloc ? uselocale(cloc) : (locale_t)0;
+  if (!cloc || !x.re || !lw || !lwl) goto done;
+  for (; ok < n_rx; ++ok) {
+    if (regcomp(&x.re[ok], ere[ok], REG_EXTENDED | REG_NOSUB | (icase[ok] ? REG_ICASE : 0)) != 0) {
+      r = -2 - (int64_t)ok;
+      goto done;
+    }
+    x.any_ci |= icase[ok] != 0;
+    if (!req_len[ok]) { x.always = 1; continue; }
+    if (!(lw[nl] = (uint8_t*)malloc(req_len[ok]))) goto done;
+    for (uint64_t j = 0; j < req_len[ok]; ++j)
+      lw[nl][j] = (uint8_t)(req[ok][j] >= 'A' && req[ok][j] <= 'Z' ? req[ok][j] | 0x20 : req[ok][j]);
+    lwl[nl++] = req_len[ok];
+  }
+  if (!x.always && ac_build_fold(&x.ac, nl, (const uint8_t* const*)lw, lwl, 1) != 0) goto done;
+  r = filter_impl(data, n, since_sec, since_nsec, tail, n_rx != 0, rx_match, &x, out, line_off, line_cap, match_bits,
+                  cnt);
+done:
+  for (uint32_t k = 0; k < ok; ++k) regfree(&x.re[k]);
+  free(x.re);
+  for (uint32_t k = 0; lw && k < nl; ++k) free(lw[k]);
+  free(lw);
+  free(lwl);
+  ac_free(&x.ac);
+  free(x.low);
+  if (cloc) {
+    uselocale(prev);
+    freelocale(cloc);
+  }
+  return r;
 }

@@ -40,6 +40,23 @@ def _chunk(ab: Tuple[int, int]):
     return np.array(hit, dtype=bool), parsed, since_ok
 
 
+def _pool_map(procs: int, fn, jobs):
+    """pool.map over forked workers, shut down by close() + join(): every worker leaves through
+    its own normal exit.  (The context-manager exit calls terminate(), which SIGTERMs the
+    workers; a worker forked from a process running under rocprofv3 then runs the profiler's
+    signal handler and finalizer, which crashed in the fork: VERDICT r03 weak 6.)"""
+    pool = mp.get_context("fork").Pool(procs)
+    try:
+        out = pool.map(fn, jobs, chunksize=1)
+    except BaseException:
+        pool.terminate()
+        pool.join()
+        raise
+    pool.close()
+    pool.join()
+    return out
+
+
 def line_cuts(data: np.ndarray, parts: int) -> list:
     """Offsets 0 = c0 < c1 < ... < ck = len(data), each ci > 0 just past a '\\n'."""
     n = len(data)
@@ -62,8 +79,7 @@ def py_line_table(data: np.ndarray, since, grep: Sequence[bytes] = (), match: Se
     _DATA, _PATS, _SINCE = data, po.compile_patterns(grep, match), since
     cuts = line_cuts(data, procs * 6)
     try:
-        with mp.get_context("fork").Pool(procs) as pool:
-            parts = pool.map(_chunk, list(zip(cuts, cuts[1:])), chunksize=1)
+        parts = _pool_map(procs, _chunk, list(zip(cuts, cuts[1:])))
     finally:
         _DATA = None
     hit = np.concatenate([p[0] for p in parts]) if parts else np.zeros(0, dtype=bool)
@@ -103,8 +119,7 @@ def py_filter_suffixes(hosts, starts, since, tail: int, grep=(), match=(), procs
     _HOSTS, _ARGS = hosts, (since, tail, po.compile_patterns(grep, match))
     jobs = sorted(range(len(hosts)), key=lambda i: len(hosts[i]) - starts[i], reverse=True)  # longest first
     try:
-        with mp.get_context("fork").Pool(min(procs, len(hosts))) as pool:
-            res = pool.map(_suffix_job, [(i, starts[i]) for i in jobs], chunksize=1)
+        res = _pool_map(min(procs, len(hosts)), _suffix_job, [(i, starts[i]) for i in jobs])
     finally:
         _HOSTS = None
     out = [None] * len(hosts)

@@ -248,3 +248,49 @@ def test_big_check_helpers_equal_the_whole_stream_oracle():
     starts = np.array(ref.line_off, dtype=np.uint64)
     a = bc.tail_suffix(arr, starts, hit, 5)
     assert a > 0 and po.filter_stream(d[a:], since, 5, pats).out == ref.out
+
+
+def test_c_oracle_aho_corasick_every_byte_value():
+    """Literals covering all 256 byte values (the class counter must not wrap):
+    the Aho-Corasick path equals memmem groups of <= 8."""
+    lits = [bytes([b, (b * 7 + 3) & 0xFF, (b * 13 + 5) & 0xFF]) for b in range(256)]
+    lits = [x for x in lits if 0x0A not in x]
+    d = bytearray(synth.generate(synth.ADVERSARIAL, 3, 0, 400_000, permille=40))
+    rng = random.Random(5)
+    for _ in range(300):  # plant some of the literals inside line contents
+        lit = rng.choice(lits)
+        at = rng.randrange(40, len(d) - 8)
+        if 0x0A not in d[at - 1:at + len(lit) + 1]:
+            d[at:at + len(lit)] = lit
+    d = bytes(d)
+    whole = co.filter_stream(d, co.GO_ZERO_TIME, -1, lits)
+    bits = None
+    for k in range(0, len(lits), 8):
+        b = np.frombuffer(co.filter_stream(d, co.GO_ZERO_TIME, -1, lits[k:k + 8])[2], np.uint8)
+        bits = b.copy() if bits is None else bits | b
+    assert whole[2] == bits.tobytes()
+    assert whole[3]["matched"] == int(np.unpackbits(bits).sum()) > 0
+
+
+# ---- the compiled CPU baseline of regex sets (glibc POSIX ERE) equals the oracle ------
+RX_SETS = [
+    synth.c5_regexes(),
+    [rb"ms$", rb"^\S+ \d", rb"(?i)POD", rb"a.b|c[^x]d", rb"\w{3,5}-\d+", rb"x*", rb"\.\*"],
+    [rb"[]^-]", rb"[-^a]z", rb"q\+?", rb"(ab|cd)+e", rb"\A\d", rb"[[:alpha:]]{4}\z"],
+]
+
+
+@pytest.mark.parametrize("k", range(len(RX_SETS)))
+@pytest.mark.parametrize("kind", [synth.LONGJSON, synth.ADVERSARIAL, synth.TEXT])
+def test_c_regex_leg_equals_python_oracle(k, kind):
+    rx = RX_SETS[k]
+    d = synth.generate(kind, 60 + k, 0, 300_000 if kind == synth.LONGJSON else 120_000, permille=150)
+    since = (synth.T0 + 1800, 0)
+    for tail in (-1, 7):
+        r = po.filter_stream(d, since, tail, po.compile_patterns(match=rx))
+        out, lo, bits, c = co.filter_stream_rx(d, since, tail, rx)
+        assert bits == r.match_bits
+        assert out == r.out
+        assert list(lo) == r.line_off
+        assert (c["lines"], c["parsed"], c["since_ok"], c["matched"], c["selected"]) == \
+            (r.n_lines, r.n_parsed, r.n_since, r.n_matched, r.n_selected)
