@@ -126,12 +126,20 @@ struct klf_engine {
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   hipEvent_t copy_done = nullptr;
   bool ran = false;                    // klf_run since the last klf_reset (stage -> ESTATE)
-  std::unique_ptr<klf::CopyPool> copier;
+  std::unique_ptr<klf::CopyPool> copier;  // started by the first klf_stage (device-resident runs never stage)
+  std::once_flag copier_once;
   DevBuf d_asm;                        // k_assemble piece table
   DevBuf d_scratch;                    // small query results (klf_result_last_unparsed)
   DevBuf d_ac_out, d_ac_dict, d_pcount, d_pairs;  // per-pattern counts
   uint32_t pairs_log2 = 20;            // (line, pattern) pair set: 2^20 entries, grows on overflow
   uint32_t n_user = 0;                 // patterns as given to klf_open
+  // a set with an always-pattern beside others (CompiledSet::also_all_pending): the patterns,
+  // compiled in full on the first run that asks for per-pattern counts
+  std::vector<std::vector<uint8_t>> pend_pats;
+  std::vector<uint32_t> pend_kinds;
+  bool tune_later = true;
+  int counts_code = KLF_OK;            // that compile failed: counts unavailable (the filter is kAll's)
+  std::string counts_err;
   // device pattern tables
   DevBuf d_lit, d_ac_class, d_ac_next, d_ac_accept, d_rx_class, d_rx_b, d_rx_follow, d_rx_vec, d_rx_flags, d_rx_pre;
   DevBuf d_qf_bitmap, d_qf_head, d_qf_ent, d_qf_nbytes, d_cand, d_rx_vec4, d_qhits, d_hslots, d_hist, d_hflat, d_qf_anc;
@@ -290,6 +298,113 @@ static hipError_t upload_prefilter(klf_engine* e) {
   return hipSuccess;
 }
 
+// Host tables -> device buffers through the pinned staging buffer: one memcpy each into it,
+// async copies in stream order, no host sync (the next staged upload waits for this one's
+// event before it rewrites the buffer).  klf_open's pattern tables go up this way.
+struct TableItem {
+  DevBuf* dst;
+  const void* src;
+  size_t bytes;
+};
+static hipError_t stage_tables(klf_engine* e, const std::vector<TableItem>& items) {
+  hipError_t h;
+  if (e->stage_ev_pending && (h = hipEventSynchronize(e->stage_ev)) != hipSuccess) return h;
+  e->stage_ev_pending = false;
+  size_t total = 0;
+  for (auto& it : items) {
+    if ((h = it.dst->ensure(std::max<size_t>(it.bytes, 16))) != hipSuccess) return h;
+    total += (it.bytes + 255) & ~(size_t)255;
+  }
+  if ((h = e->h_stage.ensure(total + 256)) != hipSuccess) return h;
+  size_t off = 0;
+  for (auto& it : items) {
+    if (it.bytes) {
+      memcpy(e->h_stage.as<uint8_t>() + off, it.src, it.bytes);
+      if ((h = hipMemcpyAsync(it.dst->p, e->h_stage.as<uint8_t>() + off, it.bytes, hipMemcpyHostToDevice, e->stream)) !=
+          hipSuccess)
+        return h;
+    }
+    off += (it.bytes + 255) & ~(size_t)255;
+  }
+  if ((h = hipEventRecord(e->stage_ev, e->stream)) != hipSuccess) return h;
+  e->stage_ev_pending = true;
+  return hipSuccess;
+}
+template <class T>
+static TableItem item(DevBuf& b, const std::vector<T>& v) {
+  return TableItem{&b, v.data(), v.size() * sizeof(T)};
+}
+
+// The compiled set's matcher tables to the device (the prefilter layout only when it is
+// placed already: tune_later = the first batch's statistics will place it).
+static hipError_t upload_pattern_tables(klf_engine* e, bool tune_later) {
+  const auto& cs = e->cs;
+  hipError_t h;
+  std::vector<TableItem> items;
+  std::vector<uint8_t> padded;
+  std::vector<uint64_t> vec, vec4;
+  std::vector<uint32_t> pre0;
+  if (cs.mode == klf::CompiledSet::kLiteral1) {
+    padded = cs.literal;
+    padded.resize((cs.literal.size() + 3) / 4 * 4 + 4, 0);  // bytes, then dword view at +0
+    items.push_back(item(e->d_lit, padded));
+  } else if (cs.mode == klf::CompiledSet::kGeneral) {
+    klf::DevPatterns& P = e->dpats;
+    if (cs.ac_states) {
+      for (auto x : {item(e->d_ac_class, cs.ac_class), item(e->d_ac_next, cs.ac_next), item(e->d_ac_accept, cs.ac_accept),
+                     item(e->d_ac_out, cs.ac_out), item(e->d_ac_dict, cs.ac_dict)})
+        items.push_back(x);
+      P.ac_states = cs.ac_states;
+      P.ac_classes = cs.ac_classes;
+    }
+    if (cs.rx_count) {
+      // first | last | init0 | end, each [rx_count]; and [rx][4] interleaved for k_nfa
+      for (const auto* v : {&cs.rx_first, &cs.rx_last, &cs.rx_init0, &cs.rx_end}) vec.insert(vec.end(), v->begin(), v->end());
+      for (uint32_t r = 0; r < cs.rx_count; ++r)
+        for (const auto* v : {&cs.rx_first, &cs.rx_last, &cs.rx_init0, &cs.rx_end}) vec4.push_back((*v)[r]);
+      pre0 = cs.rx_pre.empty() ? std::vector<uint32_t>(cs.rx_count, klf::kRxPreUnbounded) : cs.rx_pre;
+      for (auto x : {item(e->d_rx_class, cs.rx_class), item(e->d_rx_b, cs.rx_b), item(e->d_rx_follow, cs.rx_follow),
+                     item(e->d_rx_vec, vec), item(e->d_rx_flags, cs.rx_flags), item(e->d_rx_pre, pre0),
+                     item(e->d_rx_vec4, vec4)})
+        items.push_back(x);
+      P.rx_unbounded = (uint32_t)std::count(pre0.begin(), pre0.end(), klf::kRxPreUnbounded);
+      P.rx_count = cs.rx_count;
+      P.rx_classes = cs.rx_classes;
+      P.rx_maxpos = std::max<uint32_t>(1, cs.rx_maxpos);
+    }
+  }
+  if (!items.empty() && (h = stage_tables(e, items)) != hipSuccess) return h;
+  if (cs.mode == klf::CompiledSet::kGeneral) {  // device pointers of the staged tables
+    klf::DevPatterns& P = e->dpats;
+    if (cs.ac_states) {
+      P.ac_class = e->d_ac_class.as<uint8_t>();
+      P.ac_next = e->d_ac_next.as<uint32_t>();
+      P.ac_accept = e->d_ac_accept.as<uint8_t>();
+      P.ac_out = e->d_ac_out.as<int32_t>();
+      P.ac_dict = e->d_ac_dict.as<uint32_t>();
+    }
+    if (cs.rx_count) {
+      const uint64_t* v = e->d_rx_vec.as<uint64_t>();
+      P.rx_class = e->d_rx_class.as<uint8_t>();
+      P.rx_b = e->d_rx_b.as<uint64_t>();
+      P.rx_follow = e->d_rx_follow.as<uint64_t>();
+      P.rx_first = v;
+      P.rx_last = v + cs.rx_count;
+      P.rx_init0 = v + 2 * cs.rx_count;
+      P.rx_end = v + 3 * cs.rx_count;
+      P.rx_flags = e->d_rx_flags.as<uint32_t>();
+      P.rx_pre = e->d_rx_pre.as<uint32_t>();
+      P.rx_vec = e->d_rx_vec4.as<uint64_t>();
+    }
+    if (cs.qf_on) {
+      if (!tune_later && (h = upload_prefilter(e)) != hipSuccess) return h;
+      P.qf_on = 1;
+      P.qf_fold = cs.qf_fold;
+    }
+  }
+  return hipSuccess;
+}
+
 extern "C" int klf_open(const klf_config* cfg, klf_engine** out) {
   if (!cfg || !out || (cfg->n_patterns && !cfg->patterns)) return KLF_EINVAL;
   *out = nullptr;
@@ -307,7 +422,16 @@ extern "C" int klf_open(const klf_config* cfg, klf_engine** out) {
   int code = KLF_OK;
   std::string err;
   const auto t_open0 = std::chrono::steady_clock::now();
-  const bool compiled = klf::compile_set(pats, kinds, e->cs, err, code);
+  // the prefilter layout waits for the first batch's statistics (the first run places the
+  // needles), unless tuning is off (KLF_QF_TUNE=0: placed here, from byte-class estimates)
+  const char* tune_env = getenv("KLF_QF_TUNE");
+  const bool tune_later = !(tune_env && strcmp(tune_env, "0") == 0);
+  const bool compiled = klf::compile_set(pats, kinds, e->cs, err, code, !tune_later, true);
+  e->tune_later = tune_later;
+  if (compiled && e->cs.also_all_pending) {
+    e->pend_pats = pats;
+    e->pend_kinds = kinds;
+  }
   if (getenv("KLF_DIAG"))
     fprintf(stderr, "[klf] open: pattern compile %.1f us\n",
             std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t_open0).count());
@@ -324,9 +448,9 @@ extern "C" int klf_open(const klf_config* cfg, klf_engine** out) {
   e->dpats.n_lits = e->cs.n_lits;
   hipError_t h = hipSetDevice(cfg->device);
   if (h != hipSuccess) { e->err = std::string("hipSetDevice: ") + hipGetErrorString(h); *out = e; return KLF_EHIP; }
-  hipDeviceProp_t prop;
-  if (hipGetDeviceProperties(&prop, cfg->device) == hipSuccess && prop.multiProcessorCount > 0)
-    e->num_cus = prop.multiProcessorCount;
+  int ncu = 0;  // (one attribute query: hipGetDeviceProperties fills the whole struct, ~ms)
+  if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, cfg->device) == hipSuccess && ncu > 0)
+    e->num_cus = ncu;
   if (cfg->hip_stream) {
     e->stream = static_cast<hipStream_t>(cfg->hip_stream);
   } else {
@@ -350,85 +474,13 @@ extern "C" int klf_open(const klf_config* cfg, klf_engine** out) {
     *out = e;
     return hip_err(e, h, "side stream");
   }
-  {
-    int nw = 3;  // staging copy workers (+ the calling thread)
-    if (const char* v = getenv("KLF_STAGE_THREADS")) nw = std::max(0, std::min(atoi(v), 32));
-    e->copier.reset(new klf::CopyPool(nw));
-  }
+  if (getenv("KLF_DIAG"))
+    fprintf(stderr, "[klf] open: device setup done at %.1f us\n",
+            std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t_open0).count());
   // 3) pattern tables to the device
-  const auto& cs = e->cs;
-  hipStream_t st = e->stream;
-  if (cs.mode == klf::CompiledSet::kLiteral1) {
-    std::vector<uint8_t> padded = cs.literal;
-    padded.resize((cs.literal.size() + 3) / 4 * 4 + 4, 0);  // bytes, then dword view at +0
-    h = upload(e->d_lit, padded, st);
-    if (h != hipSuccess) { *out = e; return hip_err(e, h, "upload literal"); }
-  } else if (cs.mode == klf::CompiledSet::kGeneral) {
-    klf::DevPatterns& P = e->dpats;
-    if (cs.ac_states) {
-      if ((h = upload(e->d_ac_class, cs.ac_class, st)) != hipSuccess ||
-          (h = upload(e->d_ac_next, cs.ac_next, st)) != hipSuccess ||
-          (h = upload(e->d_ac_accept, cs.ac_accept, st)) != hipSuccess) {
-        *out = e;
-        return hip_err(e, h, "upload AC tables");
-      }
-      P.ac_class = e->d_ac_class.as<uint8_t>();
-      P.ac_next = e->d_ac_next.as<uint32_t>();
-      P.ac_accept = e->d_ac_accept.as<uint8_t>();
-      if ((h = upload(e->d_ac_out, cs.ac_out, st)) != hipSuccess || (h = upload(e->d_ac_dict, cs.ac_dict, st)) != hipSuccess) {
-        *out = e;
-        return hip_err(e, h, "upload AC output tables");
-      }
-      P.ac_out = e->d_ac_out.as<int32_t>();
-      P.ac_dict = e->d_ac_dict.as<uint32_t>();
-      P.ac_states = cs.ac_states;
-      P.ac_classes = cs.ac_classes;
-    }
-    if (cs.rx_count) {
-      std::vector<uint64_t> vec;  // first | last | init0 | end, each [rx_count]
-      vec.insert(vec.end(), cs.rx_first.begin(), cs.rx_first.end());
-      vec.insert(vec.end(), cs.rx_last.begin(), cs.rx_last.end());
-      vec.insert(vec.end(), cs.rx_init0.begin(), cs.rx_init0.end());
-      vec.insert(vec.end(), cs.rx_end.begin(), cs.rx_end.end());
-      if ((h = upload(e->d_rx_class, cs.rx_class, st)) != hipSuccess ||
-          (h = upload(e->d_rx_b, cs.rx_b, st)) != hipSuccess ||
-          (h = upload(e->d_rx_follow, cs.rx_follow, st)) != hipSuccess ||
-          (h = upload(e->d_rx_vec, vec, st)) != hipSuccess ||
-          (h = upload(e->d_rx_flags, cs.rx_flags, st)) != hipSuccess ||
-          (h = upload(e->d_rx_pre, cs.rx_pre.empty() ? std::vector<uint32_t>(cs.rx_count, klf::kRxPreUnbounded) : cs.rx_pre,
-                      st)) != hipSuccess) {
-        *out = e;
-        return hip_err(e, h, "upload regex tables");
-      }
-      const uint64_t* v = e->d_rx_vec.as<uint64_t>();
-      P.rx_class = e->d_rx_class.as<uint8_t>();
-      P.rx_b = e->d_rx_b.as<uint64_t>();
-      P.rx_follow = e->d_rx_follow.as<uint64_t>();
-      P.rx_first = v;
-      P.rx_last = v + cs.rx_count;
-      P.rx_init0 = v + 2 * cs.rx_count;
-      P.rx_end = v + 3 * cs.rx_count;
-      P.rx_flags = e->d_rx_flags.as<uint32_t>();
-      P.rx_pre = e->d_rx_pre.as<uint32_t>();
-      P.rx_unbounded = cs.rx_pre.empty() ? cs.rx_count
-                                         : (uint32_t)std::count(cs.rx_pre.begin(), cs.rx_pre.end(), klf::kRxPreUnbounded);
-      std::vector<uint64_t> vec4;  // [rx][4] interleaved for k_nfa
-      for (uint32_t r = 0; r < cs.rx_count; ++r)
-        for (const auto* v : {&cs.rx_first, &cs.rx_last, &cs.rx_init0, &cs.rx_end}) vec4.push_back((*v)[r]);
-      if ((h = upload(e->d_rx_vec4, vec4, st)) != hipSuccess) { *out = e; return hip_err(e, h, "upload regex vec"); }
-      P.rx_vec = e->d_rx_vec4.as<uint64_t>();
-      P.rx_count = cs.rx_count;
-      P.rx_classes = cs.rx_classes;
-      P.rx_maxpos = std::max<uint32_t>(1, cs.rx_maxpos);
-    }
-    if (cs.qf_on) {
-      if ((h = upload_prefilter(e)) != hipSuccess) {
-        *out = e;
-        return hip_err(e, h, "upload prefilter tables");
-      }
-      P.qf_on = 1;
-      P.qf_fold = cs.qf_fold;
-    }
+  if ((h = upload_pattern_tables(e, tune_later)) != hipSuccess) {
+    *out = e;
+    return hip_err(e, h, "upload pattern tables");
   }
   if (const char* cc = getenv("KLF_CAND_CAP"))  // tests: force the queue-overflow fallback
     e->cand_cap = (uint32_t)std::max(1L, std::min(atol(cc), 1L << 28));
@@ -616,6 +668,11 @@ extern "C" int klf_stage(klf_engine* e, uint32_t id, const uint8_t* p, size_t n)
     }
     dst = e->staged[id].get();  // stable: the table holds pointers, only the table moves
   }
+  std::call_once(e->copier_once, [e] {
+    int nw = 3;  // staging copy workers (+ the calling thread)
+    if (const char* v = getenv("KLF_STAGE_THREADS")) nw = std::max(0, std::min(atoi(v), 32));
+    e->copier.reset(new klf::CopyPool(nw));
+  });
   while (n) {
     if (!dst->cur.p && !take_chunk(e, &dst->cur)) {
       std::lock_guard<std::mutex> g(e->mu);
@@ -747,6 +804,24 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
   r->gen = ++e->gen;
   r->n_streams = n_streams;
   r->seg_of.assign(n_streams, -1);
+  if (e->cs.also_all_pending && (f->flags & KLF_FILTER_PATTERN_COUNTS)) {
+    // the first run asking for per-pattern counts of a set with an always-pattern: compile
+    // the other patterns now (klf_open kept the set as kAll); if that fails the filter stays
+    // kAll's and the counts are reported unavailable
+    klf::CompiledSet full;
+    std::string cerr;
+    int ccode = KLF_OK;
+    if (klf::compile_set(e->pend_pats, e->pend_kinds, full, cerr, ccode, !e->tune_later, false)) {
+      e->cs = std::move(full);
+      e->dpats.n_cids = e->cs.n_cids;
+      e->dpats.n_lits = e->cs.n_lits;
+      HIPCHK(e, upload_pattern_tables(e, e->tune_later), "upload pattern tables");
+    } else {
+      e->cs.also_all_pending = false;
+      e->counts_code = ccode;
+      e->counts_err = "per-pattern counts unavailable: " + cerr;
+    }
+  }
   auto mode = e->cs.mode;
   // a set with an always-pattern (also_all) filters as kAll; its other patterns are
   // evaluated only when the run counts per pattern
@@ -799,10 +874,15 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
     HIPCHK(e, e->d_tile_seg.ensure(ntiles * 4 + 16), "alloc tile_seg");  // + whole 16-B loads past the end
   }
   mark("segs");
+  // First batch of a prefiltered set: the data's own gram statistics (k_gramhist over a
+  // sample) place the needles' sampling windows.  The sample's readback is in flight while
+  // the host maps the workspace below; the layout and its upload follow the sync.  The
+  // sample's newline share also sizes the first run's line arrays (no phase-1 readback).
+  bool tune_pending = false;
+  std::chrono::steady_clock::time_point t_tune0;
   if (mode == klf::CompiledSet::kGeneral && e->cs.qf_on && !e->cs.qf_tuned) {
-    // first batch: place the needles' sampling windows on the data's own gram statistics
     e->cs.qf_tuned = true;
-    const auto t_tune0 = std::chrono::steady_clock::now();
+    t_tune0 = std::chrono::steady_clock::now();
     const char* tune = getenv("KLF_QF_TUNE");
     if (!tune || strcmp(tune, "0") != 0) {
       const size_t nh = klf::kGramHistWords;
@@ -811,34 +891,40 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
       HIPCHK(e, klf::launch_gramhist(d_bytes, e->d_segs.as<SegDesc>(), nsegs, klf::kGramHistSample, e->cs.qf_fold,
                                      e->d_hist.as<uint32_t>(), st), "gram histogram");
       HIPCHK(e, hipMemcpyAsync(e->h_hist.p, e->d_hist.p, nh * 4, hipMemcpyDeviceToHost, st), "D2H hist");
-      HIPCHK(e, hipStreamSynchronize(st), "sync hist");
-      const auto t_hist = std::chrono::steady_clock::now();
-      const uint32_t* hv = e->h_hist.as<uint32_t>();
-      klf::DataStats ds;
-      ds.gram3.assign(hv, hv + klf::kQfHistBins);
-      ds.gram4.assign(hv + klf::kQfHistBins, hv + 2 * klf::kQfHistBins);
-      for (auto& c : ds.gram3) c *= klf::kGramHistStride;  // grams were counted at every 4th position
-      for (auto& c : ds.gram4) c *= klf::kGramHistStride;
-      ds.bytes.assign(256, 0);
-      for (int c = 0; c < 256; ++c) {
-        ds.bytes[c] = hv[2 * klf::kQfHistBins + c];
-        ds.nbytes += ds.bytes[c];
-      }
-      klf::place_needles(e->cs, &ds);
-      const auto t_place = std::chrono::steady_clock::now();
-      if (getenv("KLF_DIAG"))
-        fprintf(stderr, "[klf] prefilter layout from %llu sampled bytes: %s\n", (unsigned long long)ds.nbytes,
-                e->cs.qf_layout.c_str());
-      HIPCHK(e, upload_prefilter(e), "upload prefilter tables");
-      if (getenv("KLF_DIAG"))
-        fprintf(stderr, "[klf] first-batch tuning: statistics %.1f us, layout %.1f us, uploads %.1f us\n",
-                std::chrono::duration<double, std::micro>(t_hist - t_tune0).count(),
-                std::chrono::duration<double, std::micro>(t_place - t_hist).count(),
-                std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t_place).count());
+      tune_pending = true;
     }
+  }
+  double est_density = 0.0;  // lines per byte of the first batch's sample (0: none)
+  auto finish_tune = [&]() -> int {
+    HIPCHK(e, hipStreamSynchronize(st), "sync hist");
+    const auto t_hist = std::chrono::steady_clock::now();
+    const uint32_t* hv = e->h_hist.as<uint32_t>();
+    klf::DataStats ds;
+    ds.gram3.assign(hv, hv + klf::kQfHistBins);
+    ds.gram4.assign(hv + klf::kQfHistBins, hv + 2 * klf::kQfHistBins);
+    for (auto& c : ds.gram3) c *= klf::kGramHistStride;  // grams were counted at every 4th position
+    for (auto& c : ds.gram4) c *= klf::kGramHistStride;
+    ds.bytes.assign(256, 0);
+    for (int c = 0; c < 256; ++c) {
+      ds.bytes[c] = hv[2 * klf::kQfHistBins + c];
+      ds.nbytes += ds.bytes[c];
+    }
+    if (ds.nbytes) est_density = (double)(ds.bytes['\n'] + 1) / (double)ds.nbytes;
+    klf::place_needles(e->cs, &ds);
+    const auto t_place = std::chrono::steady_clock::now();
+    if (getenv("KLF_DIAG"))
+      fprintf(stderr, "[klf] prefilter layout from %llu sampled bytes: %s\n", (unsigned long long)ds.nbytes,
+              e->cs.qf_layout.c_str());
+    HIPCHK(e, upload_prefilter(e), "upload prefilter tables");
+    if (getenv("KLF_DIAG"))
+      fprintf(stderr, "[klf] first-batch tuning: statistics %.1f us (with the workspace mapped meanwhile), layout %.1f us, uploads %.1f us\n",
+              std::chrono::duration<double, std::micro>(t_hist - t_tune0).count(),
+              std::chrono::duration<double, std::micro>(t_place - t_hist).count(),
+              std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t_place).count());
     tune_ns = (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t_tune0).count();
     mark("first-batch tuning");
-  }
+    return KLF_OK;
+  };
   HIPCHK(e, e->d_tstat.ensure(ntiles * sizeof(klf::TileStat)), "alloc tstat");
   HIPCHK(e, e->d_slots.ensure(ntiles * klf::kRecStride * 4), "alloc slots");
   HIPCHK(e, e->d_tile_base.ensure(ntiles * 8), "alloc tile_base");
@@ -896,6 +982,15 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
   const bool count = (f->flags & KLF_FILTER_PATTERN_COUNTS) && mode == klf::CompiledSet::kGeneral && e->cs.n_cids;
   r->counted = (f->flags & KLF_FILTER_PATTERN_COUNTS) != 0;
   mark("workspace");
+  if (tune_pending) {
+    const int rc = finish_tune();
+    if (rc != KLF_OK) return rc;
+  }
+  // a first run with the sample's line density: the line arrays from it (x2 + a margin:
+  // an overflow reruns with exact sizes), in one launch phase
+  const bool density_cap = e->line_density == 0.0 && est_density > 0.0 && !getenv("KLF_TWO_PHASE");
+  if (density_cap)
+    cap = std::min<uint64_t>(cap, (uint64_t)(est_density * (double)total_bytes * 2.0) + 2ull * nsegs + 65536);
   bool overflow = false, pairs_over = false;
   for (int attempt = 0, line_reruns = 0, pair_reruns = 0; attempt < 4; ++attempt) {
     if (count) {
@@ -907,7 +1002,7 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
     // An engine's first run sizes its line arrays from its own line count: the pipeline
     // runs up to the tile index, the count is read back, the arrays are allocated, the
     // rest follows (one extra sync, first runs only).
-    const bool two_phase = attempt == 0 && e->line_density == 0.0 && !getenv("KLF_ONE_PHASE");
+    const bool two_phase = attempt == 0 && e->line_density == 0.0 && !density_cap && !getenv("KLF_ONE_PHASE");
     // the arrays indexed by global line (and the compaction's per-block tables)
     auto alloc_lines = [&](klf::RunArgs& x, uint64_t c) -> hipError_t {
       const uint64_t mcb = c / klf::kCompactLines + 2;
@@ -1464,6 +1559,7 @@ extern "C" int klf_result_pattern_counts(klf_result* r, uint32_t id, uint64_t* c
   klf_engine* e = r->e;
   if (n) *n = e->n_user;
   if (!r->counted) return set_err(e, KLF_ESTATE, "the run did not ask for per-pattern counts (KLF_FILTER_PATTERN_COUNTS)");
+  if (e->counts_code != KLF_OK) return set_err(e, e->counts_code, e->counts_err);
   const auto& cs = e->cs;
   const int64_t s = r->seg_of[id];
   const bool general = cs.mode == klf::CompiledSet::kGeneral;

@@ -20,25 +20,33 @@ namespace {
 
 using ByteSet = std::bitset<256>;
 
-ByteSet range_set(int lo, int hi) {
+ByteSet range_set(int lo, int hi) {  // bits lo..hi (whole-word shifts, no per-bit loop)
   ByteSet s;
-  for (int c = lo; c <= hi; ++c) s.set(c);
+  if (hi < lo) return s;
+  s.set();
+  s >>= 255 - (hi - lo);
+  s <<= lo;
   return s;
 }
-ByteSet perl_d() { return range_set('0', '9'); }
-ByteSet perl_w() { return range_set('0', '9') | range_set('A', 'Z') | range_set('a', 'z') | range_set('_', '_'); }
-ByteSet perl_s() {
-  ByteSet s;
-  for (int c : {'\t', '\n', '\f', '\r', ' '}) s.set(c);  // Go \s has no \v
-  return s;
+const ByteSet& perl_d() {
+  static const ByteSet d = range_set('0', '9');
+  return d;
 }
-ByteSet fold(const ByteSet& s) {
-  ByteSet o = s;
-  for (int c = 'A'; c <= 'Z'; ++c) {
-    if (s.test(c)) o.set(c + 32);
-    if (s.test(c + 32)) o.set(c);
-  }
-  return o;
+const ByteSet& perl_w() {
+  static const ByteSet w = range_set('0', '9') | range_set('A', 'Z') | range_set('a', 'z') | range_set('_', '_');
+  return w;
+}
+const ByteSet& perl_s() {
+  static const ByteSet sp = [] {
+    ByteSet x;
+    for (int c : {'\t', '\n', '\f', '\r', ' '}) x.set(c);  // Go \s has no \v
+    return x;
+  }();
+  return sp;
+}
+ByteSet fold(const ByteSet& s) {  // ASCII case pairs: 'A'..'Z' <-> 'a'..'z' are 32 bits apart
+  static const ByteSet up = range_set('A', 'Z'), lo = range_set('a', 'z');
+  return s | ((s & up) << 32) | ((s & lo) >> 32);
 }
 
 struct RNode {
@@ -657,8 +665,10 @@ FInfo factor_of(const FactorCtx& cx, const std::vector<RNode>& pool, int x) {
       f.maxlen = 1;
       const size_t c = n.set.count();
       int b0 = -1, b1 = -1;
-      for (int b = 0; b < 256 && c <= 2; ++b)
-        if (n.set.test(b)) { if (b0 < 0) b0 = b; else b1 = b; }
+      if (c <= 2) {
+        b0 = (int)n.set._Find_first();
+        if (c == 2) b1 = (int)n.set._Find_next((size_t)b0);
+      }
       if (c == 1) {
         f.has_exact = true;
         f.exact.assign(1, (char)b0);
@@ -751,18 +761,17 @@ FInfo factor_of(const FactorCtx& cx, const std::vector<RNode>& pool, int x) {
 
 }  // namespace
 
-bool regex_factors(const uint8_t* pat, size_t n, std::vector<std::string>& alts, bool& loose, uint32_t* pre,
-                   size_t want) {
+// Required factors of a parsed regex (regex_factors without the parse).
+static bool factors_of(const std::vector<RNode>& pool, int root, std::vector<std::string>& alts, bool& loose,
+                       uint32_t* pre, size_t want) {
   alts.clear();
   loose = false;
   if (pre) *pre = kUnbounded;
-  Parser ps(pat, n);
-  const int root = ps.parse();
   if (root < 0) return false;
   FactorCtx cx;
   cx.want = want;
   uint32_t p = kUnbounded;
-  alts = req_or_exact(factor_of(cx, ps.pool, root), loose, &p);
+  alts = req_or_exact(factor_of(cx, pool, root), loose, &p);
   if (req_score(alts) == 0) { alts.clear(); return false; }
   for (auto& s : alts) {
     if (s.size() > kQfMaxFactor) s.resize(kQfMaxFactor);  // a substring of a factor is one too (its own start: same pre)
@@ -775,21 +784,21 @@ bool regex_factors(const uint8_t* pat, size_t n, std::vector<std::string>& alts,
   return true;
 }
 
+bool regex_factors(const uint8_t* pat, size_t n, std::vector<std::string>& alts, bool& loose, uint32_t* pre,
+                   size_t want) {
+  Parser ps(pat, n);
+  const int root = ps.parse();
+  return factors_of(ps.pool, root, alts, loose, pre, want);
+}
+
 void build_prefilter(const std::vector<std::vector<uint8_t>>& lits,
                      const std::vector<std::vector<std::vector<std::string>>>& fac_v,
                      const std::vector<std::vector<bool>>& loose_v, const std::vector<std::vector<uint32_t>>& pre_v,
-                     CompiledSet& out);
+                     CompiledSet& out, bool place);
 
-bool compile_regex(const uint8_t* pat, size_t n, GlushkovTables& out, std::string& err,
-                   int& err_code) {
-  Parser ps(pat, n);
-  int root = ps.parse();
-  if (root < 0) {
-    err = ps.err;
-    err_code = KLF_EPATTERN;
-    return false;
-  }
-  Builder b(ps.pool);
+// Glushkov tables of a parsed regex (the pool is rewritten: {m,n} expansion).
+static bool build_glushkov(std::vector<RNode>& pool, int root, GlushkovTables& out, std::string& err, int& err_code) {
+  Builder b(pool);
   if (b.count_pos(root) > kMaxRegexPositions) {
     err = "regex needs more than 64 Glushkov positions after {m,n} expansion";
     err_code = KLF_ETOOBIG;
@@ -804,8 +813,13 @@ bool compile_regex(const uint8_t* pat, size_t n, GlushkovTables& out, std::strin
   out.last = info.last;
   for (auto& s : b.pos_set) {
     std::vector<uint8_t> v(256);
-    for (int c = 0; c < 256; ++c) v[c] = s.test(c);
-    out.pos_bytes.push_back(v);
+    std::array<uint64_t, 4> m{0, 0, 0, 0};
+    for (size_t c = s._Find_first(); c < 256; c = s._Find_next(c)) {
+      v[c] = 1;
+      m[c >> 6] |= 1ull << (c & 63);
+    }
+    out.pos_bytes.push_back(std::move(v));
+    out.pos_bits.push_back(m);
   }
   bool acc0 = false;
   out.init0 = closure(info.first, b.a_bot, b.follow, info.last, &acc0);
@@ -824,6 +838,18 @@ bool compile_regex(const uint8_t* pat, size_t n, GlushkovTables& out, std::strin
   }
   out.end_accept = ea;
   return true;
+}
+
+bool compile_regex(const uint8_t* pat, size_t n, GlushkovTables& out, std::string& err,
+                   int& err_code) {
+  Parser ps(pat, n);
+  int root = ps.parse();
+  if (root < 0) {
+    err = ps.err;
+    err_code = KLF_EPATTERN;
+    return false;
+  }
+  return build_glushkov(ps.pool, root, out, err, err_code);
 }
 
 bool glushkov_match(const GlushkovTables& g, const uint8_t* s, size_t n) {
@@ -852,7 +878,7 @@ int log_byte_class(uint8_t c) {
 }
 
 bool compile_set(const std::vector<std::vector<uint8_t>>& pats, const std::vector<uint32_t>& kinds,
-                 CompiledSet& out, std::string& err, int& err_code) {
+                 CompiledSet& out, std::string& err, int& err_code, bool place, bool defer_also_all) {
   out = CompiledSet();
   if (pats.empty()) {
     out.mode = CompiledSet::kNone;
@@ -869,6 +895,9 @@ bool compile_set(const std::vector<std::vector<uint8_t>>& pats, const std::vecto
   std::vector<bool> rx_loose;
   std::vector<uint32_t> rx_pre;
   std::vector<size_t> rx_src;  // pattern index of each kept regex
+  std::vector<std::vector<RNode>> rx_tree;  // parse tree of each kept regex
+  std::vector<int> rx_root;
+  std::vector<size_t> always_rx;  // regexes that match every content
   bool always = false;
   auto drop_nl = [](std::vector<std::string>& alts) {  // content never holds '\n'
     alts.erase(std::remove_if(alts.begin(), alts.end(),
@@ -882,20 +911,33 @@ bool compile_set(const std::vector<std::vector<uint8_t>>& pats, const std::vecto
       if (std::find(l.begin(), l.end(), (uint8_t)'\n') != l.end()) continue;  // never in content
       lits.push_back(l);
     } else if (kinds[k] == KLF_PAT_REGEX) {
-      GlushkovTables g;
-      if (!compile_regex(pats[k].data(), pats[k].size(), g, err, err_code)) {
-        err = "pattern " + std::to_string(k) + ": " + err;
+      // parsed once: the factor analyses read the tree, the Glushkov build rewrites a copy
+      Parser ps(pats[k].data(), pats[k].size());
+      const int root = ps.parse();
+      if (root < 0) {
+        err = "pattern " + std::to_string(k) + ": " + ps.err;
+        err_code = KLF_EPATTERN;
         return false;
       }
-      if (g.accept_at_start && g.accept_empty) { always = true; continue; }
+      GlushkovTables g;
+      {
+        std::vector<RNode> work = ps.pool;
+        if (!build_glushkov(work, root, g, err, err_code)) {
+          err = "pattern " + std::to_string(k) + ": " + err;
+          return false;
+        }
+      }
+      if (g.accept_at_start && g.accept_empty) { always_rx.push_back(k); always = true; continue; }
       rxs.push_back(std::move(g));
       std::vector<std::string> alts;
       bool loose = false;
       uint32_t pre = kRxPreUnbounded;
-      if (regex_factors(pats[k].data(), pats[k].size(), alts, loose, &pre)) {
+      rx_tree.push_back(std::move(ps.pool));
+      rx_root.push_back(root);
+      if (factors_of(rx_tree.back(), root, alts, loose, &pre, SIZE_MAX)) {
         // such alternatives cannot occur; none left = no match ever
         drop_nl(alts);
-        if (alts.empty()) { rxs.pop_back(); continue; }
+        if (alts.empty()) { rxs.pop_back(); rx_tree.pop_back(); rx_root.pop_back(); continue; }
       }
       rx_fac.push_back(alts);
       rx_loose.push_back(loose);
@@ -935,8 +977,7 @@ bool compile_set(const std::vector<std::vector<uint8_t>>& pats, const std::vecto
         std::vector<std::string> alts;
         bool loose = false;
         uint32_t pre = kRxPreUnbounded;
-        const size_t k = rx_src[r];
-        if (!regex_factors(pats[k].data(), pats[k].size(), alts, loose, &pre, want)) continue;
+        if (!factors_of(rx_tree[r], rx_root[r], alts, loose, &pre, want)) continue;
         drop_nl(alts);
         size_t m = SIZE_MAX;
         for (auto& x : alts) m = std::min(m, x.size());
@@ -972,21 +1013,18 @@ bool compile_set(const std::vector<std::vector<uint8_t>>& pats, const std::vecto
         if (r < rx_src.size() && rx_src[r] == k) out.user_map[k] = (int32_t)(lits.size() + r);
       }
     }
-    // regexes that match every content
-    for (size_t k = 0; k < pats.size(); ++k)
-      if (kinds[k] == KLF_PAT_REGEX && out.user_map[k] == CompiledSet::kCidNever) {
-        GlushkovTables g;
-        std::string e2;
-        int c2 = 0;
-        if (compile_regex(pats[k].data(), pats[k].size(), g, e2, c2) && g.accept_at_start && g.accept_empty)
-          out.user_map[k] = CompiledSet::kCidAlways;
-      }
+    for (size_t k : always_rx) out.user_map[k] = CompiledSet::kCidAlways;  // regexes that match every content
   }
   if (always && lits.empty() && rxs.empty()) { out.mode = CompiledSet::kAll; return true; }
   if (lits.empty() && rxs.empty()) { out.mode = CompiledSet::kNever; return true; }
   // an always-pattern beside real ones: the general tables (counted per pattern), kAll's
-  // filter (also_all)
+  // filter (also_all); deferred, kAll until a run asks for per-pattern counts
   out.also_all = always;
+  if (always && defer_also_all) {
+    out.mode = CompiledSet::kAll;
+    out.also_all_pending = true;
+    return true;
+  }
   if (!always && rxs.empty() && lits.size() == 1 && lits[0].size() <= 256) {
     out.mode = CompiledSet::kLiteral1;
     out.literal = lits[0];
@@ -1011,86 +1049,81 @@ bool compile_set(const std::vector<std::vector<uint8_t>>& pats, const std::vecto
         if (used[c]) out.ac_class[c] = (uint8_t)std::min(ncls++, 255);
       if (ncls > 256) { err = "literal alphabet too large"; err_code = KLF_ETOOBIG; return false; }
     }
-    std::vector<std::map<int, int>> go(1);
-    std::vector<uint8_t> term(1, 0);
-    std::vector<int32_t> term_id(1, -1);  // literal id ending exactly at a state
-    for (auto& l : lits) {
-      int s = 0;
-      for (uint8_t c : l) {
-        int cl = out.ac_class[c];
-        auto it = go[s].find(cl);
-        if (it == go[s].end()) {
-          go.push_back({});
-          term.push_back(0);
-          go[s][cl] = (int)go.size() - 1;
-          s = (int)go.size() - 1;
-        } else {
-          s = it->second;
-        }
+    // goto trie straight into the DFA table (0 = no child: the root is nobody's child),
+    // then BFS: a state's missing edges copy its fail state's finished row
+    size_t cap = 1;
+    for (auto& l : lits) cap += l.size();
+    std::vector<uint32_t> nxt(cap * (size_t)ncls, 0u);
+    std::vector<uint8_t> term(cap, 0);
+    std::vector<int32_t> term_id(cap, -1);  // literal id ending exactly at a state
+    size_t ns = 1;
+    for (size_t li = 0; li < lits.size(); ++li) {
+      uint32_t st = 0;
+      for (uint8_t c : lits[li]) {
+        uint32_t& t = nxt[(size_t)st * ncls + out.ac_class[c]];
+        if (!t) t = (uint32_t)ns++;
+        st = t;
       }
-      term[s] = 1;
-      term_id.resize(go.size(), -1);
-      term_id[s] = (int32_t)(&l - &lits[0]);
+      term[st] = 1;
+      term_id[st] = (int32_t)li;
     }
-    const size_t ns = go.size();
     if (ns >= (1u << 31)) { err = "AC automaton too large"; err_code = KLF_ETOOBIG; return false; }
+    nxt.resize(ns * (size_t)ncls);
     out.ac_states = (uint32_t)ns;
     out.ac_classes = (uint32_t)ncls;
-    out.ac_next.assign(ns * ncls, 0);
     out.ac_accept.assign(ns, 0);
-    term_id.resize(ns, -1);
-    out.ac_out.assign(term_id.begin(), term_id.end());
+    out.ac_out.assign(term_id.begin(), term_id.begin() + ns);
     out.ac_dict.assign(ns, 0u);
-    std::vector<int> fail(ns, 0);
-    std::queue<int> q;
-    for (int c = 0; c < ncls; ++c) {
-      auto it = go[0].find(c);
-      int t = it == go[0].end() ? 0 : it->second;
-      out.ac_next[c] = (uint32_t)t;
-      if (t) { fail[t] = 0; q.push(t); }
-    }
+    std::vector<uint32_t> fail(ns, 0), queue;
+    queue.reserve(ns);
+    for (int c = 0; c < ncls; ++c)
+      if (const uint32_t t = nxt[c]) queue.push_back(t);
     out.ac_accept[0] = term[0];
-    while (!q.empty()) {
-      int s = q.front();
-      q.pop();
-      out.ac_accept[s] = term[s] | out.ac_accept[fail[s]];
+    for (size_t qh = 0; qh < queue.size(); ++qh) {
+      const uint32_t st = queue[qh];
+      const uint32_t fs = fail[st];
+      out.ac_accept[st] = term[st] | out.ac_accept[fs];
       // dictionary link: the nearest state on the fail chain where a literal ends
-      out.ac_dict[s] = (uint32_t)(term_id[fail[s]] >= 0 ? fail[s] : (int)out.ac_dict[fail[s]]);
+      out.ac_dict[st] = (uint32_t)(term_id[fs] >= 0 ? (int)fs : (int)out.ac_dict[fs]);
+      uint32_t* row = &nxt[(size_t)st * ncls];
+      const uint32_t* frow = &nxt[(size_t)fs * ncls];
       for (int c = 0; c < ncls; ++c) {
-        auto it = go[s].find(c);
-        if (it != go[s].end()) {
-          int t = it->second;
-          fail[t] = (int)out.ac_next[(size_t)fail[s] * ncls + c];
-          out.ac_next[(size_t)s * ncls + c] = (uint32_t)t;
-          q.push(t);
+        if (const uint32_t t = row[c]) {  // a trie child (its row is still pure trie)
+          fail[t] = frow[c];
+          queue.push_back(t);
         } else {
-          out.ac_next[(size_t)s * ncls + c] = out.ac_next[(size_t)fail[s] * ncls + c];
+          row[c] = frow[c];
         }
       }
     }
+    out.ac_next = std::move(nxt);
   }
 
   // ---- regexes: shared byte classes by partition refinement ----
   out.rx_count = (uint32_t)rxs.size();
   if (!rxs.empty()) {
-    std::map<std::vector<uint64_t>, int> sig2cls;
-    out.rx_class.assign(256, 0);
+    // a byte's signature = the positions (per regex) whose set holds it; equal signatures
+    // share a class, numbered in order of the first byte that has it
     const size_t words = rxs.size();
+    std::vector<uint64_t> sig((size_t)256 * words, 0);
+    for (size_t r = 0; r < words; ++r)
+      for (int p = 0; p < rxs[r].npos; ++p)
+        for (int w = 0; w < 4; ++w)
+          for (uint64_t m = rxs[r].pos_bits[p][w]; m; m &= m - 1)
+            sig[(size_t)(w * 64 + __builtin_ctzll(m)) * words + r] |= 1ull << p;
+    std::unordered_map<std::string, int> sig2cls;
+    std::vector<int> rep;  // first byte of each class
+    out.rx_class.assign(256, 0);
     for (int c = 0; c < 256; ++c) {
-      std::vector<uint64_t> sig(words, 0);
-      for (size_t r = 0; r < rxs.size(); ++r)
-        for (int p = 0; p < rxs[r].npos; ++p)
-          if (rxs[r].pos_bytes[p][c]) sig[r] |= 1ull << p;
-      auto it = sig2cls.find(sig);
-      int cl;
-      if (it == sig2cls.end()) { cl = (int)sig2cls.size(); sig2cls[sig] = cl; }
-      else cl = it->second;
-      out.rx_class[c] = (uint8_t)cl;
+      std::string key(reinterpret_cast<const char*>(&sig[(size_t)c * words]), words * 8);
+      auto it = sig2cls.emplace(std::move(key), (int)rep.size());
+      if (it.second) rep.push_back(c);
+      out.rx_class[c] = (uint8_t)it.first->second;
     }
-    out.rx_classes = (uint32_t)sig2cls.size();
+    out.rx_classes = (uint32_t)rep.size();
     out.rx_b.assign((size_t)rxs.size() * out.rx_classes, 0);
-    for (auto& kv : sig2cls)
-      for (size_t r = 0; r < rxs.size(); ++r) out.rx_b[r * out.rx_classes + kv.second] = kv.first[r];
+    for (size_t cl = 0; cl < rep.size(); ++cl)
+      for (size_t r = 0; r < rxs.size(); ++r) out.rx_b[r * out.rx_classes + cl] = sig[(size_t)rep[cl] * words + r];
     out.rx_follow.assign((size_t)rxs.size() * 64, 0);
     for (size_t r = 0; r < rxs.size(); ++r) {
       for (int p = 0; p < rxs[r].npos; ++p) out.rx_follow[r * 64 + p] = rxs[r].follow[p];
@@ -1102,7 +1135,7 @@ bool compile_set(const std::vector<std::vector<uint8_t>>& pats, const std::vecto
       out.rx_flags.push_back((rxs[r].accept_at_start ? 1u : 0u) | (rxs[r].accept_empty ? 2u : 0u));
     }
   }
-  build_prefilter(lits, fac_v, loose_v, pre_v, out);
+  build_prefilter(lits, fac_v, loose_v, pre_v, out, place);
   return true;
 }
 
@@ -1116,7 +1149,7 @@ bool compile_set(const std::vector<std::vector<uint8_t>>& pats, const std::vecto
 void build_prefilter(const std::vector<std::vector<uint8_t>>& lits,
                      const std::vector<std::vector<std::vector<std::string>>>& fac_v,
                      const std::vector<std::vector<bool>>& loose_v, const std::vector<std::vector<uint32_t>>& pre_v,
-                     CompiledSet& out) {
+                     CompiledSet& out, bool place) {
   out.qf_variants.clear();
   bool loose = false;
   for (size_t v = 0; v < fac_v.size(); ++v) {
@@ -1149,7 +1182,7 @@ void build_prefilter(const std::vector<std::vector<uint8_t>>& lits,
   }
   out.qf_fold = loose ? 0x20202020u : 0u;  // grams of every variant fold alike
   out.qf_on = true;
-  place_needles(out, nullptr);
+  if (place) place_needles(out, nullptr);
 }
 
 namespace {
@@ -1280,15 +1313,18 @@ double layout_cost(const CompiledSet& c, const DataStats& st) {
   auto share = [&](const std::vector<uint32_t>& h, uint32_t g) {
     return std::min(h[qf_hist_bin0(g)], h[qf_hist_bin1(g)]) / nb;
   };
-  std::set<uint32_t> grams;
+  std::vector<uint32_t> grams;
+  grams.reserve(c.qf_ent.size() / 4);
   for (size_t e = 0; e + 3 < c.qf_ent.size(); e += 4) {  // the probed grams, read back from the needles
     if (c.qf_ent[e + 1] & kQfAnchored) continue;
     const uint32_t off = c.qf_ent[e], len = c.qf_ent[e + 1] & 0xFFFFu, k = (c.qf_ent[e + 1] >> 16) & 0xFFu;
     const uint8_t* nb8 = reinterpret_cast<const uint8_t*>(c.qf_nbytes.data() + off);
     uint32_t g = 0;
     for (uint32_t b = 0; b < c.qf_q && k + b < len; ++b) g |= (uint32_t)nb8[k + b] << (8 * b);
-    grams.insert((g | c.qf_fold) & c.qf_mask);
+    grams.push_back((g | c.qf_fold) & c.qf_mask);
   }
+  std::sort(grams.begin(), grams.end());
+  grams.erase(std::unique(grams.begin(), grams.end()), grams.end());
   double hit_share = 0;  // probed grams (the anchored ones only reach a bucket through an anchor)
   for (uint32_t g : grams) hit_share += share(sk, g);
   const double samples = 8192.0 / c.qf_stride;
@@ -1323,16 +1359,21 @@ void place_needles(CompiledSet& out, const DataStats* st) {
   std::vector<uint8_t> ac_accept;
   std::vector<int32_t> ac_out;
   std::vector<uint64_t> rx_b, rx_follow;
+  std::vector<CompiledSet::NeedleSet> variants;  // read-only here: not copied per candidate
+  std::vector<int32_t> user_map;
   ac_next.swap(out.ac_next);
   ac_dict.swap(out.ac_dict);
   ac_accept.swap(out.ac_accept);
   ac_out.swap(out.ac_out);
   rx_b.swap(out.rx_b);
   rx_follow.swap(out.rx_follow);
+  variants.swap(out.qf_variants);
+  user_map.swap(out.user_map);
   CompiledSet best;
   double best_cost = 0;
   bool have = false;
-  for (uint32_t v = 0; v < out.qf_variants.size(); ++v)
+  std::vector<std::string> seen;  // layouts already placed (a 3-byte cap can give the 4-byte one's)
+  for (uint32_t v = 0; v < variants.size(); ++v)
     for (int cand = 0; cand < 4; ++cand) {
       const int anchored = cand & 1;
       const uint32_t qmax = cand < 2 ? 4u : 3u;  // 3-byte grams: a cheaper probe, more hits
@@ -1340,7 +1381,7 @@ void place_needles(CompiledSet& out, const DataStats* st) {
       if (const char* qv = getenv("KLF_QF_QMAX"))  // ablation: one gram length at the data's layout
         if (st && st->nbytes && (uint32_t)atoi(qv) != qmax) continue;
       CompiledSet c = out;
-      const auto& ns = c.qf_variants[v];
+      const auto& ns = variants[v];
       c.qf_variant = v;
       c.qf_needle = ns.s;
       c.qf_nflags = ns.flags;
@@ -1349,6 +1390,11 @@ void place_needles(CompiledSet& out, const DataStats* st) {
       c.rx_pre = ns.rx_pre;
       choose_layout(c, st, anchored != 0, qmax);
       if (anchored && !c.qf_anc_on) continue;  // nothing to anchor: same as the probed layout
+      {
+        const std::string key = std::to_string(v) + "/" + c.qf_layout;
+        if (std::find(seen.begin(), seen.end(), key) != seen.end()) continue;  // placed already
+        seen.push_back(key);
+      }
       place_tables(c, st);
       double cost;
       if (st && st->nbytes) {
@@ -1367,6 +1413,8 @@ void place_needles(CompiledSet& out, const DataStats* st) {
       }
     }
   if (have) out = std::move(best);  // (every candidate skipped: the layout stays as it was)
+  out.qf_variants.swap(variants);
+  out.user_map.swap(user_map);
   out.ac_next.swap(ac_next);
   out.ac_dict.swap(ac_dict);
   out.ac_accept.swap(ac_accept);
@@ -1405,7 +1453,8 @@ void place_tables(CompiledSet& out, const DataStats* st) {
   };
   std::unordered_map<uint32_t, int> used;  // gram -> needles sampling it so far
   used.reserve(out.qf_needle.size() * S * 2);
-  std::vector<std::vector<uint32_t>> buckets(kQfWords);
+  std::vector<std::pair<uint32_t, uint32_t>> bent;  // (bucket, needle << 8 | gram offset), in needle order
+  bent.reserve(out.qf_needle.size() * S);
   const size_t n = out.qf_needle.size();
   size_t nprobed = 0;
   for (size_t i = 0; i < n; ++i) nprobed += out.qf_nshort[i] ? 0 : 1;
@@ -1415,7 +1464,7 @@ void place_tables(CompiledSet& out, const DataStats* st) {
     const std::string& s = out.qf_needle[i];
     if (out.qf_nshort[i]) {  // anchored: the bucket of the gram at the anchor
       const uint32_t k = out.qf_nanc[i], g = gram_at(s, k);
-      buckets[qf_bucket(g, w24, out.qf_k)].push_back(i << 8 | k);
+      bent.push_back({qf_bucket(g, w24, out.qf_k), i << 8 | k});
       continue;
     }
     const uint32_t amax = (uint32_t)std::min<size_t>(s.size() - (q + S - 1), 255 - (S - 1));
@@ -1444,7 +1493,7 @@ void place_tables(CompiledSet& out, const DataStats* st) {
       const uint32_t h = qf_hash(g, w24, out.qf_k);
       const uint32_t bw = qf_bucket(g, w24, out.qf_k);
       out.qf_bitmap[bw] |= qf_bits(g, h, out.qf_k);
-      buckets[bw].push_back(i << 8 | k);
+      bent.push_back({bw, i << 8 | k});
     }
   }
   // needle bytes (loose needles are already stored OR 0x20), then 16-B entries per bucket
@@ -1457,19 +1506,21 @@ void place_tables(CompiledSet& out, const DataStats* st) {
       out.qf_nbytes.push_back(w);
     }
   }
+  // entries grouped by bucket, in needle order within one (a stable counting sort)
   out.qf_head.assign(kQfWords + 1, 0u);
-  for (uint32_t b = 0; b < buckets.size(); ++b) {
-    out.qf_head[b] = (uint32_t)(out.qf_ent.size() / 4);
-    for (uint32_t v : buckets[b]) {
-      const uint32_t i = v >> 8;
-      out.qf_ent.push_back(noff[i]);
-      out.qf_ent.push_back((uint32_t)out.qf_needle[i].size() | (v & 0xFFu) << 16 | out.qf_nflags[i] |
-                           (out.qf_nshort[i] ? kQfAnchored : 0u));
-      out.qf_ent.push_back(out.qf_nrx[i]);
-      out.qf_ent.push_back(out.qf_nbytes[noff[i]]);  // first dword: the pre-check
-    }
+  for (auto& be : bent) out.qf_head[be.first + 1]++;
+  for (uint32_t b = 0; b < kQfWords; ++b) out.qf_head[b + 1] += out.qf_head[b];
+  out.qf_ent.assign((size_t)bent.size() * 4, 0u);
+  std::vector<uint32_t> fill(out.qf_head.begin(), out.qf_head.end() - 1);
+  for (auto& be : bent) {
+    const uint32_t v = be.second, i = v >> 8;
+    uint32_t* en = &out.qf_ent[(size_t)fill[be.first]++ * 4];
+    en[0] = noff[i];
+    en[1] = (uint32_t)out.qf_needle[i].size() | (v & 0xFFu) << 16 | out.qf_nflags[i] |
+            (out.qf_nshort[i] ? kQfAnchored : 0u);
+    en[2] = out.qf_nrx[i];
+    en[3] = out.qf_nbytes[noff[i]];  // first dword: the pre-check
   }
-  out.qf_head[buckets.size()] = (uint32_t)(out.qf_ent.size() / 4);
 }
 
 }  // namespace

@@ -13,6 +13,7 @@
 #include <stdint.h>
 #include <stddef.h>
 
+#include <array>
 #include <string>
 #include <vector>
 
@@ -31,6 +32,7 @@ struct GlushkovTables {
   bool accept_at_start = false;  // matches at boundary 0 of a non-empty content
   bool accept_empty = false;     // matches the empty content
   std::vector<std::vector<uint8_t>> pos_bytes;  // byte set (256 flags) per position
+  std::vector<std::array<uint64_t, 4>> pos_bits;  // the same sets as 256-bit masks
   int npos = 0;
 };
 
@@ -47,6 +49,10 @@ struct CompiledSet {
   // --grep, or a regex such as `x*`).  The filter is then kAll's (every parsed line); the
   // other patterns are compiled so that a run with per-pattern counts can evaluate them.
   bool also_all = false;
+  // compile_set(defer_also_all): such a set comes back as kAll with also_all_pending set and
+  // no matcher tables; the engine compiles it in full on the first run that asks for
+  // per-pattern counts (a run without them never reads the tables)
+  bool also_all_pending = false;
   std::vector<uint8_t> literal;  // kLiteral1
   uint32_t literal_anchor = 0;   // kLiteral1: index of its rarest byte in log text
 
@@ -172,9 +178,13 @@ bool prefilter_match(const CompiledSet& cs, const uint8_t* s, size_t n, uint32_t
 bool compile_regex(const uint8_t* pat, size_t n, GlushkovTables& out, std::string& err,
                    int& err_code);
 
-// Compiles a whole OR'ed pattern set.  kinds[i]: 0 literal, 1 regex.
+// Compiles a whole OR'ed pattern set.  kinds[i]: 0 literal, 1 regex.  place = false leaves
+// the prefilter layout (qf_stride, windows, bitmap, buckets) to a later place_needles call
+// with the first batch's statistics (the engine's first run): placing without them first
+// is wasted work on the klf_open path.
 bool compile_set(const std::vector<std::vector<uint8_t>>& pats, const std::vector<uint32_t>& kinds,
-                 CompiledSet& out, std::string& err, int& err_code);
+                 CompiledSet& out, std::string& err, int& err_code, bool place = true,
+                 bool defer_also_all = false);
 
 // Expected-frequency class of a byte in log text (lower = rarer); picks scan anchors.
 int log_byte_class(uint8_t c);
