@@ -128,6 +128,8 @@ struct klf_engine {
   bool ran = false;                    // klf_run since the last klf_reset (stage -> ESTATE)
   std::unique_ptr<klf::CopyPool> copier;  // started by the first klf_stage (device-resident runs never stage)
   std::once_flag copier_once;
+  std::once_flag copy_stream_once;     // the copy stream: created by the first klf_stage / klf_run
+  hipError_t copy_stream_err = hipSuccess;
   DevBuf d_asm;                        // k_assemble piece table
   DevBuf d_scratch;                    // small query results (klf_result_last_unparsed)
   DevBuf d_ac_out, d_ac_dict, d_pcount, d_pairs;  // per-pattern counts
@@ -462,11 +464,9 @@ extern "C" int klf_open(const klf_config* cfg, klf_engine** out) {
     h = hipEventCreate(&x);
     if (h != hipSuccess) { e->err = "hipEventCreate failed"; *out = e; return KLF_EHIP; }
   }
-  if ((h = hipStreamCreateWithFlags(&e->copy_stream, hipStreamNonBlocking)) != hipSuccess ||
-      (h = hipEventCreateWithFlags(&e->copy_done, hipEventDisableTiming)) != hipSuccess) {
-    *out = e;
-    return hip_err(e, h, "copy stream");
-  }
+  if (getenv("KLF_DIAG"))
+    fprintf(stderr, "[klf] open: events done at %.1f us\n",
+            std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t_open0).count());
   if ((h = hipStreamCreateWithFlags(&e->aux_stream, hipStreamNonBlocking)) != hipSuccess ||
       (h = hipEventCreateWithFlags(&e->ev_fork, hipEventDisableTiming)) != hipSuccess ||
       (h = hipEventCreateWithFlags(&e->ev_join, hipEventDisableTiming)) != hipSuccess ||
@@ -544,6 +544,17 @@ extern "C" void klf_close(klf_engine* e) {
 
 static constexpr size_t kStageChunk = 64u << 20;  // pinned staging chunk = device chunk
 static constexpr size_t kMaxInflight = 8;         // pinned chunks with an H2D in flight (512 MiB)
+
+// The copy stream of the host staging path (and its event), made on first use: a
+// device-resident caller (klf_run_device) never pays for it.
+static hipError_t ensure_copy_stream(klf_engine* e) {
+  std::call_once(e->copy_stream_once, [e] {
+    hipError_t h = hipStreamCreateWithFlags(&e->copy_stream, hipStreamNonBlocking);
+    if (h == hipSuccess) h = hipEventCreateWithFlags(&e->copy_done, hipEventDisableTiming);
+    e->copy_stream_err = h;
+  });
+  return e->copy_stream_err;
+}
 
 static void grow_table(klf_engine* e, size_t n) {  // caller holds e->mu
   while (e->staged.size() < n) e->staged.emplace_back(new klf_engine::StagedStream());
@@ -668,6 +679,7 @@ extern "C" int klf_stage(klf_engine* e, uint32_t id, const uint8_t* p, size_t n)
     }
     dst = e->staged[id].get();  // stable: the table holds pointers, only the table moves
   }
+  if (hipError_t h = ensure_copy_stream(e); h != hipSuccess) return hip_err(e, h, "copy stream");
   std::call_once(e->copier_once, [e] {
     int nw = 3;  // staging copy workers (+ the calling thread)
     if (const char* v = getenv("KLF_STAGE_THREADS")) nw = std::max(0, std::min(atoi(v), 32));
@@ -712,7 +724,7 @@ static void release_staged(klf_engine* e) {  // caller holds e->mu; no H2D may b
 extern "C" int klf_reset(klf_engine* e) {
   if (!e) return KLF_EINVAL;
   std::lock_guard<std::mutex> g(e->mu);
-  (void)hipStreamSynchronize(e->copy_stream);  // early DMAs read the pinned chunks
+  if (e->copy_stream) (void)hipStreamSynchronize(e->copy_stream);  // early DMAs read the pinned chunks
   (void)hipStreamSynchronize(e->stream);       // k_assemble reads the device chunks
   release_staged(e);
   return KLF_OK;
@@ -1275,6 +1287,7 @@ extern "C" int klf_retail(klf_engine* e, klf_result* prev, int64_t tail, klf_res
 extern "C" int klf_run(klf_engine* e, const klf_filter* f, klf_result** out) {
   if (!e || !f || !out) return KLF_EINVAL;
   HIPCHK(e, hipSetDevice(e->device), "hipSetDevice");
+  HIPCHK(e, ensure_copy_stream(e), "copy stream");
   std::lock_guard<std::mutex> g(e->mu);
   const uint32_t n = (uint32_t)e->staged.size();
   std::vector<uint64_t> lens(n), base(n);

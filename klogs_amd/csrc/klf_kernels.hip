@@ -825,25 +825,30 @@ __global__ __launch_bounds__(kThreads, (MODE == kScanGen || FUSE) ? 3 : KLF_SCAN
         uint32_t h, p, m, a;  // a: byte offset of the bitmap word in LDS (qf_bucket * 4)
       };
       constexpr bool kMidIdx = QQ == 3 && QK == 2;  // word from h bits 18..29 (qf_bucket)
+      constexpr bool K3 = QK == 3 || QK == (int)kQfTwoLevel;  // three bits per gram
+      constexpr bool TWO = QK == (int)kQfTwoLevel;            // pair stage first (stride 4 only)
+      static_assert(!TWO || QS == 4, "the two-level probe runs at stride 4");
       // (the 24-bit multiplies ignore bits 24..31 of f: no mask)
       auto probe = [&](uint32_t g) __attribute__((always_inline)) -> Probe {
         const uint32_t gf = g | fold;
-        const uint32_t f = QK == 3 ? gf ^ bfe_u32(gf, 13, 11) : gf;
+        const uint32_t f = K3 ? gf ^ bfe_u32(gf, 13, 11) : gf;
         Probe r;
         r.h = mul_u24(f, 0x9E3779u);
         if (QQ == 4) r.h = mad_u24(gf >> 8, 0x7F4A7Du, r.h);  // + bytes 1..3 * C2
-        r.p = QK == 3 ? mul_hi_u24(f, 0xC2B2AEu) : 0u;  // K = 2: both bits from h (qf_bits)
-        r.m = QK == 3 ? mul_u24(f, 0x5BD1E9u) : 0u;
-        r.a = kMidIdx ? ((r.h >> 16) & ((kQfWords - 1u) << 2)) : ((r.h >> (32 - kQfBucketBits)) << 2);
+        r.p = K3 ? mul_hi_u24(f, 0xC2B2AEu) : 0u;  // K = 2: both bits from h (qf_bits)
+        r.m = K3 ? mul_u24(f, 0x5BD1E9u) : 0u;
+        r.a = TWO ? (((r.h >> 21) << 2) + kQfPairWords * 4u)  // the Bloom half, 11-bit word
+              : kMidIdx ? ((r.h >> 16) & ((kQfWords - 1u) << 2)) : ((r.h >> (32 - kQfBucketBits)) << 2);
         return r;
       };
       auto word = [&](const Probe& r) __attribute__((always_inline)) -> uint32_t {
         return *reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(s_qf) + r.a);
       };
       auto test = [&](uint32_t w, const Probe& r) __attribute__((always_inline)) -> uint32_t {
-        uint32_t t = QK == 3 ? (w >> ((r.m >> 24) & 31u)) & (w >> (r.p & 31u))
-                             : shr_byte1(w, r.h) & (w >> ((r.h >> 16) & 31u));
-        if (QK == 3) t &= w >> ((r.h >> 16) & 31u);
+        uint32_t t = K3 ? (w >> ((r.m >> 24) & 31u)) & (w >> (r.p & 31u))
+                        : shr_byte1(w, r.h) & (w >> ((r.h >> 16) & 31u));
+        if (K3) t &= w >> ((r.h >> 16) & 31u);
+        if (TWO) t &= shr_byte1(w, r.m);  // the fourth bit: m bits 8..12 (qf_bits)
         return t;
       };
       auto hbits = [&](uint32_t g) __attribute__((always_inline)) -> uint32_t {
@@ -867,7 +872,44 @@ __global__ __launch_bounds__(kThreads, (MODE == kScanGen || FUSE) ? 3 : KLF_SCAN
       // fast pass: one OR-accumulated bit per chunk (no positions); most tiles stop here
       uint32_t chit = 0;
       const uint32_t rot = ((uint32_t)lane >> 1) & 7u;
-      if (QS == 4) {
+      uint32_t hq0 = 0, hq1 = 0, hq2 = 0, hq3 = 0;
+      if (TWO) {
+        // stage 1: the exact set of the probed grams' low two bytes (pair words [0, 2048)):
+        // sv bit i = the sample at my0 + 4i passes (each chunk's four dwords, two chunks per
+        // step with their eight word reads in flight)
+        uint32_t sv = 0;
+#pragma unroll
+        for (int v = 0; v < (ABL(4) ? 0 : 8); v += 2) {
+          const uint32_t ca = ((uint32_t)v + rot) & 7u, cb = ((uint32_t)v + 1u + rot) & 7u;
+          const uint4 xa = *reinterpret_cast<const uint4*>(s_tile + my0 + 16u * ca);
+          const uint4 xb = *reinterpret_cast<const uint4*>(s_tile + my0 + 16u * cb);
+          const uint32_t g[8] = {xa.x | fold, xa.y | fold, xa.z | fold, xa.w | fold,
+                                 xb.x | fold, xb.y | fold, xb.z | fold, xb.w | fold};
+          uint32_t w[8];
+#pragma unroll
+          for (int k = 0; k < 8; ++k)
+            w[k] = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(s_qf) + (bfe_u32(g[k], 5, 11) << 2));
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            const uint32_t bit = __builtin_amdgcn_ubfe(w[k], g[k], 1u);  // bit g mod 32 (v_bfe_u32 reads offset[4:0])
+            sv |= bit << (4u * (k < 4 ? ca : cb) + (uint32_t)(k & 3));
+          }
+        }
+        // samples at or past the tile's end (4i >= nvalid) do not count
+        sv &= nvalid >= kLaneBytes ? ~0u : ((1u << ((uint32_t)(nvalid + 3) >> 2)) - 1u);
+        // stage 2: the survivors' 3-bit probe into the Bloom half; a hit's byte position
+        // 4i -> its 32-B group q = i / 8, bit 4i mod 32
+        for (uint32_t m = sv; m; m &= m - 1u) {
+          const uint32_t i = (uint32_t)__builtin_ctz(m);
+          if (hbits(s32[(my0 >> 2) + i]) & 1u) {
+            const uint32_t q = i >> 3, b = 1u << ((4u * i) & 31u);
+            hq0 |= q == 0 ? b : 0u;
+            hq1 |= q == 1 ? b : 0u;
+            hq2 |= q == 2 ? b : 0u;
+            hq3 |= q == 3 ? b : 0u;
+          }
+        }
+      } else if (QS == 4) {
         // stride 4: a chunk's samples are its four dwords.  Two chunks per step, their
         // eight bitmap reads issued before the first test (one LDS round trip per step,
         // not one per probe)
@@ -901,8 +943,7 @@ __global__ __launch_bounds__(kThreads, (MODE == kScanGen || FUSE) ? 3 : KLF_SCAN
         }
       }
       // chunks with a possible hit: the sample positions (past the tile's end clipped)
-      uint32_t hq0 = 0, hq1 = 0, hq2 = 0, hq3 = 0;
-      if (__any(chit != 0)) {
+      if (!TWO && __any(chit != 0)) {
         for (uint32_t m = chit; m; m &= m - 1u) {
           const uint32_t c = (uint32_t)__builtin_ctz(m);
           uint32_t hm = 0;
@@ -3424,6 +3465,9 @@ hipError_t launch_scan(const RunArgs& a, hipStream_t st, int num_cus) {
 }
 template <int QS, int QQ>
 hipError_t launch_gen_q(const RunArgs& a, hipStream_t st, int num_cus) {
+  if constexpr (QS == 4)
+    if (a.pats.qf_k == kQfTwoLevel)  // the two-level probe (stride 4, no anchor)
+      return launch_scan<kScanGen, 4, (int)kQfTwoLevel, QQ>(a, st, num_cus);
   if (QS == 8 && a.pats.qf_anc_on)  // short needles anchored (only beside stride-8 probes)
     return a.pats.qf_k == 2 ? launch_scan<kScanGen, QS, 2, QQ, true>(a, st, num_cus)
                             : launch_scan<kScanGen, QS, 3, QQ, true>(a, st, num_cus);

@@ -82,9 +82,16 @@ constexpr uint32_t kRxPreNone = 0xFFFFFFFFu;         // rx_pre: no bound (= klf_
 // previous design cost ~14 / ~18.  Measured on the C4 / C5 sets and data (host emulation,
 // tools in tests/test_prefilter.py): 0.9 / 0.01 bitmap hits per 8 KiB tile (before: 2.2 /
 // 0.017).
+// Two-level layout (qf_k = kQfTwoLevel, large sets at stride 4): the samples first test an
+// exact set of the probed grams' low two bytes (bitmap words [0, kQfPairWords): bit
+// (g & 0xFFFF)); only the survivors (~5 % of log text for the 1,024-literal C4 set) take the
+// 3-bit probe, into a Bloom filter of the remaining kQfPairWords words (11-bit buckets).
+constexpr uint32_t kQfTwoLevel = 5;
+constexpr uint32_t kQfPairWords = 2048;
+__host__ __device__ inline bool qf_k3(uint32_t k) { return k == 3 || k == kQfTwoLevel; }
 __host__ __device__ inline uint32_t qf_f(uint32_t g, uint32_t k) {
   const uint32_t g24 = g & 0xFFFFFFu;
-  return k == 3 ? g24 ^ (g24 >> 13) : g24;
+  return qf_k3(k) ? g24 ^ (g24 >> 13) : g24;
 }
 __host__ __device__ inline uint32_t qf_hash(uint32_t g, uint32_t w24, uint32_t k) {  // w24 = 24 (q = 4) or 0 (q = 3)
   const uint32_t hi = w24 ? (g >> 8) & 0xFFFFFFu : 0u;
@@ -98,14 +105,27 @@ __host__ __device__ inline uint32_t qf_word(uint32_t h) { return h >> (32 - kQfB
 // v_mul_hi_u32_u24: 54x the hits -- a product's top bits follow the gram's top byte.)
 __host__ __device__ inline uint32_t qf_bucket(uint32_t g, uint32_t w24, uint32_t k) {
   if (w24 == 0 && k == 2) return (qf_hash(g, w24, k) >> 18) & (kQfWords - 1u);
+  if (k == kQfTwoLevel) return qf_hash(g, w24, k) >> 21;  // [0, kQfPairWords)
   return qf_word(qf_hash(g, w24, k));
+}
+// the Bloom bitmap word of gram g (two-level: behind the pair words)
+__host__ __device__ inline uint32_t qf_bloom_word(uint32_t g, uint32_t w24, uint32_t k) {
+  return (k == kQfTwoLevel ? kQfPairWords : 0u) + qf_bucket(g, w24, k);
 }
 __host__ __device__ inline uint32_t qf_bits(uint32_t g, uint32_t h, uint32_t k) {
   const uint32_t f = qf_f(g, k);
   const uint32_t m = f * 0x5BD1E9u;
-  if (k != 3) return (1u << ((h >> 8) & 31u)) | (1u << ((h >> 16) & 31u));
+  if (!qf_k3(k)) return (1u << ((h >> 8) & 31u)) | (1u << ((h >> 16) & 31u));
   const uint32_t p = (uint32_t)(((uint64_t)f * 0xC2B2AEu) >> 32);
-  return (1u << ((m >> 24) & 31u)) | (1u << (p & 31u)) | (1u << ((h >> 16) & 31u));
+  const uint32_t b3 = (1u << ((m >> 24) & 31u)) | (1u << (p & 31u)) | (1u << ((h >> 16) & 31u));
+  return k == kQfTwoLevel ? b3 | (1u << ((m >> 8) & 31u)) : b3;  // two-level: a fourth bit (survivors only)
+}
+// The whole probe of a (folded, masked) gram against the bitmap (host emulation; the scan
+// computes the same from its LDS copy)
+__host__ __device__ inline bool qf_pass(const uint32_t* bm, uint32_t gq, uint32_t w24, uint32_t k) {
+  if (k == kQfTwoLevel && !((bm[(gq & 0xFFFFu) >> 5] >> (gq & 31u)) & 1u)) return false;
+  const uint32_t h = qf_hash(gq, w24, k), bits = qf_bits(gq, h, k);
+  return (bm[qf_bloom_word(gq, w24, k)] & bits) == bits;
 }
 // Gram statistics of the window choice: a count-min sketch, 2 rows of 2^16 bins, for the
 // 3-byte and for the 4-byte grams, then a byte histogram (k_gramhist)

@@ -1246,17 +1246,25 @@ void choose_layout(CompiledSet& out, const DataStats* st, bool allow_anchor, uin
     double best = limit;
     int best_c = -1;
     for (uint32_t qq = ql; qq >= 3 && best_c < 0; --qq) {
-      for (uint32_t c = 0; c < 256; ++c) {
-        if (c == '\n') continue;
-        if (afold && ((c | 0x20u) != c)) continue;  // stored loose bytes carry bit 5
-        bool ok = true;
-        for (size_t i = 0; i < n && ok; ++i) {
-          if (nd[i].size() >= 10) continue;
-          const size_t lim = nd[i].size() - qq;
-          const size_t pos = nd[i].find((char)c);
-          ok = pos != std::string::npos && pos <= lim;
+      // bytes every short needle holds at an offset <= len - qq: the intersection of the
+      // needles' byte sets (first occurrences, as the pre-check records them)
+      std::bitset<256> common;
+      common.set();
+      for (size_t i = 0; i < n && common.any(); ++i) {
+        if (nd[i].size() >= 10) continue;
+        const size_t lim = nd[i].size() - qq;
+        std::bitset<256> has, seen_b;
+        for (size_t k = 0; k < nd[i].size(); ++k) {
+          const uint8_t b = (uint8_t)nd[i][k];
+          if (seen_b.test(b)) continue;  // (its first occurrence decides)
+          seen_b.set(b);
+          if (k <= lim) has.set(b);
         }
-        if (!ok) continue;
+        common &= has;
+      }
+      for (uint32_t c = 0; c < 256; ++c) {
+        if (!common.test(c) || c == '\n') continue;
+        if (afold && ((c | 0x20u) != c)) continue;  // stored loose bytes carry bit 5
         const double sh = byte_share(c, afold, st);
         if (sh < best) { best = sh; best_c = (int)c; }
       }
@@ -1332,7 +1340,9 @@ double layout_cost(const CompiledSet& c, const DataStats& st) {
   // VALU per probe (the scan's ISA, its unrolled fast pass / 32 probes): 6.9 for a 3-byte
   // gram with two bits (fold, multiply, word offset, two shifts, and / or), 9.9 with the
   // fourth byte, 13.4 for 3 bits (folded gram, two more multiplies, a shift)
-  const double per_probe = 7.0 + (c.qf_q == 4 ? 3.0 : 0.0) + (c.qf_k == 3 ? 6.5 : 0.0);
+  // (two-level: ~5 per sample for the pair stage, the 3-bit probe on the ~5 % survivors)
+  const double per_probe = c.qf_k == kQfTwoLevel ? 6.0 + (c.qf_q == 4 ? 1.0 : 0.0)
+                                                 : 7.0 + (c.qf_q == 4 ? 3.0 : 0.0) + (c.qf_k == 3 ? 6.5 : 0.0);
   double cost = per_probe * samples / 64.0;
   if (c.qf_anc_on) {
     cost += 60.0;
@@ -1458,7 +1468,11 @@ void place_tables(CompiledSet& out, const DataStats* st) {
   const size_t n = out.qf_needle.size();
   size_t nprobed = 0;
   for (size_t i = 0; i < n; ++i) nprobed += out.qf_nshort[i] ? 0 : 1;
-  out.qf_k = nprobed * S <= kQfK2MaxGrams ? 2u : 3u;  // few grams: two bits per gram keep the false hits rare
+  // few grams: two bits per gram keep the false hits rare; many at stride 4: the two-level
+  // probe (an exact 2-gram stage, then three bits; KLF_QF_TWO=0 keeps the one-level one)
+  const char* two = getenv("KLF_QF_TWO");
+  out.qf_k = nprobed * S <= kQfK2MaxGrams ? 2u
+             : (S == 4 && !out.qf_anc_on && !(two && !strcmp(two, "0"))) ? kQfTwoLevel : 3u;
   const uint32_t w24 = q == 4 ? 24u : 0u;
   for (uint32_t i = 0; i < n; ++i) {
     const std::string& s = out.qf_needle[i];
@@ -1492,7 +1506,8 @@ void place_tables(CompiledSet& out, const DataStats* st) {
       used[g]++;
       const uint32_t h = qf_hash(g, w24, out.qf_k);
       const uint32_t bw = qf_bucket(g, w24, out.qf_k);
-      out.qf_bitmap[bw] |= qf_bits(g, h, out.qf_k);
+      out.qf_bitmap[qf_bloom_word(g, w24, out.qf_k)] |= qf_bits(g, h, out.qf_k);
+      if (out.qf_k == kQfTwoLevel) out.qf_bitmap[(g & 0xFFFFu) >> 5] |= 1u << (g & 31u);
       bent.push_back({bw, i << 8 | k});
     }
   }
@@ -1555,8 +1570,7 @@ PrefilterHits prefilter_hits(const CompiledSet& cs, const uint8_t* s, size_t n) 
     if (p % S == 0) {
       ++r.probes;
       const uint32_t gq = (g | cs.qf_fold) & cs.qf_mask;
-      const uint32_t h = qf_hash(gq, w24, cs.qf_k), bits = qf_bits(gq, h, cs.qf_k);
-      hit = (cs.qf_bitmap[qf_bucket(gq, w24, cs.qf_k)] & bits) == bits;
+      hit = qf_pass(cs.qf_bitmap.data(), gq, w24, cs.qf_k);
       r.bitmap_hits += hit;
     }
     if (!hit && cs.qf_anc_on && ((uint32_t)s[p] | (cs.qf_anc_fold & 0xFFu)) == cs.qf_anc_byte) {
@@ -1612,8 +1626,7 @@ bool prefilter_match(const CompiledSet& cs, const uint8_t* s, size_t n, uint32_t
     bool hit = false;
     if (p % S == phase % S) {
       const uint32_t gq = (g | cs.qf_fold) & cs.qf_mask;
-      const uint32_t h = qf_hash(gq, cs.qf_q == 4 ? 24u : 0u, cs.qf_k), bits = qf_bits(gq, h, cs.qf_k);
-      hit = (cs.qf_bitmap[qf_bucket(gq, cs.qf_q == 4 ? 24u : 0u, cs.qf_k)] & bits) == bits;
+      hit = qf_pass(cs.qf_bitmap.data(), gq, cs.qf_q == 4 ? 24u : 0u, cs.qf_k);
     }
     if (!hit && cs.qf_anc_on && ((uint32_t)s[p] | (cs.qf_anc_fold & 0xFFu)) == cs.qf_anc_byte)
       for (size_t j = 0; j + 1 < cs.qf_anc_pre.size() && !hit; j += 2)

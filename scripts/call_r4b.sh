@@ -1,5 +1,6 @@
 set -e
 O=gpurun_out/r4b; mkdir -p $O
+timeout -k 10 60 ./scripts/mb_depth > $O/mb_depth.txt 2>&1; cat $O/mb_depth.txt
 timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_pattern_counts.py tests/test_gpu_staging.py tests/test_gpu_large.py -m gpu -x -q --timeout 200 --timeout-method thread > $O/pytest_gpu.log 2>&1 || { tail -30 $O/pytest_gpu.log; exit 1; }
 tail -1 $O/pytest_gpu.log
 for c in c5 c4; do
