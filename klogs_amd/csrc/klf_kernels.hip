@@ -419,6 +419,9 @@ __device__ __forceinline__ bool parse_fast(const uint8_t* lds, uint32_t o, const
 #ifndef KLF_COPY_U
 #define KLF_COPY_U 1
 #endif
+#ifndef KLF_ANY_BATCH
+#define KLF_ANY_BATCH 8  // chunk reads in flight in the scan's newline any-test
+#endif
 #ifndef KLF_SCAN_OCC
 // plain / literal scans: waves per SIMD the launch bounds ask for.  3 leaves the compiler
 // up to 168 VGPRs: C3's plain scan 1.84 -> 1.67 ms, C2's literal scan unchanged within the
@@ -604,16 +607,21 @@ __global__ __launch_bounds__(kThreads, (MODE == kScanGen || FUSE) ? 3 : KLF_SCAN
     uint32_t nlc = 0, anc = 0;
     {
       const uint32_t rot = ((uint32_t)lane >> 1) & 7u;
-      // all eight reads in flight before the first test (one LDS round trip, not eight)
-      uint4 xs[8];
+      // KLF_ANY_BATCH reads in flight before the first test (8: one LDS round trip, not
+      // eight; 4: two round trips, 16 fewer VGPRs)
 #pragma unroll
-      for (int v = 0; v < 8; ++v) xs[v] = *reinterpret_cast<const uint4*>(s_tile + my0 + 16u * (((uint32_t)v + rot) & 7u));
+      for (int v0 = 0; v0 < 8; v0 += KLF_ANY_BATCH) {
+        uint4 xs[KLF_ANY_BATCH];
 #pragma unroll
-      for (int v = 0; v < 8; ++v) {
-        const uint32_t c = ((uint32_t)v + rot) & 7u;
-        nlc |= any_eq16(xs[v], 0x0A0A0A0Au) ? (1u << c) : 0u;
-        if (LIT && !ABL(2)) anc |= any_eq16(xs[v], pat) ? (1u << c) : 0u;
-        if (ANC) anc |= any_eq16(afold ? or4(xs[v], afold) : xs[v], pat) ? (1u << c) : 0u;
+        for (int v = 0; v < KLF_ANY_BATCH; ++v)
+          xs[v] = *reinterpret_cast<const uint4*>(s_tile + my0 + 16u * (((uint32_t)(v0 + v) + rot) & 7u));
+#pragma unroll
+        for (int v = 0; v < KLF_ANY_BATCH; ++v) {
+          const uint32_t c = ((uint32_t)(v0 + v) + rot) & 7u;
+          nlc |= any_eq16(xs[v], 0x0A0A0A0Au) ? (1u << c) : 0u;
+          if (LIT && !ABL(2)) anc |= any_eq16(xs[v], pat) ? (1u << c) : 0u;
+          if (ANC) anc |= any_eq16(afold ? or4(xs[v], afold) : xs[v], pat) ? (1u << c) : 0u;
+        }
       }
       if (nvalid < kLaneBytes) {
         const uint32_t vm = (1u << ((nvalid + 15) >> 4)) - 1u;
@@ -3488,7 +3496,7 @@ hipError_t launch_pipeline(const RunArgs& a0, hipStream_t st, hipEvent_t* ev, in
   hipError_t e;
 #define KLF_TRY(x) do { e = (x); if (e != hipSuccess) return e; } while (0)
   if (phase != 2) {
-  KLF_TRY(hipEventRecord(ev[0], st));
+  if (ev) KLF_TRY(hipEventRecord(ev[0], st));
   {
     const uint32_t nw = a.nsegs * (uint32_t)(sizeof(SegOut) / 8);
     uint32_t g = (nw + 255) / 256;
@@ -3505,7 +3513,7 @@ hipError_t launch_pipeline(const RunArgs& a0, hipStream_t st, hipEvent_t* ev, in
   }
   // ev[1] only with stage times: each event record idles the GPU for a few us, and the
   // scan's own time is then taken from ev[0] (k_init in front of it: ~2 us)
-  if (a.stage_times) KLF_TRY(hipEventRecord(ev[1], st));
+  if (ev && a.stage_times) KLF_TRY(hipEventRecord(ev[1], st));
   {
     if (a.fused)
       KLF_TRY((launch_scan<kScanPlain, 1, 3, 4, false, true>(a, st, num_cus)));
@@ -3521,7 +3529,7 @@ hipError_t launch_pipeline(const RunArgs& a0, hipStream_t st, hipEvent_t* ev, in
       KLF_TRY((launch_gen<1>(a, st, num_cus)));
     else
       KLF_TRY((launch_scan<kScanPlain, 1>(a, st, num_cus)));
-    KLF_TRY(hipEventRecord(ev[6], st));  // k_scan alone (the roofline kernel)
+    if (ev) KLF_TRY(hipEventRecord(ev[6], st));  // k_scan alone (the roofline kernel)
     if (!a.tindex_wide) {
       hipLaunchKernelGGL((k_tindex<4, 0>), dim3((a.ntiles + 1023) / 1024), dim3(256), 0, st, a);
       KLF_TRY(hipGetLastError());
@@ -3558,12 +3566,12 @@ hipError_t launch_pipeline(const RunArgs& a0, hipStream_t st, hipEvent_t* ev, in
     hipLaunchKernelGGL(k_scatter, dim3(sg), dim3(256), 0, st, a);
     KLF_TRY(hipGetLastError());
   }
-  if (a.stage_times && !fork) KLF_TRY(hipEventRecord(ev[2], st));  // ~5 us of idle GPU each
+  if (ev && a.stage_times && !fork) KLF_TRY(hipEventRecord(ev[2], st));  // ~5 us of idle GPU each
   if (a.grep_mode == kGrepGeneral && a.pats.qf_on) {
     hipLaunchKernelGGL(k_verify, dim3(num_cus * 8), dim3(256), 0, st, a);
     KLF_TRY(hipGetLastError());
     if (fork) KLF_TRY(hipStreamWaitEvent(st, ev_join, 0));
-    if (a.stage_times && fork) KLF_TRY(hipEventRecord(ev[2], st));
+    if (ev && a.stage_times && fork) KLF_TRY(hipEventRecord(ev[2], st));
     if (a.count_pats) {
       hipLaunchKernelGGL(k_fixcount, dim3(num_cus * 2), dim3(256), 0, st, a);
       KLF_TRY(hipGetLastError());
@@ -3588,9 +3596,9 @@ hipError_t launch_pipeline(const RunArgs& a0, hipStream_t st, hipEvent_t* ev, in
     hipLaunchKernelGGL(k_match, dim3(num_cus * 8), dim3(256), 0, st, a);
     KLF_TRY(hipGetLastError());
   }
-  if (a.stage_times) KLF_TRY(hipEventRecord(ev[3], st));  // ~5 us of idle GPU each
+  if (ev && a.stage_times) KLF_TRY(hipEventRecord(ev[3], st));  // ~5 us of idle GPU each
   KLF_TRY(launch_tail_stage(a, st, ev, num_cus));
-  KLF_TRY(hipEventRecord(ev[5], st));
+  if (ev) KLF_TRY(hipEventRecord(ev[5], st));
 #undef KLF_TRY
   return hipSuccess;
 }
@@ -3608,7 +3616,7 @@ static hipError_t launch_tail_stage(const RunArgs& a, hipStream_t st, hipEvent_t
   }
   hipLaunchKernelGGL(k_tailw, dim3(a.nsegs), dim3(256), 0, st, a);
   KLF_TRY(hipGetLastError());
-  if (a.stage_times) KLF_TRY(hipEventRecord(ev[4], st));  // ~5 us of idle GPU each
+  if (ev && a.stage_times) KLF_TRY(hipEventRecord(ev[4], st));  // ~5 us of idle GPU each
   if (a.fused) return hipSuccess;  // the scan copied the output
   {
     const uint32_t gt = (a.ntiles + 4 * kTkBatch - 1) / (4 * kTkBatch);

@@ -309,6 +309,7 @@ struct RunArgs {
 // scan, ev[3] after the general matcher, ev[4] after counts+tail+window prefix, ev[5]
 // after compaction.  Returns a hipError_t.
 // aux (may be null) with the fork / join events: a side stream for k_scatter beside k_verify.
+// ev may be null: no event records (the grouped runs of the engine time the whole batch).
 // phase: 0 the whole pipeline; 1 up to the tile index (k_init .. k_tindex: the line arrays
 // are not touched, a.bits may be null); 2 the rest (k_scatter on), after the host sized
 // the line arrays from phase 1's line count (an engine's first run).

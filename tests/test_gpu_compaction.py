@@ -183,3 +183,49 @@ def test_output_buffer_grown_on_demand(gpu, compact, tails, monkeypatch):
                 assert g.out == out, (tail, i, len(g.out), len(out))
                 assert g.counts["selected"] == c["selected"], (tail, i)
         r.free()
+
+
+@pytest.mark.parametrize("since", [None, SINCE])
+def test_grouped_runs_equal_oracle(gpu, monkeypatch, since):
+    """Stream groups (KLF_GROUP_MB: each group of consecutive whole streams a pipeline over
+    its own workspace slice, two launch streams; C3's dense copy re-reads from the Infinity
+    Cache): an engine's second and later -l runs go grouped and must equal the C oracle in
+    output bytes, counts and line offsets (with empty streams, fragments and dense tiles among
+    them), as must klf_result_last_unparsed; klf_retail refuses a grouped result."""
+    monkeypatch.setenv("KLF_GROUP_MB", "1")
+    streams = []
+    for i in range(23):
+        k = i % 5
+        if k == 0:
+            streams.append(b"")
+        elif k == 1:
+            streams.append(synth.generate(synth.TEXT, 90 + i, i, 400_000 + 7_919 * i))
+        elif k == 2:
+            streams.append(synth.generate(synth.ADVERSARIAL, 90 + i, i, 150_000, drop_final_nl=True, permille=40))
+        elif k == 3:
+            streams.append(synth.generate(synth.LONGJSON, 90 + i, i, 900_000, permille=5))
+        else:
+            streams.append(synth.generate(synth.TEXT, 90 + i, i, 1_300_000))
+    from test_shard import _last_unparsed
+    with E.Engine(0) as eng:
+        for rep in range(3):  # the first run learns the line density (ungrouped), then grouped
+            eng.reset()
+            eng.set_streams(len(streams))
+            for i, s in enumerate(streams):
+                if s:
+                    eng.stage(i, s)
+            r = eng.run(since=since, n_streams=len(streams))
+            for i, s in enumerate(streams):
+                out, lo, _, c = co.filter_stream(s, since or co.GO_ZERO_TIME, -1, [])
+                so = r.stream(i)
+                assert so.out == out, (rep, i)
+                assert np.array_equal(r.lines(i), lo), (rep, i)
+                for k in ("lines", "parsed", "since_ok", "selected", "out_bytes"):
+                    assert so.counts[k] == c[k], (rep, i, k)
+                if s and rep == 2:
+                    assert r.last_unparsed(i) == _last_unparsed(s), i
+            if rep == 2:
+                with pytest.raises(E.KlfError) as ei:
+                    r.retail(5)
+                assert ei.value.code == E.KLF_ESTATE
+            r.free()

@@ -147,12 +147,18 @@ def check_against_py(streams, since, tail, grep=(), match=()):
             [ref.n_lines, ref.n_parsed, ref.n_since, ref.n_matched, ref.n_selected], (i, g_c)
 
 
+@pytest.mark.parametrize("two", [True, False])
 @pytest.mark.parametrize("since,tail", [(None, -1), ((synth.T0 + 1800, 0), 50)])
-def test_c4_literal_set_mixed_lines(gpu, since, tail):
-    """BASELINE config 4 shape at test size: 1,024 literals over mixed-length lines."""
+def test_c4_literal_set_mixed_lines(gpu, monkeypatch, since, tail, two):
+    """BASELINE config 4 shape at test size: 1,024 literals over mixed-length lines, through
+    the two-level probe (exact 2-gram stage, then 4 Bloom bits; the default for such sets)
+    and the one-level 3-bit probe (KLF_QF_TWO=0)."""
+    if not two:
+        monkeypatch.setenv("KLF_QF_TWO", "0")
     lits = synth.c4_literals(1024)
     assert E.debug_prefilter(b"", grep=lits)[1]["on"]
     d = synth.generate(synth.MIXED, 4, 0, 3_000_000, permille=5)
+    assert E.debug_prefilter_hits(d[:1 << 20], d[:1 << 16], grep=lits)["k"] == (5 if two else 3)
     check_against_c([d, synth.generate(synth.MIXED, 4, 1, 700_000, permille=50)], since, tail, lits)
 
 
