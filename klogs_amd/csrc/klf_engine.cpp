@@ -1130,6 +1130,8 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
     HIPCHK(e, e->d_wpre.ensure((nsegs + ng) * 8), "alloc wpre");
     HIPCHK(e, e->d_pool.ensure(gpool * ng * 4), "alloc pool");
     HIPCHK(e, e->d_gsegs.ensure(nsegs * sizeof(SegDesc)), "alloc group segs");
+    // outputs at their groups' input offsets: the buffer spans the batch, alignment gaps too
+    HIPCHK(e, e->d_out.ensure(segs[nsegs - 1].base + segs[nsegs - 1].len + 64), "alloc out");
     std::vector<SegDesc> gsegs(segs);  // tile0 relative to the group's first tile
     for (auto& g : groups)
       for (uint32_t i = g.s0; i < g.s1; ++i) gsegs[i].tile0 -= g.t0;
