@@ -129,6 +129,8 @@ struct klf_engine {
   std::unique_ptr<klf::CopyPool> copier;  // started by the first klf_stage (device-resident runs never stage)
   std::once_flag copier_once;
   std::once_flag copy_stream_once;     // the copy stream: created by the first klf_stage / klf_run
+  std::once_flag aux_once;             // the side stream + fork / join events: the first run
+  hipError_t aux_err = hipSuccess;
   hipError_t copy_stream_err = hipSuccess;
   DevBuf d_asm;                        // k_assemble piece table
   DevBuf d_scratch;                    // small query results (klf_result_last_unparsed)
@@ -470,12 +472,9 @@ extern "C" int klf_open(const klf_config* cfg, klf_engine** out) {
   if (getenv("KLF_DIAG"))
     fprintf(stderr, "[klf] open: events done at %.1f us\n",
             std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t_open0).count());
-  if ((h = hipStreamCreateWithFlags(&e->aux_stream, hipStreamNonBlocking)) != hipSuccess ||
-      (h = hipEventCreateWithFlags(&e->ev_fork, hipEventDisableTiming)) != hipSuccess ||
-      (h = hipEventCreateWithFlags(&e->ev_join, hipEventDisableTiming)) != hipSuccess ||
-      (h = hipEventCreateWithFlags(&e->stage_ev, hipEventDisableTiming)) != hipSuccess) {
+  if ((h = hipEventCreateWithFlags(&e->stage_ev, hipEventDisableTiming)) != hipSuccess) {
     *out = e;
-    return hip_err(e, h, "side stream");
+    return hip_err(e, h, "staging event");
   }
   if (getenv("KLF_DIAG"))
     fprintf(stderr, "[klf] open: device setup done at %.1f us\n",
@@ -557,6 +556,18 @@ static hipError_t ensure_copy_stream(klf_engine* e) {
     e->copy_stream_err = h;
   });
   return e->copy_stream_err;
+}
+
+// The pipeline's side stream and its fork / join events, made by the first run (while its
+// first-batch statistics kernel runs), not by klf_open.
+static hipError_t ensure_aux_stream(klf_engine* e) {
+  std::call_once(e->aux_once, [e] {
+    hipError_t h = hipStreamCreateWithFlags(&e->aux_stream, hipStreamNonBlocking);
+    if (h == hipSuccess) h = hipEventCreateWithFlags(&e->ev_fork, hipEventDisableTiming);
+    if (h == hipSuccess) h = hipEventCreateWithFlags(&e->ev_join, hipEventDisableTiming);
+    e->aux_err = h;
+  });
+  return e->aux_err;
 }
 
 static void grow_table(klf_engine* e, size_t n) {  // caller holds e->mu
@@ -909,6 +920,7 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
       tune_pending = true;
     }
   }
+  HIPCHK(e, ensure_aux_stream(e), "side stream");  // (the first run: beside the statistics kernel)
   double est_density = 0.0;  // lines per byte of the first batch's sample (0: none)
   auto finish_tune = [&]() -> int {
     HIPCHK(e, hipStreamSynchronize(st), "sync hist");
