@@ -155,7 +155,6 @@ struct klf_engine {
   std::vector<SegDesc> last_segs;  // tile_seg cache key
   DevBuf d_tile_seg;
   DevBuf d_cmap, d_cseg;
-  DevBuf d_fstate;  // fused compaction turn records
   DevBuf d_batch, d_segs, d_tstat, d_slots, d_pool, d_tile_base, d_bsum, d_cstatus, d_counters, d_line_off,
       d_meta, d_bits, d_segout, d_wpre, d_out, d_mpart, d_trec, d_truns, d_kbase;
   uint64_t pool_cap = 1 << 20;
@@ -509,7 +508,7 @@ extern "C" void klf_close(klf_engine* e) {
                     &e->d_rx_follow, &e->d_rx_vec, &e->d_rx_flags, &e->d_rx_pre, &e->d_qf_bitmap, &e->d_qf_head,
                     &e->d_qf_ent, &e->d_qf_nbytes, &e->d_qf_anc, &e->d_rx_vec4, &e->d_qhits, &e->d_hslots, &e->d_hist, &e->d_hflat, &e->d_cand, &e->d_batch, &e->d_segs, &e->d_tstat,
                     &e->d_slots, &e->d_pool, &e->d_tile_base, &e->d_bsum, &e->d_cstatus, &e->d_counters, &e->d_cmap, &e->d_cseg,
-                    &e->d_fstate, &e->d_line_off, &e->d_meta, &e->d_bits, &e->d_segout, &e->d_wpre, &e->d_out, &e->d_tile_seg, &e->d_mpart, &e->d_trec, &e->d_truns, &e->d_kbase})
+                    &e->d_line_off, &e->d_meta, &e->d_bits, &e->d_segout, &e->d_wpre, &e->d_out, &e->d_tile_seg, &e->d_mpart, &e->d_trec, &e->d_truns, &e->d_kbase})
     b->release();
   e->d_asm.release();
   e->d_scratch.release();
@@ -793,7 +792,6 @@ static hipError_t grow_out_retail(klf_engine* e, klf::RunArgs& a, std::vector<Se
     if (h != hipSuccess) return h;
     a.out = e->d_out.as<uint8_t>();
     a.out_cap = e->d_out.cap;
-    a.fused = 0;
     if ((h = klf::launch_retail(a, e->stream, e->ev, e->num_cus)) != hipSuccess) return h;
     uint32_t* rb = static_cast<uint32_t*>(e->h_rb.p);  // counters, then the stream records
     if ((h = hipMemcpyAsync(rb, e->d_counters.p, 32 * 4, hipMemcpyDeviceToHost, e->stream)) != hipSuccess) return h;
@@ -968,23 +966,12 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
   HIPCHK(e, e->d_kbase.ensure(ntiles * 16), "alloc kbase");
   uint32_t compact_mode = 0;  // tests: force either compaction path
   if (const char* v = getenv("KLF_COMPACT")) compact_mode = !strcmp(v, "sparse") ? 1u : !strcmp(v, "dense") ? 2u : 0u;
-  // Fused compaction (opt-in, KLF_FUSE=1): every line is decided where it starts (--tail -1,
-  // no patterns), so the scan can copy the output itself and read the input once.  Not the
-  // default: on MI355X the decoupled look-back it needs per workgroup turn waits on
-  // cross-XCD loads of several us under full HBM load, and the turn tiles it holds in LDS
-  // leave no room to overlap them (C3: 5.2-10 ms fused vs 5.9 ms two-pass; DESIGN.md
-  // section 4).  Off when a compaction path is forced (tests) or past 1 TiB of output.
-  bool fused = false;
-  if (const char* v = getenv("KLF_FUSE"))
-    fused = strcmp(v, "0") != 0 && mode == klf::CompiledSet::kNone && f->tail == -1 && compact_mode == 0 &&
-            total_bytes < (1ull << 40);
-  if (fused) HIPCHK(e, e->d_fstate.ensure(((ntiles + 3) / 4) * 8 + 16), "alloc fused turns");
   // The output buffer: sized for the whole input up front when the run keeps about as much
-  // as it reads (no --tail limit: C3-like; the fused scan writes it as it goes), else grown
+  // as it reads (no --tail limit: C3-like), else grown
   // on demand -- the compaction skips a copy that would not fit, the host grows the buffer
   // to the run's output and reruns the tail stage (first runs only: the buffer is kept).
   // A --tail run then never maps an input-sized buffer (34 GB for C4 / C5).
-  if (fused || f->tail < 0) HIPCHK(e, e->d_out.ensure(total_bytes + 64), "alloc out");
+  if (f->tail < 0) HIPCHK(e, e->d_out.ensure(total_bytes + 64), "alloc out");
   else if (!e->d_out.p) {  // a first --tail run: room for a typical tail window (no rerun to grow)
     uint64_t first = 64ull << 20;
     if (const char* v = getenv("KLF_DEBUG_OUT_INIT")) first = (uint64_t)std::max(1L, atol(v));  // tests: force growth
@@ -1071,8 +1058,6 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
     a.truns = want_truns ? e->d_truns.as<uint32_t>() : nullptr;
     a.kbase = e->d_kbase.as<uint64_t>();
     a.compact_mode = compact_mode;
-    a.fused = fused ? 1u : 0u;
-    a.fstate = fused ? e->d_fstate.as<uint64_t>() : nullptr;
     a.count_pats = count ? 1u : 0u;
     a.pcount = count ? e->d_pcount.as<uint32_t>() : nullptr;
     a.pairs = count ? e->d_pairs.as<uint64_t>() : nullptr;
@@ -1092,7 +1077,7 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
     const char* v = getenv("KLF_GROUP_MB");
     return v ? (uint64_t)std::max(0L, atol(v)) << 20 : (uint64_t)0;
   }();
-  if (group_bytes && mode == klf::CompiledSet::kNone && f->tail < 0 && !fused && nsegs >= 2 &&
+  if (group_bytes && mode == klf::CompiledSet::kNone && f->tail < 0 && nsegs >= 2 &&
       total_bytes >= 2 * group_bytes && e->line_density > 0.0 && !(f->flags & KLF_FILTER_STAGE_TIMES)) {
     struct Group {
       uint32_t s0, s1;         // segments [s0, s1)
@@ -1358,15 +1343,6 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
       fprintf(stderr, "[klf] hits=%u spilled=%u hits_over=%u nfa_queue=%u queue_over=%u deferred=%u\n",
               counters[klf::kCtrVerified], counters[klf::kCtrHits], counters[klf::kCtrHitsOver],
               counters[klf::kCtrQueue], counters[klf::kCtrQOver], counters[5]);
-    if (fused && getenv("KLF_DIAG") && counters[29])
-      fprintf(stderr, "[klf] fused turns: %u workgroups, Kcycles per workgroup: scan %.1f look-back %.1f copy %.1f; rounds %u spins %u\n",
-              counters[29], (double)counters[24] / counters[29], (double)counters[25] / counters[29],
-              (double)counters[26] / counters[29], counters[27], counters[28]);
-    if (fused && counters[klf::kCtrFuseBailHost]) {  // the fused scan met a case it leaves to the two passes
-      if (getenv("KLF_DIAG")) fprintf(stderr, "[klf] fused compaction bailed (%u): rerun unfused\n", counters[klf::kCtrFuseBailHost]);
-      fused = false;
-      continue;
-    }
     overflow = (counters[2] & 1u) != 0;
     if (overflow) {  // more lines (or dense-tile slots) than estimated: rerun with exact sizes
       if (line_reruns++) break;
@@ -1467,7 +1443,6 @@ extern "C" int klf_retail(klf_engine* e, klf_result* prev, int64_t tail, klf_res
   if (nsegs) {
     klf::RunArgs a = e->last_args;
     a.tail = tail;
-    a.fused = 0;  // re-tail: the two-pass compaction over the line index
     a.stage_times = 0;
     hipStream_t st = e->stream;
     hipError_t h = klf::launch_retail(a, st, e->ev, e->num_cus);

@@ -169,84 +169,6 @@ constexpr uint32_t kCtrDefer = 5;  // counters[5]: some line of this run was def
 constexpr int kTcRuns = kTile / 20 + 8;     // + the two sentinels
 constexpr int kTcChunks = kTile / 16 + 8;
 
-// ---- fused compaction (k_scan<plain, fused>: --tail -1 and no patterns) ------------------
-// With every line decided where it starts (parsed and since_ok: SPEC.md S3/S4 with tail -1),
-// the scan copies each tile's kept bytes itself, so the input is read once.  A tile's
-// output offset is the sum of the kept bytes before it, and its carried-in line (the one
-// open at its first byte) is kept or not by the tile that started it: both reach the tile
-// through a decoupled look-back over workgroup turns (4 consecutive tiles, one per wave,
-// claimed in order from a counter, so every turn a wave waits for is held by a running
-// workgroup).  A range's aggregate is a function of the state entering it:
-//   bytes  kept bytes of the lines starting in the range (fixed),
-//   has    some line starts in the range,
-//   span   bytes from the range start to its first line start (the range when !has): the
-//          entering line's part, kept from its content start on when that line is kept,
-//   sel / crel   the line open at the range end: kept?, its content start - the range end.
-// Published per turn as one 64-bit word (sc1 store / sc1 poll: self-contained, visible
-// across XCDs): status 1 = aggregate, 2 = inclusive prefix (output offset + open line).
-constexpr uint32_t kCtrTurn = 20;       // counters[20]: fused turns claimed
-constexpr uint32_t kCtrFuseBail = 21;   // counters[21]: a fused run met what it cannot do (rerun unfused)
-struct FAgg {
-  uint32_t bytes, span;
-  int32_t crel;
-  bool has, sel;
-};
-struct FPre {
-  uint64_t off;
-  int32_t crel;  // content start of the open line - the boundary
-  bool sel;
-};
-// a content start before the boundary: kept from the boundary on, however far back (-1)
-__device__ __forceinline__ int32_t f_sat(int32_t crel) { return crel < 0 ? -1 : crel; }
-__device__ __forceinline__ uint32_t f_carried(uint32_t span, bool sel, int32_t crel) {
-  const int32_t lo = crel > 0 ? crel : 0;
-  return (sel && (int32_t)span > lo) ? (uint32_t)((int32_t)span - lo) : 0u;
-}
-// X then Y
-__device__ __forceinline__ FAgg f_combine(const FAgg& x, const FAgg& y) {
-  FAgg z;
-  z.bytes = x.bytes + y.bytes + (x.has ? f_carried(y.span, x.sel, x.crel) : 0u);
-  z.has = x.has || y.has;
-  z.span = x.has ? x.span : x.span + y.span;
-  if (y.has) { z.sel = y.sel; z.crel = y.crel; }
-  else { z.sel = x.sel; z.crel = f_sat(x.crel - (int32_t)y.span); }  // !y.has: y.span = its length
-  return z;
-}
-__device__ __forceinline__ FPre f_apply(const FPre& p, const FAgg& z) {
-  FPre r;
-  r.off = p.off + z.bytes + f_carried(z.span, p.sel, p.crel);
-  if (z.has) { r.sel = z.sel; r.crel = z.crel; }
-  else { r.sel = p.sel; r.crel = f_sat(p.crel - (int32_t)z.span); }
-  return r;
-}
-// 64-bit records: [63:62] status, then A: bytes 0-16, has 17, span 18-34, sel 35, crel 36-51
-// (16 bits signed); P: off 0-39, sel 40, crel 41-56 (16 bits signed)
-__device__ __forceinline__ uint64_t f_pack_a(const FAgg& a) {
-  return (1ull << 62) | (uint64_t)(a.bytes & 0x1FFFFu) | ((uint64_t)a.has << 17) | ((uint64_t)(a.span & 0x1FFFFu) << 18) |
-         ((uint64_t)a.sel << 35) | ((uint64_t)(uint16_t)(int16_t)a.crel << 36);
-}
-__device__ __forceinline__ FAgg f_unpack_a(uint64_t v) {
-  FAgg a;
-  a.bytes = (uint32_t)(v & 0x1FFFFu);
-  a.has = (v >> 17) & 1u;
-  a.span = (uint32_t)((v >> 18) & 0x1FFFFu);
-  a.sel = (v >> 35) & 1u;
-  a.crel = (int32_t)(int16_t)(uint16_t)(v >> 36);
-  return a;
-}
-__device__ __forceinline__ uint64_t f_pack_p(const FPre& p) {
-  return (2ull << 62) | (p.off & 0xFFFFFFFFFFull) | ((uint64_t)p.sel << 40) | ((uint64_t)(uint16_t)(int16_t)p.crel << 41);
-}
-__device__ __forceinline__ void copy_tile_runs(const uint8_t* s_buf, uint32_t* s_run, uint16_t* s_map, uint32_t nr,
-                                               uint32_t kept, uint64_t obase, uint8_t* out, int lane);
-__device__ __forceinline__ FPre f_unpack_p(uint64_t v) {
-  FPre p;
-  p.off = v & 0xFFFFFFFFFFull;
-  p.sel = (v >> 40) & 1u;
-  p.crel = (int32_t)(int16_t)(uint16_t)(v >> 41);
-  return p;
-}
-
 // Any-test: nonzero when some byte of the 16 equals the byte replicated in c4.  One
 // v_xad_u32 per dword ((x ^ c4) - 0x01..01: bit 7 of an equal byte is set) and 3-input
 // ORs; it also flags bytes with (x ^ c) >= 0x81 (non-ASCII text) and bytes above a true
@@ -401,12 +323,6 @@ __device__ __forceinline__ bool parse_fast(const uint8_t* lds, uint32_t o, const
 #ifndef KLF_ABL
 #define KLF_ABL 0
 #endif
-#ifndef KLF_FSTATIC
-#define KLF_FSTATIC 0  // timing builds: fused turns assigned round-robin instead of claimed
-#endif
-#ifndef KLF_FDIAG
-#define KLF_FDIAG 0  // timing builds: per-phase cycle sums of the fused scan (counters[24..29])
-#endif
 #ifndef KLF_CG_NT
 #define KLF_CG_NT 0
 #endif
@@ -436,28 +352,17 @@ constexpr int kScanPlain = 0, kScanLit = 1, kScanGen = 2;
 // (wave-uniform) reads compile to scalar loads: a vector load of them would be ordered
 // behind the in-flight prefetch by vmcnt and stall every tile on the next tile's bytes.
 // General sets: QS sampling stride, QK bits per gram, QQ gram bytes (3 or 4), QA (stride 8
-// only) the short needles' anchor test (DevPatterns::qf_anc_*).  FUSE (plain scan, tail -1,
-// no patterns): the compaction copy fused in (see FAgg above).
-template <int MODE, int QS, int QK, int QQ = 4, bool QA = false, bool FUSE = false>
-__global__ __launch_bounds__(kThreads, (MODE == kScanGen || FUSE) ? 3 : KLF_SCAN_OCC) void k_scan(RunArgs a, const uint32_t* __restrict__ tseg,
+// only) the short needles' anchor test (DevPatterns::qf_anc_*).
+template <int MODE, int QS, int QK, int QQ = 4, bool QA = false>
+__global__ __launch_bounds__(kThreads, MODE == kScanGen ? 3 : KLF_SCAN_OCC) void k_scan(RunArgs a, const uint32_t* __restrict__ tseg,
                                                                const SegDesc* __restrict__ segs) {
   constexpr bool LIT = MODE == kScanLit;
   constexpr bool GEN = MODE == kScanGen;
   constexpr bool ANC = GEN && QA;
   static_assert(QQ == 3 || QQ == 4, "3- or 4-byte grams");
-  static_assert(!FUSE || MODE == kScanPlain, "the fused copy serves runs without patterns");
-  if (FUSE && KLF_ABL != 0) return;  // timing builds ablate the scan: never fused (launch_pipeline)
   constexpr int kWaves = kThreads / 64;
   constexpr int kRows = kTile / 1024;  // 1 KiB rows: 16 B per lane per row
-  constexpr int kFPad = FUSE ? 16 : 0;  // the fused copy reads up to 16 B before a run
-  __shared__ __attribute__((aligned(16))) uint8_t s_tile_all[kWaves][kFPad + kTile + kHalo];
-  // fused copy: per wave the tile's kept runs and chunk map; per workgroup the turn's tile
-  // aggregates, the waves' entering prefixes, the next claimed turn
-  __shared__ uint32_t s_frun[FUSE ? kWaves : 1][FUSE ? kTcRuns : 1];
-  __shared__ __attribute__((aligned(16))) uint16_t s_fmap[FUSE ? kWaves : 1][FUSE ? kTcChunks : 1];
-  __shared__ uint64_t s_fagg[FUSE ? kWaves : 1];
-  __shared__ FPre s_fpre[FUSE ? kWaves : 1];
-  __shared__ uint32_t s_fturn;
+  __shared__ __attribute__((aligned(16))) uint8_t s_tile_all[kWaves][kTile + kHalo];
   __shared__ __attribute__((aligned(16))) uint32_t s_list_all[kWaves][kSlotStride];
   __shared__ __attribute__((aligned(16))) uint32_t s_lit[kMaxFusedLiteral / 4 + 1];  // literal, zero padded
   __shared__ uint32_t s_month[16];
@@ -468,7 +373,7 @@ __global__ __launch_bounds__(kThreads, (MODE == kScanGen || FUSE) ? 3 : KLF_SCAN
   // wv is wave-uniform; readfirstlane tells the compiler so (tile indices stay in SGPRs and
   // the descriptor reads stay scalar loads)
   const int t = threadIdx.x, lane = t & 63, wv = __builtin_amdgcn_readfirstlane(t >> 6);
-  uint8_t* s_tile = s_tile_all[wv] + kFPad;
+  uint8_t* s_tile = s_tile_all[wv];
   uint32_t* s_list = s_list_all[wv];
   uint32_t* err_flag = a.counters + 2;
   for (uint32_t i = t; i < kMaxFusedLiteral / 4 + 1; i += kThreads)
@@ -504,27 +409,6 @@ __global__ __launch_bounds__(kThreads, (MODE == kScanGen || FUSE) ? 3 : KLF_SCAN
     return (x % kScanGroup) == kScanGroup - 1 ? x + 1 + kScanGroup * (nwaves - 1) : x + 1;
   };
   uint32_t tile = (blockIdx.x * kWaves + wv) * kScanGroup;
-  // fused: workgroup turns (4 consecutive tiles, tile 4 * turn + wave) claimed in order, the
-  // current one and the next (its tile prefetched) known at every iteration's start
-  const uint32_t nturns = (a.ntiles + kWaves - 1) / kWaves;
-  uint32_t cur = 0, nxt = 0;
-  if constexpr (FUSE) {
-    if (t == 0) {
-#if KLF_FSTATIC
-      s_fagg[0] = blockIdx.x;
-      s_fagg[1] = blockIdx.x + gridDim.x;
-#else
-      const uint32_t c0 = atomicAdd(&a.counters[kCtrTurn], 1u);
-      s_fagg[0] = c0;
-      s_fagg[1] = atomicAdd(&a.counters[kCtrTurn], 1u);
-#endif
-    }
-    __syncthreads();
-    cur = __builtin_amdgcn_readfirstlane((uint32_t)s_fagg[0]);
-    nxt = __builtin_amdgcn_readfirstlane((uint32_t)s_fagg[1]);
-    tile = cur * kWaves + wv;
-    __syncthreads();  // s_fagg is reused by the first turn
-  }
   uint4 stv = make_uint4(0, 0, 0, 0);  // GEN: lane k holds the group's TileStat k
   // The segment of the prefetched tile travels with it (scalar registers): a stride of
   // nwaves tiles stays inside one stream for all but the last tiles of a long stream, so
@@ -549,24 +433,7 @@ __global__ __launch_bounds__(kThreads, (MODE == kScanGen || FUSE) ? 3 : KLF_SCAN
     __builtin_amdgcn_raw_buffer_store_b32(0u, none, 0x7FFF0000u, 0, 0);
   }
   bool any_defer = false;
-#if KLF_FDIAG
-  uint64_t fd_scan = 0, fd_look = 0, fd_copy = 0, fd_t0 = 0;
-  uint32_t fd_rounds = 0, fd_spins = 0;
-#endif
-  for (;; tile = FUSE ? tile : next_tile(tile)) {  // (fused: the turn section moves on)
-    if (FUSE ? cur >= nturns : tile >= a.ntiles) break;
-#if KLF_FDIAG
-    fd_t0 = __builtin_readcyclecounter();
-#endif
-    // fused: the turn's aggregate of this tile (identity for a wave past the last tile)
-    FAgg fa{0u, 0u, -1, false, false};
-    bool f_ok = false;  // the line list can be read back for the copy
-    uint32_t f_nlines = 0;
-    const uint32_t* f_list = nullptr;
-    int32_t f_len = 0;
-    bool f_first = false, f_last = false;
-    uint32_t f_seg = 0;
-    if (!FUSE || tile < a.ntiles) {
+  for (; tile < a.ntiles; tile = next_tile(tile)) {
     const uint32_t s = pf_s;
     const SegDesc sd = pf_sd;
     const int64_t rel_lo = (int64_t)(tile - sd.tile0) * kTile;
@@ -581,9 +448,9 @@ __global__ __launch_bounds__(kThreads, (MODE == kScanGen || FUSE) ? 3 : KLF_SCAN
       uint4* l = reinterpret_cast<uint4*>(s_tile);
       KLF_ROWS(KLF_STORE)
       if (lane < kHalo / 16) l[kTile / 16 + lane] = pfh;
-      const uint32_t nx = FUSE ? nxt * kWaves + wv : next_tile(tile);
+      const uint32_t nx = next_tile(tile);
       if (nx < a.ntiles) {
-        if (FUSE || nx - sd.tile0 >= sd.ntiles) {
+        if (nx - sd.tile0 >= sd.ntiles) {
           pf_s = tseg[nx];
           pf_sd = segs[pf_s];
         }
@@ -715,16 +582,7 @@ __global__ __launch_bounds__(kThreads, (MODE == kScanGen || FUSE) ? 3 : KLF_SCAN
           } else if (rel_lo + (int64_t)off + 31 <= seg_len) {
             fast = parse_fast(s_tile, off, s_month, a.since_day, a.since_sod, a.since_nsec, so);
           }
-          if (FUSE && !fast) {  // fused: the general parse here (no k_tindex fix-up pass)
-            TsResult r;
-            uint32_t plen = 0;
-            const bool ok = parse_line_prefix(GlobalBytes{segp, rel_lo + (int64_t)off, seg_len}, r, plen);
-            const bool so2 = ok && !time_before(r.sec, r.nsec, a.since_sec, a.since_nsec);
-            if (ok && plen >= kPlenEscape) atomicOr(&a.counters[kCtrFuseBail], 1u);  // content start not in meta
-            list[j] = off | ((uint32_t)make_meta(ok, so2, plen) << 16);
-            n_parsed += ok ? 1u : 0u;
-            n_since += so2 ? 1u : 0u;
-          } else {
+          {
             list[j] = fast ? (off | ((uint32_t)make_meta(true, so, 31) << 16)) : (off | kSlotDefer);
             n_parsed += fast ? 1u : 0u;
             n_since += (fast && so) ? 1u : 0u;
@@ -1041,195 +899,23 @@ __global__ __launch_bounds__(kThreads, (MODE == kScanGen || FUSE) ? 3 : KLF_SCAN
         const u32x4v v = u ? u32x4v{sl.x, sl.y, sl.z, sl.w} : u32x4v{w0, w1, w2, w3};
         __builtin_amdgcn_raw_buffer_store_b128(v, rrs, 16u * u, 0, 0);
       }
-      // the group's TileStats, one 128-B store at its last tile (lanes past it dropped);
-      // fused: the tile's own (its turn's tiles belong to four waves)
-      const uint32_t gk = FUSE ? 0u : tile % kScanGroup, g0 = FUSE ? tile : tile - gk;
-      if (FUSE) {
-        if (lane == 0) stv = make_uint4(w0, w1, w2, w3);
-      } else if (GEN) {
+      // the group's TileStats, one 128-B store at its last tile (lanes past it dropped)
+      const uint32_t gk = tile % kScanGroup, g0 = tile - gk;
+      if (GEN) {
         if ((uint32_t)lane == gk) stv = make_uint4(w0, w1, w2, w3);
       } else {
         if (lane == 0) s_gstat[wv][gk] = make_uint4(w0, w1, w2, w3);
         wave_lds_sync();
       }
-      const bool gend = FUSE || gk == kScanGroup - 1 || tile + 1 >= a.ntiles;
-      const uint32_t ng = FUSE ? 1u : (a.ntiles - g0 < kScanGroup ? a.ntiles - g0 : kScanGroup);
+      const bool gend = gk == kScanGroup - 1 || tile + 1 >= a.ntiles;
+      const uint32_t ng = a.ntiles - g0 < kScanGroup ? a.ntiles - g0 : kScanGroup;
       const __amdgpu_buffer_rsrc_t srs =
           __builtin_amdgcn_make_buffer_rsrc(a.tstat + g0, 0, (gend && !abl) ? (int)(16u * ng) : 0, 0x00020000);
-      const uint4 gs = (GEN || FUSE) ? stv : s_gstat[GEN ? 0 : wv][lane & (kScanGroup - 1)];
+      const uint4 gs = GEN ? stv : s_gstat[GEN ? 0 : wv][lane & (kScanGroup - 1)];
       __builtin_amdgcn_raw_buffer_store_b128(u32x4v{gs.x, gs.y, gs.z, gs.w}, srs, 16u * (uint32_t)lane, 0, 0);
     }
-    if (FUSE) {  // this tile's aggregate from its line list (every line's meta is final here)
-      f_ok = pool_ok;
-      f_nlines = nlines;
-      f_list = dense ? gslot : s_list;
-      f_len = tile_len;
-      f_first = first;
-      f_last = last;
-      f_seg = s;
-      if (dense) __threadfence_block();
-      uint32_t kb = 0, lsel = 0;
-      int32_t lcrel = -1;
-      for (uint32_t b0 = 0; f_ok && b0 < nlines; b0 += 64) {
-        const uint32_t j = b0 + (uint32_t)lane;
-        if (j < nlines) {
-          const uint32_t v = f_list[j], mt = v >> 16;
-          const int32_t c = (int32_t)(v & kSlotOff) + (int32_t)(mt >> 2);  // content start (tile offset)
-          const int32_t e = j + 1 < nlines ? (int32_t)(f_list[j + 1] & kSlotOff) : tile_len;
-          const bool sel = (mt & Meta::kParsed) && (mt & Meta::kSince);
-          kb += (sel && e > c) ? (uint32_t)(e - c) : 0u;
-          if (j + 1 == nlines) { lsel = sel ? 1u : 0u; lcrel = f_sat(c - tile_len); }
-        }
-      }
-      fa.bytes = wave_sum(kb);
-      fa.has = nlines > 0;
-      const uint32_t lastlane = nlines ? (nlines - 1) & 63u : 0u;
-      fa.sel = __builtin_amdgcn_readlane((int)lsel, (int)lastlane) != 0;
-      fa.crel = __builtin_amdgcn_readlane(lcrel, (int)lastlane);
-      fa.span = nlines ? (f_ok ? (__builtin_amdgcn_readfirstlane(f_list[0]) & kSlotOff) : 0u) : (uint32_t)tile_len;
-      if (!nlines) { fa.sel = false; fa.crel = -1; }
-    }
     asm volatile("" ::: "memory");  // the next stage overwrites the LDS region read above
-    }  // this wave's tile
-    if (FUSE) {
-      // ---- the turn: combine the four tiles, publish, look back, copy ----
-      if (lane == 0) s_fagg[wv] = f_pack_a(fa);
-      __syncthreads();
-#if KLF_FDIAG
-      const uint64_t fd_t1 = __builtin_readcyclecounter();
-      fd_scan += fd_t1 - fd_t0;
-#endif
-      if (wv == 0) {
-        // the look-back by one wave: lane i reads turn hi - i, one round of loads covers 64
-        // turns.  (Measured on C3: a 512-turn window read by the whole workgroup made each
-        // round ~3x slower for half the rounds; one thread walking a turn per load, 2x
-        // slower.)
-        FAgg ta = f_unpack_a(s_fagg[0]);
-        for (int k = 1; k < kWaves; ++k) ta = f_combine(ta, f_unpack_a(s_fagg[k]));
-        FPre p{0ull, -1, false};
-        if (cur > 0) {
-          if (lane == 0) __hip_atomic_store(&a.fstate[cur], f_pack_a(ta), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          FAgg acc{0u, 0u, -1, false, false};  // the aggregates between the window and this turn
-          int64_t hi = (int64_t)cur - 1;
-          const uint64_t p0 = f_pack_p(FPre{0ull, -1, false});  // before turn 0: nothing out
-          for (uint32_t spins = 0;;) {
-            const int64_t q = hi - lane;
-            const uint64_t v = q >= 0 ? __hip_atomic_load(&a.fstate[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : p0;
-            const uint32_t st = (uint32_t)(v >> 62);
-            const uint64_t m2 = __ballot(st == 2u), m0 = __ballot(st == 0u);
-            const uint32_t pl = m2 ? (uint32_t)__builtin_ctzll(m2) : 64u;  // nearest prefix
-            const uint64_t below = pl >= 64u ? ~0ull : ((1ull << pl) - 1ull);
-            if (m0 & below) {  // a turn in between has not published: read the window again
-              if (++spins > (1u << 18)) {  // a turn never published: fail the run, never hang
-                if (lane == 0) atomicOr(&a.counters[kCtrFuseBail], 2u);
-                p = f_apply(p, acc);
-                break;
-              }
-#if KLF_FDIAG
-              ++fd_spins;
-#endif
-              __builtin_amdgcn_s_sleep(1);
-              continue;
-            }
-#if KLF_FDIAG
-            ++fd_rounds;
-#endif
-            // lanes [0, pl) in time order (lane pl - 1 earliest): a reduction toward lane 0
-            FAgg x = (uint32_t)lane < pl ? f_unpack_a(v) : FAgg{0u, 0u, -1, false, false};
-#pragma unroll
-            for (int d = 1; d < 64; d <<= 1) {
-              FAgg y;
-              y.bytes = (uint32_t)__shfl_down((int)x.bytes, d, 64);
-              y.span = (uint32_t)__shfl_down((int)x.span, d, 64);
-              y.crel = __shfl_down(x.crel, d, 64);
-              const int fl = __shfl_down((x.has ? 1 : 0) | (x.sel ? 2 : 0), d, 64);
-              y.has = fl & 1;
-              y.sel = (fl & 2) != 0;
-              if (lane + d < 64) x = f_combine(y, x);
-            }
-            FAgg w;
-            w.bytes = (uint32_t)__builtin_amdgcn_readfirstlane((int)x.bytes);
-            w.span = (uint32_t)__builtin_amdgcn_readfirstlane((int)x.span);
-            w.crel = __builtin_amdgcn_readfirstlane(x.crel);
-            w.has = __builtin_amdgcn_readfirstlane(x.has ? 1 : 0) != 0;
-            w.sel = __builtin_amdgcn_readfirstlane(x.sel ? 1 : 0) != 0;
-            acc = f_combine(w, acc);
-            if (pl < 64u) {
-              const uint64_t pv = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), (int)pl) << 32) |
-                                  (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, (int)pl);
-              p = f_apply(f_unpack_p(pv), acc);
-              break;
-            }
-            hi -= 64;
-          }
-        }
-        if (lane == 0) {
-          FPre pk = p;
-          for (int k = 0; k < kWaves; ++k) {
-            s_fpre[k] = pk;
-            pk = f_apply(pk, f_unpack_a(s_fagg[k]));
-          }
-          __hip_atomic_store(&a.fstate[cur], f_pack_p(pk), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#if KLF_FSTATIC
-          s_fturn = nxt + gridDim.x;
-#else
-          s_fturn = atomicAdd(&a.counters[kCtrTurn], 1u);
-#endif
-        }
-      }
-      __syncthreads();
-#if KLF_FDIAG
-      const uint64_t fd_t2 = __builtin_readcyclecounter();
-      fd_look += fd_t2 - fd_t1;
-#endif
-      if (tile < a.ntiles && f_ok) {  // the kept runs: the carried-in line's, then the lines'
-        const FPre pin = s_fpre[wv];
-        uint32_t* runs = s_frun[wv];
-        const uint32_t c0 = f_carried(fa.span, pin.sel, pin.crel);
-        const uint32_t lo0 = pin.crel > 0 ? (uint32_t)pin.crel : 0u;
-        if (lane == 0 && c0) runs[0] = lo0;  // dst 0
-        uint32_t nr = c0 ? 1u : 0u, dacc = c0;
-        for (uint32_t b0 = 0; b0 < f_nlines; b0 += 64) {
-          const uint32_t j = b0 + (uint32_t)lane;
-          uint32_t src = 0, len = 0;
-          if (j < f_nlines) {
-            const uint32_t v = f_list[j], mt = v >> 16;
-            const int32_t c = (int32_t)(v & kSlotOff) + (int32_t)(mt >> 2);
-            const int32_t e = j + 1 < f_nlines ? (int32_t)(f_list[j + 1] & kSlotOff) : f_len;
-            if ((mt & Meta::kParsed) && (mt & Meta::kSince) && e > c) { src = (uint32_t)c; len = (uint32_t)(e - c); }
-          }
-          const uint32_t incl = wave_incl_scan_add(len, lane);
-          const uint64_t bm = __ballot(len != 0);
-          if (len) runs[nr + (uint32_t)__popcll(bm & ((1ull << lane) - 1ull))] = src | ((dacc + incl - len) << 16);
-          nr += (uint32_t)__popcll(bm);
-          dacc += (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
-        }
-        wave_lds_sync();
-        if (lane == 0) {
-          if (f_first) a.segout[f_seg].out_lo = pin.off;
-          if (f_last) a.segout[f_seg].out_hi = pin.off + dacc;
-        }
-        if (dacc) copy_tile_runs(s_tile, runs, s_fmap[wv], nr, dacc, pin.off, a.out, lane);
-        asm volatile("" ::: "memory");  // the next tile rewrites the wave's LDS
-      }
-      cur = nxt;
-      nxt = __builtin_amdgcn_readfirstlane(s_fturn);
-      tile = cur * kWaves + wv;
-#if KLF_FDIAG
-      fd_copy += __builtin_readcyclecounter() - fd_t2;
-#endif
-    }
   }
-#if KLF_FDIAG
-  if (FUSE && lane == 0 && wv == 0) {  // cycles summed over workgroups (wave 0), in 2^10 units
-    atomicAdd(&a.counters[24], (uint32_t)(fd_scan >> 10));
-    atomicAdd(&a.counters[25], (uint32_t)(fd_look >> 10));
-    atomicAdd(&a.counters[26], (uint32_t)(fd_copy >> 10));
-    atomicAdd(&a.counters[27], fd_rounds);
-    atomicAdd(&a.counters[28], fd_spins);
-    atomicAdd(&a.counters[29], 1u);
-  }
-#endif
   if (any_defer && lane == 0 && !abl) a.counters[kCtrDefer] = 1u;
   if (KLF_ABL != 0 && lane == 0) atomicAdd(&g_abl_waves, 1u);
 #undef ABL
@@ -2332,7 +2018,6 @@ __device__ __forceinline__ void tail_body(RunArgs& a) {
   }
   if (a.tail < 0) {
     if (t == 0) { so.win_lo = lo; so.win_hi = hi; }
-    if (a.fused && t == 0) { so.sel_lo = 0; so.sel_hi = so.since_ok; }  // every since_ok line is out
     return;
   }
   const uint64_t n = (uint64_t)a.tail;
@@ -2424,8 +2109,6 @@ __global__ __launch_bounds__(256) void k_init(RunArgs a) {
   const uint32_t nw = a.nsegs * (uint32_t)(sizeof(SegOut) / 8);
   uint64_t* so = reinterpret_cast<uint64_t*>(a.segout);
   for (uint32_t k = i; k < nw; k += gridDim.x * 256) so[k] = 0;
-  if (a.fused)  // the fused scan's turn records: none published yet
-    for (uint32_t k = i; k < (a.ntiles + 3) / 4; k += gridDim.x * 256) a.fstate[k] = 0;
 }
 
 // ======================================================= K4: compaction + gather copy ==
@@ -3455,20 +3138,18 @@ size_t nfa_lds_bytes(const DevPatterns& P) {
   return 8ull * P.rx_count * (P.rx_classes + P.rx_maxpos + 4) + 256;
 }
 
-template <int MODE, int QS, int QK = 3, int QQ = 4, bool QA = false, bool FUSE = false>
+template <int MODE, int QS, int QK = 3, int QQ = 4, bool QA = false>
 hipError_t launch_scan(const RunArgs& a, hipStream_t st, int num_cus) {
   static int occ = 0;  // queried once per variant: the host query delays the launch
   if (occ == 0) {
-    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_scan<MODE, QS, QK, QQ, QA, FUSE>, kThreads, 0);
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_scan<MODE, QS, QK, QQ, QA>, kThreads, 0);
     occ = occ < 1 ? 1 : (occ > 8 ? 8 : occ);
     if (getenv("KLF_DIAG"))
-      fprintf(stderr, "[klf] k_scan<%d,%d,%d,%d,%d,%d>: %d blocks per CU\n", MODE, QS, QK, QQ, (int)QA, (int)FUSE, occ);
+      fprintf(stderr, "[klf] k_scan<%d,%d,%d,%d,%d>: %d blocks per CU\n", MODE, QS, QK, QQ, (int)QA, occ);
   }
   uint32_t grid = (uint32_t)(num_cus * occ);
-  // fused: a workgroup per turn of 4 tiles at most (the turns are claimed dynamically)
-  const uint32_t units = FUSE ? (a.ntiles + 3) / 4 : a.ntiles;
-  if (grid > units) grid = units;
-  hipLaunchKernelGGL((k_scan<MODE, QS, QK, QQ, QA, FUSE>), dim3(grid), dim3(kThreads), 0, st, a, a.tile_seg, a.segs);
+  if (grid > a.ntiles) grid = a.ntiles;
+  hipLaunchKernelGGL((k_scan<MODE, QS, QK, QQ, QA>), dim3(grid), dim3(kThreads), 0, st, a, a.tile_seg, a.segs);
   return hipGetLastError();
 }
 template <int QS, int QQ>
@@ -3492,7 +3173,6 @@ static hipError_t launch_tail_stage(const RunArgs& a, hipStream_t st, hipEvent_t
 hipError_t launch_pipeline(const RunArgs& a0, hipStream_t st, hipEvent_t* ev, int num_cus, hipStream_t aux,
                            hipEvent_t ev_fork, hipEvent_t ev_join, int phase) {
   RunArgs a = a0;
-  if (KLF_ABL != 0) a.fused = 0;  // timing builds ablate the scan: the two-pass compaction
   hipError_t e;
 #define KLF_TRY(x) do { e = (x); if (e != hipSuccess) return e; } while (0)
   if (phase != 2) {
@@ -3500,7 +3180,6 @@ hipError_t launch_pipeline(const RunArgs& a0, hipStream_t st, hipEvent_t* ev, in
   {
     const uint32_t nw = a.nsegs * (uint32_t)(sizeof(SegOut) / 8);
     uint32_t g = (nw + 255) / 256;
-    if (a.fused && g < (a.ntiles / 4 + 255) / 256) g = (a.ntiles / 4 + 255) / 256;
     g = g < 1 ? 1 : (g > 1024 ? 1024 : g);
     hipLaunchKernelGGL(k_init, dim3(g), dim3(256), 0, st, a);
     KLF_TRY(hipGetLastError());
@@ -3515,9 +3194,7 @@ hipError_t launch_pipeline(const RunArgs& a0, hipStream_t st, hipEvent_t* ev, in
   // scan's own time is then taken from ev[0] (k_init in front of it: ~2 us)
   if (ev && a.stage_times) KLF_TRY(hipEventRecord(ev[1], st));
   {
-    if (a.fused)
-      KLF_TRY((launch_scan<kScanPlain, 1, 3, 4, false, true>(a, st, num_cus)));
-    else if (a.grep_mode == kGrepLit1)
+    if (a.grep_mode == kGrepLit1)
       KLF_TRY((launch_scan<kScanLit, 1>(a, st, num_cus)));
     else if (a.grep_mode == kGrepGeneral && a.pats.qf_on && a.pats.qf_stride == 4)
       KLF_TRY((launch_gen<4>(a, st, num_cus)));
@@ -3617,7 +3294,6 @@ static hipError_t launch_tail_stage(const RunArgs& a, hipStream_t st, hipEvent_t
   hipLaunchKernelGGL(k_tailw, dim3(a.nsegs), dim3(256), 0, st, a);
   KLF_TRY(hipGetLastError());
   if (ev && a.stage_times) KLF_TRY(hipEventRecord(ev[4], st));  // ~5 us of idle GPU each
-  if (a.fused) return hipSuccess;  // the scan copied the output
   {
     const uint32_t gt = (a.ntiles + 4 * kTkBatch - 1) / (4 * kTkBatch);
     const uint32_t gp = (uint32_t)num_cus * 8;

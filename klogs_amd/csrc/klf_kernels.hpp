@@ -57,7 +57,6 @@ constexpr uint32_t kCopyChunkMinLog2 = 12;
 constexpr uint32_t kCopyChunksTarget = 1024;  // one resident generation of k_cmove workgroups (4 per CU)
 constexpr uint32_t kCtrChunkLog2 = 16;               // counters[16]: log2 of this run's copy chunk
 constexpr uint32_t kCtrTailDone = 18;                // counters[18]: k_tailw blocks done
-constexpr uint32_t kCtrFuseBailHost = 21;            // counters[21]: the fused scan bailed (= klf_kernels.hip kCtrFuseBail)
 constexpr uint32_t kCtrVerified = 10;                // counters[10]: hits k_verify walked (diagnostics)
 constexpr uint32_t kCtrDense = 14;                   // counters[14]: dense compaction (k_tkeep / k_tcopy)
 constexpr uint32_t kCtrOutShort = 22;                // counters[22]: the output did not fit out_cap
@@ -294,10 +293,6 @@ struct RunArgs {
   uint32_t compact_mode;  // 0 auto, 1 line gather (sparse), 2 tile copy (dense)
   // per-pattern counts (KLF_FILTER_PATTERN_COUNTS): pcount[segment * n_cids + cid] lines,
   // each (line, cid) counted once through the `pairs` hash set (open addressing, u64 keys)
-  // fused compaction (k_scan<plain, fused>, --tail -1 without patterns): the per-turn
-  // look-back records (zeroed by k_init); compaction kernels skipped
-  uint32_t fused;
-  uint64_t* fstate;  // [(ntiles + 3) / 4]
   uint32_t count_pats;
   uint32_t* pcount;
   uint64_t* pairs;
