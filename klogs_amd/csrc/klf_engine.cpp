@@ -168,9 +168,9 @@ struct klf_engine {
   bool stage_ev_pending = false;
   hipEvent_t ev[7] = {};
   klf::RunArgs last_args{};  // arguments of the latest completed run (klf_retail)
-  bool last_grouped = false; // that run went in groups (klf_retail: not supported)
-  bool grouped_layout = false; // d_tile_seg holds group-relative maps
-  DevBuf d_gsegs;            // group-relative segment descriptors
+  // the latest run's global line index is still to be built (lazy index, dense path): the
+  // k_scatter launch that builds it
+  std::vector<klf::RunArgs> index_pending;
   uint64_t last_gen = 0;     // gen of that run's result
 };
 
@@ -454,9 +454,17 @@ extern "C" int klf_open(const klf_config* cfg, klf_engine** out) {
   e->dpats.n_lits = e->cs.n_lits;
   hipError_t h = hipSetDevice(cfg->device);
   if (h != hipSuccess) { e->err = std::string("hipSetDevice: ") + hipGetErrorString(h); *out = e; return KLF_EHIP; }
+  const bool diag_open = getenv("KLF_DIAG") != nullptr;
+  auto open_mark = [&](const char* what) {
+    if (diag_open)
+      fprintf(stderr, "[klf] open: %s at %.1f us\n", what,
+              std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t_open0).count());
+  };
+  open_mark("device set");
   int ncu = 0;  // (one attribute query: hipGetDeviceProperties fills the whole struct, ~ms)
   if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, cfg->device) == hipSuccess && ncu > 0)
     e->num_cus = ncu;
+  open_mark("attribute");
   if (cfg->hip_stream) {
     e->stream = static_cast<hipStream_t>(cfg->hip_stream);
   } else {
@@ -464,6 +472,7 @@ extern "C" int klf_open(const klf_config* cfg, klf_engine** out) {
     if (h != hipSuccess) { e->err = "hipStreamCreate failed"; *out = e; return KLF_EHIP; }
     e->own_stream = true;
   }
+  open_mark(cfg->hip_stream ? "caller's stream" : "stream created");
   for (auto& x : e->ev) {
     h = hipEventCreate(&x);
     if (h != hipSuccess) { e->err = "hipEventCreate failed"; *out = e; return KLF_EHIP; }
@@ -965,6 +974,10 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
   if (want_truns) HIPCHK(e, e->d_truns.ensure(ntiles * klf::kRunSlots * 4), "alloc truns");
   HIPCHK(e, e->d_kbase.ensure(ntiles * 16), "alloc kbase");
   uint32_t compact_mode = 0;  // tests: force either compaction path
+  e->index_pending.clear();
+  // lazy line index (grep none, --tail -1; KLF_LAZY_INDEX=0 turns it off)
+  const bool lazy_index = mode == klf::CompiledSet::kNone && f->tail < 0 &&
+                          !(getenv("KLF_LAZY_INDEX") && !strcmp(getenv("KLF_LAZY_INDEX"), "0"));
   if (const char* v = getenv("KLF_COMPACT")) compact_mode = !strcmp(v, "sparse") ? 1u : !strcmp(v, "dense") ? 2u : 0u;
   // The output buffer: sized for the whole input up front when the run keeps about as much
   // as it reads (no --tail limit: C3-like), else grown
@@ -1058,196 +1071,12 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
     a.truns = want_truns ? e->d_truns.as<uint32_t>() : nullptr;
     a.kbase = e->d_kbase.as<uint64_t>();
     a.compact_mode = compact_mode;
+    a.lazy_index = lazy_index ? 1u : 0u;
     a.count_pats = count ? 1u : 0u;
     a.pcount = count ? e->d_pcount.as<uint32_t>() : nullptr;
     a.pairs = count ? e->d_pairs.as<uint64_t>() : nullptr;
     a.pairs_log2 = e->pairs_log2;
   };
-  // ---- grouped run (dense output over many streams: C3) ----
-  // The streams go in groups of about KLF_GROUP_MB (consecutive whole streams; each group a
-  // whole pipeline over its own slice of the workspace: tile arrays at its first tile, line
-  // arrays at a line base from the learned density, its own counters / block tables, its
-  // output at its input offset), launched back to back on two streams without event records.
-  // A small group's copy (k_tcopy) re-reads the bytes its scan streamed moments before,
-  // while they are still in the 256 MiB Infinity Cache, instead of from HBM.  Streams are
-  // independent (since / tail / grep are per stream), so a group is a batch of its own; the
-  // results keep global line indices (with gaps between groups) and absolute output ranges.
-  // Any overflow falls back to the ungrouped run below.
-  const uint64_t group_bytes = [] {
-    const char* v = getenv("KLF_GROUP_MB");
-    return v ? (uint64_t)std::max(0L, atol(v)) << 20 : (uint64_t)0;
-  }();
-  if (group_bytes && mode == klf::CompiledSet::kNone && f->tail < 0 && nsegs >= 2 &&
-      total_bytes >= 2 * group_bytes && e->line_density > 0.0 && !(f->flags & KLF_FILTER_STAGE_TIMES)) {
-    struct Group {
-      uint32_t s0, s1;         // segments [s0, s1)
-      uint32_t t0, nt;         // tiles
-      uint64_t bytes, cap, lbase, b_bsum, b_mpart, b_csum, b_cmap, b_cseg, cmc;
-      uint32_t mcb;
-    };
-    std::vector<Group> groups;
-    for (uint32_t i = 0; i < nsegs;) {
-      Group g{};
-      g.s0 = i;
-      g.t0 = segs[i].tile0;
-      while (i < nsegs && (i == g.s0 || g.bytes + segs[i].len <= group_bytes)) g.bytes += segs[i++].len;
-      g.s1 = i;
-      g.nt = segs[i - 1].tile0 + segs[i - 1].ntiles - g.t0;
-      groups.push_back(g);
-    }
-    const uint32_t ng = (uint32_t)groups.size();
-    uint64_t lines = 0, bsum = 0, mpart = 0, csum = 0, cmap = 0, cseg = 0;
-    for (auto& g : groups) {
-      g.cap = ((uint64_t)(e->line_density * (double)g.bytes * 1.25) + 2ull * (g.s1 - g.s0) + 4096 + 31) & ~31ull;
-      g.lbase = lines;
-      lines += g.cap + 64;  // (+ the group's stream-end entries of line_off and bitmap slack)
-      g.b_bsum = bsum;
-      bsum += 4ull * (g.nt / 1024 + 2);
-      g.mcb = (uint32_t)(g.cap / klf::kCompactLines + 2);
-      g.cmc = g.mcb + std::max<uint64_t>(g.bytes / klf::kCopyChunk, klf::kCopyChunksTarget) + 2;
-      g.b_mpart = mpart;
-      mpart += g.cap / klf::kMatchChunk + 2;
-      g.b_csum = csum;
-      csum += 3ull * (g.mcb + 1);
-      g.b_cmap = cmap;
-      cmap += g.cmc;
-      g.b_cseg = cseg;
-      cseg += g.mcb + 1;
-    }
-    const uint64_t gpool = std::max<uint64_t>(e->pool_cap / ng, 65536);
-    HIPCHK(e, e->d_line_off.ensure((lines + nsegs + 1) * 8), "alloc line_off");
-    HIPCHK(e, e->d_meta.ensure(lines * 2 + 16), "alloc meta");
-    HIPCHK(e, e->d_bits.ensure((lines / 32 + 1) * 4), "alloc bits");
-    HIPCHK(e, e->d_bsum.ensure(bsum * 8), "alloc bsum");
-    HIPCHK(e, e->d_mpart.ensure(mpart * 8), "alloc mpart");
-    HIPCHK(e, e->d_cstatus.ensure(csum * 8), "alloc csum");
-    HIPCHK(e, e->d_cmap.ensure(cmap * 4), "alloc cmap");
-    HIPCHK(e, e->d_cseg.ensure(cseg * 4), "alloc cseg");
-    HIPCHK(e, e->d_counters.ensure((size_t)klf::kNumCounters * 4 * ng), "alloc counters");
-    HIPCHK(e, e->d_wpre.ensure((nsegs + ng) * 8), "alloc wpre");
-    HIPCHK(e, e->d_pool.ensure(gpool * ng * 4), "alloc pool");
-    HIPCHK(e, e->d_gsegs.ensure(nsegs * sizeof(SegDesc)), "alloc group segs");
-    // outputs at their groups' input offsets: the buffer spans the batch, alignment gaps too
-    HIPCHK(e, e->d_out.ensure(segs[nsegs - 1].base + segs[nsegs - 1].len + 64), "alloc out");
-    std::vector<SegDesc> gsegs(segs);  // tile0 relative to the group's first tile
-    for (auto& g : groups)
-      for (uint32_t i = g.s0; i < g.s1; ++i) gsegs[i].tile0 -= g.t0;
-    HIPCHK(e, hipMemcpyAsync(e->d_gsegs.p, gsegs.data(), nsegs * sizeof(SegDesc), hipMemcpyHostToDevice, st),
-           "H2D group segs");
-    const bool build = !e->grouped_layout || e->last_segs.size() != segs.size() ||
-                       memcmp(e->last_segs.data(), segs.data(), segs.size() * sizeof(SegDesc)) != 0;  // group maps
-    mark("grouped workspace");
-    HIPCHK(e, hipEventRecord(e->ev[0], st), "event");
-    HIPCHK(e, hipEventRecord(e->ev_fork, st), "event");
-    HIPCHK(e, hipStreamWaitEvent(e->aux_stream, e->ev_fork, 0), "fork");
-    for (uint32_t gi = 0; gi < ng; ++gi) {
-      const Group& g = groups[gi];
-      klf::RunArgs a;
-      fill_args(a, 1);
-      a.segs = e->d_gsegs.as<SegDesc>() + g.s0;
-      a.nsegs = g.s1 - g.s0;
-      a.ntiles = g.nt;
-      a.tile_seg = e->d_tile_seg.as<uint32_t>() + g.t0;
-      a.build_tiles = build ? 1u : 0u;
-      a.tindex_wide = 0;
-      a.tstat = e->d_tstat.as<klf::TileStat>() + g.t0;
-      a.slots = e->d_slots.as<uint32_t>() + (size_t)g.t0 * klf::kRecStride;
-      a.tile_base = e->d_tile_base.as<uint64_t>() + g.t0;
-      a.trec = e->d_trec.as<klf::TRec>() + g.t0;
-      a.truns = want_truns ? e->d_truns.as<uint32_t>() + (size_t)g.t0 * klf::kRunSlots : nullptr;
-      a.kbase = e->d_kbase.as<uint64_t>() + 2ull * g.t0;
-      a.bsum = e->d_bsum.as<uint64_t>() + g.b_bsum;
-      a.counters = e->d_counters.as<uint32_t>() + (size_t)klf::kNumCounters * gi;
-      a.segout = e->d_segout.as<SegOut>() + g.s0;
-      a.wpre = e->d_wpre.as<uint64_t>() + g.s0 + gi;
-      a.pool = e->d_pool.as<uint32_t>() + gpool * gi;
-      a.pool_cap = gpool;
-      a.line_off = e->d_line_off.as<uint64_t>() + g.lbase + g.s0;
-      a.meta = e->d_meta.as<uint16_t>() + g.lbase;
-      a.bits = e->d_bits.as<uint32_t>() + g.lbase / 32;
-      a.cap_lines = g.cap;
-      a.mpart = e->d_mpart.as<uint64_t>() + g.b_mpart;
-      a.csum = e->d_cstatus.as<uint64_t>() + g.b_csum;
-      a.cmap = e->d_cmap.as<uint32_t>() + g.b_cmap;
-      a.cmap_cap = g.cmc;
-      a.cseg = e->d_cseg.as<uint32_t>() + g.b_cseg;
-      a.max_cblocks = g.mcb;
-      a.out = e->d_out.as<uint8_t>() + segs[g.s0].base;  // the group's output at its input offset
-      a.out_cap = (g.s1 < nsegs ? segs[g.s1].base : e->d_out.cap) - segs[g.s0].base;
-      hipStream_t gs = (gi & 1) ? e->aux_stream : st;
-      HIPCHK(e, klf::launch_pipeline(a, gs, nullptr, e->num_cus, nullptr, nullptr, nullptr), "launch group");
-    }
-    HIPCHK(e, hipEventRecord(e->ev_join, e->aux_stream), "event");
-    HIPCHK(e, hipStreamWaitEvent(st, e->ev_join, 0), "join");
-    HIPCHK(e, hipEventRecord(e->ev[5], st), "event");
-    HIPCHK(e, hipEventRecord(e->ev[6], st), "event");
-    std::vector<uint32_t> gctr((size_t)klf::kNumCounters * ng);
-    r->so.resize(nsegs);
-    HIPCHK(e, e->h_rb.ensure(gctr.size() * 4 + nsegs * sizeof(SegOut)), "alloc readback");
-    uint8_t* rb = e->h_rb.as<uint8_t>();
-    HIPCHK(e, hipMemcpyAsync(rb, e->d_counters.p, gctr.size() * 4, hipMemcpyDeviceToHost, st), "D2H counters");
-    HIPCHK(e, hipMemcpyAsync(rb + gctr.size() * 4, e->d_segout.p, nsegs * sizeof(SegOut), hipMemcpyDeviceToHost, st),
-           "D2H segout");
-    HIPCHK(e, wait_stream(st, 1000 + total_bytes / 2000000), "sync");
-    mark("grouped pipeline done");
-    memcpy(gctr.data(), rb, gctr.size() * 4);
-    memcpy(r->so.data(), rb + gctr.size() * 4, nsegs * sizeof(SegOut));
-    e->grouped_layout = true;
-    e->last_segs = segs;
-    bool bad = false;
-    for (uint32_t gi = 0; gi < ng; ++gi) {
-      const uint32_t* c = &gctr[(size_t)klf::kNumCounters * gi];
-      bad |= (c[2] != 0) || c[klf::kCtrOutShort] != 0;
-    }
-    if (!bad) {
-      uint64_t lmax = 0;
-      for (uint32_t gi = 0; gi < ng; ++gi) {
-        const Group& g = groups[gi];
-        for (uint32_t i = g.s0; i < g.s1; ++i) {  // group-relative -> batch-global
-          SegOut& so = r->so[i];
-          so.line_lo += g.lbase;
-          so.line_hi += g.lbase;
-          so.win_lo += g.lbase;
-          so.win_hi += g.lbase;
-          so.out_lo += segs[g.s0].base;
-          so.out_hi += segs[g.s0].base;
-          lmax = std::max(lmax, so.line_hi);
-        }
-      }
-      klf::RunArgs la;  // what klf_result_last_unparsed reads: the global meta
-      fill_args(la, 1);
-      la.meta = e->d_meta.as<uint16_t>();
-      la.line_off = e->d_line_off.as<uint64_t>();
-      la.bits = e->d_bits.as<uint32_t>();
-      la.cap_lines = lines;
-      e->last_args = la;
-      e->last_grouped = true;
-      e->last_gen = r->gen;
-      float ms;
-      if (hipEventElapsedTime(&ms, e->ev[0], e->ev[5]) == hipSuccess) r->ms[4] = r->ms[6] = ms;
-      r->total_lines = lmax;
-      for (auto& so : r->so) r->total_out = std::max(r->total_out, so.out_hi);
-      r->pcount_ok = true;
-      if (diag_marks) {
-        std::string m = "[klf] run marks (us):";
-        auto prev = t_run0;
-        for (auto& x : marks) {
-          m += std::string(" ") + x.first + " " +
-               std::to_string((int)std::chrono::duration<double, std::micro>(x.second - prev).count()) + ";";
-          prev = x.second;
-        }
-        fprintf(stderr, "%s (%u groups)\n", m.c_str(), ng);
-      }
-      *out = rp.release();
-      return KLF_OK;
-    }
-    if (diag_marks) fprintf(stderr, "[klf] grouped run overflowed: rerun ungrouped\n");
-  }
-  if (e->grouped_layout) {  // the tile map holds group-relative entries: rebuild it
-    e->grouped_layout = false;
-    same_layout = false;
-  }
-  e->last_grouped = false;
   bool overflow = false, pairs_over = false;
   for (int attempt = 0, line_reruns = 0, pair_reruns = 0; attempt < 4; ++attempt) {
     if (count) {
@@ -1365,6 +1194,7 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
       if (getenv("KLF_DIAG")) fprintf(stderr, "[klf] output buffer grown to %zu B\n", e->d_out.cap);
     }
     e->last_args = a;
+    if (a.lazy_index && counters[klf::kCtrDense]) e->index_pending.push_back(a);
     e->last_gen = r->gen;
     e->line_density = (double)(r->so[nsegs - 1].line_hi + 1) / (double)total_bytes;
     if (f->tail >= 0 && counters[klf::kCtrDense]) e->dense_tail_seen = true;
@@ -1421,11 +1251,13 @@ extern "C" int klf_run_device(klf_engine* e, const uint8_t* d_bytes, uint32_t n,
   return run_device_impl(e, d_bytes, n, seg_base, lens, f, out);
 }
 
+static int ensure_index(klf_engine* e);
+
 extern "C" int klf_retail(klf_engine* e, klf_result* prev, int64_t tail, klf_result** out) {
   if (!e || !prev || !out || prev->e != e || tail < -1) return KLF_EINVAL;
   *out = nullptr;
   if (prev->gen != e->gen || e->last_gen != prev->gen) return set_err(e, KLF_ESTATE, "klf_retail: not the latest run");
-  if (e->last_grouped) return set_err(e, KLF_ESTATE, "klf_retail: the latest run went in stream groups (KLF_GROUP_MB)");
+  if (int rc = ensure_index(e)) return rc;
   HIPCHK(e, hipSetDevice(e->device), "hipSetDevice");
   auto* r = new (std::nothrow) klf_result();
   if (!r) return KLF_ENOMEM;
@@ -1509,6 +1341,20 @@ extern "C" int klf_run(klf_engine* e, const klf_filter* f, klf_result** out) {
 static int check_result(klf_result* r, uint32_t id) {
   if (!r || id >= r->n_streams) return KLF_EINVAL;
   if (r->e->gen != r->gen) return KLF_ESTATE;  // workspace reused by a later run
+  return KLF_OK;
+}
+
+// The latest run's global line index, built now if that run left it out (lazy index).
+static int ensure_index(klf_engine* e) {
+  if (e->index_pending.empty()) return KLF_OK;
+  HIPCHK(e, hipSetDevice(e->device), "hipSetDevice");
+  for (auto& x : e->index_pending) {
+    x.lazy_index = 0;
+    HIPCHK(e, klf::launch_scatter(x, e->stream, e->num_cus), "launch line index");
+  }
+  HIPCHK(e, hipStreamSynchronize(e->stream), "sync line index");
+  e->index_pending.clear();
+  e->last_args.lazy_index = 0;
   return KLF_OK;
 }
 
@@ -1702,6 +1548,7 @@ extern "C" int klf_result_lines(klf_result* r, uint32_t id, const uint64_t** off
     return KLF_OK;
   }
   if (!r->have_lines) {
+    if (int rc2 = ensure_index(e)) return rc2;
     const size_t nwords = r->total_lines + r->so.size();
     r->line_off.resize(nwords);
     HIPCHK(e, hipMemcpyAsync(r->line_off.data(), e->d_line_off.p, nwords * 8, hipMemcpyDeviceToHost, e->stream), "D2H lines");
@@ -1719,6 +1566,7 @@ extern "C" int klf_result_match_bits(klf_result* r, uint32_t id, const uint8_t**
   if (!r->has_bits) return KLF_EINVAL;
   klf_engine* e = r->e;
   if (!r->have_bits) {
+    if (int rc2 = ensure_index(e)) return rc2;
     const size_t nw = r->total_lines / 32 + 1;
     r->bits.assign(nw, 0);
     if (!r->so.empty()) {
@@ -1783,6 +1631,7 @@ extern "C" int klf_result_last_unparsed(klf_result* r, uint32_t id, uint64_t* ra
   const SegOut& so = r->so[s];
   const uint64_t hi = so.line_hi - (so.frag ? 1 : 0);  // newline-terminated lines only
   if (hi <= so.line_lo) return KLF_OK;
+  if (int rc2 = ensure_index(e)) return rc2;
   HIPCHK(e, e->d_scratch.ensure(64), "alloc scratch");
   uint64_t v = 0;
   HIPCHK(e, klf::launch_lastbad(e->last_args, so.line_lo, hi, e->d_scratch.as<uint64_t>(), e->stream), "lastbad");

@@ -1246,6 +1246,10 @@ struct ScatterEnt {
 __global__ __launch_bounds__(256) void k_scatter(RunArgs a) {
   __shared__ ScatterEnt s_ent[4][kScatterGroup];
   __shared__ uint32_t s_pre[4][kScatterGroup];  // inclusive line-count prefix of the group's tiles
+  // lazy line index (grep none, --tail -1): launched after k_tailw, and only the line gather
+  // needs the index; the dense path lists lines from the slots (the host builds the index
+  // on demand: klf_result_lines, klf_retail, klf_result_last_unparsed)
+  if (a.lazy_index && a.counters[kCtrDense]) return;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   uint32_t* err_flag = a.counters + 2;
   const uint32_t ngroups = (a.ntiles + kScatterGroup - 1) / kScatterGroup;
@@ -2504,6 +2508,13 @@ __device__ __forceinline__ void cgather_body(RunArgs& a) {
 //             the wave); only the two chunks shared with the neighbouring tiles are stored
 //             bytewise.
 // Input read once, output written once, the line index read once.
+//
+// Runs without patterns (grep none) list the lines from the scan's own per-tile line slots
+// instead of the global line index (4 B per line instead of 18): line l0 + j of a tile is
+// its slot j - k0 (k0 = 1 when line l0 is carried in from an earlier tile), the carried-in
+// line's start and meta are the last slot of the nearest earlier tile of the stream that
+// lists one (the k_scatter rule), and a line ends where the next one starts.  With
+// --tail -1 the dense path then needs no line index at all (RunArgs::lazy_index).
 struct TileLines {
   uint32_t s;
   SegDesc sd;
@@ -2511,7 +2522,34 @@ struct TileLines {
   int32_t tlen;    // bytes of the stream in the tile
   uint64_t l0;     // global index of the tile's first line (the one holding its byte 0)
   uint32_t nl;     // lines holding bytes of the tile
+  // grep none: the tile's slots; the carried-in line's start (stream offset) and slot word
+  const uint32_t* sl;
+  uint32_t k0, cslot;
+  int64_t cstart;
 };
+__device__ __forceinline__ const uint32_t* tile_slot_list(const RunArgs& a, const TileStat& ts, uint32_t tile) {
+  return (ts.flags & 1u) ? a.pool + ts.pool_base : a.slots + (size_t)tile * kRecStride + kRecHead;
+}
+// (wave-uniform) the slot fields of g, grep-none runs only.  The stream's first tile lists
+// its line 0 at offset 0, so the walk back always ends at a tile with a slot.
+__device__ __forceinline__ void tile_slots(const RunArgs& a, const TileStat* __restrict__ tstat, TileLines& g,
+                                           uint32_t tile, const TileStat& ts) {
+  g.sl = tile_slot_list(a, ts, tile);
+  g.k0 = g.rel_lo == 0 ? 0u : 1u;
+  g.cstart = g.rel_lo;
+  g.cslot = 0;
+  for (uint32_t pt = tile; g.k0 && pt > g.sd.tile0;) {
+    --pt;
+    const TileStat pst = tstat[pt];
+    const int64_t prel = (int64_t)(pt - g.sd.tile0) * kTile;
+    const uint32_t pk0 = prel == 0 ? 0u : 1u;
+    const uint32_t pn = pst.events + 1 > pk0 ? pst.events + 1 - pk0 : 0u;  // never the stream's last tile
+    if (pn == 0) continue;
+    g.cslot = tile_slot_list(a, pst, pt)[pn - 1];
+    g.cstart = prel + (int64_t)(g.cslot & kSlotOff);
+    break;
+  }
+}
 __device__ __forceinline__ TileLines tile_lines(const RunArgs& a, uint32_t tile) {
   TileLines g;
   g.s = a.tile_seg[tile];
@@ -2522,6 +2560,7 @@ __device__ __forceinline__ TileLines tile_lines(const RunArgs& a, uint32_t tile)
   const TileStat ts = a.tstat[tile];
   g.l0 = a.tile_base[tile];
   g.nl = rem <= kTile ? ts.events : ts.events + 1;  // the stream's end closes the last line
+  if (a.grep_mode == kGrepNone) tile_slots(a, a.tstat, g, tile, ts);
   return g;
 }
 
@@ -2538,13 +2577,25 @@ struct LineRun {
   bool has, starts;   // non-empty run; a selected line starting in the tile
 };
 // Line l0 + j's data; l clamped into the index (lines past the tile are loaded but unused).
-__device__ __forceinline__ LineData load_line(const RunArgs& a, uint32_t s, uint64_t l) {
-  l = l < a.cap_lines ? l : a.cap_lines - 1;
+// Grep none: from the tile's slots (j clamped into the tile; the tile's last line is cut at
+// the tile end, all the run needs).
+__device__ __forceinline__ LineData load_line(const RunArgs& a, const TileLines& g, uint32_t j) {
   LineData d;
+  d.bw = ~0u;
+  if (a.grep_mode == kGrepNone) {
+    const uint32_t jj = j < g.nl ? j : (g.nl ? g.nl - 1 : 0u);
+    const uint32_t v = jj < g.k0 ? g.cslot : g.sl[jj - g.k0];
+    d.m = v >> 16;
+    d.s0 = jj < g.k0 ? (uint64_t)g.cstart : (uint64_t)(g.rel_lo + (int64_t)(v & kSlotOff));
+    d.le = (uint64_t)(g.rel_lo + (jj + 1 < g.nl ? (int64_t)(g.sl[jj + 1 - g.k0] & kSlotOff) : (int64_t)g.tlen));
+    return d;
+  }
+  uint64_t l = g.l0 + j;
+  l = l < a.cap_lines ? l : a.cap_lines - 1;
   d.m = a.meta[l];
-  d.s0 = a.line_off[l + s];
-  d.le = a.line_off[l + s + 1];
-  d.bw = a.grep_mode == kGrepNone ? ~0u : a.bits[l >> 5];
+  d.s0 = a.line_off[l + g.s];
+  d.le = a.line_off[l + g.s + 1];
+  d.bw = a.bits[l >> 5];
   return d;
 }
 __device__ __forceinline__ LineRun eval_line(const RunArgs& a, const TileLines& g, uint64_t wlo, uint64_t whi,
@@ -2554,7 +2605,9 @@ __device__ __forceinline__ LineRun eval_line(const RunArgs& a, const TileLines& 
   const bool sel = j < g.nl && l >= wlo && l < whi && (d.m & Meta::kParsed) && (d.m & Meta::kSince) &&
                    ((d.bw >> (l & 31)) & 1u);
   if (!sel) return r;
-  const uint64_t cs = d.s0 + line_plen(a, (uint16_t)d.m, a.bytes + g.sd.base, d.s0, d.le);
+  // (a selected line is parsed: its prefix ends at its first space, so the stream end
+  // bounds the search as well as the line end)
+  const uint64_t cs = d.s0 + line_plen(a, (uint16_t)d.m, a.bytes + g.sd.base, d.s0, g.sd.len);
   const int64_t lo = (int64_t)cs > g.rel_lo ? (int64_t)cs : g.rel_lo;
   const int64_t hi = (int64_t)d.le < g.rel_lo + g.tlen ? (int64_t)d.le : g.rel_lo + g.tlen;
   r.has = hi > lo;
@@ -2573,7 +2626,7 @@ __device__ __forceinline__ uint32_t list_runs(const RunArgs& a, const TileLines&
   uint32_t nr = 0, dacc = 0, ns = 0;
   for (uint32_t j0 = 0; j0 < g.nl; j0 += 64) {
     const uint32_t j = j0 + (uint32_t)lane;
-    const LineData d = (j0 == 0 && pre) ? *pre : load_line(a, g.s, g.l0 + j);
+    const LineData d = (j0 == 0 && pre) ? *pre : load_line(a, g, j);
     const LineRun r = eval_line(a, g, wlo, whi, j, d);
     const uint32_t incl = wave_incl_scan_add(r.len, lane);
     const uint64_t bm = __ballot(r.has);
@@ -2616,9 +2669,10 @@ __device__ __forceinline__ void tkeep_body(RunArgs& a, const uint32_t* __restric
       const int64_t rem = (int64_t)g[u].sd.len - g[u].rel_lo;
       g[u].tlen = (int32_t)(rem < kTile ? rem : kTile);
       g[u].l0 = tbase[tile];
-      const uint32_t ev = tstat[tile].events;
-      g[u].nl = rem <= kTile ? ev : ev + 1;
-      pre[u] = load_line(a, g[u].s, g[u].l0 + (uint64_t)lane);
+      const TileStat ts = tstat[tile];
+      g[u].nl = rem <= kTile ? ts.events : ts.events + 1;
+      if (a.grep_mode == kGrepNone) tile_slots(a, tstat, g[u], tile, ts);
+      pre[u] = load_line(a, g[u], (uint32_t)lane);
     }
 #pragma unroll
     for (int u = 0; u < kTkBatch; ++u) {
@@ -3170,6 +3224,17 @@ hipError_t launch_gen(const RunArgs& a, hipStream_t st, int num_cus) {
 
 static hipError_t launch_tail_stage(const RunArgs& a, hipStream_t st, hipEvent_t* ev, int num_cus);
 
+hipError_t launch_scatter(const RunArgs& a, hipStream_t st, int num_cus) {
+#ifndef KLF_SCATTER_GRID
+#define KLF_SCATTER_GRID 8  // k_scatter workgroups per CU at most
+#endif
+  uint32_t sg = ((a.ntiles + kScatterGroup - 1) / kScatterGroup + 3) / 4;
+  if (sg > (uint32_t)num_cus * KLF_SCATTER_GRID) sg = num_cus * KLF_SCATTER_GRID;
+  if (sg == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_scatter, dim3(sg), dim3(256), 0, st, a);
+  return hipGetLastError();
+}
+
 hipError_t launch_pipeline(const RunArgs& a0, hipStream_t st, hipEvent_t* ev, int num_cus, hipStream_t aux,
                            hipEvent_t ev_fork, hipEvent_t ev_join, int phase) {
   RunArgs a = a0;
@@ -3221,11 +3286,6 @@ hipError_t launch_pipeline(const RunArgs& a0, hipStream_t st, hipEvent_t* ev, in
   }
   if (phase == 1) return hipSuccess;
   }  // phase != 2
-  uint32_t sg = ((a.ntiles + kScatterGroup - 1) / kScatterGroup + 3) / 4;
-#ifndef KLF_SCATTER_GRID
-#define KLF_SCATTER_GRID 8  // k_scatter workgroups per CU at most
-#endif
-  if (sg > (uint32_t)num_cus * KLF_SCATTER_GRID) sg = num_cus * KLF_SCATTER_GRID;
   // With a prefiltered regex set, k_scatter (bandwidth-bound) runs on the side stream
   // beside k_verify (latency-bound: a chain of dependent loads per hit), which reads the
   // line slots, not the global line index; the main stream waits for it before the first
@@ -3236,12 +3296,10 @@ hipError_t launch_pipeline(const RunArgs& a0, hipStream_t st, hipEvent_t* ev, in
   if (fork) {
     KLF_TRY(hipEventRecord(ev_fork, st));
     KLF_TRY(hipStreamWaitEvent(aux, ev_fork, 0));
-    hipLaunchKernelGGL(k_scatter, dim3(sg), dim3(256), 0, aux, a);
-    KLF_TRY(hipGetLastError());
+    KLF_TRY(launch_scatter(a, aux, num_cus));
     KLF_TRY(hipEventRecord(ev_join, aux));
-  } else {
-    hipLaunchKernelGGL(k_scatter, dim3(sg), dim3(256), 0, st, a);
-    KLF_TRY(hipGetLastError());
+  } else if (!a.lazy_index) {
+    KLF_TRY(launch_scatter(a, st, num_cus));
   }
   if (ev && a.stage_times && !fork) KLF_TRY(hipEventRecord(ev[2], st));  // ~5 us of idle GPU each
   if (a.grep_mode == kGrepGeneral && a.pats.qf_on) {
@@ -3293,6 +3351,7 @@ static hipError_t launch_tail_stage(const RunArgs& a, hipStream_t st, hipEvent_t
   }
   hipLaunchKernelGGL(k_tailw, dim3(a.nsegs), dim3(256), 0, st, a);
   KLF_TRY(hipGetLastError());
+  if (a.lazy_index) KLF_TRY(launch_scatter(a, st, num_cus));  // (exits at once on the dense path)
   if (ev && a.stage_times) KLF_TRY(hipEventRecord(ev[4], st));  // ~5 us of idle GPU each
   {
     const uint32_t gt = (a.ntiles + 4 * kTkBatch - 1) / (4 * kTkBatch);

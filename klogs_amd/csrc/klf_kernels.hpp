@@ -291,6 +291,9 @@ struct RunArgs {
   uint32_t* truns;      // [ntiles * kRunSlots] the tiles' kept runs (k_tkeep -> k_tcopy)
   uint64_t* kbase;      // [2 * ntiles]
   uint32_t compact_mode;  // 0 auto, 1 line gather (sparse), 2 tile copy (dense)
+  // grep none with --tail -1: k_scatter goes after k_tailw and builds the global line index
+  // only for the line gather; the dense path lists its lines from the scan's slots
+  uint32_t lazy_index;
   // per-pattern counts (KLF_FILTER_PATTERN_COUNTS): pcount[segment * n_cids + cid] lines,
   // each (line, cid) counted once through the `pairs` hash set (open addressing, u64 keys)
   uint32_t count_pats;
@@ -304,10 +307,12 @@ struct RunArgs {
 // scan, ev[3] after the general matcher, ev[4] after counts+tail+window prefix, ev[5]
 // after compaction.  Returns a hipError_t.
 // aux (may be null) with the fork / join events: a side stream for k_scatter beside k_verify.
-// ev may be null: no event records (the grouped runs of the engine time the whole batch).
+// ev may be null: no event records.
 // phase: 0 the whole pipeline; 1 up to the tile index (k_init .. k_tindex: the line arrays
 // are not touched, a.bits may be null); 2 the rest (k_scatter on), after the host sized
 // the line arrays from phase 1's line count (an engine's first run).
+// k_scatter alone: the global line index of a run (an engine's lazy index, on demand).
+hipError_t launch_scatter(const RunArgs& a, hipStream_t stream, int num_cus);
 hipError_t launch_pipeline(const RunArgs& a, hipStream_t stream, hipEvent_t* ev, int num_cus, hipStream_t aux,
                            hipEvent_t ev_fork, hipEvent_t ev_join, int phase = 0);
 // Re-runs matched counts, tail and compaction of the last pipeline with a.tail changed.

@@ -185,47 +185,57 @@ def test_output_buffer_grown_on_demand(gpu, compact, tails, monkeypatch):
         r.free()
 
 
-@pytest.mark.parametrize("since", [None, SINCE])
-def test_grouped_runs_equal_oracle(gpu, monkeypatch, since):
-    """Stream groups (KLF_GROUP_MB: each group of consecutive whole streams a pipeline over
-    its own workspace slice, two launch streams; C3's dense copy re-reads from the Infinity
-    Cache): an engine's second and later -l runs go grouped and must equal the C oracle in
-    output bytes, counts and line offsets (with empty streams, fragments and dense tiles among
-    them), as must klf_result_last_unparsed; klf_retail refuses a grouped result."""
-    monkeypatch.setenv("KLF_GROUP_MB", "1")
-    streams = []
-    for i in range(23):
-        k = i % 5
-        if k == 0:
-            streams.append(b"")
-        elif k == 1:
-            streams.append(synth.generate(synth.TEXT, 90 + i, i, 400_000 + 7_919 * i))
-        elif k == 2:
-            streams.append(synth.generate(synth.ADVERSARIAL, 90 + i, i, 150_000, drop_final_nl=True, permille=40))
-        elif k == 3:
-            streams.append(synth.generate(synth.LONGJSON, 90 + i, i, 900_000, permille=5))
-        else:
-            streams.append(synth.generate(synth.TEXT, 90 + i, i, 1_300_000))
+def test_long_timestamp_prefix(gpu, compact):
+    """Go's RFC3339Nano parse takes any number of fraction digits: a prefix past the meta
+    word's 14-bit content offset (kPlenEscape) is found again from the bytes, also for a line
+    that spans tiles and one carried into the next tile."""
+    base = synth.generate(synth.TEXT, 51, 0, 20_000)
+    frac = b"1" * 20_000
+    streams = [base + b"2024-10-22T00:59:59." + frac + b"Z long prefix\n" + base,
+               b"2024-10-22T00:59:59." + frac[:9000] + b"Z x\n" + base + b"2024-10-22T00:00:01." + frac + b"Z",
+               base[:5000] + b"2024-10-22T00:59:59." + frac[:8170] + b"Z tile edge\n"]
+    for since, tail in [(None, -1), (SINCE, -1), (None, 2)]:
+        check_against_c(streams, since, tail, [])
+    check_against_c(streams, None, -1, [b"prefix"])
+
+
+@pytest.mark.parametrize("lazy", ["1", "0"])
+def test_lazy_line_index(gpu, monkeypatch, lazy):
+    """Runs without patterns and --tail -1 leave the global line index out when the dense
+    path copies (its runs come from the scan's line slots); the index is built on demand by
+    klf_result_lines / klf_retail / klf_result_last_unparsed.  Either way (KLF_LAZY_INDEX=0:
+    always built) outputs, line offsets, re-tails and the last unparsed line equal the C
+    oracle, over deferred (non-canonical) prefixes, long lines carried across tiles, dense
+    tiles, fragments and empty streams."""
+    monkeypatch.setenv("KLF_LAZY_INDEX", lazy)
+    streams = [synth.generate(synth.ADVERSARIAL, 5, 0, 120_000, drop_final_nl=True, permille=40),
+               synth.generate(synth.LONGJSON, 6, 1, 700_000, permille=5), b"",
+               b"".join(b"2024-10-22T00:00:%02dZ %d\n" % (i % 60, i) for i in range(20000)),
+               synth.generate(synth.TEXT, 7, 4, 300_000)]
     from test_shard import _last_unparsed
-    with E.Engine(0) as eng:
-        for rep in range(3):  # the first run learns the line density (ungrouped), then grouped
+    with E.Engine(0, grep=[]) as eng:
+        for since in (None, SINCE):
             eng.reset()
             eng.set_streams(len(streams))
             for i, s in enumerate(streams):
                 if s:
                     eng.stage(i, s)
             r = eng.run(since=since, n_streams=len(streams))
+            want = [co.filter_stream(s, since or co.GO_ZERO_TIME, -1, []) for s in streams]
             for i, s in enumerate(streams):
-                out, lo, _, c = co.filter_stream(s, since or co.GO_ZERO_TIME, -1, [])
-                so = r.stream(i)
-                assert so.out == out, (rep, i)
-                assert np.array_equal(r.lines(i), lo), (rep, i)
-                for k in ("lines", "parsed", "since_ok", "selected", "out_bytes"):
-                    assert so.counts[k] == c[k], (rep, i, k)
-                if s and rep == 2:
-                    assert r.last_unparsed(i) == _last_unparsed(s), i
-            if rep == 2:
-                with pytest.raises(E.KlfError) as ei:
-                    r.retail(5)
-                assert ei.value.code == E.KLF_ESTATE
+                assert r.stream(i).out == want[i][0], i
+                assert r.stream(i).counts["selected"] == want[i][3]["selected"], i
+            if since is None:  # the index built by klf_retail first, then read
+                r2 = r.retail(7)
+                r.free()
+                r = r2
+                for i, s in enumerate(streams):
+                    out, lo, _, _ = co.filter_stream(s, co.GO_ZERO_TIME, 7, [])
+                    assert r.stream(i).out == out, i
+                    assert np.array_equal(r.lines(i), lo), i
+            else:  # built by klf_result_last_unparsed, then by klf_result_lines (no-op)
+                for i, s in enumerate(streams):
+                    if s:
+                        assert r.last_unparsed(i) == _last_unparsed(s), i
+                    assert np.array_equal(r.lines(i), want[i][1]), i
             r.free()
