@@ -943,6 +943,9 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
       ds.bytes[c] = hv[2 * klf::kQfHistBins + c];
       ds.nbytes += ds.bytes[c];
     }
+    ds.pair.assign(hv + klf::kGramHistPairs, hv + klf::kGramHistPairs + 65536);
+    for (auto& c : ds.pair) c *= 2;  // counted at every 2nd position
+    klf::stats_finish(ds);
     if (ds.nbytes) est_density = (double)(ds.bytes['\n'] + 1) / (double)ds.nbytes;
     klf::place_needles(e->cs, &ds);
     const auto t_place = std::chrono::steady_clock::now();

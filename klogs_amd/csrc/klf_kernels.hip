@@ -3101,6 +3101,8 @@ __global__ __launch_bounds__(256) void k_gramhist(const uint8_t* bytes, const Se
     atomicAdd(&hist[qf_hist_bin1(g3)], 1u);
     atomicAdd(&hist[kQfHistBins + qf_hist_bin0(g)], 1u);
     atomicAdd(&hist[kQfHistBins + qf_hist_bin1(g)], 1u);
+    atomicAdd(&hist[kGramHistPairs + (g & 0xFFFFu)], 1u);  // the 2-grams at even offsets
+    atomicAdd(&hist[kGramHistPairs + (g >> 16)], 1u);
 #pragma unroll
     for (int k = 0; k < 4; ++k) atomicAdd(&s_b[(w0 >> (8 * k)) & 0xFFu], 1u);
   }

@@ -127,10 +127,12 @@ __host__ __device__ inline bool qf_pass(const uint32_t* bm, uint32_t gq, uint32_
   return (bm[qf_bloom_word(gq, w24, k)] & bits) == bits;
 }
 // Gram statistics of the window choice: a count-min sketch, 2 rows of 2^16 bins, for the
-// 3-byte and for the 4-byte grams, then a byte histogram (k_gramhist)
+// 3-byte and for the 4-byte grams, then a byte histogram, then the exact 2-gram counts at
+// even positions (k_gramhist)
 constexpr int kQfHistBits = 16;
 constexpr uint32_t kQfHistBins = 2u << kQfHistBits;
-constexpr uint32_t kGramHistWords = 2 * kQfHistBins + 256;
+constexpr uint32_t kGramHistPairs = 2 * kQfHistBins + 256;  // first word of the 2-gram counts
+constexpr uint32_t kGramHistWords = kGramHistPairs + 65536;
 constexpr uint64_t kGramHistSample = 64u << 10;  // bytes sampled per segment (<= 16 segments)
 // grams counted at every kGramHistStride-th position of the sample (the host scales the
 // counts back): a quarter of the global atomics, which bound the one-off pass

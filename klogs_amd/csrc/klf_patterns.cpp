@@ -1316,11 +1316,6 @@ void choose_layout(CompiledSet& out, const DataStats* st, bool allow_anchor, uin
 // verification) at ~40.  Hits per tile = samples per tile x the summed data share of the
 // sampled grams, plus the anchors whose dword passes a pre-check.
 double layout_cost(const CompiledSet& c, const DataStats& st) {
-  const double nb = st.nbytes ? (double)st.nbytes : 1.0;
-  const std::vector<uint32_t>& sk = c.qf_q == 3 ? st.gram3 : st.gram4;
-  auto share = [&](const std::vector<uint32_t>& h, uint32_t g) {
-    return std::min(h[qf_hist_bin0(g)], h[qf_hist_bin1(g)]) / nb;
-  };
   std::vector<uint32_t> grams;
   grams.reserve(c.qf_ent.size() / 4);
   for (size_t e = 0; e + 3 < c.qf_ent.size(); e += 4) {  // the probed grams, read back from the needles
@@ -1334,7 +1329,7 @@ double layout_cost(const CompiledSet& c, const DataStats& st) {
   std::sort(grams.begin(), grams.end());
   grams.erase(std::unique(grams.begin(), grams.end()), grams.end());
   double hit_share = 0;  // probed grams (the anchored ones only reach a bucket through an anchor)
-  for (uint32_t g : grams) hit_share += share(sk, g);
+  for (uint32_t g : grams) hit_share += gram_share(st, g, c.qf_q);
   const double samples = 8192.0 / c.qf_stride;
   double hits = samples * std::min(1.0, hit_share);
   // VALU per probe (the scan's ISA, its unrolled fast pass / 32 probes): 6.9 for a 3-byte
@@ -1348,7 +1343,8 @@ double layout_cost(const CompiledSet& c, const DataStats& st) {
     cost += 60.0;
     double pass = 0;
     for (size_t j = 0; j + 1 < c.qf_anc_pre.size(); j += 2)
-      pass += c.qf_anc_pre[j + 1] == ~0u ? share(st.gram4, c.qf_anc_pre[j]) : share(st.gram3, c.qf_anc_pre[j] & 0xFFFFFFu);
+      pass += c.qf_anc_pre[j + 1] == ~0u ? gram_share(st, c.qf_anc_pre[j], 4)
+                                         : gram_share(st, c.qf_anc_pre[j] & 0xFFFFFFu, 3);
     hits += 8192.0 * std::min(1.0, pass);
   }
   return cost + 40.0 * hits;
@@ -1445,6 +1441,12 @@ void place_tables(CompiledSet& out, const DataStats* st) {
   const uint32_t q = out.qf_q, S = out.qf_stride;
   const std::vector<uint32_t>* hist = st ? (q == 3 ? &st->gram3 : &st->gram4) : nullptr;
   if (hist && hist->size() < kQfHistBins) hist = nullptr;
+  const double nsample = st && st->nbytes ? (double)st->nbytes : 1.0;
+  // a window's score: the summed shares of its S grams (one of them is sampled per
+  // occurrence), plus, under the two-level probe, a twentieth of each gram's leading pair
+  // share (the pair stage passes those samples to the hashed Bloom word, whose false
+  // positives they then risk)
+  static const double pair_w = getenv("KLF_QF_PAIRW") ? atof(getenv("KLF_QF_PAIRW")) : 0.05;
   const bool loose = out.qf_fold != 0;
   out.qf_bitmap.assign(kQfWords, 0u);
   out.qf_head.clear();
@@ -1492,12 +1494,15 @@ void place_tables(CompiledSet& out, const DataStats* st) {
         const uint64_t u = it == used.end() ? 0 : (uint64_t)it->second;
         uint64_t c;
         if (hist) {
-          c = ((uint64_t)std::min((*hist)[qf_hist_bin0(g)], (*hist)[qf_hist_bin1(g)]) << 8) + 2 * u;
+          double sh = gram_share(*st, g, q);
+          if (pair_w > 0 && out.qf_k == kQfTwoLevel && st->pair_tot > 0)  // the pair stage's survivors
+            sh += pair_w * (st->pair[g & 0xFFFFu] + 0.5) / st->pair_tot;
+          c = (uint64_t)(sh * nsample * 256.0) + 2 * u;
         } else {
           c = 2 * u;
           for (uint32_t b = 0; b < q; ++b) c += common((uint8_t)s[a + j + b]);
         }
-        sc = std::max(sc, c);
+        sc = hist ? sc + c : std::max(sc, c);
       }
       if (sc < best) { best = sc; best_a = a; }
     }
@@ -1540,9 +1545,36 @@ void place_tables(CompiledSet& out, const DataStats* st) {
 
 }  // namespace
 
+void stats_finish(DataStats& st) {
+  st.marg.assign(256, 0.0);
+  st.pair_tot = 0;
+  if (st.pair.size() >= 65536) {
+    for (uint32_t x = 0; x < 65536; ++x) st.marg[x & 0xFFu] += st.pair[x];
+    for (double m : st.marg) st.pair_tot += m;
+  }
+}
+
+double gram_share(const DataStats& st, uint32_t g, uint32_t q) {
+  const double nb = st.nbytes ? (double)st.nbytes : 1.0;
+  const std::vector<uint32_t>& sk = q == 3 ? st.gram3 : st.gram4;
+  const double sketch = sk.size() >= kQfHistBins ? std::min(sk[qf_hist_bin0(g)], sk[qf_hist_bin1(g)]) / nb : 1.0;
+  static const bool use_sketch = getenv("KLF_QF_EST") && !strcmp(getenv("KLF_QF_EST"), "sketch");  // A/B
+  if (use_sketch || st.pair.size() < 65536 || st.marg.size() != 256 || st.pair_tot <= 0) return sketch;
+  // P(b0 b1) * prod P(b_i b_i+1) / P(b_i): pair counts + 1/2, marginals from the pairs
+  const double tot = st.pair_tot;
+  auto pr = [&](uint32_t a, uint32_t b) { return (st.pair[a | b << 8] + 0.5) / tot; };
+  double p = pr(g & 0xFFu, (g >> 8) & 0xFFu);
+  for (uint32_t i = 1; i + 1 < q; ++i) {
+    const uint32_t a = (g >> (8 * i)) & 0xFFu, b = (g >> (8 * i + 8)) & 0xFFu;
+    p *= pr(a, b) / ((st.marg[a] + 128.0) / tot);
+  }
+  return p;
+}
+
 void data_stats(const uint8_t* p, size_t n, uint32_t fold, DataStats& st) {
   st.gram3.assign(kQfHistBins, 0u);
   st.gram4.assign(kQfHistBins, 0u);
+  st.pair.assign(65536, 0u);
   st.bytes.assign(256, 0u);
   st.nbytes = 0;
   for (size_t i = 0; i + 4 <= n; ++i) {
@@ -1552,12 +1584,15 @@ void data_stats(const uint8_t* p, size_t n, uint32_t fold, DataStats& st) {
     uint32_t g = 0;
     for (int b = 0; b < 4; ++b) g |= (uint32_t)p[i + b] << (8 * b);
     g |= fold;
+    st.pair[g & 0xFFFFu] += 2;  // the 2-grams at even positions (k_gramhist), counted twice
+    st.pair[g >> 16] += 2;
     const uint32_t g3 = g & 0xFFFFFFu;
     st.gram3[qf_hist_bin0(g3)] += kGramHistStride;
     st.gram3[qf_hist_bin1(g3)] += kGramHistStride;
     st.gram4[qf_hist_bin0(g)] += kGramHistStride;
     st.gram4[qf_hist_bin1(g)] += kGramHistStride;
   }
+  stats_finish(st);
 }
 
 PrefilterHits prefilter_hits(const CompiledSet& cs, const uint8_t* s, size_t n) {

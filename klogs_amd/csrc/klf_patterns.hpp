@@ -130,12 +130,24 @@ struct CompiledSet {
 };
 
 // Statistics of a data sample (k_gramhist, first batch): count-min sketches of the 3- and
-// 4-byte grams (kQfHistBins bins each, needles' fold applied) and the byte histogram.
+// 4-byte grams (kQfHistBins bins each, needles' fold applied), the exact 2-gram counts
+// (fold applied, at even positions) and the byte histogram.
 struct DataStats {
   std::vector<uint32_t> gram3, gram4;
+  std::vector<uint32_t> pair;   // [65536] 2-gram b0 | b1 << 8 (empty: none)
   std::vector<uint64_t> bytes;  // [256]
   uint64_t nbytes = 0;          // positions counted in `bytes`
+  // derived by stats_finish: 2-gram marginals and their total
+  std::vector<double> marg;
+  double pair_tot = 0;
 };
+// The derived fields, once the counts are in.
+void stats_finish(DataStats& st);
+// Estimated share of the data's positions that hold gram g (q bytes, folded): a
+// first-order Markov chain over the exact 2-gram counts, which resolves shares far below
+// one per sample where the count-min sketches only see their collision noise (those
+// remain for KLF_QF_EST=sketch, and for statistics without 2-gram counts).
+double gram_share(const DataStats& st, uint32_t g, uint32_t q);
 constexpr uint32_t kQfAncPreMax = 8;  // distinct short-needle pre-check dwords
 
 // Required literal factors of one regex (Go syntax, SPEC.md S5): every match contains
