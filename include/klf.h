@@ -68,7 +68,7 @@ typedef struct klf_config {
   int32_t device;          /* HIP device ordinal (one process per GPU)                 */
   uint32_t n_patterns;     /* OR'ed; 0 = no grep stage                                 */
   const klf_pattern* patterns;
-  void* hip_stream;        /* hipStream_t to launch on; NULL = engine-owned stream      */
+  void* hip_stream;        /* hipStream_t to launch on; NULL = HIP's null stream        */
   uint64_t staging_hint;   /* expected total staged bytes (pre-reserve), 0 = none       */
 } klf_config;
 

@@ -89,7 +89,6 @@ uint64_t align_up(uint64_t x, uint64_t a) { return (x + a - 1) / a * a; }
 struct klf_engine {
   int device = 0;
   hipStream_t stream = nullptr;
-  bool own_stream = false;
   int num_cus = 256;
   klf::CompiledSet cs;
   std::string err;
@@ -129,6 +128,7 @@ struct klf_engine {
   std::unique_ptr<klf::CopyPool> copier;  // started by the first klf_stage (device-resident runs never stage)
   std::once_flag copier_once;
   std::once_flag copy_stream_once;     // the copy stream: created by the first klf_stage / klf_run
+  uint64_t runs = 0;                   // completed runs (the first one launches without aux_stream)
   std::once_flag aux_once;             // the side stream + fork / join events: the first run
   hipError_t aux_err = hipSuccess;
   hipError_t copy_stream_err = hipSuccess;
@@ -465,14 +465,11 @@ extern "C" int klf_open(const klf_config* cfg, klf_engine** out) {
   if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, cfg->device) == hipSuccess && ncu > 0)
     e->num_cus = ncu;
   open_mark("attribute");
-  if (cfg->hip_stream) {
-    e->stream = static_cast<hipStream_t>(cfg->hip_stream);
-  } else {
-    h = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking);
-    if (h != hipSuccess) { e->err = "hipStreamCreate failed"; *out = e; return KLF_EHIP; }
-    e->own_stream = true;
-  }
-  open_mark(cfg->hip_stream ? "caller's stream" : "stream created");
+  // the caller's stream, else HIP's null stream: it exists from device init, while a new
+  // stream costs ~5 ms of host time when it brings up a hardware queue (MI355X), which a
+  // one-shot klogs invocation would pay in full
+  e->stream = static_cast<hipStream_t>(cfg->hip_stream);
+  open_mark("stream");
   for (auto& x : e->ev) {
     h = hipEventCreate(&x);
     if (h != hipSuccess) { e->err = "hipEventCreate failed"; *out = e; return KLF_EHIP; }
@@ -510,7 +507,7 @@ static void free_chunk(klf_engine::StageChunk& c);
 
 extern "C" void klf_close(klf_engine* e) {
   if (!e) return;
-  if (e->stream) (void)hipStreamSynchronize(e->stream);
+  (void)hipStreamSynchronize(e->stream);
   if (e->copy_stream) (void)hipStreamSynchronize(e->copy_stream);
   if (e->aux_stream) (void)hipStreamSynchronize(e->aux_stream);
   for (DevBuf* b : {&e->d_lit, &e->d_ac_class, &e->d_ac_next, &e->d_ac_accept, &e->d_rx_class, &e->d_rx_b,
@@ -545,7 +542,6 @@ extern "C" void klf_close(klf_engine* e) {
   if (e->ev_join) (void)hipEventDestroy(e->ev_join);
   if (e->stage_ev) (void)hipEventDestroy(e->stage_ev);
   if (e->aux_stream) (void)hipStreamDestroy(e->aux_stream);
-  if (e->own_stream && e->stream) (void)hipStreamDestroy(e->stream);
   delete e;
   (void)hipGetLastError();  // nothing above reports: leave no sticky error for the next engine
 }
@@ -927,7 +923,14 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
       tune_pending = true;
     }
   }
-  HIPCHK(e, ensure_aux_stream(e), "side stream");  // (the first run: beside the statistics kernel)
+  // The pipeline's side stream (k_scatter beside k_verify for regex sets) from an engine's
+  // second run on: a first run launches serially, since creating a stream costs ~5 ms of
+  // host time when it brings up a new hardware queue (measured on MI355X).
+  hipStream_t aux = nullptr;
+  if (e->runs > 0 && mode == klf::CompiledSet::kGeneral) {
+    HIPCHK(e, ensure_aux_stream(e), "side stream");
+    aux = e->aux_stream;
+  }
   double est_density = 0.0;  // lines per byte of the first batch's sample (0: none)
   auto finish_tune = [&]() -> int {
     HIPCHK(e, hipStreamSynchronize(st), "sync hist");
@@ -1126,7 +1129,7 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
     HIPCHK(e, e->h_rb.ensure(sizeof(counters) + nsegs * sizeof(SegOut)), "alloc readback");
     if (two_phase) {
       a.cap_lines = 1ull << 40;  // phase 1 indexes no line array (k_tindex: no overflow, no bitmap)
-      HIPCHK(e, klf::launch_pipeline(a, st, e->ev, e->num_cus, e->aux_stream, e->ev_fork, e->ev_join, 1), "launch");
+      HIPCHK(e, klf::launch_pipeline(a, st, e->ev, e->num_cus, aux, e->ev_fork, e->ev_join, 1), "launch");
       uint8_t* rb1 = e->h_rb.as<uint8_t>();
       HIPCHK(e, hipMemcpyAsync(rb1, e->d_counters.p, sizeof(counters), hipMemcpyDeviceToHost, st), "D2H counters");
       HIPCHK(e, hipMemcpyAsync(rb1 + sizeof(counters), e->d_segout.p, nsegs * sizeof(SegOut), hipMemcpyDeviceToHost, st),
@@ -1156,11 +1159,11 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
       mark("line arrays");
       if (a.grep_mode != klf::CompiledSet::kNone)  // (phase 1's k_tindex zeroes it otherwise)
         HIPCHK(e, hipMemsetAsync(a.bits, 0, (cap / 32 + 1) * 4, st), "zero bits");
-      HIPCHK(e, klf::launch_pipeline(a, st, e->ev, e->num_cus, e->aux_stream, e->ev_fork, e->ev_join, 2), "launch");
+      HIPCHK(e, klf::launch_pipeline(a, st, e->ev, e->num_cus, aux, e->ev_fork, e->ev_join, 2), "launch");
       mark("phase 2 launched");
     } else {
       HIPCHK(e, alloc_lines(a, cap), "alloc line arrays");
-      HIPCHK(e, klf::launch_pipeline(a, st, e->ev, e->num_cus, e->aux_stream, e->ev_fork, e->ev_join), "launch");
+      HIPCHK(e, klf::launch_pipeline(a, st, e->ev, e->num_cus, aux, e->ev_fork, e->ev_join), "launch");
     }
     uint8_t* rb = e->h_rb.as<uint8_t>();
     HIPCHK(e, hipMemcpyAsync(rb, e->d_counters.p, sizeof(counters), hipMemcpyDeviceToHost, st), "D2H counters");
@@ -1197,6 +1200,7 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
       if (getenv("KLF_DIAG")) fprintf(stderr, "[klf] output buffer grown to %zu B\n", e->d_out.cap);
     }
     e->last_args = a;
+    ++e->runs;
     if (a.lazy_index && counters[klf::kCtrDense]) e->index_pending.push_back(a);
     e->last_gen = r->gen;
     e->line_density = (double)(r->so[nsegs - 1].line_hi + 1) / (double)total_bytes;
