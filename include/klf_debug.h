@@ -28,8 +28,9 @@ int klf_debug_prefilter(const klf_pattern* pats, uint32_t n, const uint8_t* cont
 
 /* The prefilter's layout chosen on the statistics of `sample` (the host twin of the first
  * batch's k_gramhist; slen 0: the compile-time layout), then its work over `data`:
- * out[8] = {stride, q, K, 0x100 | anchor byte (0: none), probes, bitmap hits, anchor hits,
- * verified needle occurrences}; layout (cap bytes) gets the layout's description. */
+ * out[9] = {stride, q, K, 0x100 | anchor byte (0: none), probes, bitmap hits, anchor hits,
+ * verified needle occurrences, samples past the two-level probe's 2-gram stage}; layout
+ * (cap bytes) gets the layout's description. */
 int klf_debug_prefilter_hits(const klf_pattern* pats, uint32_t n, const uint8_t* sample, size_t slen,
                              const uint8_t* data, size_t dlen, uint64_t* out, char* layout, size_t cap);
 

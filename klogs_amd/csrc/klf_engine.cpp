@@ -1881,6 +1881,7 @@ extern "C" int klf_debug_prefilter_hits(const klf_pattern* pats, uint32_t n, con
   out[5] = h.bitmap_hits;
   out[6] = h.anchor_hits;
   out[7] = h.verified;
+  out[8] = h.pair_pass;
   if (layout && cap) { strncpy(layout, cs.qf_layout.c_str(), cap - 1); layout[cap - 1] = 0; }
   return KLF_OK;
 }

@@ -1607,6 +1607,7 @@ PrefilterHits prefilter_hits(const CompiledSet& cs, const uint8_t* s, size_t n) 
       const uint32_t gq = (g | cs.qf_fold) & cs.qf_mask;
       hit = qf_pass(cs.qf_bitmap.data(), gq, w24, cs.qf_k);
       r.bitmap_hits += hit;
+      if (cs.qf_k == kQfTwoLevel) r.pair_pass += (cs.qf_bitmap[(gq & 0xFFFFu) >> 5] >> (gq & 31u)) & 1u;
     }
     if (!hit && cs.qf_anc_on && ((uint32_t)s[p] | (cs.qf_anc_fold & 0xFFu)) == cs.qf_anc_byte) {
       for (size_t j = 0; j + 1 < cs.qf_anc_pre.size() && !hit; j += 2)

@@ -168,6 +168,7 @@ void data_stats(const uint8_t* p, size_t n, uint32_t fold, DataStats& st);
 // positions, bitmap hits, anchor hits (pre-check passed), verified needle occurrences.
 struct PrefilterHits {
   uint64_t probes = 0, bitmap_hits = 0, anchor_hits = 0, verified = 0;
+  uint64_t pair_pass = 0;  // two-level probe: samples past the exact 2-gram stage
 };
 PrefilterHits prefilter_hits(const CompiledSet& cs, const uint8_t* data, size_t n);
 

@@ -227,15 +227,16 @@ def debug_prefilter(content: bytes, grep=(), match=(), phase: int = 0):
 
 def debug_prefilter_hits(sample: bytes, data: bytes, grep=(), match=()):
     """The prefilter layout chosen on `sample`'s statistics and its work over `data` (host):
-    {stride, q, k, anchor, probes, bitmap_hits, anchor_hits, verified, layout}."""
+    {stride, q, k, anchor, probes, bitmap_hits, anchor_hits, verified, pair_pass, layout}."""
     arr, n, keep = _patterns(grep, match)
-    out = (C.c_uint64 * 8)()
+    out = (C.c_uint64 * 9)()
     lay = C.create_string_buffer(256)
     sb = C.create_string_buffer(sample, len(sample) or 1)
     db = C.create_string_buffer(data, len(data) or 1)
     _check(_lib.klf_debug_prefilter_hits(arr, n, sb, len(sample), db, len(data), out, lay, 256))
     return dict(stride=out[0], q=out[1], k=out[2], anchor=(out[3] & 0xFF) if out[3] else None, probes=out[4],
-                bitmap_hits=out[5], anchor_hits=out[6], verified=out[7], layout=lay.value.decode())
+                bitmap_hits=out[5], anchor_hits=out[6], verified=out[7], pair_pass=out[8],
+                layout=lay.value.decode())
 
 
 def debug_factors(pattern: bytes, want: int = 0):
