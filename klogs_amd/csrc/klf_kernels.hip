@@ -17,6 +17,7 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <type_traits>
 
 #include "klf_kernels.hpp"
 #include "klf_ts.hpp"
@@ -337,6 +338,9 @@ __device__ __forceinline__ bool parse_fast(const uint8_t* lds, uint32_t o, const
 #endif
 #ifndef KLF_ANY_BATCH
 #define KLF_ANY_BATCH 8  // chunk reads in flight in the scan's newline any-test
+#endif
+#ifndef KLF_TWO_NOFOLD
+#define KLF_TWO_NOFOLD 1  // two-level probe: a fold-free copy of the pair stage for case-sensitive sets
 #endif
 #ifndef KLF_SCAN_OCC
 // plain / literal scans: waves per SIMD the launch bounds ask for.  3 leaves the compiler
@@ -744,23 +748,28 @@ __global__ __launch_bounds__(kThreads, MODE == kScanGen ? 3 : KLF_SCAN_OCC) void
         // sv bit i = the sample at my0 + 4i passes (each chunk's four dwords, two chunks per
         // step with their eight word reads in flight)
         uint32_t sv = 0;
+        // (a case-sensitive set, fold 0, takes a copy of the loop without the OR per sample)
+        auto pair_stage = [&](auto folded) __attribute__((always_inline)) {
 #pragma unroll
-        for (int v = 0; v < (ABL(4) ? 0 : 8); v += 2) {
-          const uint32_t ca = ((uint32_t)v + rot) & 7u, cb = ((uint32_t)v + 1u + rot) & 7u;
-          const uint4 xa = *reinterpret_cast<const uint4*>(s_tile + my0 + 16u * ca);
-          const uint4 xb = *reinterpret_cast<const uint4*>(s_tile + my0 + 16u * cb);
-          const uint32_t g[8] = {xa.x | fold, xa.y | fold, xa.z | fold, xa.w | fold,
-                                 xb.x | fold, xb.y | fold, xb.z | fold, xb.w | fold};
-          uint32_t w[8];
+          for (int v = 0; v < (ABL(4) ? 0 : 8); v += 2) {
+            const uint32_t ca = ((uint32_t)v + rot) & 7u, cb = ((uint32_t)v + 1u + rot) & 7u;
+            const uint4 xa = *reinterpret_cast<const uint4*>(s_tile + my0 + 16u * ca);
+            const uint4 xb = *reinterpret_cast<const uint4*>(s_tile + my0 + 16u * cb);
+            const uint32_t f = decltype(folded)::value ? fold : 0u;
+            const uint32_t g[8] = {xa.x | f, xa.y | f, xa.z | f, xa.w | f, xb.x | f, xb.y | f, xb.z | f, xb.w | f};
+            uint32_t w[8];
 #pragma unroll
-          for (int k = 0; k < 8; ++k)
-            w[k] = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(s_qf) + (bfe_u32(g[k], 5, 11) << 2));
+            for (int k = 0; k < 8; ++k)
+              w[k] = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(s_qf) + (bfe_u32(g[k], 5, 11) << 2));
 #pragma unroll
-          for (int k = 0; k < 8; ++k) {
-            const uint32_t bit = __builtin_amdgcn_ubfe(w[k], g[k], 1u);  // bit g mod 32 (v_bfe_u32 reads offset[4:0])
-            sv |= bit << (4u * (k < 4 ? ca : cb) + (uint32_t)(k & 3));
+            for (int k = 0; k < 8; ++k) {
+              const uint32_t bit = __builtin_amdgcn_ubfe(w[k], g[k], 1u);  // bit g mod 32 (v_bfe_u32 reads offset[4:0])
+              sv |= bit << (4u * (k < 4 ? ca : cb) + (uint32_t)(k & 3));
+            }
           }
-        }
+        };
+        if (KLF_TWO_NOFOLD && fold == 0u) pair_stage(std::false_type{});
+        else pair_stage(std::true_type{});
         // samples at or past the tile's end (4i >= nvalid) do not count
         sv &= nvalid >= kLaneBytes ? ~0u : ((1u << ((uint32_t)(nvalid + 3) >> 2)) - 1u);
         // stage 2: the survivors' 3-bit probe into the Bloom half; a hit's byte position
