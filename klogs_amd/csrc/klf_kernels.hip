@@ -725,10 +725,17 @@ __global__ __launch_bounds__(kThreads, MODE == kScanGen ? 3 : KLF_SCAN_OCC) void
         const Probe r = probe(g);
         return test(word(r), r);
       };
-      // the samples of chunk c (16 B) -> their grams, in order (QS = 8: dwords 0 and 2)
+      // the samples of chunk c (16 B) -> their grams, in order (QS = 8: dwords 0 and 2;
+      // QS = 6: the grid's bytes 0, 6 and 12, qf_sampled)
       auto chunk_grams = [&](uint32_t c, auto&& f) __attribute__((always_inline)) {
         const uint32_t o0 = my0 + 16u * c;
         const uint4 x = *reinterpret_cast<const uint4*>(s_tile + o0);
+        if constexpr (QS == 6) {
+          f(x.x, 0);
+          f(__builtin_amdgcn_alignbyte(x.z, x.y, 2u), 6);
+          f(x.w, 12);
+          return;
+        }
         const uint32_t w4 = QS < 4 ? s32[(o0 >> 2) + 4] : 0u;
         const uint32_t w[5] = {x.x, x.y, x.z, x.w, w4};
 #pragma unroll
@@ -784,27 +791,35 @@ __global__ __launch_bounds__(kThreads, MODE == kScanGen ? 3 : KLF_SCAN_OCC) void
             hq3 |= q == 3 ? b : 0u;
           }
         }
-      } else if (QS == 4) {
-        // stride 4: a chunk's samples are its four dwords.  Two chunks per step, their
-        // eight bitmap reads issued before the first test (one LDS round trip per step,
-        // not one per probe)
+      } else if (QS == 4 || QS == 6) {
+        // stride 4: a chunk's samples are its four dwords (the grid: bytes 0, 6, 12).  Two
+        // chunks per step, their bitmap reads issued before the first test (one LDS round
+        // trip per step, not one per probe)
+        constexpr int kPer = QS == 4 ? 4 : 3;
 #pragma unroll
         for (int v = 0; v < (ABL(4) ? 0 : 8); v += 2) {
           const uint32_t ca = ((uint32_t)v + rot) & 7u, cb = ((uint32_t)v + 1u + rot) & 7u;
           const uint4 xa = *reinterpret_cast<const uint4*>(s_tile + my0 + 16u * ca);
           const uint4 xb = *reinterpret_cast<const uint4*>(s_tile + my0 + 16u * cb);
-          const uint32_t g[8] = {xa.x, xa.y, xa.z, xa.w, xb.x, xb.y, xb.z, xb.w};
-          Probe r[8];
-          uint32_t w[8];
+          uint32_t g[2 * kPer];
+          if constexpr (QS == 4) {
+            g[0] = xa.x; g[1] = xa.y; g[2] = xa.z; g[3] = xa.w;
+            g[4] = xb.x; g[5] = xb.y; g[6] = xb.z; g[7] = xb.w;
+          } else {
+            g[0] = xa.x; g[1] = __builtin_amdgcn_alignbyte(xa.z, xa.y, 2u); g[2] = xa.w;
+            g[3] = xb.x; g[4] = __builtin_amdgcn_alignbyte(xb.z, xb.y, 2u); g[5] = xb.w;
+          }
+          Probe r[2 * kPer];
+          uint32_t w[2 * kPer];
 #pragma unroll
-          for (int k = 0; k < 8; ++k) r[k] = probe(g[k]);
+          for (int k = 0; k < 2 * kPer; ++k) r[k] = probe(g[k]);
 #pragma unroll
-          for (int k = 0; k < 8; ++k) w[k] = word(r[k]);
+          for (int k = 0; k < 2 * kPer; ++k) w[k] = word(r[k]);
           uint32_t acc_a = 0, acc_b = 0;
 #pragma unroll
-          for (int k = 0; k < 8; ++k) {
+          for (int k = 0; k < 2 * kPer; ++k) {
             const uint32_t t = test(w[k], r[k]);
-            if (k < 4) acc_a |= t; else acc_b |= t;
+            if (k < kPer) acc_a |= t; else acc_b |= t;
           }
           chit |= ((acc_a & 1u) << ca) | ((acc_b & 1u) << cb);
         }
@@ -3274,6 +3289,8 @@ hipError_t launch_pipeline(const RunArgs& a0, hipStream_t st, hipEvent_t* ev, in
       KLF_TRY((launch_scan<kScanLit, 1>(a, st, num_cus)));
     else if (a.grep_mode == kGrepGeneral && a.pats.qf_on && a.pats.qf_stride == 4)
       KLF_TRY((launch_gen<4>(a, st, num_cus)));
+    else if (a.grep_mode == kGrepGeneral && a.pats.qf_on && a.pats.qf_stride == 6)
+      KLF_TRY((launch_gen<6>(a, st, num_cus)));
     else if (a.grep_mode == kGrepGeneral && a.pats.qf_on && a.pats.qf_stride == 8)
       KLF_TRY((launch_gen<8>(a, st, num_cus)));
     else if (a.grep_mode == kGrepGeneral && a.pats.qf_on && a.pats.qf_stride == 2)

@@ -142,7 +142,19 @@ __host__ __device__ inline uint32_t qf_hist_bin0(uint32_t g) { return qf_h1(g) >
 __host__ __device__ inline uint32_t qf_hist_bin1(uint32_t g) {
   return (1u << kQfHistBits) + ((g * 0x85EBCA77u) >> (32 - kQfHistBits));
 }
-constexpr uint32_t kQfK2MaxGrams = 1536;  // up to this many sampled grams K = 2 bits, else 3
+constexpr uint32_t kQfK2MaxGrams = 1536;
+// The prefilter's sampled positions (tile / stream offsets; tiles and streams start
+// 16-B aligned): p = 0 mod S, except S = 6, the grid p mod 16 in {0, 6, 12}: three samples
+// per 16-B chunk whose gaps never exceed 6, so every run of 6 consecutive positions holds
+// one (windows of q + 5 bytes, as a stride of 6 would need) at 3/4 the samples of stride 4.
+__host__ __device__ inline bool qf_sampled(uint64_t p, uint32_t S) {
+  if (S == 6) {
+    const uint32_t r = (uint32_t)(p & 15u);
+    return r == 0 || r == 6 || r == 12;
+  }
+  return p % S == 0;
+}
+__host__ __device__ inline double qf_samples_per_tile(uint32_t S) { return S == 6 ? 8192.0 * 3 / 16 : 8192.0 / S; }  // up to this many sampled grams K = 2 bits, else 3
 
 // Dense compaction: per-tile copy record written by k_tkeep, read by k_ksum / k_kbase /
 // k_tcopy (16 B), and up to kRunSlots kept runs per tile (u32: tile offset of the run's

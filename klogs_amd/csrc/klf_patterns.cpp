@@ -967,8 +967,13 @@ bool compile_set(const std::vector<std::vector<uint8_t>>& pats, const std::vecto
     for (auto& l : lits) g = std::min(g, l.size());
     for (auto& f : rx_fac)
       for (auto& x : f) g = std::min(g, x.size());
-    const size_t want0 = g >= 10 ? 10 : g >= 6 ? 6 : g >= 4 ? 4 : 3;  // = the stride rule
-    for (size_t want : {want0, (size_t)10}) {
+    const size_t want0 = g >= 10 ? 10 : g >= 8 ? 8 : g >= 6 ? 6 : g >= 4 ? 4 : 3;  // = the stride rule
+    // (8-byte needles allow the stride-6 grid, whose windows then span a whole needle of 8:
+    // the 6-byte choice at stride 4 stays a candidate, the layout cost decides)
+    std::vector<size_t> wants = {want0};
+    if (want0 == 8) wants.push_back(6);
+    if (want0 != 10) wants.push_back(10);
+    for (size_t want : wants) {
       auto fac = rx_fac;
       auto lo = rx_loose;
       auto pr = rx_pre;
@@ -986,11 +991,10 @@ bool compile_set(const std::vector<std::vector<uint8_t>>& pats, const std::vecto
         lo[r] = loose;
         pr[r] = pre;
       }
-      if (!fac_v.empty() && fac == fac_v[0]) break;  // nothing longer to prefer
+      if (std::find(fac_v.begin(), fac_v.end(), fac) != fac_v.end()) continue;  // the same choice
       fac_v.push_back(fac);
       loose_v.push_back(lo);
       pre_v.push_back(pr);
-      if (want0 == 10) break;
     }
   }
   out.rx_pre = pre_v[0];
@@ -1188,11 +1192,13 @@ void build_prefilter(const std::vector<std::vector<uint8_t>>& lits,
 namespace {
 
 // The widest sampling stride whose windows (q + S - 1 bytes, grams of q >= 3 bytes) fit
-// every needle of length >= minlen (each probe costs ~12-17 VALU in the scan, so S = 8
-// halves the probe work of S = 4), then the longest gram that stride allows.
+// every needle of length >= minlen (each probe costs ~6-13 VALU in the scan, so S = 8
+// halves the probe work of S = 4; S = 6 is the 3-per-16-B grid, qf_sampled), then the
+// longest gram that stride allows.
 void stride_rule(size_t minlen, uint32_t& S, uint32_t& q) {
   const size_t sw = std::min<size_t>(8, minlen - 2);
-  S = sw >= 8 ? 8 : (sw >= 4 ? 4 : (sw >= 2 ? 2 : 1));
+  static const bool grid6 = !(getenv("KLF_QF_GRID6") && !strcmp(getenv("KLF_QF_GRID6"), "0"));
+  S = sw >= 8 ? 8 : (sw >= 6 && grid6) ? 6 : (sw >= 4 ? 4 : (sw >= 2 ? 2 : 1));
   q = (uint32_t)std::min<size_t>(4, minlen - S + 1);
 }
 
@@ -1330,7 +1336,7 @@ double layout_cost(const CompiledSet& c, const DataStats& st) {
   grams.erase(std::unique(grams.begin(), grams.end()), grams.end());
   double hit_share = 0;  // probed grams (the anchored ones only reach a bucket through an anchor)
   for (uint32_t g : grams) hit_share += gram_share(st, g, c.qf_q);
-  const double samples = 8192.0 / c.qf_stride;
+  const double samples = qf_samples_per_tile(c.qf_stride);
   double hits = samples * std::min(1.0, hit_share);
   // VALU per probe (the scan's ISA, its unrolled fast pass / 32 probes): 6.9 for a 3-byte
   // gram with two bits (fold, multiply, word offset, two shifts, and / or), 9.9 with the
@@ -1406,7 +1412,7 @@ void place_needles(CompiledSet& out, const DataStats* st) {
       if (st && st->nbytes) {
         cost = layout_cost(c, *st);
       } else {  // no statistics: stride first (8 is ~2x cheaper than 4), then the anchor's share
-        cost = 1e6 / c.qf_stride + (c.qf_anc_on ? c.qf_anc_share * 1e3 : 0.0);
+        cost = 1e6 * qf_samples_per_tile(c.qf_stride) / 8192.0 + (c.qf_anc_on ? c.qf_anc_share * 1e3 : 0.0);
       }
       char buf[64];
       snprintf(buf, sizeof buf, " [est %.0f VALU/tile]", cost);
@@ -1473,8 +1479,9 @@ void place_tables(CompiledSet& out, const DataStats* st) {
   // few grams: two bits per gram keep the false hits rare; many at stride 4: the two-level
   // probe (an exact 2-gram stage, then three bits; KLF_QF_TWO=0 keeps the one-level one)
   const char* two = getenv("KLF_QF_TWO");
-  out.qf_k = nprobed * S <= kQfK2MaxGrams ? 2u
-             : (S == 4 && !out.qf_anc_on && !(two && !strcmp(two, "0"))) ? kQfTwoLevel : 3u;
+  const bool two_ok = S == 4 && !out.qf_anc_on && !(two && !strcmp(two, "0"));
+  out.qf_k = (two_ok && two && !strcmp(two, "force")) ? kQfTwoLevel
+             : nprobed * S <= kQfK2MaxGrams ? 2u : two_ok ? kQfTwoLevel : 3u;
   const uint32_t w24 = q == 4 ? 24u : 0u;
   for (uint32_t i = 0; i < n; ++i) {
     const std::string& s = out.qf_needle[i];
@@ -1602,7 +1609,7 @@ PrefilterHits prefilter_hits(const CompiledSet& cs, const uint8_t* s, size_t n) 
     uint32_t g = 0;
     for (uint32_t b = 0; b < 4; ++b) g |= (uint32_t)(p + b < n ? s[p + b] : 0) << (8 * b);
     bool hit = false;
-    if (p % S == 0) {
+    if (qf_sampled(p, S)) {
       ++r.probes;
       const uint32_t gq = (g | cs.qf_fold) & cs.qf_mask;
       hit = qf_pass(cs.qf_bitmap.data(), gq, w24, cs.qf_k);
@@ -1660,7 +1667,7 @@ bool prefilter_match(const CompiledSet& cs, const uint8_t* s, size_t n, uint32_t
     uint32_t g = 0;
     for (uint32_t b = 0; b < 4; ++b) g |= (uint32_t)(p + b < n ? s[p + b] : 0) << (8 * b);
     bool hit = false;
-    if (p % S == phase % S) {
+    if (qf_sampled(p + 16 - phase % 16, S)) {
       const uint32_t gq = (g | cs.qf_fold) & cs.qf_mask;
       hit = qf_pass(cs.qf_bitmap.data(), gq, cs.qf_q == 4 ? 24u : 0u, cs.qf_k);
     }

@@ -84,11 +84,12 @@ struct CompiledSet {
   // kGeneral: q-gram prefilter fused into the scan (qf_on).  Needles = the literals
   // (final: a verified hit is a match) and one required factor set per regex (a verified
   // hit makes the line a candidate the Glushkov NFA then decides).  Sampled positions
-  // p = 0 mod qf_stride of every 8 KiB tile probe a hashed bitmap of the needles' q-grams
-  // at offsets 0..stride-1; bitmap hits are verified against the needles of the bucket.
+  // p (qf_sampled: 0 mod qf_stride, or the 3-per-16-B grid for 6) of every 8 KiB tile probe
+  // a hashed bitmap of the needles' q-grams at window offsets 0..stride-1; bitmap hits are
+  // verified against the needles of the bucket.
   bool qf_on = false;
   uint32_t qf_q = 4;         // gram length (bytes)
-  uint32_t qf_stride = 1;    // 1, 2 or 4
+  uint32_t qf_stride = 1;    // 1, 2, 4, 6 (grid) or 8
   uint32_t qf_fold = 0;      // 0x20202020 when some needle compares case-insensitively
   uint32_t qf_mask = ~0u;    // gram bytes (q < 4: low q bytes)
   uint32_t qf_k = 3;         // bitmap bits per gram (qf_bits)

@@ -163,6 +163,16 @@ def test_c4_literal_set_mixed_lines(gpu, monkeypatch, since, tail, two):
 
 
 @pytest.mark.parametrize("since,tail", [(None, -1), ((synth.T0 + 1800, 0), 50)])
+def test_grid6_needles(gpu, since, tail):
+    """Literal sets whose shortest needle is 8-9 bytes: the 3-per-16-B sampling grid
+    (stride 6, k_scan<gen, 6>), each needle's window spanning 8 bytes."""
+    lits = [l for l in synth.c4_literals(1024) if 8 <= len(l) <= 9][:200]
+    d = synth.generate(synth.MIXED, 12, 0, 3_000_000, permille=20)
+    assert E.debug_prefilter_hits(d[:1 << 16], d[:1 << 16], grep=lits)["stride"] == 6
+    check_against_c([d, synth.generate(synth.MIXED, 12, 1, 700_000, permille=80)], since, tail, lits)
+
+
+@pytest.mark.parametrize("since,tail", [(None, -1), ((synth.T0 + 1800, 0), 50)])
 def test_long_needles_stride8(gpu, since, tail):
     """Literal sets whose shortest needle allows an 8-byte sampling stride (k_scan<gen, 8>)."""
     lits = [l for l in synth.c4_literals(1024) if len(l) >= 12][:300]

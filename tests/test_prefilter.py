@@ -26,7 +26,9 @@ def _check(grep, match, contents):
     for s in contents:
         want = _want(s, grep, match)
         assert E.debug_match(s, grep=grep, match=match) == want, s
-        for ph in range(4):
+        got, info = E.debug_prefilter(s, grep=grep, match=match, phase=0)
+        assert got == want, (s, 0, info)
+        for ph in range(1, 16 if info["stride"] >= 6 else 4):  # (the grid of stride 6 repeats every 16)
             got, info = E.debug_prefilter(s, grep=grep, match=match, phase=ph)
             assert got == want, (s, ph, info)
     return info
@@ -106,7 +108,8 @@ def test_prefilter_off_falls_back(grep, match, why):
     ([], [rb"(?i)timeout"], 4, 4),
     ([b"abcdefghij", b"0123456789AB"], [], 3, 8),
     ([b"abcdefghijk"], [rb"x+connection reset"], 4, 8),
-    ([b"abcdefghi", b"0123456789AB"], [], 4, 4),
+    ([b"abcdefghi", b"0123456789AB"], [], 4, 6),
+    ([b"abcdefgh", b"0123456789AB"], [], 3, 6),
 ])
 def test_gram_and_stride_choice(grep, match, q, stride):
     _, info = E.debug_prefilter(b"", grep=grep, match=match)
