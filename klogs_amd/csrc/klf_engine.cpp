@@ -121,16 +121,11 @@ struct klf_engine {
   std::deque<Inflight> inflight;       // pinned chunks whose H2D may still be running
   std::vector<hipEvent_t> ev_pool;
   hipStream_t copy_stream = nullptr;   // early H2D of full chunks
-  hipStream_t aux_stream = nullptr;    // side stream of the pipeline (k_scatter beside k_verify)
-  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   hipEvent_t copy_done = nullptr;
   bool ran = false;                    // klf_run since the last klf_reset (stage -> ESTATE)
   std::unique_ptr<klf::CopyPool> copier;  // started by the first klf_stage (device-resident runs never stage)
   std::once_flag copier_once;
   std::once_flag copy_stream_once;     // the copy stream: created by the first klf_stage / klf_run
-  uint64_t runs = 0;                   // completed runs (the first one launches without aux_stream)
-  std::once_flag aux_once;             // the side stream + fork / join events: the first run
-  hipError_t aux_err = hipSuccess;
   hipError_t copy_stream_err = hipSuccess;
   DevBuf d_asm;                        // k_assemble piece table
   DevBuf d_scratch;                    // small query results (klf_result_last_unparsed)
@@ -509,7 +504,6 @@ extern "C" void klf_close(klf_engine* e) {
   if (!e) return;
   (void)hipStreamSynchronize(e->stream);
   if (e->copy_stream) (void)hipStreamSynchronize(e->copy_stream);
-  if (e->aux_stream) (void)hipStreamSynchronize(e->aux_stream);
   for (DevBuf* b : {&e->d_lit, &e->d_ac_class, &e->d_ac_next, &e->d_ac_accept, &e->d_rx_class, &e->d_rx_b,
                     &e->d_rx_follow, &e->d_rx_vec, &e->d_rx_flags, &e->d_rx_pre, &e->d_qf_bitmap, &e->d_qf_head,
                     &e->d_qf_ent, &e->d_qf_nbytes, &e->d_qf_anc, &e->d_rx_vec4, &e->d_qhits, &e->d_hslots, &e->d_hist, &e->d_hflat, &e->d_cand, &e->d_batch, &e->d_segs, &e->d_tstat,
@@ -537,11 +531,7 @@ extern "C" void klf_close(klf_engine* e) {
     if (x) (void)hipEventDestroy(x);
   if (e->copy_done) (void)hipEventDestroy(e->copy_done);
   if (e->copy_stream) (void)hipStreamDestroy(e->copy_stream);
-  if (e->aux_stream) (void)hipStreamSynchronize(e->aux_stream);
-  if (e->ev_fork) (void)hipEventDestroy(e->ev_fork);
-  if (e->ev_join) (void)hipEventDestroy(e->ev_join);
   if (e->stage_ev) (void)hipEventDestroy(e->stage_ev);
-  if (e->aux_stream) (void)hipStreamDestroy(e->aux_stream);
   delete e;
   (void)hipGetLastError();  // nothing above reports: leave no sticky error for the next engine
 }
@@ -560,18 +550,6 @@ static hipError_t ensure_copy_stream(klf_engine* e) {
     e->copy_stream_err = h;
   });
   return e->copy_stream_err;
-}
-
-// The pipeline's side stream and its fork / join events, made by the first run (while its
-// first-batch statistics kernel runs), not by klf_open.
-static hipError_t ensure_aux_stream(klf_engine* e) {
-  std::call_once(e->aux_once, [e] {
-    hipError_t h = hipStreamCreateWithFlags(&e->aux_stream, hipStreamNonBlocking);
-    if (h == hipSuccess) h = hipEventCreateWithFlags(&e->ev_fork, hipEventDisableTiming);
-    if (h == hipSuccess) h = hipEventCreateWithFlags(&e->ev_join, hipEventDisableTiming);
-    e->aux_err = h;
-  });
-  return e->aux_err;
 }
 
 static void grow_table(klf_engine* e, size_t n) {  // caller holds e->mu
@@ -923,14 +901,6 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
       tune_pending = true;
     }
   }
-  // The pipeline's side stream (k_scatter beside k_verify for regex sets) from an engine's
-  // second run on: a first run launches serially, since creating a stream costs ~5 ms of
-  // host time when it brings up a new hardware queue (measured on MI355X).
-  hipStream_t aux = nullptr;
-  if (e->runs > 0 && mode == klf::CompiledSet::kGeneral) {
-    HIPCHK(e, ensure_aux_stream(e), "side stream");
-    aux = e->aux_stream;
-  }
   double est_density = 0.0;  // lines per byte of the first batch's sample (0: none)
   auto finish_tune = [&]() -> int {
     HIPCHK(e, hipStreamSynchronize(st), "sync hist");
@@ -1129,7 +1099,7 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
     HIPCHK(e, e->h_rb.ensure(sizeof(counters) + nsegs * sizeof(SegOut)), "alloc readback");
     if (two_phase) {
       a.cap_lines = 1ull << 40;  // phase 1 indexes no line array (k_tindex: no overflow, no bitmap)
-      HIPCHK(e, klf::launch_pipeline(a, st, e->ev, e->num_cus, aux, e->ev_fork, e->ev_join, 1), "launch");
+      HIPCHK(e, klf::launch_pipeline(a, st, e->ev, e->num_cus, 1), "launch");
       uint8_t* rb1 = e->h_rb.as<uint8_t>();
       HIPCHK(e, hipMemcpyAsync(rb1, e->d_counters.p, sizeof(counters), hipMemcpyDeviceToHost, st), "D2H counters");
       HIPCHK(e, hipMemcpyAsync(rb1 + sizeof(counters), e->d_segout.p, nsegs * sizeof(SegOut), hipMemcpyDeviceToHost, st),
@@ -1159,11 +1129,11 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
       mark("line arrays");
       if (a.grep_mode != klf::CompiledSet::kNone)  // (phase 1's k_tindex zeroes it otherwise)
         HIPCHK(e, hipMemsetAsync(a.bits, 0, (cap / 32 + 1) * 4, st), "zero bits");
-      HIPCHK(e, klf::launch_pipeline(a, st, e->ev, e->num_cus, aux, e->ev_fork, e->ev_join, 2), "launch");
+      HIPCHK(e, klf::launch_pipeline(a, st, e->ev, e->num_cus, 2), "launch");
       mark("phase 2 launched");
     } else {
       HIPCHK(e, alloc_lines(a, cap), "alloc line arrays");
-      HIPCHK(e, klf::launch_pipeline(a, st, e->ev, e->num_cus, aux, e->ev_fork, e->ev_join), "launch");
+      HIPCHK(e, klf::launch_pipeline(a, st, e->ev, e->num_cus), "launch");
     }
     uint8_t* rb = e->h_rb.as<uint8_t>();
     HIPCHK(e, hipMemcpyAsync(rb, e->d_counters.p, sizeof(counters), hipMemcpyDeviceToHost, st), "D2H counters");
@@ -1200,7 +1170,6 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
       if (getenv("KLF_DIAG")) fprintf(stderr, "[klf] output buffer grown to %zu B\n", e->d_out.cap);
     }
     e->last_args = a;
-    ++e->runs;
     if (a.lazy_index && counters[klf::kCtrDense]) e->index_pending.push_back(a);
     e->last_gen = r->gen;
     e->line_density = (double)(r->so[nsegs - 1].line_hi + 1) / (double)total_bytes;

@@ -1267,9 +1267,14 @@ struct ScatterEnt {
   uint32_t pad[2];
 };
 
-__global__ __launch_bounds__(256) void k_scatter(RunArgs a) {
-  __shared__ ScatterEnt s_ent[4][kScatterGroup];
-  __shared__ uint32_t s_pre[4][kScatterGroup];  // inclusive line-count prefix of the group's tiles
+struct ScatterLds {
+  ScatterEnt ent[4][kScatterGroup];
+  uint32_t pre[4][kScatterGroup];  // inclusive line-count prefix of the group's tiles
+};
+// Block bid of nb (k_scatter alone, or the first nb blocks of k_scatter_verify).
+__device__ __forceinline__ void scatter_body(RunArgs& a, uint32_t bid, uint32_t nb, ScatterLds& L) {
+  auto& s_ent = L.ent;
+  auto& s_pre = L.pre;
   // lazy line index (grep none, --tail -1): launched after k_tailw, and only the line gather
   // needs the index; the dense path lists lines from the slots (the host builds the index
   // on demand: klf_result_lines, klf_retail, klf_result_last_unparsed)
@@ -1277,7 +1282,7 @@ __global__ __launch_bounds__(256) void k_scatter(RunArgs a) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   uint32_t* err_flag = a.counters + 2;
   const uint32_t ngroups = (a.ntiles + kScatterGroup - 1) / kScatterGroup;
-  for (uint32_t g = blockIdx.x * 4 + wv; g < ngroups; g += gridDim.x * 4) {
+  for (uint32_t g = bid * 4 + wv; g < ngroups; g += nb * 4) {
     const uint32_t tile = g * kScatterGroup + lane;
     uint32_t n = 0;
     if (tile < a.ntiles) {
@@ -1369,6 +1374,10 @@ __global__ __launch_bounds__(256) void k_scatter(RunArgs a) {
     }
     asm volatile("" ::: "memory");  // the next group rewrites the wave's LDS tables
   }
+}
+__global__ __launch_bounds__(256) void k_scatter(RunArgs a) {
+  __shared__ ScatterLds L;
+  scatter_body(a, blockIdx.x, gridDim.x, L);
 }
 
 // ============================================= K2: general pattern sets (per line) ==
@@ -1545,15 +1554,19 @@ __device__ void verify_hit(const RunArgs& a, uint32_t tile, uint32_t s, int32_t 
 // descriptor -> gram -> bucket) runs for kVerifyBatch hits at once: the kernel is bound
 // by that latency (most hits are prefilter false positives that end at the bucket).
 constexpr int kVerifyBatch = 4;
-__global__ __launch_bounds__(256) void k_verify(RunArgs a) {
-  __shared__ uint32_t s_qn[4];
-  __shared__ uint64_t s_qbuf[4][kVerifyQ][2];
+struct VerifyLds {
+  uint32_t qn[4];
+  uint64_t qbuf[4][kVerifyQ][2];
+};
+__device__ __forceinline__ void verify_body(RunArgs& a, uint32_t bid, uint32_t nb, VerifyLds& L) {
+  auto& s_qn = L.qn;
+  auto& s_qbuf = L.qbuf;
   if (a.counters[2] || a.counters[kCtrHitsOver]) return;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   if (lane == 0) s_qn[wv] = 0;
   wave_lds_sync();
   const VerifyQ vq{&s_qn[wv], s_qbuf[wv]};
-  const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x, stride = gridDim.x * blockDim.x;
+  const uint32_t gid = bid * blockDim.x + threadIdx.x, stride = nb * blockDim.x;
   const uint32_t nf = a.counters[kCtrFlatHits];
   const DevPatterns& P = a.pats;
   for (uint32_t i0 = gid; i0 < nf; i0 += kVerifyBatch * stride) {
@@ -1621,6 +1634,22 @@ __global__ __launch_bounds__(256) void k_verify(RunArgs a) {
       }
     }
   }
+}
+__global__ __launch_bounds__(256) void k_verify(RunArgs a) {
+  __shared__ VerifyLds L;
+  verify_body(a, blockIdx.x, gridDim.x, L);
+}
+// Regex sets: k_scatter (bandwidth-bound) and k_verify (latency-bound: a chain of dependent
+// loads per hit) as one launch, blocks [0, nsb) scattering, the rest verifying, so the two
+// overlap on the chip without a second stream (k_verify reads the line slots, not the
+// global line index).
+__global__ __launch_bounds__(256) void k_scatter_verify(RunArgs a, uint32_t nsb) {
+  __shared__ union {
+    ScatterLds s;
+    VerifyLds v;
+  } L;
+  if (blockIdx.x < nsb) scatter_body(a, blockIdx.x, nsb, L.s);
+  else verify_body(a, blockIdx.x - nsb, gridDim.x - nsb, L.v);
 }
 
 // K2b: the prefiltered regex stage.  One lane per queued (batch offset, regex) candidate:
@@ -3261,8 +3290,7 @@ hipError_t launch_scatter(const RunArgs& a, hipStream_t st, int num_cus) {
   return hipGetLastError();
 }
 
-hipError_t launch_pipeline(const RunArgs& a0, hipStream_t st, hipEvent_t* ev, int num_cus, hipStream_t aux,
-                           hipEvent_t ev_fork, hipEvent_t ev_join, int phase) {
+hipError_t launch_pipeline(const RunArgs& a0, hipStream_t st, hipEvent_t* ev, int num_cus, int phase) {
   RunArgs a = a0;
   hipError_t e;
 #define KLF_TRY(x) do { e = (x); if (e != hipSuccess) return e; } while (0)
@@ -3314,27 +3342,26 @@ hipError_t launch_pipeline(const RunArgs& a0, hipStream_t st, hipEvent_t* ev, in
   }
   if (phase == 1) return hipSuccess;
   }  // phase != 2
-  // With a prefiltered regex set, k_scatter (bandwidth-bound) runs on the side stream
-  // beside k_verify (latency-bound: a chain of dependent loads per hit), which reads the
-  // line slots, not the global line index; the main stream waits for it before the first
-  // kernel that reads the index.  Measured: C5 (64 regexes) -0.10 ms per step; a literal
-  // set's heavier verification (C4: 1,024 literals) contends with it instead (+0.08 ms),
-  // so literal-only sets keep the serial order.
-  const bool fork = a.grep_mode == kGrepGeneral && a.pats.qf_on && a.pats.rx_count && aux != nullptr;
-  if (fork) {
-    KLF_TRY(hipEventRecord(ev_fork, st));
-    KLF_TRY(hipStreamWaitEvent(aux, ev_fork, 0));
-    KLF_TRY(launch_scatter(a, aux, num_cus));
-    KLF_TRY(hipEventRecord(ev_join, aux));
+  // Regex sets: k_scatter and k_verify as one launch (k_scatter_verify; measured with two
+  // streams: C5 -0.10 ms per step); a literal set's heavier verification (C4: 1,024 literals)
+  // contends with the scatter instead (+0.08 ms), so literal-only sets keep the serial order.
+  const bool fused_sv = a.grep_mode == kGrepGeneral && a.pats.qf_on && a.pats.rx_count;
+  if (fused_sv) {
+    uint32_t nsb = ((a.ntiles + kScatterGroup - 1) / kScatterGroup + 3) / 4;
+    if (nsb > (uint32_t)num_cus * 4) nsb = num_cus * 4;
+    if (nsb == 0) nsb = 1;
+    hipLaunchKernelGGL(k_scatter_verify, dim3(nsb + num_cus * 8), dim3(256), 0, st, a, nsb);
+    KLF_TRY(hipGetLastError());
   } else if (!a.lazy_index) {
     KLF_TRY(launch_scatter(a, st, num_cus));
   }
-  if (ev && a.stage_times && !fork) KLF_TRY(hipEventRecord(ev[2], st));  // ~5 us of idle GPU each
+  if (ev && a.stage_times && !fused_sv) KLF_TRY(hipEventRecord(ev[2], st));  // ~5 us of idle GPU each
   if (a.grep_mode == kGrepGeneral && a.pats.qf_on) {
-    hipLaunchKernelGGL(k_verify, dim3(num_cus * 8), dim3(256), 0, st, a);
-    KLF_TRY(hipGetLastError());
-    if (fork) KLF_TRY(hipStreamWaitEvent(st, ev_join, 0));
-    if (ev && a.stage_times && fork) KLF_TRY(hipEventRecord(ev[2], st));
+    if (!fused_sv) {
+      hipLaunchKernelGGL(k_verify, dim3(num_cus * 8), dim3(256), 0, st, a);
+      KLF_TRY(hipGetLastError());
+    }
+    if (ev && a.stage_times && fused_sv) KLF_TRY(hipEventRecord(ev[2], st));
     if (a.count_pats) {
       hipLaunchKernelGGL(k_fixcount, dim3(num_cus * 2), dim3(256), 0, st, a);
       KLF_TRY(hipGetLastError());

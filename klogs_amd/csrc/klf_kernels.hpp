@@ -320,15 +320,13 @@ struct RunArgs {
 // per-kernel timing: ev[0] start, ev[1] after the workspace memsets, ev[2] after the
 // scan, ev[3] after the general matcher, ev[4] after counts+tail+window prefix, ev[5]
 // after compaction.  Returns a hipError_t.
-// aux (may be null) with the fork / join events: a side stream for k_scatter beside k_verify.
 // ev may be null: no event records.
 // phase: 0 the whole pipeline; 1 up to the tile index (k_init .. k_tindex: the line arrays
 // are not touched, a.bits may be null); 2 the rest (k_scatter on), after the host sized
 // the line arrays from phase 1's line count (an engine's first run).
 // k_scatter alone: the global line index of a run (an engine's lazy index, on demand).
 hipError_t launch_scatter(const RunArgs& a, hipStream_t stream, int num_cus);
-hipError_t launch_pipeline(const RunArgs& a, hipStream_t stream, hipEvent_t* ev, int num_cus, hipStream_t aux,
-                           hipEvent_t ev_fork, hipEvent_t ev_join, int phase = 0);
+hipError_t launch_pipeline(const RunArgs& a, hipStream_t stream, hipEvent_t* ev, int num_cus, int phase = 0);
 // Re-runs matched counts, tail and compaction of the last pipeline with a.tail changed.
 hipError_t launch_retail(const RunArgs& a, hipStream_t stream, hipEvent_t* ev, int num_cus);
 // Data statistics (kGramHistWords u32, zeroed here) of the first `sample` bytes of each of
