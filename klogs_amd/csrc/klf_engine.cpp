@@ -907,13 +907,9 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
     const auto t_hist = std::chrono::steady_clock::now();
     const uint32_t* hv = e->h_hist.as<uint32_t>();
     klf::DataStats ds;
-    ds.gram3.assign(hv, hv + klf::kQfHistBins);
-    ds.gram4.assign(hv + klf::kQfHistBins, hv + 2 * klf::kQfHistBins);
-    for (auto& c : ds.gram3) c *= klf::kGramHistStride;  // grams were counted at every 4th position
-    for (auto& c : ds.gram4) c *= klf::kGramHistStride;
     ds.bytes.assign(256, 0);
     for (int c = 0; c < 256; ++c) {
-      ds.bytes[c] = hv[2 * klf::kQfHistBins + c];
+      ds.bytes[c] = hv[c];
       ds.nbytes += ds.bytes[c];
     }
     ds.pair.assign(hv + klf::kGramHistPairs, hv + klf::kGramHistPairs + 65536);

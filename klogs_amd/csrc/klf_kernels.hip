@@ -3148,19 +3148,14 @@ __global__ __launch_bounds__(256) void k_gramhist(const uint8_t* bytes, const Se
     if (o + 8 > sd.len) continue;
     const uint32_t* p = reinterpret_cast<const uint32_t*>(bytes + sd.base + o);
     const uint32_t w0 = p[0];
-    static_assert(kGramHistStride == 4, "one gram per dword");
-    const uint32_t g = w0 | fold, g3 = g & 0xFFFFFFu;  // (the host scales the counts by 4)
-    atomicAdd(&hist[qf_hist_bin0(g3)], 1u);
-    atomicAdd(&hist[qf_hist_bin1(g3)], 1u);
-    atomicAdd(&hist[kQfHistBins + qf_hist_bin0(g)], 1u);
-    atomicAdd(&hist[kQfHistBins + qf_hist_bin1(g)], 1u);
+    const uint32_t g = w0 | fold;
     atomicAdd(&hist[kGramHistPairs + (g & 0xFFFFu)], 1u);  // the 2-grams at even offsets
     atomicAdd(&hist[kGramHistPairs + (g >> 16)], 1u);
 #pragma unroll
     for (int k = 0; k < 4; ++k) atomicAdd(&s_b[(w0 >> (8 * k)) & 0xFFu], 1u);
   }
   __syncthreads();
-  if (s_b[threadIdx.x]) atomicAdd(&hist[2 * kQfHistBins + threadIdx.x], s_b[threadIdx.x]);
+  if (s_b[threadIdx.x]) atomicAdd(&hist[threadIdx.x], s_b[threadIdx.x]);
 }
 
 // Capture assembly: block b copies 1 MiB of piece b / kAsmBlocks (pieces are 64 MiB

@@ -126,22 +126,11 @@ __host__ __device__ inline bool qf_pass(const uint32_t* bm, uint32_t gq, uint32_
   const uint32_t h = qf_hash(gq, w24, k), bits = qf_bits(gq, h, k);
   return (bm[qf_bloom_word(gq, w24, k)] & bits) == bits;
 }
-// Gram statistics of the window choice: a count-min sketch, 2 rows of 2^16 bins, for the
-// 3-byte and for the 4-byte grams, then a byte histogram, then the exact 2-gram counts at
-// even positions (k_gramhist)
-constexpr int kQfHistBits = 16;
-constexpr uint32_t kQfHistBins = 2u << kQfHistBits;
-constexpr uint32_t kGramHistPairs = 2 * kQfHistBins + 256;  // first word of the 2-gram counts
+// Data statistics of the window choice (k_gramhist over a sample of the first batch): a
+// byte histogram, then the exact 2-gram counts (fold applied) at even offsets
+constexpr uint32_t kGramHistPairs = 256;  // first word of the 2-gram counts
 constexpr uint32_t kGramHistWords = kGramHistPairs + 65536;
 constexpr uint64_t kGramHistSample = 64u << 10;  // bytes sampled per segment (<= 16 segments)
-// grams counted at every kGramHistStride-th position of the sample (the host scales the
-// counts back): a quarter of the global atomics, which bound the one-off pass
-constexpr uint32_t kGramHistStride = 4;
-__host__ __device__ inline uint32_t qf_h1(uint32_t g) { return (g ^ (g >> 13)) * 0x9E3779B1u; }
-__host__ __device__ inline uint32_t qf_hist_bin0(uint32_t g) { return qf_h1(g) >> (32 - kQfHistBits); }
-__host__ __device__ inline uint32_t qf_hist_bin1(uint32_t g) {
-  return (1u << kQfHistBits) + ((g * 0x85EBCA77u) >> (32 - kQfHistBits));
-}
 constexpr uint32_t kQfK2MaxGrams = 1536;
 // The prefilter's sampled positions (tile / stream offsets; tiles and streams start
 // 16-B aligned): p = 0 mod S, except S = 6, the grid p mod 16 in {0, 6, 12}: three samples
@@ -330,8 +319,8 @@ hipError_t launch_pipeline(const RunArgs& a, hipStream_t stream, hipEvent_t* ev,
 // Re-runs matched counts, tail and compaction of the last pipeline with a.tail changed.
 hipError_t launch_retail(const RunArgs& a, hipStream_t stream, hipEvent_t* ev, int num_cus);
 // Data statistics (kGramHistWords u32, zeroed here) of the first `sample` bytes of each of
-// up to 16 segments, every position: 3-gram and 4-gram sketches (folded like the
-// prefilter's grams), byte counts.
+// up to 16 segments: byte counts, and the 2-grams at even offsets (folded like the
+// prefilter's grams).
 hipError_t launch_gramhist(const uint8_t* bytes, const SegDesc* segs, uint32_t nsegs, uint64_t sample, uint32_t fold,
                            uint32_t* hist, hipStream_t stream);
 // Staged capture (klf_run): device chunks of the early H2D -> their places in the batch.

@@ -3,6 +3,7 @@
 #include "klf_patterns.hpp"
 
 #include <algorithm>
+#include <chrono>
 #include <bitset>
 #include <cstdio>
 #include <cstdlib>
@@ -1407,7 +1408,9 @@ void place_needles(CompiledSet& out, const DataStats* st) {
         if (std::find(seen.begin(), seen.end(), key) != seen.end()) continue;  // placed already
         seen.push_back(key);
       }
+      const auto t0 = std::chrono::steady_clock::now();
       place_tables(c, st);
+      const auto t1 = std::chrono::steady_clock::now();
       double cost;
       if (st && st->nbytes) {
         cost = layout_cost(c, *st);
@@ -1417,7 +1420,10 @@ void place_needles(CompiledSet& out, const DataStats* st) {
       char buf[64];
       snprintf(buf, sizeof buf, " [est %.0f VALU/tile]", cost);
       c.qf_layout += buf;
-      if (getenv("KLF_DIAG")) fprintf(stderr, "[klf] layout candidate (variant %u): %s\n", v, c.qf_layout.c_str());
+      if (getenv("KLF_DIAG"))
+        fprintf(stderr, "[klf] layout candidate (variant %u): %s (tables %.0f us, cost %.0f us)\n", v, c.qf_layout.c_str(),
+                std::chrono::duration<double, std::micro>(t1 - t0).count(),
+                std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t1).count());
       if (!have || cost < best_cost) {
         best = std::move(c);
         best_cost = cost;
@@ -1438,15 +1444,14 @@ void place_needles(CompiledSet& out, const DataStats* st) {
 namespace {
 
 // Window choice + tables.  Each probed needle is sampled through q + S - 1 of its bytes:
-// the window whose S grams are the least frequent -- in the gram sketch of the data when
-// one is given (k_gramhist count-min sketch over a sample of the first batch), else by a
+// the window whose S grams are the least frequent -- by gram_share on the data's 2-gram
+// statistics when given (k_gramhist over a sample of the first batch), else by a
 // byte-class estimate -- with a small penalty for grams other needles already sample
 // (bucket length).  Every probed gram sets K bits of one bitmap word (blocked Bloom); an
 // anchored needle has one bucket entry, at its anchor's gram, and no bitmap bits.
 void place_tables(CompiledSet& out, const DataStats* st) {
   const uint32_t q = out.qf_q, S = out.qf_stride;
-  const std::vector<uint32_t>* hist = st ? (q == 3 ? &st->gram3 : &st->gram4) : nullptr;
-  if (hist && hist->size() < kQfHistBins) hist = nullptr;
+  const bool hist = st && st->pair.size() >= 65536 && st->pair_tot > 0;  // data statistics
   const double nsample = st && st->nbytes ? (double)st->nbytes : 1.0;
   // a window's score: the summed shares of its S grams (one of them is sampled per
   // occurrence), plus, under the two-level probe, a twentieth of each gram's leading pair
@@ -1469,8 +1474,30 @@ void place_tables(CompiledSet& out, const DataStats* st) {
     if (strchr("\":,=./{}-TZ", c) && c) return 3;                                  // JSON / timestamp punctuation
     return 1;  // upper case, '_', other punctuation, control and high bytes
   };
-  std::unordered_map<uint32_t, int> used;  // gram -> needles sampling it so far
-  used.reserve(out.qf_needle.size() * S * 2);
+  // gram -> needles sampling it so far: a flat open-addressing table (grams are < 2^32 - 1)
+  struct Used {
+    std::vector<uint32_t> key, cnt;
+    uint32_t mask;
+    explicit Used(size_t n) {
+      size_t cap = 64;
+      while (cap < 2 * n) cap <<= 1;
+      key.assign(cap, ~0u);
+      cnt.assign(cap, 0u);
+      mask = (uint32_t)cap - 1;
+    }
+    uint32_t slot(uint32_t g) const {
+      uint32_t i = (g * 0x9E3779B1u) & mask;
+      while (key[i] != ~0u && key[i] != g) i = (i + 1) & mask;
+      return i;
+    }
+    uint32_t get(uint32_t g) const { return cnt[slot(g)]; }
+    void add(uint32_t g) {
+      const uint32_t i = slot(g);
+      key[i] = g;
+      ++cnt[i];
+    }
+  } used(out.qf_needle.size() * S + 1);
+  std::vector<uint64_t> gcost;             // a needle's gram costs by offset
   std::vector<std::pair<uint32_t, uint32_t>> bent;  // (bucket, needle << 8 | gram offset), in needle order
   bent.reserve(out.qf_needle.size() * S);
   const size_t n = out.qf_needle.size();
@@ -1491,31 +1518,33 @@ void place_tables(CompiledSet& out, const DataStats* st) {
       continue;
     }
     const uint32_t amax = (uint32_t)std::min<size_t>(s.size() - (q + S - 1), 255 - (S - 1));
+    // each gram's cost once (a gram lies in up to S windows), then the windows
+    gcost.resize(amax + S);
+    for (uint32_t k = 0; k < amax + S; ++k) {
+      const uint32_t g = gram_at(s, k);
+      const uint64_t u = used.get(g);
+      uint64_t c;
+      if (hist) {
+        double sh = gram_share(*st, g, q);
+        if (pair_w > 0 && out.qf_k == kQfTwoLevel && st->pair_tot > 0)  // the pair stage's survivors
+          sh += pair_w * (st->pair[g & 0xFFFFu] + 0.5) / st->pair_tot;
+        c = (uint64_t)(sh * nsample * 256.0) + 2 * u;
+      } else {
+        c = 2 * u;
+        for (uint32_t b = 0; b < q; ++b) c += common((uint8_t)s[k + b]);
+      }
+      gcost[k] = c;
+    }
     uint32_t best_a = 0;
     uint64_t best = UINT64_MAX;
     for (uint32_t a = 0; a <= amax; ++a) {
       uint64_t sc = 0;
-      for (uint32_t j = 0; j < S; ++j) {
-        const uint32_t g = gram_at(s, a + j);
-        auto it = used.find(g);
-        const uint64_t u = it == used.end() ? 0 : (uint64_t)it->second;
-        uint64_t c;
-        if (hist) {
-          double sh = gram_share(*st, g, q);
-          if (pair_w > 0 && out.qf_k == kQfTwoLevel && st->pair_tot > 0)  // the pair stage's survivors
-            sh += pair_w * (st->pair[g & 0xFFFFu] + 0.5) / st->pair_tot;
-          c = (uint64_t)(sh * nsample * 256.0) + 2 * u;
-        } else {
-          c = 2 * u;
-          for (uint32_t b = 0; b < q; ++b) c += common((uint8_t)s[a + j + b]);
-        }
-        sc = hist ? sc + c : std::max(sc, c);
-      }
+      for (uint32_t j = 0; j < S; ++j) sc = hist ? sc + gcost[a + j] : std::max(sc, gcost[a + j]);
       if (sc < best) { best = sc; best_a = a; }
     }
     for (uint32_t j = 0; j < S; ++j) {
       const uint32_t k = best_a + j, g = gram_at(s, k);
-      used[g]++;
+      used.add(g);
       const uint32_t h = qf_hash(g, w24, out.qf_k);
       const uint32_t bw = qf_bucket(g, w24, out.qf_k);
       out.qf_bitmap[qf_bloom_word(g, w24, out.qf_k)] |= qf_bits(g, h, out.qf_k);
@@ -1562,11 +1591,7 @@ void stats_finish(DataStats& st) {
 }
 
 double gram_share(const DataStats& st, uint32_t g, uint32_t q) {
-  const double nb = st.nbytes ? (double)st.nbytes : 1.0;
-  const std::vector<uint32_t>& sk = q == 3 ? st.gram3 : st.gram4;
-  const double sketch = sk.size() >= kQfHistBins ? std::min(sk[qf_hist_bin0(g)], sk[qf_hist_bin1(g)]) / nb : 1.0;
-  static const bool use_sketch = getenv("KLF_QF_EST") && !strcmp(getenv("KLF_QF_EST"), "sketch");  // A/B
-  if (use_sketch || st.pair.size() < 65536 || st.marg.size() != 256 || st.pair_tot <= 0) return sketch;
+  if (st.pair.size() < 65536 || st.marg.size() != 256 || st.pair_tot <= 0) return 1.0;
   // P(b0 b1) * prod P(b_i b_i+1) / P(b_i): pair counts + 1/2, marginals from the pairs
   const double tot = st.pair_tot;
   auto pr = [&](uint32_t a, uint32_t b) { return (st.pair[a | b << 8] + 0.5) / tot; };
@@ -1579,25 +1604,18 @@ double gram_share(const DataStats& st, uint32_t g, uint32_t q) {
 }
 
 void data_stats(const uint8_t* p, size_t n, uint32_t fold, DataStats& st) {
-  st.gram3.assign(kQfHistBins, 0u);
-  st.gram4.assign(kQfHistBins, 0u);
   st.pair.assign(65536, 0u);
   st.bytes.assign(256, 0u);
   st.nbytes = 0;
   for (size_t i = 0; i + 4 <= n; ++i) {
     st.bytes[p[i]]++;
     st.nbytes++;
-    if (i % kGramHistStride) continue;  // grams at every 4th position, counted 4 times (k_gramhist)
+    if (i % 4) continue;  // the 2-grams at even positions (k_gramhist: two per dword), counted twice
     uint32_t g = 0;
     for (int b = 0; b < 4; ++b) g |= (uint32_t)p[i + b] << (8 * b);
     g |= fold;
-    st.pair[g & 0xFFFFu] += 2;  // the 2-grams at even positions (k_gramhist), counted twice
+    st.pair[g & 0xFFFFu] += 2;
     st.pair[g >> 16] += 2;
-    const uint32_t g3 = g & 0xFFFFFFu;
-    st.gram3[qf_hist_bin0(g3)] += kGramHistStride;
-    st.gram3[qf_hist_bin1(g3)] += kGramHistStride;
-    st.gram4[qf_hist_bin0(g)] += kGramHistStride;
-    st.gram4[qf_hist_bin1(g)] += kGramHistStride;
   }
   stats_finish(st);
 }

@@ -130,12 +130,10 @@ struct CompiledSet {
   uint32_t qf_variant = 0;
 };
 
-// Statistics of a data sample (k_gramhist, first batch): count-min sketches of the 3- and
-// 4-byte grams (kQfHistBins bins each, needles' fold applied), the exact 2-gram counts
-// (fold applied, at even positions) and the byte histogram.
+// Statistics of a data sample (k_gramhist, first batch): the exact 2-gram counts (fold
+// applied, at even positions, scaled to every position) and the byte histogram.
 struct DataStats {
-  std::vector<uint32_t> gram3, gram4;
-  std::vector<uint32_t> pair;   // [65536] 2-gram b0 | b1 << 8 (empty: none)
+  std::vector<uint32_t> pair;   // [65536] 2-gram b0 | b1 << 8
   std::vector<uint64_t> bytes;  // [256]
   uint64_t nbytes = 0;          // positions counted in `bytes`
   // derived by stats_finish: 2-gram marginals and their total
@@ -146,8 +144,8 @@ struct DataStats {
 void stats_finish(DataStats& st);
 // Estimated share of the data's positions that hold gram g (q bytes, folded): a
 // first-order Markov chain over the exact 2-gram counts, which resolves shares far below
-// one per sample where the count-min sketches only see their collision noise (those
-// remain for KLF_QF_EST=sketch, and for statistics without 2-gram counts).
+// one occurrence per sample (round 3's count-min sketches of the 3- and 4-grams saw only
+// their collision noise there).
 double gram_share(const DataStats& st, uint32_t g, uint32_t q);
 constexpr uint32_t kQfAncPreMax = 8;  // distinct short-needle pre-check dwords
 
@@ -161,8 +159,8 @@ constexpr uint32_t kRxPreUnbounded = 0xFFFFFFFFu;
 bool regex_factors(const uint8_t* pat, size_t n, std::vector<std::string>& alts, bool& loose,
                    uint32_t* pre = nullptr, size_t want = SIZE_MAX);
 
-// Host twin of k_gramhist over one sample (tests / diagnostics): every position's 3- and
-// 4-gram (OR fold) into the sketches, every byte into the histogram.
+// Host twin of k_gramhist over one sample (tests / diagnostics): the 2-grams (OR fold) at
+// even positions, every byte into the histogram.
 void data_stats(const uint8_t* p, size_t n, uint32_t fold, DataStats& st);
 
 // Diagnostics of the prefiltered scan over `data` with the current layout: sampled
