@@ -37,10 +37,14 @@ static std::atomic<uint64_t> g_alloc_ns{0};
 struct DevBuf {
   void* p = nullptr;
   size_t cap = 0;
+  bool borrowed = false;  // p lies in an engine's workspace block (not freed here)
   hipError_t ensure(size_t bytes) {
     if (bytes <= cap && p) return hipSuccess;
     const auto t0 = std::chrono::steady_clock::now();
-    if (p) { (void)hipFree(p); p = nullptr; cap = 0; }
+    if (p && !borrowed) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+    borrowed = false;
     size_t want = std::max<size_t>(bytes, 256);
     hipError_t e = hipMalloc(&p, want);
     if (e == hipSuccess) cap = want;
@@ -51,13 +55,39 @@ struct DevBuf {
     return e;
   }
   void release() {
-    if (p) (void)hipFree(p);
+    if (p && !borrowed) (void)hipFree(p);
     p = nullptr;
     cap = 0;
+    borrowed = false;
   }
   template <class T>
   T* as() const { return static_cast<T*>(p); }
 };
+
+// An engine's first run maps its workspace buffers as one allocation (each hipMalloc costs
+// tens of us of host time, ~20 of them add up in a one-shot run): buffers not yet mapped
+// get 256-B aligned pieces of one block; later growth maps a buffer of its own.
+static hipError_t ensure_all(DevBuf& block, const std::vector<std::pair<DevBuf*, size_t>>& req) {
+  size_t total = 0;
+  for (auto& r : req)
+    if (!r.first->p) total += (std::max<size_t>(r.second, 256) + 255) & ~(size_t)255;
+  if (total && !block.p) {
+    hipError_t h = block.ensure(total);
+    if (h != hipSuccess) return h;
+    size_t off = 0;
+    for (auto& r : req) {
+      if (r.first->p) continue;
+      const size_t n = (std::max<size_t>(r.second, 256) + 255) & ~(size_t)255;
+      r.first->p = static_cast<uint8_t*>(block.p) + off;
+      r.first->cap = n;
+      r.first->borrowed = true;
+      off += n;
+    }
+  }
+  for (auto& r : req)
+    if (hipError_t h = r.first->ensure(r.second); h != hipSuccess) return h;
+  return hipSuccess;
+}
 
 // Pinned host buffer (hipHostMalloc): per-run readbacks land here with one async DMA each
 // and a single stream sync (a pageable destination costs a staged copy and a wait per call).
@@ -150,6 +180,7 @@ struct klf_engine {
   std::vector<SegDesc> last_segs;  // tile_seg cache key
   DevBuf d_tile_seg;
   DevBuf d_cmap, d_cseg;
+  DevBuf d_block;  // the first run's workspace buffers (ensure_all), freed last
   DevBuf d_batch, d_segs, d_tstat, d_slots, d_pool, d_tile_base, d_bsum, d_cstatus, d_counters, d_line_off,
       d_meta, d_bits, d_segout, d_wpre, d_out, d_mpart, d_trec, d_truns, d_kbase;
   uint64_t pool_cap = 1 << 20;
@@ -516,6 +547,7 @@ extern "C" void klf_close(klf_engine* e) {
   e->h_hist.release();
   e->h_stage.release();
   for (DevBuf* b : {&e->d_ac_out, &e->d_ac_dict, &e->d_pcount, &e->d_pairs}) b->release();
+  e->d_block.release();
   e->copier.reset();
   {
     std::lock_guard<std::mutex> g(e->mu);
@@ -931,20 +963,16 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
     mark("first-batch tuning");
     return KLF_OK;
   };
-  HIPCHK(e, e->d_tstat.ensure(ntiles * sizeof(klf::TileStat)), "alloc tstat");
-  HIPCHK(e, e->d_slots.ensure(ntiles * klf::kRecStride * 4), "alloc slots");
-  HIPCHK(e, e->d_tile_base.ensure(ntiles * 8), "alloc tile_base");
-  HIPCHK(e, e->d_bsum.ensure((ntiles / 1024 + 2) * 4 * 8), "alloc bsum");
-  HIPCHK(e, e->d_counters.ensure(klf::kNumCounters * 4), "alloc counters");
-  HIPCHK(e, e->d_segout.ensure(nsegs * sizeof(SegOut)), "alloc segout");
-  HIPCHK(e, e->d_wpre.ensure((nsegs + 1) * 8), "alloc wpre");
-  HIPCHK(e, e->d_trec.ensure(ntiles * sizeof(klf::TRec)), "alloc trec");
+  std::vector<std::pair<DevBuf*, size_t>> ws = {
+      {&e->d_tstat, ntiles * sizeof(klf::TileStat)}, {&e->d_slots, ntiles * klf::kRecStride * 4},
+      {&e->d_tile_base, ntiles * 8}, {&e->d_bsum, (ntiles / 1024 + 2) * 4 * 8},
+      {&e->d_counters, klf::kNumCounters * 4}, {&e->d_segout, nsegs * sizeof(SegOut)},
+      {&e->d_wpre, (nsegs + 1) * 8}, {&e->d_trec, ntiles * sizeof(klf::TRec)}, {&e->d_kbase, ntiles * 16}};
   // the dense compaction's per-tile run table (512 B per tile: 2.1 GB for 32 GiB) only for
   // runs without a --tail limit or after a --tail run took the dense path (k_tcopy lists
   // the runs itself without it)
   const bool want_truns = f->tail < 0 || e->dense_tail_seen;
-  if (want_truns) HIPCHK(e, e->d_truns.ensure(ntiles * klf::kRunSlots * 4), "alloc truns");
-  HIPCHK(e, e->d_kbase.ensure(ntiles * 16), "alloc kbase");
+  if (want_truns) ws.push_back({&e->d_truns, ntiles * klf::kRunSlots * 4});
   uint32_t compact_mode = 0;  // tests: force either compaction path
   e->index_pending.clear();
   // lazy line index (grep none, --tail -1; KLF_LAZY_INDEX=0 turns it off)
@@ -963,7 +991,7 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
     HIPCHK(e, e->d_out.ensure(std::min<uint64_t>(total_bytes + 64, first)), "alloc out");
   }
   const bool need_cand = mode == klf::CompiledSet::kGeneral && e->cs.qf_on && e->cs.rx_count;
-  if (need_cand) HIPCHK(e, e->d_cand.ensure((size_t)e->cand_cap * 16), "alloc cand");
+  if (need_cand) ws.push_back({&e->d_cand, (size_t)e->cand_cap * 16});
   const bool need_hits = mode == klf::CompiledSet::kGeneral && e->cs.qf_on;
   // bitmap hits: < 1 per 8 KiB tile on log text, kHitSlots per tile recorded in place;
   // spills beyond 1 per 1 KiB of input -> k_match decides
@@ -973,10 +1001,11 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
   const uint64_t hflat_cap = std::min<uint64_t>(std::max<uint64_t>(total_bytes / 512, 1u << 20),
                                                 (uint64_t)ntiles * klf::kHitSlots);
   if (need_hits) {
-    HIPCHK(e, e->d_qhits.ensure((size_t)qhits_cap * 8), "alloc qhits");
-    HIPCHK(e, e->d_hslots.ensure((size_t)ntiles * klf::kHitSlots * 2), "alloc hslots");
-    HIPCHK(e, e->d_hflat.ensure((size_t)hflat_cap * 4), "alloc hflat");
+    ws.push_back({&e->d_qhits, (size_t)qhits_cap * 8});
+    ws.push_back({&e->d_hslots, (size_t)ntiles * klf::kHitSlots * 2});
+    ws.push_back({&e->d_hflat, (size_t)hflat_cap * 4});
   }
+  HIPCHK(e, ensure_all(e->d_block, ws), "alloc workspace");
 
   const bool count = (f->flags & KLF_FILTER_PATTERN_COUNTS) && mode == klf::CompiledSet::kGeneral && e->cs.n_cids;
   r->counted = (f->flags & KLF_FILTER_PATTERN_COUNTS) != 0;

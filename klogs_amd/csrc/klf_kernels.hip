@@ -2713,19 +2713,72 @@ __device__ __forceinline__ void tkeep_body(RunArgs& a, const uint32_t* __restric
   for (uint32_t t0 = (blockIdx.x * 4 + wv) * kTkBatch; t0 < a.ntiles; t0 += nw * kTkBatch) {
     TileLines g[kTkBatch];
     LineData pre[kTkBatch];
+    if (a.grep_mode == kGrepNone) {
+      // the batch's descriptors in phases, every load of a phase in flight together: the
+      // tiles' and their predecessors' records, then the carried-in lines' slots (the last
+      // slot of tile - 1; a tile without line starts before it sends the walk further back)
+      TileStat ts[kTkBatch], tp[kTkBatch];
 #pragma unroll
-    for (int u = 0; u < kTkBatch; ++u) {
-      const uint32_t tile = t0 + u < a.ntiles ? t0 + u : a.ntiles - 1;
-      g[u].s = tseg[tile];
-      g[u].sd = segs[g[u].s];
-      g[u].rel_lo = (int64_t)(tile - g[u].sd.tile0) * kTile;
-      const int64_t rem = (int64_t)g[u].sd.len - g[u].rel_lo;
-      g[u].tlen = (int32_t)(rem < kTile ? rem : kTile);
-      g[u].l0 = tbase[tile];
-      const TileStat ts = tstat[tile];
-      g[u].nl = rem <= kTile ? ts.events : ts.events + 1;
-      if (a.grep_mode == kGrepNone) tile_slots(a, tstat, g[u], tile, ts);
-      pre[u] = load_line(a, g[u], (uint32_t)lane);
+      for (int u = 0; u < kTkBatch; ++u) {
+        const uint32_t tile = t0 + u < a.ntiles ? t0 + u : a.ntiles - 1;
+        g[u].s = tseg[tile];
+      }
+#pragma unroll
+      for (int u = 0; u < kTkBatch; ++u) {
+        const uint32_t tile = t0 + u < a.ntiles ? t0 + u : a.ntiles - 1;
+        g[u].sd = segs[g[u].s];
+        g[u].l0 = tbase[tile];
+        ts[u] = tstat[tile];
+        tp[u] = tstat[tile > 0 ? tile - 1 : 0];
+      }
+      uint32_t cs[kTkBatch];
+#pragma unroll
+      for (int u = 0; u < kTkBatch; ++u) {
+        const uint32_t tile = t0 + u < a.ntiles ? t0 + u : a.ntiles - 1;
+        g[u].rel_lo = (int64_t)(tile - g[u].sd.tile0) * kTile;
+        const int64_t rem = (int64_t)g[u].sd.len - g[u].rel_lo;
+        g[u].tlen = (int32_t)(rem < kTile ? rem : kTile);
+        g[u].nl = rem <= kTile ? ts[u].events : ts[u].events + 1;
+        g[u].sl = tile_slot_list(a, ts[u], tile);
+        g[u].k0 = g[u].rel_lo == 0 ? 0u : 1u;
+        g[u].cstart = g[u].rel_lo;  // (the carried-in line: set below, lane 0 reloads it)
+        g[u].cslot = 0;
+        const uint32_t pk0 = g[u].rel_lo == kTile ? 0u : 1u;  // tile - 1 the stream's first
+        const uint32_t pn = tp[u].events + 1 > pk0 ? tp[u].events + 1 - pk0 : 0u;
+        cs[u] = (g[u].k0 && pn) ? tile_slot_list(a, tp[u], tile - 1)[pn - 1] : 0u;
+        pre[u] = load_line(a, g[u], (uint32_t)lane);  // (own slots only: load_line reads cslot later)
+      }
+#pragma unroll
+      for (int u = 0; u < kTkBatch; ++u) {
+        const uint32_t tile = t0 + u < a.ntiles ? t0 + u : a.ntiles - 1;
+        if (!g[u].k0) continue;
+        const uint32_t pk0 = g[u].rel_lo == kTile ? 0u : 1u;
+        if (tp[u].events + 1 > pk0) {  // the common case: tile - 1 lists a line start
+          g[u].cslot = cs[u];
+          g[u].cstart = g[u].rel_lo - kTile + (int64_t)(cs[u] & kSlotOff);
+        } else {
+          TileLines h = g[u];
+          h.rel_lo -= kTile;
+          tile_slots(a, tstat, h, tile - 1, tp[u]);  // tile - 1 carries the same line in
+          g[u].cslot = h.cslot;
+          g[u].cstart = h.cstart;
+        }
+        if ((uint32_t)lane < g[u].k0) pre[u] = load_line(a, g[u], (uint32_t)lane);  // lane 0: the carried-in line
+      }
+    } else {
+#pragma unroll
+      for (int u = 0; u < kTkBatch; ++u) {
+        const uint32_t tile = t0 + u < a.ntiles ? t0 + u : a.ntiles - 1;
+        g[u].s = tseg[tile];
+        g[u].sd = segs[g[u].s];
+        g[u].rel_lo = (int64_t)(tile - g[u].sd.tile0) * kTile;
+        const int64_t rem = (int64_t)g[u].sd.len - g[u].rel_lo;
+        g[u].tlen = (int32_t)(rem < kTile ? rem : kTile);
+        g[u].l0 = tbase[tile];
+        const TileStat ts = tstat[tile];
+        g[u].nl = rem <= kTile ? ts.events : ts.events + 1;
+        pre[u] = load_line(a, g[u], (uint32_t)lane);
+      }
     }
 #pragma unroll
     for (int u = 0; u < kTkBatch; ++u) {
