@@ -800,6 +800,7 @@ static hipError_t wait_stream(hipStream_t st, uint64_t spin_us) {
 // the buffer to the run's output and rerun the tail stage over the line index and bitmap
 // still in HBM (k_mcount .. k_tcopy, tens of us), then read the stream records back.
 static hipError_t grow_out_retail(klf_engine* e, klf::RunArgs& a, std::vector<SegOut>& so) {
+  a.plan_runs = 0;  // the tile plans were consumed (k_cmove rewrote them): list the runs again
   for (int k = 0; k < 2; ++k) {
     uint64_t need = 0;
     for (auto& s : so) need = std::max(need, s.out_hi);
@@ -1073,6 +1074,8 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
     a.kbase = e->d_kbase.as<uint64_t>();
     a.compact_mode = compact_mode;
     a.lazy_index = lazy_index ? 1u : 0u;
+    a.plan_runs = (lazy_index && want_truns && compact_mode != 1 &&
+                   !(getenv("KLF_PLAN_RUNS") && !strcmp(getenv("KLF_PLAN_RUNS"), "0"))) ? 1u : 0u;
     a.count_pats = count ? 1u : 0u;
     a.pcount = count ? e->d_pcount.as<uint32_t>() : nullptr;
     a.pairs = count ? e->d_pairs.as<uint64_t>() : nullptr;
@@ -1277,6 +1280,7 @@ extern "C" int klf_retail(klf_engine* e, klf_result* prev, int64_t tail, klf_res
     klf::RunArgs a = e->last_args;
     a.tail = tail;
     a.stage_times = 0;
+    a.plan_runs = 0;  // (plans assume --tail -1 and are consumed by the run)
     hipStream_t st = e->stream;
     hipError_t h = klf::launch_retail(a, st, e->ev, e->num_cus);
     uint32_t short_out = 0;

@@ -170,6 +170,92 @@ constexpr uint32_t kCtrDefer = 5;  // counters[5]: some line of this run was def
 constexpr int kTcRuns = kTile / 20 + 8;     // + the two sentinels
 constexpr int kTcChunks = kTile / 16 + 8;
 
+// ---- planned dense compaction (RunArgs::plan_runs: no patterns, --tail -1) ---------------
+// With every line decided where it starts (parsed and since_ok: SPEC.md S3/S4 with tail -1)
+// the scan lists each tile's kept runs of the lines starting in it, and the tile's output
+// offset and carried-in run follow from a scan over tile aggregates (k_cmid / k_cmove, no
+// line-index pass).  A range's aggregate is a function of the state entering it:
+//   bytes  kept bytes of the lines starting in the range,
+//   has    some line starts in the range,
+//   span   bytes from the range start to its first line start (the range when !has): the
+//          entering line's part, kept from its content start on when that line is kept,
+//   sel / crel   the line open at the range end: kept?, its content start - the range end.
+// A stream's first tile lists its line 0 at offset 0 (span 0), so nothing carries across
+// streams.  Deferred lines (non-canonical prefixes, decided later by fix_tile) void the
+// plan: the run then lists its tiles from the line slots (k_tkeep).
+struct FAgg {
+  uint32_t bytes, span;
+  int32_t crel;
+  bool has, sel;
+};
+struct FPre {
+  uint64_t off;
+  int32_t crel;  // content start of the open line - the boundary
+  bool sel;
+};
+// a content start before the boundary: kept from the boundary on, however far back (-1)
+__device__ __forceinline__ int32_t f_sat(int32_t crel) { return crel < 0 ? -1 : crel; }
+__device__ __forceinline__ uint32_t f_carried(uint32_t span, bool sel, int32_t crel) {
+  const int32_t lo = crel > 0 ? crel : 0;
+  return (sel && (int32_t)span > lo) ? (uint32_t)((int32_t)span - lo) : 0u;
+}
+// X then Y
+__device__ __forceinline__ FAgg f_combine(const FAgg& x, const FAgg& y) {
+  FAgg z;
+  z.bytes = x.bytes + y.bytes + (x.has ? f_carried(y.span, x.sel, x.crel) : 0u);
+  z.has = x.has || y.has;
+  z.span = x.has ? x.span : x.span + y.span;
+  if (y.has) { z.sel = y.sel; z.crel = y.crel; }
+  else { z.sel = x.sel; z.crel = f_sat(x.crel - (int32_t)y.span); }  // !y.has: y.span = its length
+  return z;
+}
+__device__ __forceinline__ FPre f_apply(const FPre& p, const FAgg& z) {
+  FPre r;
+  r.off = p.off + z.bytes + f_carried(z.span, p.sel, p.crel);
+  if (z.has) { r.sel = z.sel; r.crel = z.crel; }
+  else { r.sel = p.sel; r.crel = f_sat(p.crel - (int32_t)z.span); }
+  return r;
+}
+// a tile's plan (the scan -> trec[tile] until k_cmove rewrites it): x = bytes | span << 14
+// | has << 28 | sel << 29, y = crel (16 bits signed) | nsel << 16, z = own runs (or
+// kRunsRecompute), w = kPlanTag
+constexpr uint32_t kPlanTag = 0x504C414Eu;
+constexpr uint32_t kRunsShifted = 0x4000u;  // TRec.nruns: runs 1.. shift by TRec.nsel (run 0 = carried)
+__device__ __forceinline__ bool planned(const RunArgs& a) { return a.plan_runs && !a.counters[kCtrDefer]; }
+__device__ __forceinline__ FAgg plan_agg(const uint4& r) {
+  FAgg a;
+  a.bytes = r.x & 0x3FFFu;
+  a.span = (r.x >> 14) & 0x3FFFu;
+  a.has = (r.x >> 28) & 1u;
+  a.sel = (r.x >> 29) & 1u;
+  a.crel = (int32_t)(int16_t)(uint16_t)(r.y & 0xFFFFu);
+  return a;
+}
+__device__ __forceinline__ FAgg wave_incl_scan_fagg(FAgg x, int lane) {
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    FAgg y;
+    y.bytes = (uint32_t)__shfl_up((int)x.bytes, d, 64);
+    y.span = (uint32_t)__shfl_up((int)x.span, d, 64);
+    y.crel = __shfl_up(x.crel, d, 64);
+    const int fl = __shfl_up((x.has ? 1 : 0) | (x.sel ? 2 : 0), d, 64);
+    y.has = fl & 1;
+    y.sel = (fl & 2) != 0;
+    if (lane >= d) x = f_combine(y, x);
+  }
+  return x;
+}
+__device__ __forceinline__ FAgg fagg_lane(const FAgg& x, int src) {
+  FAgg y;
+  y.bytes = (uint32_t)__builtin_amdgcn_readlane((int)x.bytes, src);
+  y.span = (uint32_t)__builtin_amdgcn_readlane((int)x.span, src);
+  y.crel = __builtin_amdgcn_readlane(x.crel, src);
+  const int fl = __builtin_amdgcn_readlane((x.has ? 1 : 0) | (x.sel ? 2 : 0), src);
+  y.has = fl & 1;
+  y.sel = (fl & 2) != 0;
+  return y;
+}
+
 // Any-test: nonzero when some byte of the 16 equals the byte replicated in c4.  One
 // v_xad_u32 per dword ((x ^ c4) - 0x01..01: bit 7 of an equal byte is set) and 3-input
 // ORs; it also flags bytes with (x ^ c) >= 0x81 (non-ASCII text) and bytes above a true
@@ -592,6 +678,59 @@ __global__ __launch_bounds__(kThreads, MODE == kScanGen ? 3 : KLF_SCAN_OCC) void
             n_since += (fast && so) ? 1u : 0u;
             n_defer += fast ? 0u : 1u;
           }
+        }
+      }
+      // ---- planned dense compaction: the tile's own kept runs and aggregate (FAgg above).
+      // Two rounds of 64 lines, each ending in one buffer store of the runs (lanes without a
+      // run, or past the record, dropped) and the plan in one more: a fixed store count per
+      // tile (see the record stores below).  Tiles with more lines leave their runs to
+      // k_tcopy (kRunsRecompute).
+      if constexpr (MODE == kScanPlain) {
+        if (a.plan_runs) {
+          if (dense) __threadfence_block();
+          wave_lds_sync();
+          typedef uint32_t u32x4p __attribute__((ext_vector_type(4)));
+          const bool fits = nlines <= 128u && !abl;
+          const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(
+              a.truns + (size_t)tile * kRunSlots, 0, fits ? kRunSlots * 4 : 0, 0x00020000);
+          uint32_t nr = 0, dacc = 0, ns = 0, lsel = 0;
+          int32_t lcrel = -1;
+          auto round = [&](uint32_t b0, bool store) __attribute__((always_inline)) {
+            const uint32_t j = b0 + (uint32_t)lane;
+            uint32_t src = 0, len = 0;
+            bool sel = false, starts = false;
+            if (j < nlines) {
+              const uint32_t v = list[j], off = v & kSlotOff, mt = v >> 16;
+              sel = !(v & kSlotDefer) && (mt & Meta::kParsed) && (mt & Meta::kSince);
+              const uint32_t c = off + (mt >> 2);
+              const uint32_t e = j + 1 < nlines ? (list[j + 1] & kSlotOff) : (uint32_t)tile_len;
+              if (sel && e > c) { src = c; len = e - c; }
+              starts = off < (uint32_t)tile_len;
+              if (j + 1 == nlines) { lsel = sel ? 1u : 0u; lcrel = f_sat((int32_t)c - tile_len); }
+            }
+            const uint32_t incl = wave_incl_scan_add(len, lane);
+            const uint64_t bm = __ballot(len != 0);
+            const uint32_t idx = nr + (uint32_t)__popcll(bm & ((1ull << lane) - 1ull));
+            // slot 0 is the carried-in run's (k_cmove)
+            if (store)
+              __builtin_amdgcn_raw_buffer_store_b32(src | ((dacc + incl - len) << 16), rr,
+                                                    len ? 4u * (idx + 1u) : 0x7FFF0000u, 0, 0);
+            nr += (uint32_t)__popcll(bm);
+            dacc += (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+            ns += (uint32_t)__popcll(__ballot(sel && starts));
+          };
+          round(0u, true);
+          round(64u, true);
+          for (uint32_t b0 = 128u; b0 < nlines; b0 += 64) round(b0, false);  // (no runs stored)
+          const uint32_t lastl = nlines ? ((nlines - 1u) & 63u) : 0u;
+          const uint32_t psel = nlines ? (uint32_t)__builtin_amdgcn_readlane((int)lsel, (int)lastl) : 0u;
+          const int32_t pcrel = nlines ? __builtin_amdgcn_readlane(lcrel, (int)lastl) : -1;
+          const uint32_t span = nlines ? (list[0] & kSlotOff) : (uint32_t)tile_len;
+          const uint32_t px = (dacc & 0x3FFFu) | ((span & 0x3FFFu) << 14) | ((nlines ? 1u : 0u) << 28) | (psel << 29);
+          const uint32_t py = ((uint32_t)(uint16_t)(int16_t)pcrel) | (ns << 16);
+          const uint32_t pz = (fits && nr + 1u <= (uint32_t)kRunSlots) ? nr : (uint32_t)kRunsRecompute;
+          const __amdgpu_buffer_rsrc_t pr = __builtin_amdgcn_make_buffer_rsrc(a.trec + tile, 0, abl ? 0 : 16, 0x00020000);
+          __builtin_amdgcn_raw_buffer_store_b128(u32x4p{px, py, pz, kPlanTag}, pr, lane ? 0x7FFF0000u : 0u, 0, 0);
         }
       }
       // number of listed line starts at or before tile offset pos
@@ -2706,7 +2845,7 @@ constexpr int kTkBatch = 4;
 __device__ __forceinline__ void tkeep_body(RunArgs& a, const uint32_t* __restrict__ tseg,
                                            const SegDesc* __restrict__ segs, const TileStat* __restrict__ tstat,
                                            const uint64_t* __restrict__ tbase, const SegOut* __restrict__ sout) {
-  if (a.counters[2] || !a.counters[kCtrDense]) return;
+  if (a.counters[2] || !a.counters[kCtrDense] || planned(a)) return;  // (planned: the scan listed the runs)
   const int lane = threadIdx.x & 63;
   const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t nw = gridDim.x * 4;
@@ -2801,11 +2940,138 @@ __device__ __forceinline__ void tkeep_body(RunArgs& a, const uint32_t* __restric
   }
 }
 
+// Planned runs (the scan's plans, FAgg above): the tile aggregates' ordered reduce-then-scan,
+// 256 threads x R consecutive tiles per block.  bsum per block: bytes, then span | has << 32
+// | sel << 33 | crel << 34 (16 bits), then the selected lines.
+__device__ __forceinline__ uint64_t pack_blk(const FAgg& b) {
+  return (uint64_t)b.span | ((uint64_t)b.has << 32) | ((uint64_t)b.sel << 33) | ((uint64_t)(uint16_t)(int16_t)b.crel << 34);
+}
+__device__ __forceinline__ FAgg unpack_blk(uint64_t bytes, uint64_t v) {
+  FAgg b;
+  b.bytes = (uint32_t)bytes;
+  b.span = (uint32_t)v;
+  b.has = (v >> 32) & 1u;
+  b.sel = (v >> 33) & 1u;
+  b.crel = (int32_t)(int16_t)(uint16_t)(v >> 34);
+  return b;
+}
+constexpr FAgg kFAggNone{0u, 0u, -1, false, false};
+// the ordered total of the block's thread values (every thread gets it); s_a / s_n: [4]
+__device__ __forceinline__ FAgg block_fagg_total(FAgg x, uint64_t n, FAgg* s_a, uint64_t* s_n, uint64_t* total_n) {
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const FAgg w = wave_incl_scan_fagg(x, lane);
+  const uint64_t wn = wave_sum(n);
+  __syncthreads();
+  if (lane == 63) s_a[wv] = w;
+  if (lane == 0) s_n[wv] = wn;
+  __syncthreads();
+  FAgg b = s_a[0];
+  for (int k = 1; k < 4; ++k) b = f_combine(b, s_a[k]);
+  *total_n = s_n[0] + s_n[1] + s_n[2] + s_n[3];
+  return b;
+}
+template <int R>
+__device__ __forceinline__ void ksum_plan(RunArgs& a) {
+  __shared__ FAgg s_a[4];
+  __shared__ uint64_t s_n[4];
+  const uint4* rec = reinterpret_cast<const uint4*>(a.trec);
+  const uint32_t t0 = blockIdx.x * (256 * R) + threadIdx.x * R;
+  FAgg acc = kFAggNone;
+  uint64_t ns = 0;
+  for (int r = 0; r < R; ++r)
+    if (t0 + r < a.ntiles) {
+      const uint4 q = rec[t0 + r];
+      acc = f_combine(acc, plan_agg(q));
+      ns += q.y >> 16;
+    }
+  uint64_t tn;
+  const FAgg b = block_fagg_total(acc, ns, s_a, s_n, &tn);
+  if (threadIdx.x == 0) {
+    a.bsum[4 * blockIdx.x] = b.bytes;
+    a.bsum[4 * blockIdx.x + 1] = pack_blk(b);
+    a.bsum[4 * blockIdx.x + 2] = tn;
+  }
+}
+template <int R>
+__device__ __forceinline__ void kbase_plan(RunArgs& a) {
+  __shared__ FAgg s_a[4];
+  __shared__ uint64_t s_n[4];
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  // the aggregate of the blocks before this one (each thread a consecutive range of them)
+  FPre cur{0ull, -1, false};
+  uint64_t nc = 0;
+  {
+    const uint32_t nb = blockIdx.x, per = (nb + 255) / 256;
+    FAgg acc = kFAggNone;
+    uint64_t ns = 0;
+    for (uint32_t k = t * per; k < nb && k < (t + 1) * per; ++k) {
+      acc = f_combine(acc, unpack_blk(a.bsum[4 * k], a.bsum[4 * k + 1]));
+      ns += a.bsum[4 * k + 2];
+    }
+    uint64_t tn;
+    const FAgg b = block_fagg_total(acc, ns, s_a, s_n, &tn);
+    cur = f_apply(cur, b);
+    nc = tn;
+  }
+  // this thread's tiles: their aggregate, then the exclusive ordered scan over the threads
+  const uint4* rec = reinterpret_cast<const uint4*>(a.trec);
+  const uint32_t t0 = blockIdx.x * (256 * R) + (uint32_t)t * R;
+  FAgg acc = kFAggNone;
+  uint64_t ns = 0;
+  for (int r = 0; r < R; ++r)
+    if (t0 + r < a.ntiles) {
+      const uint4 q = rec[t0 + r];
+      acc = f_combine(acc, plan_agg(q));
+      ns += q.y >> 16;
+    }
+  const FAgg incl = wave_incl_scan_fagg(acc, lane);
+  const uint64_t nincl = wave_incl_scan_add(ns, lane);
+  __syncthreads();
+  if (lane == 63) { s_a[wv] = incl; s_n[wv] = nincl; }
+  __syncthreads();
+  for (int k = 0; k < wv; ++k) { cur = f_apply(cur, s_a[k]); nc += s_n[k]; }
+  {
+    FAgg ex;  // lanes before mine (lane 0: none)
+    ex.bytes = (uint32_t)__shfl_up((int)incl.bytes, 1, 64);
+    ex.span = (uint32_t)__shfl_up((int)incl.span, 1, 64);
+    ex.crel = __shfl_up(incl.crel, 1, 64);
+    const int fl = __shfl_up((incl.has ? 1 : 0) | (incl.sel ? 2 : 0), 1, 64);
+    ex.has = fl & 1;
+    ex.sel = (fl & 2) != 0;
+    if (lane) cur = f_apply(cur, ex);
+    nc += nincl - ns;
+  }
+  // the tiles: output base, carried-in run, the copy record k_tcopy reads (TRec with the
+  // runs' destination shift in place of the selected lines), run slot 0
+  for (int r = 0; r < R; ++r) {
+    const uint32_t tile = t0 + r;
+    if (tile >= a.ntiles) break;
+    const uint4 q = rec[tile];
+    const FAgg x = plan_agg(q);
+    const uint32_t carried = f_carried(x.span, cur.sel, cur.crel);
+    const uint32_t lo = cur.crel > 0 ? (uint32_t)cur.crel : 0u;
+    const uint32_t kept = x.bytes + carried, nsel = q.y >> 16, own = q.z;
+    const uint32_t s = a.tile_seg[tile];
+    const SegDesc sd = a.segs[s];
+    const uint64_t src = sd.base + (uint64_t)(tile - sd.tile0) * kTile;
+    a.kbase[2 * tile] = cur.off;
+    a.kbase[2 * tile + 1] = nc;
+    const uint32_t nruns = own == kRunsRecompute ? (uint32_t)kRunsRecompute : ((own + 1u) | kRunsShifted);
+    reinterpret_cast<uint4*>(a.trec)[tile] = make_uint4((uint32_t)src, (uint32_t)(src >> 32), kept, nruns | (carried << 16));
+    if (own != kRunsRecompute) a.truns[(size_t)tile * kRunSlots] = lo;  // (length: up to run 1's destination)
+    if (tile == sd.tile0) { a.segout[s].out_lo = cur.off; a.segout[s].sel_lo = nc; }
+    if (tile + 1 == sd.tile0 + sd.ntiles) { a.segout[s].out_hi = cur.off + kept; a.segout[s].sel_hi = nc + nsel; }
+    cur = f_apply(cur, x);
+    nc += nsel;
+  }
+}
+
 // Reduce-then-scan of the tiles' (kept bytes, selected lines): 256 x R tiles per block.
 template <int R>
 __device__ __forceinline__ void ksum_body(RunArgs& a) {
   __shared__ uint64_t s_w[2][4];
   if (a.counters[2] || !a.counters[kCtrDense]) return;
+  if (planned(a)) { ksum_plan<R>(a); return; }
   const uint32_t t0 = blockIdx.x * (256 * R) + threadIdx.x;
   uint64_t b = 0, c = 0;
 #pragma unroll
@@ -2831,6 +3097,7 @@ __device__ __forceinline__ void kbase_body(RunArgs& a) {
   __shared__ uint64_t s_base[2];
   if (a.counters[2] || !a.counters[kCtrDense]) return;
   if (blockIdx.x * (256u * R) >= a.ntiles) return;  // launched on k_cgather's grid (k_cmove)
+  if (planned(a)) { kbase_plan<R>(a); return; }
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const uint32_t t0 = blockIdx.x * (256 * R) + t;
   {
@@ -3106,7 +3373,11 @@ __global__ __launch_bounds__(64 * kTcWaves) void k_tcopy(RunArgs a, const uint4*
     r.src = (uint64_t)q.x | ((uint64_t)q.y << 32);
     r.kept = q.z;
     r.nruns = (uint16_t)(q.w & 0xFFFFu);
-    r.nsel = (uint16_t)(q.w >> 16);
+    // nsel becomes the destination shift of runs 1.. (planned runs: run 0 is the carried-in
+    // line's, set by k_cmove after the scan listed the others), else 0
+    const bool shifted = r.nruns != kRunsRecompute && (r.nruns & kRunsShifted);
+    r.nsel = shifted ? (uint16_t)(q.w >> 16) : (uint16_t)0;
+    if (r.nruns != kRunsRecompute) r.nruns = (uint16_t)(r.nruns & ~kRunsShifted);
     return r;
   };
   auto issue = [&](uint32_t t, const TRec& r) __attribute__((always_inline)) {
@@ -3148,8 +3419,9 @@ __global__ __launch_bounds__(64 * kTcWaves) void k_tcopy(RunArgs a, const uint4*
       uint4* l = reinterpret_cast<uint4*>(s_buf);
       KLF_TC_ROWS(KLF_TC_STORE)
       if (cr.nruns != kRunsRecompute) {
-        if ((uint32_t)lane < cr.nruns) s_run[lane] = rw0;
-        if ((uint32_t)lane + 64 < cr.nruns) s_run[lane + 64] = rw1;
+        const uint32_t sh = (uint32_t)cr.nsel << 16;
+        if ((uint32_t)lane < cr.nruns) s_run[lane] = rw0 + (lane ? sh : 0u);
+        if ((uint32_t)lane + 64 < cr.nruns) s_run[lane + 64] = rw1 + sh;
       }
     }
     // the next tile's loads go out before this tile's copy

@@ -297,6 +297,9 @@ struct RunArgs {
   // grep none with --tail -1: k_scatter goes after k_tailw and builds the global line index
   // only for the line gather; the dense path lists its lines from the scan's slots
   uint32_t lazy_index;
+  // the scan plans the dense compaction (kept runs per tile + tile aggregates; needs truns):
+  // k_tkeep's listing pass is skipped unless a line was deferred
+  uint32_t plan_runs;
   // per-pattern counts (KLF_FILTER_PATTERN_COUNTS): pcount[segment * n_cids + cid] lines,
   // each (line, cid) counted once through the `pairs` hash set (open addressing, u64 keys)
   uint32_t count_pats;

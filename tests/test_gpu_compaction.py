@@ -239,3 +239,40 @@ def test_lazy_line_index(gpu, monkeypatch, lazy):
                         assert r.last_unparsed(i) == _last_unparsed(s), i
                     assert np.array_equal(r.lines(i), want[i][1]), i
             r.free()
+
+
+@pytest.mark.parametrize("plan", ["1", "0"])
+def test_planned_runs(gpu, monkeypatch, plan):
+    """Runs without patterns and --tail -1 take the dense copy from the scan's own plans (each
+    tile's kept runs and aggregate; k_cmid / k_cmove scan the aggregates for the output
+    offsets and carried-in runs, no listing pass).  Over lines spanning several tiles, tiles
+    of more than 128 lines (runs listed by k_tcopy), a prefix straddling a tile edge, empty
+    contents, fragments and empty streams, since on and off, KLF_PLAN_RUNS=0 (k_tkeep lists
+    every tile) and 1 equal the C oracle; a re-tail of the result lists the runs again."""
+    monkeypatch.setenv("KLF_PLAN_RUNS", plan)
+    monkeypatch.setenv("KLF_COMPACT", "dense")
+    edge = synth.generate(synth.TEXT, 3, 0, 8180)
+    edge = edge[:edge.rfind(b"\n") + 1]
+    edge = edge + b"x" * (8192 - 10 - len(edge)) + b"\n" + b"2024-10-22T00:59:59.123456789Z straddles\n"
+    streams = [synth.generate(synth.LONGJSON, 8, 0, 900_000, permille=5), b"",
+               b"".join(b"2024-10-22T00:00:%02dZ %d\n" % (i % 60, i % 7) for i in range(30000)),
+               synth.generate(synth.TEXT, 9, 3, 500_000, drop_final_nl=True), edge,
+               b"2024-10-22T00:00:01Z \n2024-10-22T00:00:02Z \n2024-10-22T00:00:03Z"]
+    with E.Engine(0, grep=[]) as eng:
+        for since in (None, SINCE):
+            eng.reset()
+            eng.set_streams(len(streams))
+            for i, s in enumerate(streams):
+                if s:
+                    eng.stage(i, s)
+            r = eng.run(since=since, n_streams=len(streams))
+            for i, s in enumerate(streams):
+                out, _, _, c = co.filter_stream(s, since or co.GO_ZERO_TIME, -1, [], want_lines=False, want_bits=False)
+                assert r.stream(i).out == out, (since, i)
+                assert r.stream(i).counts["selected"] == c["selected"], (since, i)
+            r2 = r.retail(40)
+            r.free()
+            for i, s in enumerate(streams):
+                out, _, _, _ = co.filter_stream(s, since or co.GO_ZERO_TIME, 40, [], want_lines=False, want_bits=False)
+                assert r2.stream(i).out == out, (since, i)
+            r2.free()
