@@ -705,7 +705,9 @@ __global__ __launch_bounds__(kThreads, MODE == kScanGen ? 3 : KLF_SCAN_OCC) void
               const uint32_t c = off + (mt >> 2);
               const uint32_t e = j + 1 < nlines ? (list[j + 1] & kSlotOff) : (uint32_t)tile_len;
               if (sel && e > c) { src = c; len = e - c; }
-              starts = off < (uint32_t)tile_len;
+              // (a line starting at the tile end -- the last byte is '\n' -- starts the next
+              // tile, whose list does not hold it: counted here, in its stream)
+              starts = off <= (uint32_t)tile_len;
               if (j + 1 == nlines) { lsel = sel ? 1u : 0u; lcrel = f_sat((int32_t)c - tile_len); }
             }
             const uint32_t incl = wave_incl_scan_add(len, lane);

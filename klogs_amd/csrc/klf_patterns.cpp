@@ -1468,12 +1468,15 @@ void place_tables(CompiledSet& out, const DataStats* st) {
     for (uint32_t b = 0; b < q; ++b) g |= (uint32_t)(uint8_t)s[k + b] << (8 * b);
     return (g | out.qf_fold) & out.qf_mask;
   };
-  auto common = [&](uint8_t c) -> int {  // rough frequency rank of a byte in log text
+  uint8_t rank[256];  // rough frequency rank of a byte in log text
+  for (uint32_t c0 = 0; c0 < 256; ++c0) {
+    uint8_t c = (uint8_t)c0;
     if (loose && c >= 'A' && c <= 'Z') c |= 0x20;
-    if ((c >= 'a' && c <= 'z') || c == ' ' || (c >= '0' && c <= '9')) return 4;  // words, numbers, timestamps
-    if (strchr("\":,=./{}-TZ", c) && c) return 3;                                  // JSON / timestamp punctuation
-    return 1;  // upper case, '_', other punctuation, control and high bytes
-  };
+    rank[c0] = ((c >= 'a' && c <= 'z') || c == ' ' || (c >= '0' && c <= '9')) ? 4  // words, numbers, timestamps
+               : (c && strchr("\":,=./{}-TZ", c)) ? 3                             // JSON / timestamp punctuation
+               : 1;  // upper case, '_', other punctuation, control and high bytes
+  }
+  auto common = [&](uint8_t c) -> int { return rank[c]; };
   // gram -> needles sampling it so far: a flat open-addressing table (grams are < 2^32 - 1)
   struct Used {
     std::vector<uint32_t> key, cnt;
