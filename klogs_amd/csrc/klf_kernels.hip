@@ -184,7 +184,8 @@ constexpr int kTcChunks = kTile / 16 + 8;
 // streams.  Deferred lines (non-canonical prefixes, decided later by fix_tile) void the
 // plan: the run then lists its tiles from the line slots (k_tkeep).
 struct FAgg {
-  uint32_t bytes, span;
+  uint64_t bytes;  // (the blocks before a k_cmove block: the whole output so far, past 4 GiB)
+  uint32_t span;
   int32_t crel;
   bool has, sel;
 };
@@ -235,7 +236,7 @@ __device__ __forceinline__ FAgg wave_incl_scan_fagg(FAgg x, int lane) {
 #pragma unroll
   for (int d = 1; d < 64; d <<= 1) {
     FAgg y;
-    y.bytes = (uint32_t)__shfl_up((int)x.bytes, d, 64);
+    y.bytes = __shfl_up(x.bytes, d, 64);
     y.span = (uint32_t)__shfl_up((int)x.span, d, 64);
     y.crel = __shfl_up(x.crel, d, 64);
     const int fl = __shfl_up((x.has ? 1 : 0) | (x.sel ? 2 : 0), d, 64);
@@ -244,16 +245,6 @@ __device__ __forceinline__ FAgg wave_incl_scan_fagg(FAgg x, int lane) {
     if (lane >= d) x = f_combine(y, x);
   }
   return x;
-}
-__device__ __forceinline__ FAgg fagg_lane(const FAgg& x, int src) {
-  FAgg y;
-  y.bytes = (uint32_t)__builtin_amdgcn_readlane((int)x.bytes, src);
-  y.span = (uint32_t)__builtin_amdgcn_readlane((int)x.span, src);
-  y.crel = __builtin_amdgcn_readlane(x.crel, src);
-  const int fl = __builtin_amdgcn_readlane((x.has ? 1 : 0) | (x.sel ? 2 : 0), src);
-  y.has = fl & 1;
-  y.sel = (fl & 2) != 0;
-  return y;
 }
 
 // Any-test: nonzero when some byte of the 16 equals the byte replicated in c4.  One
@@ -2950,7 +2941,7 @@ __device__ __forceinline__ uint64_t pack_blk(const FAgg& b) {
 }
 __device__ __forceinline__ FAgg unpack_blk(uint64_t bytes, uint64_t v) {
   FAgg b;
-  b.bytes = (uint32_t)bytes;
+  b.bytes = bytes;
   b.span = (uint32_t)v;
   b.has = (v >> 32) & 1u;
   b.sel = (v >> 33) & 1u;
@@ -3034,7 +3025,7 @@ __device__ __forceinline__ void kbase_plan(RunArgs& a) {
   for (int k = 0; k < wv; ++k) { cur = f_apply(cur, s_a[k]); nc += s_n[k]; }
   {
     FAgg ex;  // lanes before mine (lane 0: none)
-    ex.bytes = (uint32_t)__shfl_up((int)incl.bytes, 1, 64);
+    ex.bytes = __shfl_up(incl.bytes, 1, 64);
     ex.span = (uint32_t)__shfl_up((int)incl.span, 1, 64);
     ex.crel = __shfl_up(incl.crel, 1, 64);
     const int fl = __shfl_up((incl.has ? 1 : 0) | (incl.sel ? 2 : 0), 1, 64);
@@ -3052,7 +3043,7 @@ __device__ __forceinline__ void kbase_plan(RunArgs& a) {
     const FAgg x = plan_agg(q);
     const uint32_t carried = f_carried(x.span, cur.sel, cur.crel);
     const uint32_t lo = cur.crel > 0 ? (uint32_t)cur.crel : 0u;
-    const uint32_t kept = x.bytes + carried, nsel = q.y >> 16, own = q.z;
+    const uint32_t kept = (uint32_t)x.bytes + carried, nsel = q.y >> 16, own = q.z;
     const uint32_t s = a.tile_seg[tile];
     const SegDesc sd = a.segs[s];
     const uint64_t src = sd.base + (uint64_t)(tile - sd.tile0) * kTile;
