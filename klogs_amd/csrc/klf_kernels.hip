@@ -686,7 +686,8 @@ __global__ __launch_bounds__(kThreads, MODE == kScanGen ? 3 : KLF_SCAN_OCC) void
               a.truns + (size_t)tile * kRunSlots, 0, fits ? kRunSlots * 4 : 0, 0x00020000);
           uint32_t nr = 0, dacc = 0, ns = 0, lsel = 0;
           int32_t lcrel = -1;
-          auto round = [&](uint32_t b0, bool store) __attribute__((always_inline)) {
+          // one round of 64 lines: the run word and its store offset (dropped: none)
+          auto round = [&](uint32_t b0, uint32_t& w, uint32_t& o) __attribute__((always_inline)) {
             const uint32_t j = b0 + (uint32_t)lane;
             uint32_t src = 0, len = 0;
             bool sel = false, starts = false;
@@ -705,16 +706,21 @@ __global__ __launch_bounds__(kThreads, MODE == kScanGen ? 3 : KLF_SCAN_OCC) void
             const uint64_t bm = __ballot(len != 0);
             const uint32_t idx = nr + (uint32_t)__popcll(bm & ((1ull << lane) - 1ull));
             // slot 0 is the carried-in run's (k_cmove)
-            if (store)
-              __builtin_amdgcn_raw_buffer_store_b32(src | ((dacc + incl - len) << 16), rr,
-                                                    len ? 4u * (idx + 1u) : 0x7FFF0000u, 0, 0);
+            w = src | ((dacc + incl - len) << 16);
+            o = len ? 4u * (idx + 1u) : 0x7FFF0000u;
             nr += (uint32_t)__popcll(bm);
             dacc += (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
             ns += (uint32_t)__popcll(__ballot(sel && starts));
           };
-          round(0u, true);
-          round(64u, true);
-          for (uint32_t b0 = 128u; b0 < nlines; b0 += 64) round(b0, false);  // (no runs stored)
+          uint32_t w0 = 0, o0 = 0x7FFF0000u, w1 = 0, o1 = 0x7FFF0000u;
+          round(0u, w0, o0);
+          __builtin_amdgcn_raw_buffer_store_b32(w0, rr, o0, 0, 0);
+          if (nlines > 64u) round(64u, w1, o1);  // (its store issues either way: a fixed count)
+          __builtin_amdgcn_raw_buffer_store_b32(w1, rr, o1, 0, 0);
+          for (uint32_t b0 = 128u; b0 < nlines; b0 += 64) {  // (no runs stored)
+            uint32_t w, o;
+            round(b0, w, o);
+          }
           const uint32_t lastl = nlines ? ((nlines - 1u) & 63u) : 0u;
           const uint32_t psel = nlines ? (uint32_t)__builtin_amdgcn_readlane((int)lsel, (int)lastl) : 0u;
           const int32_t pcrel = nlines ? __builtin_amdgcn_readlane(lcrel, (int)lastl) : -1;
