@@ -979,6 +979,7 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
   // lazy line index (grep none, --tail -1; KLF_LAZY_INDEX=0 turns it off)
   const bool lazy_index = mode == klf::CompiledSet::kNone && f->tail < 0 &&
                           !(getenv("KLF_LAZY_INDEX") && !strcmp(getenv("KLF_LAZY_INDEX"), "0"));
+  bool win_ok = true;  // (a run that needs every line's index -- k_match's fallback -- turns it off)
   if (const char* v = getenv("KLF_COMPACT")) compact_mode = !strcmp(v, "sparse") ? 1u : !strcmp(v, "dense") ? 2u : 0u;
   // The output buffer: sized for the whole input up front when the run keeps about as much
   // as it reads (no --tail limit: C3-like), else grown
@@ -1076,6 +1077,9 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
     a.lazy_index = lazy_index ? 1u : 0u;
     a.plan_runs = (lazy_index && want_truns && compact_mode != 1 &&
                    !(getenv("KLF_PLAN_RUNS") && !strcmp(getenv("KLF_PLAN_RUNS"), "0"))) ? 1u : 0u;
+    a.win_index = (win_ok && mode == klf::CompiledSet::kGeneral && e->cs.qf_on && e->cs.rx_count == 0 && !count &&
+                   !e->cs.also_all && !(getenv("KLF_WIN_INDEX") && !strcmp(getenv("KLF_WIN_INDEX"), "0"))) ? 1u : 0u;
+    a.scatter_mode = 0;
     a.count_pats = count ? 1u : 0u;
     a.pcount = count ? e->d_pcount.as<uint32_t>() : nullptr;
     a.pairs = count ? e->d_pairs.as<uint64_t>() : nullptr;
@@ -1183,6 +1187,10 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
       e->pool_cap = std::max<uint64_t>(e->pool_cap, (uint64_t)counters[klf::kCtrPool] + 1024);
       continue;
     }
+    if (a.win_index && counters[klf::kCtrRedo]) {  // k_match needed the whole index: rerun with it
+      win_ok = false;
+      continue;
+    }
     pairs_over = count && counters[klf::kCtrPairsOver] != 0;
     if (pairs_over && pair_reruns < 2 && e->pairs_log2 < 28) {  // the pair set filled: a larger one
       // distinct pairs <= the set's capacity + the failed inserts; size for load <= 1/2
@@ -1198,7 +1206,7 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
       if (getenv("KLF_DIAG")) fprintf(stderr, "[klf] output buffer grown to %zu B\n", e->d_out.cap);
     }
     e->last_args = a;
-    if (a.lazy_index && counters[klf::kCtrDense]) e->index_pending.push_back(a);
+    if ((a.lazy_index && counters[klf::kCtrDense]) || a.win_index) e->index_pending.push_back(a);
     e->last_gen = r->gen;
     e->line_density = (double)(r->so[nsegs - 1].line_hi + 1) / (double)total_bytes;
     if (f->tail >= 0 && counters[klf::kCtrDense]) e->dense_tail_seen = true;
@@ -1355,11 +1363,14 @@ static int ensure_index(klf_engine* e) {
   HIPCHK(e, hipSetDevice(e->device), "hipSetDevice");
   for (auto& x : e->index_pending) {
     x.lazy_index = 0;
+    x.win_index = 0;
+    x.scatter_mode = 0;
     HIPCHK(e, klf::launch_scatter(x, e->stream, e->num_cus), "launch line index");
   }
   HIPCHK(e, hipStreamSynchronize(e->stream), "sync line index");
   e->index_pending.clear();
   e->last_args.lazy_index = 0;
+  e->last_args.win_index = 0;
   return KLF_OK;
 }
 

@@ -1432,6 +1432,12 @@ __device__ __forceinline__ void scatter_body(RunArgs& a, uint32_t bid, uint32_t 
       const uint32_t k0 = first ? 0 : 1, k1 = last ? ts.events : ts.events + 1;
       n = k1 > k0 ? k1 - k0 : 0;
       const uint64_t base = a.tile_base[tile];
+      if (a.scatter_mode == 1 && !(ts.flags & 4u)) n = 0;  // (no deferred line here)
+      if (a.scatter_mode == 2) {  // lines of the tail window and the one after it (its end)
+        const SegOut& so = a.segout[s];
+        const uint64_t f = base + k0;
+        if (so.win_hi <= so.win_lo || f > so.win_hi || f + n <= so.win_lo) n = 0;
+      }
       ScatterEnt e;
       e.base = base + k0;
       e.rel_lo = (uint64_t)rel_lo;
@@ -2045,6 +2051,10 @@ __global__ __launch_bounds__(256) void k_match(RunArgs a) {
   const bool prefiltered =
       a.grep_mode == kGrepGeneral && a.pats.qf_on && !a.counters[kCtrQOver] && !a.counters[kCtrHitsOver];
   if (prefiltered && !a.match_all) return;
+  if (a.win_index) {  // every line's index is needed: the host reruns with the whole index
+    if (blockIdx.x == 0 && threadIdx.x == 0) a.counters[kCtrRedo] = 1u;
+    return;
+  }
   const uint64_t L = a.segout[a.nsegs - 1].line_hi;
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   for (uint64_t l = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; l < L; l += stride) {
@@ -3671,6 +3681,10 @@ hipError_t launch_pipeline(const RunArgs& a0, hipStream_t st, hipEvent_t* ev, in
     if (nsb == 0) nsb = 1;
     hipLaunchKernelGGL(k_scatter_verify, dim3(nsb + num_cus * 8), dim3(256), 0, st, a, nsb);
     KLF_TRY(hipGetLastError());
+  } else if (a.win_index) {  // tiles with deferred lines now: their match bits come from the slots
+    RunArgs w = a;
+    w.scatter_mode = 1;
+    KLF_TRY(launch_scatter(w, st, num_cus));
   } else if (!a.lazy_index) {
     KLF_TRY(launch_scatter(a, st, num_cus));
   }
@@ -3726,6 +3740,11 @@ static hipError_t launch_tail_stage(const RunArgs& a, hipStream_t st, hipEvent_t
   hipLaunchKernelGGL(k_tailw, dim3(a.nsegs), dim3(256), 0, st, a);
   KLF_TRY(hipGetLastError());
   if (a.lazy_index) KLF_TRY(launch_scatter(a, st, num_cus));  // (exits at once on the dense path)
+  if (a.win_index) {  // the tail windows' lines
+    RunArgs w = a;
+    w.scatter_mode = 2;
+    KLF_TRY(launch_scatter(w, st, num_cus));
+  }
   if (ev && a.stage_times) KLF_TRY(hipEventRecord(ev[4], st));  // ~5 us of idle GPU each
   {
     const uint32_t gt = (a.ntiles + 4 * kTkBatch - 1) / (4 * kTkBatch);

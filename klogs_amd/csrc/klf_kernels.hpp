@@ -42,6 +42,7 @@ constexpr uint32_t kCtrQueue = 6;                   // counters[6]: NFA candidat
 constexpr uint32_t kCtrQOver = 7;                    // counters[7]: queue overflow -> k_match
 constexpr uint32_t kHitSlots = 32;                   // prefilter hits a tile records itself
 constexpr uint32_t kCtrHits = 8;                     // counters[8]: spilled prefilter hits
+constexpr uint32_t kCtrRedo = 20;                    // counters[20]: a windowed-index run needs the whole index (rerun)
 constexpr uint32_t kCtrHitsOver = 9;                 // counters[9]: hit list overflow -> k_match
 constexpr uint32_t kCtrFlatHits = 12;                // counters[12]: hit slots flattened by k_tbase
 constexpr uint32_t kCtrCopyChunks = 11;              // counters[11]: output copy chunks (k_cgather)
@@ -300,6 +301,11 @@ struct RunArgs {
   // the scan plans the dense compaction (kept runs per tile + tile aggregates; needs truns):
   // k_tkeep's listing pass is skipped unless a line was deferred
   uint32_t plan_runs;
+  // literal-only pattern sets (no regex, no per-pattern counts): the global line index is
+  // built after k_tailw for the lines of the tail windows only (k_scatter mode 2); tiles
+  // with deferred lines before k_mcount (mode 1: their match bits come from the slots)
+  uint32_t win_index;
+  uint32_t scatter_mode;  // k_scatter: 0 every tile, 1 tiles with deferred lines, 2 tiles meeting a window
   // per-pattern counts (KLF_FILTER_PATTERN_COUNTS): pcount[segment * n_cids + cid] lines,
   // each (line, cid) counted once through the `pairs` hash set (open addressing, u64 keys)
   uint32_t count_pats;

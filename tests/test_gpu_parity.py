@@ -380,3 +380,23 @@ def test_clamped_capacity_with_regex_set_fails_cleanly(gpu, monkeypatch):
         ref = po.filter_stream(d, GZ, -1, po.compile_patterns([], rx))
         assert r.stream(0).out == ref.out
         r.free()
+
+
+@pytest.mark.parametrize("win", ["1", "0"])
+def test_windowed_line_index(gpu, monkeypatch, win):
+    """Literal-only sets build the global line index after the tail rule, for the tail
+    windows' lines only (k_scatter mode 2; tiles with deferred lines before the counts,
+    mode 1).  Against the C oracle with KLF_WIN_INDEX on and off: tails from none to all
+    lines, non-canonical prefixes (deferred lines that match), both compaction paths; the
+    whole index on demand (line offsets, klf_retail); and the hit-list overflow, whose
+    k_match fallback needs every line (the run is redone with the whole index)."""
+    monkeypatch.setenv("KLF_WIN_INDEX", win)
+    lits = [l for l in synth.c4_literals(1024)][:300] + [b"ms"]
+    streams = [synth.generate(synth.MIXED, 21, 0, 600_000, permille=30),
+               synth.generate(synth.ADVERSARIAL, 22, 1, 80_000, drop_final_nl=True, permille=40), b"",
+               synth.generate(synth.MIXED, 23, 3, 300_000, permille=5)]
+    for tail in (-1, 0, 1, 100, 10**9):
+        check_against_c(streams, None, tail, lits)
+    check_against_c(streams, (synth.T0 + 1800, 0), 25, lits)
+    monkeypatch.setenv("KLF_HITS_CAP", "16")
+    check_against_c(streams, None, 50, lits)
