@@ -1077,8 +1077,10 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
     a.lazy_index = lazy_index ? 1u : 0u;
     a.plan_runs = (lazy_index && want_truns && compact_mode != 1 &&
                    !(getenv("KLF_PLAN_RUNS") && !strcmp(getenv("KLF_PLAN_RUNS"), "0"))) ? 1u : 0u;
-    a.win_index = (win_ok && mode == klf::CompiledSet::kGeneral && e->cs.qf_on && e->cs.rx_count == 0 && !count &&
-                   !e->cs.also_all && !(getenv("KLF_WIN_INDEX") && !strcmp(getenv("KLF_WIN_INDEX"), "0"))) ? 1u : 0u;
+    a.win_index = (win_ok &&
+                   (mode == klf::CompiledSet::kLiteral1 ||
+                    (mode == klf::CompiledSet::kGeneral && e->cs.qf_on && e->cs.rx_count == 0 && !count && !e->cs.also_all)) &&
+                   !(getenv("KLF_WIN_INDEX") && !strcmp(getenv("KLF_WIN_INDEX"), "0"))) ? 1u : 0u;
     a.scatter_mode = 0;
     a.count_pats = count ? 1u : 0u;
     a.pcount = count ? e->d_pcount.as<uint32_t>() : nullptr;

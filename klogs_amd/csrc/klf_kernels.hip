@@ -635,7 +635,7 @@ __global__ __launch_bounds__(kThreads, MODE == kScanGen ? 3 : KLF_SCAN_OCC) void
 
     // The per-tile work on the line list, instantiated for the LDS list (normal tiles) and
     // the global pool (dense tiles).
-    uint32_t n_parsed = 0, n_since = 0, n_defer = 0, carry = 0;
+    uint32_t n_parsed = 0, n_since = 0, n_defer = 0, carry = 0, n_hit = 0;
     auto work = [&](uint32_t* list) __attribute__((always_inline)) {
       // ---- line starts -> list[j] = start offset in the tile ----
       if (first && lane == 0) list[0] = 0u;
@@ -747,8 +747,10 @@ __global__ __launch_bounds__(kThreads, MODE == kScanGen ? 3 : KLF_SCAN_OCC) void
         if (lo > 0) {  // the line starts in this tile: deferred lines are searched by k_fixup
           const uint32_t v = list[lo - 1];
           const uint32_t mt = v >> 16;
-          if (!(v & kSlotDefer) && (mt & Meta::kParsed) && (uint32_t)pos >= (v & kSlotOff) + (mt >> 2))
+          if (!(v & kSlotDefer) && (mt & Meta::kParsed) && (uint32_t)pos >= (v & kSlotOff) + (mt >> 2)) {
             atomicOr(&list[lo - 1], kSlotHit);
+            ++n_hit;
+          }
         } else {  // carried in from an earlier tile: k_scatter decides (furthest hit wins)
           const uint32_t c1 = (uint32_t)(pos + 1 + (int32_t)kCarryBias);  // pos >= -kCarryBias
           carry = carry > c1 ? carry : c1;
@@ -1050,7 +1052,8 @@ __global__ __launch_bounds__(kThreads, MODE == kScanGen ? 3 : KLF_SCAN_OCC) void
        // the pool).  16 B per lane: narrower per-lane stores cost several times more per byte.
       const uint32_t w0 = agg, w1 = dense ? pool_base : 0u;
       const uint32_t w2 = (pp & 0xFFFFu) | (qq << 16);
-      const uint32_t w3 = ((dense ? 1u : 0u) | (carry ? 2u : 0u) | (dd ? 4u : 0u)) |
+      const bool hh = LIT && __any(n_hit != 0);  // some line starting here holds the literal
+      const uint32_t w3 = ((dense ? 1u : 0u) | (carry ? 2u : 0u) | (dd ? 4u : 0u) | (hh ? 8u : 0u)) |
                           ((uint32_t)(uint16_t)(GEN ? tile_hits : carry) << 16);  // GEN: hit slots used
       const uint32_t nunits = abl ? 0u : (dense ? 8u : ((kRecHead + nlines + 31u) & ~31u) / 4u);
       const __amdgpu_buffer_rsrc_t rrs = __builtin_amdgcn_make_buffer_rsrc(trec, 0, (int)(nunits * 16u), 0x00020000);
@@ -1432,7 +1435,7 @@ __device__ __forceinline__ void scatter_body(RunArgs& a, uint32_t bid, uint32_t 
       const uint32_t k0 = first ? 0 : 1, k1 = last ? ts.events : ts.events + 1;
       n = k1 > k0 ? k1 - k0 : 0;
       const uint64_t base = a.tile_base[tile];
-      if (a.scatter_mode == 1 && !(ts.flags & 4u)) n = 0;  // (no deferred line here)
+      if (a.scatter_mode == 1 && !(ts.flags & 12u)) n = 0;  // (no deferred line, no literal hit here)
       if (a.scatter_mode == 2) {  // lines of the tail window and the one after it (its end)
         const SegOut& so = a.segout[s];
         const uint64_t f = base + k0;

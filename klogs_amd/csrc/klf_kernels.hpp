@@ -166,7 +166,7 @@ struct TileStat {
   uint32_t pool_base;  // dense tiles: first pool slot
   uint16_t parsed, since_ok;
   uint16_t flags;      // bit0 dense (slots in the pool), bit1 literal hit in the carried-in line,
-                       // bit2 some line deferred to k_fixup
+                       // bit2 some line deferred to k_fixup, bit3 literal hit in a line starting here
   uint16_t carry_off;  // literal: 1 + kCarryBias + tile offset of the furthest hit in the
                        // carried-in line (0 = none); general sets: hit slots used
 };
@@ -301,9 +301,10 @@ struct RunArgs {
   // the scan plans the dense compaction (kept runs per tile + tile aggregates; needs truns):
   // k_tkeep's listing pass is skipped unless a line was deferred
   uint32_t plan_runs;
-  // literal-only pattern sets (no regex, no per-pattern counts): the global line index is
-  // built after k_tailw for the lines of the tail windows only (k_scatter mode 2); tiles
-  // with deferred lines before k_mcount (mode 1: their match bits come from the slots)
+  // literal patterns only (one literal, or a set without regexes and per-pattern counts):
+  // the global line index is built after k_tailw for the lines of the tail windows only
+  // (k_scatter mode 2); tiles with deferred lines or single-literal hits before k_mcount
+  // (mode 1: their match bits come from the slots)
   uint32_t win_index;
   uint32_t scatter_mode;  // k_scatter: 0 every tile, 1 tiles with deferred lines, 2 tiles meeting a window
   // per-pattern counts (KLF_FILTER_PATTERN_COUNTS): pcount[segment * n_cids + cid] lines,

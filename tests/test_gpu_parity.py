@@ -384,8 +384,8 @@ def test_clamped_capacity_with_regex_set_fails_cleanly(gpu, monkeypatch):
 
 @pytest.mark.parametrize("win", ["1", "0"])
 def test_windowed_line_index(gpu, monkeypatch, win):
-    """Literal-only sets build the global line index after the tail rule, for the tail
-    windows' lines only (k_scatter mode 2; tiles with deferred lines before the counts,
+    """Literal patterns (a set without regexes, or one literal) build the global line index
+    after the tail rule, for the tail windows' lines only (k_scatter mode 2; tiles with deferred lines before the counts,
     mode 1).  Against the C oracle with KLF_WIN_INDEX on and off: tails from none to all
     lines, non-canonical prefixes (deferred lines that match), both compaction paths; the
     whole index on demand (line offsets, klf_retail); and the hit-list overflow, whose
@@ -395,8 +395,9 @@ def test_windowed_line_index(gpu, monkeypatch, win):
     streams = [synth.generate(synth.MIXED, 21, 0, 600_000, permille=30),
                synth.generate(synth.ADVERSARIAL, 22, 1, 80_000, drop_final_nl=True, permille=40), b"",
                synth.generate(synth.MIXED, 23, 3, 300_000, permille=5)]
-    for tail in (-1, 0, 1, 100, 10**9):
-        check_against_c(streams, None, tail, lits)
-    check_against_c(streams, (synth.T0 + 1800, 0), 25, lits)
+    for grep in (lits, [synth.NEEDLE], [b"ms"]):  # a set; one literal (k_scan<lit>: hit tiles flagged)
+        for tail in (-1, 0, 1, 100, 10**9):
+            check_against_c(streams, None, tail, grep)
+        check_against_c(streams, (synth.T0 + 1800, 0), 25, grep)
     monkeypatch.setenv("KLF_HITS_CAP", "16")
     check_against_c(streams, None, 50, lits)
