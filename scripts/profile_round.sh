@@ -18,7 +18,7 @@ if [ "$what" != pmc ]; then
   echo "trace done"
   for c in c3 c4 c5; do  # per-config kernel splits (the bench trace mixes C2 with the extras)
     timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/trace_$c" -o run \
-      -- python3 scripts/run_config.py "$c" --steps 3 > "$out/run_$c.json" 2> "$out/run_$c.err"
+      -- python3 scripts/run_config.py "$c" --steps 8 > "$out/run_$c.json" 2> "$out/run_$c.err"
     echo "trace $c done"
   done
 fi
