@@ -416,9 +416,6 @@ __device__ __forceinline__ bool parse_fast(const uint8_t* lds, uint32_t o, const
 #ifndef KLF_ANY_BATCH
 #define KLF_ANY_BATCH 8  // chunk reads in flight in the scan's newline any-test
 #endif
-#ifndef KLF_TWO_NOFOLD
-#define KLF_TWO_NOFOLD 1  // two-level probe: a fold-free copy of the pair stage for case-sensitive sets
-#endif
 #ifndef KLF_SCAN_OCC
 // plain / literal scans: waves per SIMD the launch bounds ask for.  3 leaves the compiler
 // up to 168 VGPRs: C3's plain scan 1.84 -> 1.67 ms, C2's literal scan unchanged within the
@@ -893,30 +890,26 @@ __global__ __launch_bounds__(kThreads, MODE == kScanGen ? 3 : KLF_SCAN_OCC) void
       if (TWO) {
         // stage 1: the exact set of the probed grams' low two bytes (pair words [0, 2048)):
         // sv bit i = the sample at my0 + 4i passes (each chunk's four dwords, two chunks per
-        // step with their eight word reads in flight)
+        // step with their eight word reads in flight).  The raw bytes probe: for a folded set
+        // the host lists every case variant of a pair (p with p | 0x2020 in the set), so the
+        // stage has no fold OR and the word's bit is the sample's own low five bits.  Step v
+        // puts chunk (v + rot) & 7 at bits 4v.. (constant shifts); one rotate at the end
         uint32_t sv = 0;
-        // (a case-sensitive set, fold 0, takes a copy of the loop without the OR per sample)
-        auto pair_stage = [&](auto folded) __attribute__((always_inline)) {
 #pragma unroll
-          for (int v = 0; v < (ABL(4) ? 0 : 8); v += 2) {
-            const uint32_t ca = ((uint32_t)v + rot) & 7u, cb = ((uint32_t)v + 1u + rot) & 7u;
-            const uint4 xa = *reinterpret_cast<const uint4*>(s_tile + my0 + 16u * ca);
-            const uint4 xb = *reinterpret_cast<const uint4*>(s_tile + my0 + 16u * cb);
-            const uint32_t f = decltype(folded)::value ? fold : 0u;
-            const uint32_t g[8] = {xa.x | f, xa.y | f, xa.z | f, xa.w | f, xb.x | f, xb.y | f, xb.z | f, xb.w | f};
-            uint32_t w[8];
+        for (int v = 0; v < (ABL(4) ? 0 : 8); v += 2) {
+          const uint32_t ca = ((uint32_t)v + rot) & 7u, cb = ((uint32_t)v + 1u + rot) & 7u;
+          const uint4 xa = *reinterpret_cast<const uint4*>(s_tile + my0 + 16u * ca);
+          const uint4 xb = *reinterpret_cast<const uint4*>(s_tile + my0 + 16u * cb);
+          const uint32_t g[8] = {xa.x, xa.y, xa.z, xa.w, xb.x, xb.y, xb.z, xb.w};
+          uint32_t w[8];
 #pragma unroll
-            for (int k = 0; k < 8; ++k)
-              w[k] = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(s_qf) + (bfe_u32(g[k], 5, 11) << 2));
+          for (int k = 0; k < 8; ++k)
+            w[k] = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(s_qf) + (bfe_u32(g[k], 5, 11) << 2));
 #pragma unroll
-            for (int k = 0; k < 8; ++k) {
-              const uint32_t bit = __builtin_amdgcn_ubfe(w[k], g[k], 1u);  // bit g mod 32 (v_bfe_u32 reads offset[4:0])
-              sv |= bit << (4u * (k < 4 ? ca : cb) + (uint32_t)(k & 3));
-            }
-          }
-        };
-        if (KLF_TWO_NOFOLD && fold == 0u) pair_stage(std::false_type{});
-        else pair_stage(std::true_type{});
+          for (int k = 0; k < 8; ++k)
+            sv |= __builtin_amdgcn_ubfe(w[k], g[k], 1u) << (4 * v + k);  // bit g mod 32 (v_bfe_u32 reads offset[4:0])
+        }
+        sv = __builtin_amdgcn_alignbit(sv, sv, 32u - 4u * rot);  // rotate left by 4 rot (shift mod 32): chunk c at bits 4c..
         // samples at or past the tile's end (4i >= nvalid) do not count
         sv &= nvalid >= kLaneBytes ? ~0u : ((1u << ((uint32_t)(nvalid + 3) >> 2)) - 1u);
         // stage 2: the survivors' 3-bit probe into the Bloom half; a hit's byte position

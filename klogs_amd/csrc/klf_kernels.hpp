@@ -84,7 +84,8 @@ constexpr uint32_t kRxPreNone = 0xFFFFFFFFu;         // rx_pre: no bound (= klf_
 // 0.017).
 // Two-level layout (qf_k = kQfTwoLevel, large sets at stride 4): the samples first test an
 // exact set of the probed grams' low two bytes (bitmap words [0, kQfPairWords): bit
-// (g & 0xFFFF)); only the survivors (~5 % of log text for the 1,024-literal C4 set) take the
+// (g & 0xFFFF), over raw bytes: a folded set lists every case variant of its pairs, so the
+// scan probes the data's bytes as they are); only the survivors (~5 % of log text for the 1,024-literal C4 set) take the
 // 3-bit probe, into a Bloom filter of the remaining kQfPairWords words (11-bit buckets).
 constexpr uint32_t kQfTwoLevel = 5;
 constexpr uint32_t kQfPairWords = 2048;

@@ -1551,7 +1551,14 @@ void place_tables(CompiledSet& out, const DataStats* st) {
       const uint32_t h = qf_hash(g, w24, out.qf_k);
       const uint32_t bw = qf_bucket(g, w24, out.qf_k);
       out.qf_bitmap[qf_bloom_word(g, w24, out.qf_k)] |= qf_bits(g, h, out.qf_k);
-      if (out.qf_k == kQfTwoLevel) out.qf_bitmap[(g & 0xFFFFu) >> 5] |= 1u << (g & 31u);
+      if (out.qf_k == kQfTwoLevel) {  // the exact pair set, over raw bytes: every case variant
+        const uint32_t g16 = g & 0xFFFFu, fv = out.qf_fold & 0xFFFFu & g16;
+        for (uint32_t x = fv;; x = (x - 1u) & fv) {  // subsets of the folded bits
+          const uint32_t pr = g16 & ~x;
+          out.qf_bitmap[pr >> 5] |= 1u << (pr & 31u);
+          if (!x) break;
+        }
+      }
       bent.push_back({bw, i << 8 | k});
     }
   }

@@ -162,6 +162,27 @@ def test_c4_literal_set_mixed_lines(gpu, monkeypatch, since, tail, two):
     check_against_c([d, synth.generate(synth.MIXED, 4, 1, 700_000, permille=50)], since, tail, lits)
 
 
+def test_two_level_folded(gpu, monkeypatch):
+    """The two-level probe of a case-folded set: the pair stage tests the data's raw bytes
+    against a bitmap that lists every case variant of the needles' pairs (p with p | 0x2020
+    in the folded set).  The C5 regexes (loose factors) and case-insensitive literals whose
+    occurrences in the data are re-cased."""
+    monkeypatch.setenv("KLF_QF_TWO", "force")
+    rx = synth.c5_regexes()
+    streams = [synth.generate(synth.LONGJSON, 7, i, 1_000_000, permille=30) for i in range(2)]
+    assert E.debug_prefilter_hits(streams[0][:1 << 16], streams[0][:1 << 16], match=rx)["k"] == 5
+    check_against_py(streams, None, -1, match=rx)
+    lits = [l for l in synth.c4_literals(1024) if len(l) >= 6][:40]
+    pats = [b"(?i)" + b"".join(b"\\%c" % c if c in b".^$*+?()[]{}|\\" else b"%c" % c for c in l) for l in lits]
+    rng = random.Random(3)
+    recase = lambda b: bytes(c ^ 0x20 if (65 <= c <= 90 or 97 <= c <= 122) and rng.random() < 0.5 else c
+                             for c in b)
+    d = _with_inserts(synth.generate(synth.MIXED, 13, 0, 600_000, permille=5), [recase(l) for l in lits], 5, 40)
+    assert E.debug_prefilter_hits(d[:1 << 16], d[:1 << 16], match=pats)["k"] == 5
+    check_against_py([d], None, -1, match=pats)
+    check_against_py([d], (synth.T0 + 1800, 0), 30, match=pats)
+
+
 @pytest.mark.parametrize("since,tail", [(None, -1), ((synth.T0 + 1800, 0), 50)])
 def test_grid6_needles(gpu, since, tail):
     """Literal sets whose shortest needle is 8-9 bytes: the 3-per-16-B sampling grid
