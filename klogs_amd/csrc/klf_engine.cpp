@@ -190,9 +190,18 @@ struct klf_engine {
   bool dense_tail_seen = false;  // a --tail run took the dense compaction (keep its run table)
   HostBuf h_rb;  // run readback: counters (64 B), then the SegOut table
   HostBuf h_stage;  // pinned staging of the prefilter tables (upload_prefilter)
+  // The literals' Aho-Corasick automaton (deferred lines, the fallback matcher): klf_open
+  // starts a host thread that builds it and uploads it as one block (d_acblk, one
+  // synchronous copy); ensure_ac joins it before the first launch that may read it, so the
+  // build overlaps the first run's sampling and needle placement
+  std::thread ac_thread;
+  std::vector<std::vector<uint8_t>> ac_lits;
+  klf::AcTables ac_tabs;
+  hipError_t ac_err = hipSuccess;
+  DevBuf d_acblk;
   hipEvent_t stage_ev = nullptr;  // the staged copies have drained
   bool stage_ev_pending = false;
-  hipEvent_t ev[7] = {};
+  hipEvent_t ev[9] = {};  // [7], [8]: k_scan's dispatch (hipExtLaunchKernel start / stop)
   klf::RunArgs last_args{};  // arguments of the latest completed run (klf_retail)
   // the latest run's global line index is still to be built (lazy index, dense path): the
   // k_scatter launch that builds it
@@ -437,6 +446,59 @@ static hipError_t upload_pattern_tables(klf_engine* e, bool tune_later) {
   return hipSuccess;
 }
 
+// the automaton thread: build, then one block on the device and one copy
+static void ac_build_upload(klf_engine* e) {
+  klf::build_ac(e->ac_lits, e->ac_tabs);
+  const klf::AcTables& t = e->ac_tabs;
+  hipError_t h = hipSetDevice(e->device);
+  const std::pair<const void*, size_t> parts[5] = {
+      {t.cls.data(), t.cls.size()}, {t.next.data(), t.next.size() * 4}, {t.accept.data(), t.accept.size()},
+      {t.out.data(), t.out.size() * 4}, {t.dict.data(), t.dict.size() * 4}};
+  DevBuf* dst[5] = {&e->d_ac_class, &e->d_ac_next, &e->d_ac_accept, &e->d_ac_out, &e->d_ac_dict};
+  size_t off[5], total = 0;
+  for (int k = 0; k < 5; ++k) {
+    off[k] = total;
+    total += (std::max<size_t>(parts[k].second, 256) + 255) & ~(size_t)255;
+  }
+  std::vector<uint8_t> host(total, 0);
+  for (int k = 0; k < 5; ++k) memcpy(host.data() + off[k], parts[k].first, parts[k].second);
+  if (h == hipSuccess) h = e->d_acblk.ensure(total);
+  if (h == hipSuccess) h = hipMemcpy(e->d_acblk.p, host.data(), total, hipMemcpyHostToDevice);
+  if (h == hipSuccess)
+    for (int k = 0; k < 5; ++k) {
+      dst[k]->release();
+      dst[k]->p = e->d_acblk.as<uint8_t>() + off[k];
+      dst[k]->cap = (std::max<size_t>(parts[k].second, 256) + 255) & ~(size_t)255;
+      dst[k]->borrowed = true;
+    }
+  e->ac_err = h;
+}
+
+// Joins the automaton thread (if any) and points the device patterns at its tables.
+static int ensure_ac(klf_engine* e) {
+  if (!e->ac_thread.joinable()) return KLF_OK;
+  e->ac_thread.join();
+  if (e->ac_err != hipSuccess) return hip_err(e, e->ac_err, "Aho-Corasick tables");
+  klf::CompiledSet& cs = e->cs;
+  klf::AcTables& t = e->ac_tabs;
+  cs.ac_states = t.states;
+  cs.ac_classes = t.classes;
+  cs.ac_class = std::move(t.cls);
+  cs.ac_next = std::move(t.next);
+  cs.ac_accept = std::move(t.accept);
+  cs.ac_out = std::move(t.out);
+  cs.ac_dict = std::move(t.dict);
+  klf::DevPatterns& P = e->dpats;
+  P.ac_states = cs.ac_states;
+  P.ac_classes = cs.ac_classes;
+  P.ac_class = e->d_ac_class.as<uint8_t>();
+  P.ac_next = e->d_ac_next.as<uint32_t>();
+  P.ac_accept = e->d_ac_accept.as<uint8_t>();
+  P.ac_out = e->d_ac_out.as<int32_t>();
+  P.ac_dict = e->d_ac_dict.as<uint32_t>();
+  return KLF_OK;
+}
+
 extern "C" int klf_open(const klf_config* cfg, klf_engine** out) {
   if (!cfg || !out || (cfg->n_patterns && !cfg->patterns)) return KLF_EINVAL;
   *out = nullptr;
@@ -458,8 +520,9 @@ extern "C" int klf_open(const klf_config* cfg, klf_engine** out) {
   // needles), unless tuning is off (KLF_QF_TUNE=0: placed here, from byte-class estimates)
   const char* tune_env = getenv("KLF_QF_TUNE");
   const bool tune_later = !(tune_env && strcmp(tune_env, "0") == 0);
-  const bool compiled = klf::compile_set(pats, kinds, e->cs, err, code, !tune_later, true);
+  const bool compiled = klf::compile_set(pats, kinds, e->cs, err, code, !tune_later, true, true);
   e->tune_later = tune_later;
+  e->ac_lits.swap(e->cs.ac_lits);  // (the automaton thread's input; built after the device setup)
   if (compiled && e->cs.also_all_pending) {
     e->pend_pats = pats;
     e->pend_kinds = kinds;
@@ -521,6 +584,13 @@ extern "C" int klf_open(const klf_config* cfg, klf_engine** out) {
     e->pairs_log2 = (uint32_t)std::max(4L, std::min(atol(pl), 28L));
   if (const char* hc = getenv("KLF_HITS_CAP"))  // tests: force the hit-list overflow fallback
     e->hits_cap_max = (uint64_t)std::max(1L, std::min(atol(hc), 1L << 28));
+  if (!e->ac_lits.empty()) {
+    try {
+      e->ac_thread = std::thread(ac_build_upload, e);
+    } catch (...) {  // no thread: build it here
+      ac_build_upload(e);
+    }
+  }
   if (getenv("KLF_DIAG"))
     fprintf(stderr, "[klf] open: total %.1f us\n",
             std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t_open0).count());
@@ -533,6 +603,7 @@ static void free_chunk(klf_engine::StageChunk& c);
 
 extern "C" void klf_close(klf_engine* e) {
   if (!e) return;
+  if (e->ac_thread.joinable()) e->ac_thread.join();
   (void)hipStreamSynchronize(e->stream);
   if (e->copy_stream) (void)hipStreamSynchronize(e->copy_stream);
   for (DevBuf* b : {&e->d_lit, &e->d_ac_class, &e->d_ac_next, &e->d_ac_accept, &e->d_rx_class, &e->d_rx_b,
@@ -548,6 +619,7 @@ extern "C" void klf_close(klf_engine* e) {
   e->h_stage.release();
   for (DevBuf* b : {&e->d_ac_out, &e->d_ac_dict, &e->d_pcount, &e->d_pairs}) b->release();
   e->d_block.release();
+  e->d_acblk.release();
   e->copier.reset();
   {
     std::lock_guard<std::mutex> g(e->mu);
@@ -845,6 +917,7 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
   r->n_streams = n_streams;
   r->seg_of.assign(n_streams, -1);
   if (e->cs.also_all_pending && (f->flags & KLF_FILTER_PATTERN_COUNTS)) {
+    if (const int rc = ensure_ac(e); rc != KLF_OK) return rc;
     // the first run asking for per-pattern counts of a set with an always-pattern: compile
     // the other patterns now (klf_open kept the set as kAll); if that fails the filter stays
     // kAll's and the counts are reported unavailable
@@ -1087,6 +1160,8 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
     a.pairs = count ? e->d_pairs.as<uint64_t>() : nullptr;
     a.pairs_log2 = e->pairs_log2;
   };
+  if (const int rc = ensure_ac(e); rc != KLF_OK) return rc;  // (before fill_args copies dpats)
+  mark("automaton");
   bool overflow = false, pairs_over = false;
   for (int attempt = 0, line_reruns = 0, pair_reruns = 0; attempt < 4; ++attempt) {
     if (count) {
@@ -1251,9 +1326,11 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
   if (f->flags & KLF_FILTER_STAGE_TIMES) {
     if (hipEventElapsedTime(&ms, e->ev[0], e->ev[1]) == hipSuccess) r->ms[5] = ms;
     if (hipEventElapsedTime(&ms, e->ev[1], e->ev[6]) == hipSuccess) r->ms[6] = ms;
-  } else if (hipEventElapsedTime(&ms, e->ev[0], e->ev[6]) == hipSuccess) {
-    r->ms[6] = ms;  // the scan with the run's k_init (~2 us) in front of it
   }
+  if (hipEventElapsedTime(&ms, e->ev[7], e->ev[8]) == hipSuccess)
+    r->ms[6] = ms;  // k_scan's dispatch alone
+  else if (hipEventElapsedTime(&ms, e->ev[0], e->ev[6]) == hipSuccess && !(f->flags & KLF_FILTER_STAGE_TIMES))
+    r->ms[6] = ms;  // the scan with the run's k_init (~2 us) in front of it
   r->total_lines = r->so[nsegs - 1].line_hi;
   for (auto& s : r->so) r->total_out = std::max(r->total_out, s.out_hi);
   *out = rp.release();

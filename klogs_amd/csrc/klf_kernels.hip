@@ -13,6 +13,7 @@
 //                  blocks) + content gather copy
 // Semantics: SPEC.md (kubelet logs.go ReadLogs / tail.go FindTailLineStartIndex /
 // Go time.Parse(RFC3339Nano) / bytes.Contains / regexp.Match).
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -3461,31 +3462,43 @@ __global__ __launch_bounds__(64 * kTcWaves) void k_tcopy(RunArgs a, const uint4*
 }
 
 // Data statistics for the prefilter's layout and window choice (one-off, first batch): the
-// grams at every 4th byte position of a sample of the batch into the 3-gram and 4-gram
-// count-min sketches (two rows each, global atomics: they bound the pass) and every byte
-// into the histogram (LDS per block, one global add per bin and block).
+// 2-grams at even offsets of a sample of the batch and every byte, counted per block in LDS
+// (65,536 u16 pair counters, two per dword: a block's 1,024 dwords add at most 2,048 to one
+// counter) and added to the global histogram once per nonzero counter and block.  Global
+// atomics per sample serialised on the hot pairs of log text (`""`, `  `): 257 us for
+// C5's 1 MiB sample.
+constexpr uint32_t kGhDwords = 1024;  // sampled dwords per block
 __global__ __launch_bounds__(256) void k_gramhist(const uint8_t* bytes, const SegDesc* segs, uint32_t nsegs,
                                                   uint64_t sample, uint32_t fold, uint32_t* hist) {
+  __shared__ uint32_t s_p[32768];
   __shared__ uint32_t s_b[256];
-  s_b[threadIdx.x] = 0;
+  const uint32_t t = threadIdx.x;
+  for (uint32_t i = t; i < 32768u; i += 256u) s_p[i] = 0;
+  s_b[t] = 0;
   __syncthreads();
   const uint32_t nseg = nsegs < 16 ? nsegs : 16;
   const uint32_t step = nsegs / nseg;
   const uint64_t per = sample / 4;  // dwords per segment sample
-  for (uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; w < per * nseg; w += (uint64_t)gridDim.x * blockDim.x) {
+  const uint64_t w0b = (uint64_t)blockIdx.x * kGhDwords, w1b = w0b + kGhDwords;
+  for (uint64_t w = w0b + t; w < w1b && w < per * nseg; w += 256u) {
     const SegDesc sd = segs[(uint32_t)(w / per) * step];
     const uint64_t o = (w % per) * 4;
     if (o + 8 > sd.len) continue;
-    const uint32_t* p = reinterpret_cast<const uint32_t*>(bytes + sd.base + o);
-    const uint32_t w0 = p[0];
-    const uint32_t g = w0 | fold;
-    atomicAdd(&hist[kGramHistPairs + (g & 0xFFFFu)], 1u);  // the 2-grams at even offsets
-    atomicAdd(&hist[kGramHistPairs + (g >> 16)], 1u);
+    const uint32_t x = *reinterpret_cast<const uint32_t*>(bytes + sd.base + o);
+    const uint32_t g = x | fold;
+    const uint32_t lo = g & 0xFFFFu, hi = g >> 16;
+    atomicAdd(&s_p[lo >> 1], 1u << ((lo & 1u) * 16u));
+    atomicAdd(&s_p[hi >> 1], 1u << ((hi & 1u) * 16u));
 #pragma unroll
-    for (int k = 0; k < 4; ++k) atomicAdd(&s_b[(w0 >> (8 * k)) & 0xFFu], 1u);
+    for (int k = 0; k < 4; ++k) atomicAdd(&s_b[(x >> (8 * k)) & 0xFFu], 1u);
   }
   __syncthreads();
-  if (s_b[threadIdx.x]) atomicAdd(&hist[threadIdx.x], s_b[threadIdx.x]);
+  for (uint32_t i = t; i < 32768u; i += 256u) {
+    const uint32_t v = s_p[i];
+    if (v & 0xFFFFu) atomicAdd(&hist[kGramHistPairs + 2u * i], v & 0xFFFFu);
+    if (v >> 16) atomicAdd(&hist[kGramHistPairs + 2u * i + 1u], v >> 16);
+  }
+  if (s_b[t]) atomicAdd(&hist[t], s_b[t]);
 }
 
 // Capture assembly: block b copies 1 MiB of piece b / kAsmBlocks (pieces are 64 MiB
@@ -3562,8 +3575,8 @@ hipError_t launch_gramhist(const uint8_t* bytes, const SegDesc* segs, uint32_t n
   hipError_t e = hipMemsetAsync(hist, 0, kGramHistWords * 4, st);
   if (e != hipSuccess) return e;
   const uint32_t nseg = nsegs < 16 ? nsegs : 16;
-  const uint64_t threads = nseg * (sample / 4);
-  const uint32_t grid = (uint32_t)((threads + 255) / 256 < 1024 ? (threads + 255) / 256 : 1024);
+  const uint64_t dwords = nseg * (sample / 4);
+  const uint32_t grid = (uint32_t)((dwords + kGhDwords - 1) / kGhDwords);
   hipLaunchKernelGGL(k_gramhist, dim3(grid ? grid : 1), dim3(256), 0, st, bytes, segs, nsegs, sample, fold, hist);
   return hipGetLastError();
 }
@@ -3571,6 +3584,9 @@ hipError_t launch_gramhist(const uint8_t* bytes, const SegDesc* segs, uint32_t n
 size_t nfa_lds_bytes(const DevPatterns& P) {
   return 8ull * P.rx_count * (P.rx_classes + P.rx_maxpos + 4) + 256;
 }
+
+// the scan's timing events for the current launch_pipeline call (ev[7], ev[8]), else null
+thread_local hipEvent_t t_scan_ev[2] = {nullptr, nullptr};
 
 template <int MODE, int QS, int QK = 3, int QQ = 4, bool QA = false>
 hipError_t launch_scan(const RunArgs& a, hipStream_t st, int num_cus) {
@@ -3583,7 +3599,11 @@ hipError_t launch_scan(const RunArgs& a, hipStream_t st, int num_cus) {
   }
   uint32_t grid = (uint32_t)(num_cus * occ);
   if (grid > a.ntiles) grid = a.ntiles;
-  hipLaunchKernelGGL((k_scan<MODE, QS, QK, QQ, QA>), dim3(grid), dim3(kThreads), 0, st, a, a.tile_seg, a.segs);
+  if (t_scan_ev[0])  // the dispatch's own start / end timestamps (no event record beside it)
+    hipExtLaunchKernelGGL((k_scan<MODE, QS, QK, QQ, QA>), dim3(grid), dim3(kThreads), 0, st, t_scan_ev[0],
+                          t_scan_ev[1], 0, a, a.tile_seg, a.segs);
+  else
+    hipLaunchKernelGGL((k_scan<MODE, QS, QK, QQ, QA>), dim3(grid), dim3(kThreads), 0, st, a, a.tile_seg, a.segs);
   return hipGetLastError();
 }
 template <int QS, int QQ>
@@ -3638,6 +3658,9 @@ hipError_t launch_pipeline(const RunArgs& a0, hipStream_t st, hipEvent_t* ev, in
   // scan's own time is then taken from ev[0] (k_init in front of it: ~2 us)
   if (ev && a.stage_times) KLF_TRY(hipEventRecord(ev[1], st));
   {
+    // k_scan alone (the roofline kernel): ev[7] / ev[8] carry the dispatch's own timestamps
+    t_scan_ev[0] = ev ? ev[7] : nullptr;
+    t_scan_ev[1] = ev ? ev[8] : nullptr;
     if (a.grep_mode == kGrepLit1)
       KLF_TRY((launch_scan<kScanLit, 1>(a, st, num_cus)));
     else if (a.grep_mode == kGrepGeneral && a.pats.qf_on && a.pats.qf_stride == 4)
@@ -3652,7 +3675,8 @@ hipError_t launch_pipeline(const RunArgs& a0, hipStream_t st, hipEvent_t* ev, in
       KLF_TRY((launch_gen<1>(a, st, num_cus)));
     else
       KLF_TRY((launch_scan<kScanPlain, 1>(a, st, num_cus)));
-    if (ev) KLF_TRY(hipEventRecord(ev[6], st));  // k_scan alone (the roofline kernel)
+    t_scan_ev[0] = t_scan_ev[1] = nullptr;
+    if (ev) KLF_TRY(hipEventRecord(ev[6], st));
     if (!a.tindex_wide) {
       hipLaunchKernelGGL((k_tindex<4, 0>), dim3((a.ntiles + 1023) / 1024), dim3(256), 0, st, a);
       KLF_TRY(hipGetLastError());

@@ -878,8 +878,76 @@ int log_byte_class(uint8_t c) {
   return 6;                                                    // lowercase, space, common punctuation
 }
 
+bool ac_alphabet_ok(const std::vector<std::vector<uint8_t>>& lits) {
+  std::bitset<256> used;
+  for (auto& l : lits)
+    for (uint8_t c : l) used[c] = true;
+  return used.count() <= 255;
+}
+
+void build_ac(const std::vector<std::vector<uint8_t>>& lits, AcTables& t) {
+  t = AcTables();
+  t.cls.assign(256, 0);
+  uint32_t ncls = 1;
+  {
+    std::bitset<256> used;
+    for (auto& l : lits)
+      for (uint8_t c : l) used[c] = true;
+    for (int c = 0; c < 256; ++c)
+      if (used[c]) t.cls[c] = (uint8_t)ncls++;
+  }
+  // goto trie straight into the DFA table (0 = no child: the root is nobody's child),
+  // then BFS: a state's missing edges copy its fail state's finished row
+  size_t cap = 1;
+  for (auto& l : lits) cap += l.size();
+  std::vector<uint32_t> nxt(cap * (size_t)ncls, 0u);
+  std::vector<uint8_t> term(cap, 0);
+  std::vector<int32_t> term_id(cap, -1);  // literal id ending exactly at a state
+  size_t ns = 1;
+  for (size_t li = 0; li < lits.size(); ++li) {
+    uint32_t st = 0;
+    for (uint8_t c : lits[li]) {
+      uint32_t& x = nxt[(size_t)st * ncls + t.cls[c]];
+      if (!x) x = (uint32_t)ns++;
+      st = x;
+    }
+    term[st] = 1;
+    term_id[st] = (int32_t)li;
+  }
+  nxt.resize(ns * (size_t)ncls);
+  t.states = (uint32_t)ns;
+  t.classes = ncls;
+  t.accept.assign(ns, 0);
+  t.out.assign(term_id.begin(), term_id.begin() + ns);
+  t.dict.assign(ns, 0u);
+  std::vector<uint32_t> fail(ns, 0), queue;
+  queue.reserve(ns);
+  for (uint32_t c = 0; c < ncls; ++c)
+    if (const uint32_t x = nxt[c]) queue.push_back(x);
+  t.accept[0] = term[0];
+  for (size_t qh = 0; qh < queue.size(); ++qh) {
+    const uint32_t st = queue[qh];
+    const uint32_t fs = fail[st];
+    t.accept[st] = term[st] | t.accept[fs];
+    // dictionary link: the nearest state on the fail chain where a literal ends
+    t.dict[st] = (uint32_t)(term_id[fs] >= 0 ? (int)fs : (int)t.dict[fs]);
+    uint32_t* row = &nxt[(size_t)st * ncls];
+    const uint32_t* frow = &nxt[(size_t)fs * ncls];
+    for (uint32_t c = 0; c < ncls; ++c) {
+      if (const uint32_t x = row[c]) {  // a trie child (its row is still pure trie)
+        fail[x] = frow[c];
+        queue.push_back(x);
+      } else {
+        row[c] = frow[c];
+      }
+    }
+  }
+  t.next = std::move(nxt);
+}
+
 bool compile_set(const std::vector<std::vector<uint8_t>>& pats, const std::vector<uint32_t>& kinds,
-                 CompiledSet& out, std::string& err, int& err_code, bool place, bool defer_also_all) {
+                 CompiledSet& out, std::string& err, int& err_code, bool place, bool defer_also_all,
+                 bool defer_ac) {
   out = CompiledSet();
   if (pats.empty()) {
     out.mode = CompiledSet::kNone;
@@ -1044,64 +1112,20 @@ bool compile_set(const std::vector<std::vector<uint8_t>>& pats, const std::vecto
 
   // ---- Aho-Corasick over the literals ----
   if (!lits.empty()) {
-    out.ac_class.assign(256, 0);
-    int ncls = 1;
-    {
-      std::vector<bool> used(256, false);
-      for (auto& l : lits)
-        for (uint8_t c : l) used[c] = true;
-      for (int c = 0; c < 256; ++c)
-        if (used[c]) out.ac_class[c] = (uint8_t)std::min(ncls++, 255);
-      if (ncls > 256) { err = "literal alphabet too large"; err_code = KLF_ETOOBIG; return false; }
+    if (!ac_alphabet_ok(lits)) { err = "literal alphabet too large"; err_code = KLF_ETOOBIG; return false; }
+    if (defer_ac) {
+      out.ac_lits = lits;
+    } else {
+      AcTables t;
+      build_ac(lits, t);
+      out.ac_states = t.states;
+      out.ac_classes = t.classes;
+      out.ac_class = std::move(t.cls);
+      out.ac_next = std::move(t.next);
+      out.ac_accept = std::move(t.accept);
+      out.ac_out = std::move(t.out);
+      out.ac_dict = std::move(t.dict);
     }
-    // goto trie straight into the DFA table (0 = no child: the root is nobody's child),
-    // then BFS: a state's missing edges copy its fail state's finished row
-    size_t cap = 1;
-    for (auto& l : lits) cap += l.size();
-    std::vector<uint32_t> nxt(cap * (size_t)ncls, 0u);
-    std::vector<uint8_t> term(cap, 0);
-    std::vector<int32_t> term_id(cap, -1);  // literal id ending exactly at a state
-    size_t ns = 1;
-    for (size_t li = 0; li < lits.size(); ++li) {
-      uint32_t st = 0;
-      for (uint8_t c : lits[li]) {
-        uint32_t& t = nxt[(size_t)st * ncls + out.ac_class[c]];
-        if (!t) t = (uint32_t)ns++;
-        st = t;
-      }
-      term[st] = 1;
-      term_id[st] = (int32_t)li;
-    }
-    if (ns >= (1u << 31)) { err = "AC automaton too large"; err_code = KLF_ETOOBIG; return false; }
-    nxt.resize(ns * (size_t)ncls);
-    out.ac_states = (uint32_t)ns;
-    out.ac_classes = (uint32_t)ncls;
-    out.ac_accept.assign(ns, 0);
-    out.ac_out.assign(term_id.begin(), term_id.begin() + ns);
-    out.ac_dict.assign(ns, 0u);
-    std::vector<uint32_t> fail(ns, 0), queue;
-    queue.reserve(ns);
-    for (int c = 0; c < ncls; ++c)
-      if (const uint32_t t = nxt[c]) queue.push_back(t);
-    out.ac_accept[0] = term[0];
-    for (size_t qh = 0; qh < queue.size(); ++qh) {
-      const uint32_t st = queue[qh];
-      const uint32_t fs = fail[st];
-      out.ac_accept[st] = term[st] | out.ac_accept[fs];
-      // dictionary link: the nearest state on the fail chain where a literal ends
-      out.ac_dict[st] = (uint32_t)(term_id[fs] >= 0 ? (int)fs : (int)out.ac_dict[fs]);
-      uint32_t* row = &nxt[(size_t)st * ncls];
-      const uint32_t* frow = &nxt[(size_t)fs * ncls];
-      for (int c = 0; c < ncls; ++c) {
-        if (const uint32_t t = row[c]) {  // a trie child (its row is still pure trie)
-          fail[t] = frow[c];
-          queue.push_back(t);
-        } else {
-          row[c] = frow[c];
-        }
-      }
-    }
-    out.ac_next = std::move(nxt);
   }
 
   // ---- regexes: shared byte classes by partition refinement ----

@@ -36,6 +36,22 @@ struct GlushkovTables {
   int npos = 0;
 };
 
+// Aho-Corasick DFA over a literal set (byte classes; a state's missing edges are its fail
+// state's, so every byte is one table step).
+struct AcTables {
+  uint32_t states = 0, classes = 0;
+  std::vector<uint8_t> cls;       // [256] byte -> class
+  std::vector<uint32_t> next;     // [states * classes]
+  std::vector<uint8_t> accept;    // [states] 1 if a literal ends here (via fail links)
+  std::vector<int32_t> out;       // [states] id of the literal ending exactly here, -1 none
+  std::vector<uint32_t> dict;     // [states] nearest fail-chain state with out >= 0 (0 none)
+};
+// The literals' byte classes need at most 255 (class 0 = bytes in no literal): checked
+// before the build, so a deferred build cannot fail.
+bool ac_alphabet_ok(const std::vector<std::vector<uint8_t>>& lits);
+// lits: sorted, deduplicated (ids = positions), no empty literal.
+void build_ac(const std::vector<std::vector<uint8_t>>& lits, AcTables& t);
+
 struct CompiledSet {
   enum Mode : uint32_t {
     kNone = 0,      // no patterns: G = every line
@@ -56,7 +72,11 @@ struct CompiledSet {
   std::vector<uint8_t> literal;  // kLiteral1
   uint32_t literal_anchor = 0;   // kLiteral1: index of its rarest byte in log text
 
-  // kGeneral: Aho-Corasick over the literals (empty when no literal).
+  // kGeneral: Aho-Corasick over the literals (empty when no literal).  compile_set(defer_ac)
+  // leaves it unbuilt (ac_states 0) and the literals in ac_lits: the engine builds and
+  // uploads it on a host thread while its first run samples the data and places the needles
+  // (the automaton serves only deferred lines and the fallback matcher).
+  std::vector<std::vector<uint8_t>> ac_lits;
   uint32_t ac_states = 0;
   uint32_t ac_classes = 0;
   std::vector<uint8_t> ac_class;    // [256] byte -> class
@@ -196,7 +216,7 @@ bool compile_regex(const uint8_t* pat, size_t n, GlushkovTables& out, std::strin
 // is wasted work on the klf_open path.
 bool compile_set(const std::vector<std::vector<uint8_t>>& pats, const std::vector<uint32_t>& kinds,
                  CompiledSet& out, std::string& err, int& err_code, bool place = true,
-                 bool defer_also_all = false);
+                 bool defer_also_all = false, bool defer_ac = false);
 
 // Expected-frequency class of a byte in log text (lower = rarer); picks scan anchors.
 int log_byte_class(uint8_t c);
