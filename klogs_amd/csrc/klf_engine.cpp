@@ -981,9 +981,10 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
                      memcmp(segs.data(), e->last_segs.data(), segs.size() * sizeof(SegDesc)) == 0;
   if (!same_layout) {
     HIPCHK(e, e->d_segs.ensure(nsegs * sizeof(SegDesc)), "alloc segs");
+    // (a pageable source: the runtime stages it before the call returns, so `segs` may go
+    // out of scope with no stream sync, which would wait for klf_open's table uploads)
     HIPCHK(e, hipMemcpyAsync(e->d_segs.p, segs.data(), nsegs * sizeof(SegDesc), hipMemcpyHostToDevice, st),
            "H2D segs");
-    HIPCHK(e, hipStreamSynchronize(st), "sync segs");
     HIPCHK(e, e->d_tile_seg.ensure(ntiles * 4 + 16), "alloc tile_seg");  // + whole 16-B loads past the end
   }
   mark("segs");

@@ -1504,16 +1504,19 @@ void place_tables(CompiledSet& out, const DataStats* st) {
   // gram -> needles sampling it so far: a flat open-addressing table (grams are < 2^32 - 1)
   struct Used {
     std::vector<uint32_t> key, cnt;
-    uint32_t mask;
+    uint32_t mask, shift;
     explicit Used(size_t n) {
       size_t cap = 64;
-      while (cap < 2 * n) cap <<= 1;
+      shift = 26;
+      while (cap < 2 * n) cap <<= 1, --shift;
       key.assign(cap, ~0u);
       cnt.assign(cap, 0u);
       mask = (uint32_t)cap - 1;
     }
+    // the product's top bits (its low bits follow only the gram's low bytes, which needles
+    // with a common prefix share: linear probing then walked long clusters)
     uint32_t slot(uint32_t g) const {
-      uint32_t i = (g * 0x9E3779B1u) & mask;
+      uint32_t i = (g * 0x9E3779B1u) >> shift;
       while (key[i] != ~0u && key[i] != g) i = (i + 1) & mask;
       return i;
     }
@@ -1617,22 +1620,27 @@ void place_tables(CompiledSet& out, const DataStats* st) {
 
 void stats_finish(DataStats& st) {
   st.marg.assign(256, 0.0);
+  st.inv_marg.assign(256, 0.0);
   st.pair_tot = 0;
+  st.inv_tot = 0;
   if (st.pair.size() >= 65536) {
     for (uint32_t x = 0; x < 65536; ++x) st.marg[x & 0xFFu] += st.pair[x];
     for (double m : st.marg) st.pair_tot += m;
+    if (st.pair_tot > 0) {
+      st.inv_tot = 1.0 / st.pair_tot;
+      for (int c = 0; c < 256; ++c) st.inv_marg[c] = st.pair_tot / (st.marg[c] + 128.0);
+    }
   }
 }
 
 double gram_share(const DataStats& st, uint32_t g, uint32_t q) {
-  if (st.pair.size() < 65536 || st.marg.size() != 256 || st.pair_tot <= 0) return 1.0;
-  // P(b0 b1) * prod P(b_i b_i+1) / P(b_i): pair counts + 1/2, marginals from the pairs
-  const double tot = st.pair_tot;
-  auto pr = [&](uint32_t a, uint32_t b) { return (st.pair[a | b << 8] + 0.5) / tot; };
-  double p = pr(g & 0xFFu, (g >> 8) & 0xFFu);
+  if (st.pair.size() < 65536 || st.inv_marg.size() != 256 || st.pair_tot <= 0) return 1.0;
+  // P(b0 b1) * prod P(b_i b_i+1) / P(b_i): pair counts + 1/2, marginals (+ 128) from the pairs
+  const double it = st.inv_tot;
+  double p = (st.pair[g & 0xFFFFu] + 0.5) * it;
   for (uint32_t i = 1; i + 1 < q; ++i) {
-    const uint32_t a = (g >> (8 * i)) & 0xFFu, b = (g >> (8 * i + 8)) & 0xFFu;
-    p *= pr(a, b) / ((st.marg[a] + 128.0) / tot);
+    const uint32_t a = (g >> (8 * i)) & 0xFFu, ab = (g >> (8 * i)) & 0xFFFFu;
+    p *= (st.pair[ab] + 0.5) * it * st.inv_marg[a];
   }
   return p;
 }

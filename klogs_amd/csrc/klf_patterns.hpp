@@ -156,9 +156,12 @@ struct DataStats {
   std::vector<uint32_t> pair;   // [65536] 2-gram b0 | b1 << 8
   std::vector<uint64_t> bytes;  // [256]
   uint64_t nbytes = 0;          // positions counted in `bytes`
-  // derived by stats_finish: 2-gram marginals and their total
+  // derived by stats_finish: 2-gram marginals and their total, and the reciprocals
+  // gram_share multiplies by (it runs ~20 K times per layout candidate of a large set)
   std::vector<double> marg;
   double pair_tot = 0;
+  double inv_tot = 0;
+  std::vector<double> inv_marg;  // [256] tot / (marg + 128)
 };
 // The derived fields, once the counts are in.
 void stats_finish(DataStats& st);
