@@ -293,7 +293,7 @@ def main():
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic, "traffic_source": traffic_src, "alg_bytes_per_launch": scan_alg,
                      "avg_launch_ms": round(scan_avg_s * 1e3, 4),
-                     "frac_source": "HIP events on the launch stream around k_scan, this run",
+                     "frac_source": "HIP events carrying the k_scan dispatch's own start / end timestamps (hipExtLaunchKernel), this run",
                      "frac_rocprof_committed": trace_frac, "rocprof_source": trace_src},
         "cpu_baseline": cpu,
         "extra": {"device_ms_per_step": round(dev_avg_s * 1e3, 4),

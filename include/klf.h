@@ -191,9 +191,9 @@ int klf_result_write(klf_result* r, const int* fds, uint32_t n_fds, uint64_t* wr
  * [0] scan stage (newline + line index + timestamp + since + fused grep prefilter),
  * [1] pattern verification / matchers, [2] counts + tail + window prefix, [3] compaction
  * (these four only with KLF_FILTER_STAGE_TIMES, else 0), [4] total device time,
- * [5] workspace memsets (KLF_FILTER_STAGE_TIMES, else 0), [6] the k_scan kernel (part of
- * [0]; without KLF_FILTER_STAGE_TIMES it includes the ~2 us workspace memset kernel in
- * front of it: one event fewer in the run).  n = entries written. */
+ * [5] workspace memsets (KLF_FILTER_STAGE_TIMES, else 0), [6] the k_scan kernel alone
+ * (part of [0]): the start / end timestamps of its own dispatch (hipExtLaunchKernel
+ * events, no event record beside it).  n = entries written. */
 int klf_result_timing(const klf_result* r, double* ms, uint32_t cap, uint32_t* n);
 /* Totals across streams. */
 int klf_result_totals(const klf_result* r, klf_counts* totals);
