@@ -3309,10 +3309,9 @@ __device__ __forceinline__ void copy_tile_runs(const uint8_t* s_buf, uint32_t* s
       }
       typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
       const u32x4 ov = {o[0], o[1], o[2], o[3]};
-#ifndef KLF_TC_ST_AUX
-#define KLF_TC_ST_AUX 0  // cache-policy bits of the output stores (timing variants)
-#endif
-      __builtin_amdgcn_raw_buffer_store_b128(ov, orsrc, c < c_end ? 16u * c : kDrop, 0, KLF_TC_ST_AUX);
+      // (non-temporal stores and / or loads measured no faster: C3 step 5.50-5.56 ms against
+      // 5.14-5.41, gpurun_out/r4r)
+      __builtin_amdgcn_raw_buffer_store_b128(ov, orsrc, c < c_end ? 16u * c : kDrop, 0, 0);
     }
     // head / tail chunks shared with the neighbouring tiles: only this tile's bytes, one
     // byte per lane (lanes 0-15 the head chunk, 16-31 the tail chunk; a chunk holding both
@@ -3372,19 +3371,7 @@ __global__ __launch_bounds__(64 * kTcWaves) void k_tcopy(RunArgs a, const uint4*
   // (named registers: an array here is put on the scratch stack)
 #define KLF_TC_ROWS(X) X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7)
 #define KLF_TC_DECL(q) uint4 v##q = make_uint4(0, 0, 0, 0);
-#ifndef KLF_TC_NT_LOAD
-#define KLF_TC_NT_LOAD 0  // 1: the tile's rows as non-temporal loads
-#endif
-#if KLF_TC_NT_LOAD
-#define KLF_TC_LOAD(q)                                                                       \
-  {                                                                                          \
-    typedef uint32_t u32x4n __attribute__((ext_vector_type(4)));                             \
-    const u32x4n t = __builtin_nontemporal_load(reinterpret_cast<const u32x4n*>(gp) + q * 64 + lane); \
-    v##q = make_uint4(t.x, t.y, t.z, t.w);                                                   \
-  }
-#else
 #define KLF_TC_LOAD(q) v##q = gp[q * 64 + lane];
-#endif
 #define KLF_TC_STORE(q) l[q * 64 + lane] = v##q;
   KLF_TC_ROWS(KLF_TC_DECL)
   uint32_t rw0 = 0, rw1 = 0;
