@@ -763,7 +763,7 @@ def run_extra(name: str, args, local: int, now: int) -> dict:
     else:  # the batch was dropped for the checks: the stage split of the timed runs' last
         stage = last.timing()
     n = sum(lens)
-    scan_s = float(np.mean(scan_ms)) / 1e3
+    scan_s = max(float(np.mean(scan_ms)) / 1e3, 1e-12)  # (0: a build without the scan's events)
     dev_s = float(np.mean(total_ms)) / 1e3
     step_alg = n + 8 * (tot["lines"] + len(lens)) + 4 * (tot["lines"] // 32 + 1) + tot["out_bytes"]
     out = {

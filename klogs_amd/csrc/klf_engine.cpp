@@ -201,7 +201,7 @@ struct klf_engine {
   DevBuf d_acblk;
   hipEvent_t stage_ev = nullptr;  // the staged copies have drained
   bool stage_ev_pending = false;
-  hipEvent_t ev[9] = {};  // [7], [8]: k_scan's dispatch (hipExtLaunchKernel start / stop)
+  hipEvent_t ev[9] = {};  // [7], [8]: k_scan's dispatch (hipExtLaunchKernel start / stop); [6] unused
   klf::RunArgs last_args{};  // arguments of the latest completed run (klf_retail)
   // the latest run's global line index is still to be built (lazy index, dense path): the
   // k_scatter launch that builds it
@@ -1324,14 +1324,10 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
     for (int k = 0; k < 4; ++k)  // scan stage, match, tail stage, compaction
       if (hipEventElapsedTime(&ms, e->ev[k + 1], e->ev[k + 2]) == hipSuccess) r->ms[k] = ms;
   if (hipEventElapsedTime(&ms, e->ev[0], e->ev[5]) == hipSuccess) r->ms[4] = ms;
-  if (f->flags & KLF_FILTER_STAGE_TIMES) {
+  if (f->flags & KLF_FILTER_STAGE_TIMES)
     if (hipEventElapsedTime(&ms, e->ev[0], e->ev[1]) == hipSuccess) r->ms[5] = ms;
-    if (hipEventElapsedTime(&ms, e->ev[1], e->ev[6]) == hipSuccess) r->ms[6] = ms;
-  }
-  if (hipEventElapsedTime(&ms, e->ev[7], e->ev[8]) == hipSuccess)
-    r->ms[6] = ms;  // k_scan's dispatch alone
-  else if (hipEventElapsedTime(&ms, e->ev[0], e->ev[6]) == hipSuccess && !(f->flags & KLF_FILTER_STAGE_TIMES))
-    r->ms[6] = ms;  // the scan with the run's k_init (~2 us) in front of it
+  if (hipEventElapsedTime(&ms, e->ev[7], e->ev[8]) == hipSuccess) r->ms[6] = ms;  // k_scan's dispatch alone
+  (void)hipGetLastError();  // an event pair this run did not record: no sticky error for the next launch check
   r->total_lines = r->so[nsegs - 1].line_hi;
   for (auto& s : r->so) r->total_out = std::max(r->total_out, s.out_hi);
   *out = rp.release();
@@ -1381,6 +1377,7 @@ extern "C" int klf_retail(klf_engine* e, klf_result* prev, int64_t tail, klf_res
     if (h != hipSuccess) { delete r; return hip_err(e, h, "klf_retail"); }
     float ms;
     if (hipEventElapsedTime(&ms, e->ev[0], e->ev[5]) == hipSuccess) r->ms[4] = ms;
+    (void)hipGetLastError();
   }
   for (auto& s : r->so) r->total_out = std::max(r->total_out, s.out_hi);
   r->gen = ++e->gen;  // prev's output buffer is rewritten: prev is stale from here on

@@ -18,6 +18,7 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <type_traits>
 
 #include "klf_kernels.hpp"
@@ -3661,8 +3662,9 @@ hipError_t launch_pipeline(const RunArgs& a0, hipStream_t st, hipEvent_t* ev, in
   if (ev && a.stage_times) KLF_TRY(hipEventRecord(ev[1], st));
   {
     // k_scan alone (the roofline kernel): ev[7] / ev[8] carry the dispatch's own timestamps
-    t_scan_ev[0] = ev ? ev[7] : nullptr;
-    t_scan_ev[1] = ev ? ev[8] : nullptr;
+    static const bool no_ev = getenv("KLF_SCAN_EVENTS") && !strcmp(getenv("KLF_SCAN_EVENTS"), "0");  // A/B
+    t_scan_ev[0] = ev && !no_ev ? ev[7] : nullptr;
+    t_scan_ev[1] = ev && !no_ev ? ev[8] : nullptr;
     if (a.grep_mode == kGrepLit1)
       KLF_TRY((launch_scan<kScanLit, 1>(a, st, num_cus)));
     else if (a.grep_mode == kGrepGeneral && a.pats.qf_on && a.pats.qf_stride == 4)
@@ -3677,8 +3679,7 @@ hipError_t launch_pipeline(const RunArgs& a0, hipStream_t st, hipEvent_t* ev, in
       KLF_TRY((launch_gen<1>(a, st, num_cus)));
     else
       KLF_TRY((launch_scan<kScanPlain, 1>(a, st, num_cus)));
-    t_scan_ev[0] = t_scan_ev[1] = nullptr;
-    if (ev) KLF_TRY(hipEventRecord(ev[6], st));
+    t_scan_ev[0] = t_scan_ev[1] = nullptr;  // (no event record behind it: each idles the GPU ~6 us)
     if (!a.tindex_wide) {
       hipLaunchKernelGGL((k_tindex<4, 0>), dim3((a.ntiles + 1023) / 1024), dim3(256), 0, st, a);
       KLF_TRY(hipGetLastError());

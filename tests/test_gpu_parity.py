@@ -422,3 +422,17 @@ def test_windowed_line_index(gpu, monkeypatch, win):
         check_against_c(streams, (synth.T0 + 1800, 0), 25, grep)
     monkeypatch.setenv("KLF_HITS_CAP", "16")
     check_against_c(streams, None, 50, lits)
+
+
+def test_literal_automaton_thread(gpu, monkeypatch):
+    """A literal set's Aho-Corasick automaton is built and uploaded by a host thread that
+    klf_open starts and the first run joins: engines closed before any run (the thread
+    joined by klf_close), runs right after open, and runs whose matcher is the automaton
+    itself (the prefilter's hit list forced to overflow: k_match over every line)."""
+    lits = synth.c4_literals(1024)[:500]
+    for _ in range(8):
+        E.Engine(0, grep=lits).close()
+    d = synth.generate(synth.MIXED, 31, 0, 400_000, permille=20)
+    check_against_c([d], None, 40, lits)
+    monkeypatch.setenv("KLF_HITS_CAP", "1")
+    check_against_c([d, synth.generate(synth.ADVERSARIAL, 32, 1, 30_000, permille=40)], (synth.T0 + 1800, 0), -1, lits)
