@@ -1042,7 +1042,7 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
       {&e->d_tstat, ntiles * sizeof(klf::TileStat)}, {&e->d_slots, ntiles * klf::kRecStride * 4},
       {&e->d_tile_base, ntiles * 8}, {&e->d_bsum, (ntiles / 1024 + 2) * 4 * 8},
       {&e->d_counters, klf::kNumCounters * 4}, {&e->d_segout, nsegs * sizeof(SegOut)},
-      {&e->d_wpre, (nsegs + 1) * 8}, {&e->d_trec, ntiles * sizeof(klf::TRec)}, {&e->d_kbase, ntiles * 16}};
+      {&e->d_wpre, (3 * (size_t)nsegs + 2) * 8} /* + wgrp */, {&e->d_trec, ntiles * sizeof(klf::TRec)}, {&e->d_kbase, ntiles * 16}};
   // the dense compaction's per-tile run table (512 B per tile: 2.1 GB for 32 GiB) only for
   // runs without a --tail limit or after a --tail run took the dense path (k_tcopy lists
   // the runs itself without it)
@@ -1134,6 +1134,7 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
     a.counters = e->d_counters.as<uint32_t>();
     a.segout = e->d_segout.as<SegOut>();
     a.wpre = e->d_wpre.as<uint64_t>();
+    a.wgrp = a.wpre + nsegs + 1;
     a.out = e->d_out.as<uint8_t>();
     a.out_cap = e->d_out.p ? e->d_out.cap : 0;
     a.stage_times = (f->flags & KLF_FILTER_STAGE_TIMES) ? 1u : 0u;

@@ -1418,7 +1418,21 @@ __device__ __forceinline__ void scatter_body(RunArgs& a, uint32_t bid, uint32_t 
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   uint32_t* err_flag = a.counters + 2;
   const uint32_t ngroups = (a.ntiles + kScatterGroup - 1) / kScatterGroup;
-  for (uint32_t g = bid * 4 + wv; g < ngroups; g += nb * 4) {
+  // the window pass visits only the groups k_tailw listed per stream (flat index f over
+  // their concatenation: the stream by a search of the prefix)
+  const bool wpass = a.scatter_mode == 2;
+  const uint64_t F = wpass ? (a.counters[2] ? 0 : a.wgrp[2 * a.nsegs]) : ngroups;  // (overflow: no list)
+  for (uint64_t f = bid * 4 + wv; f < F; f += nb * 4) {
+    uint32_t g = (uint32_t)f;
+    if (wpass) {
+      uint32_t lo = 0, hi = a.nsegs;  // the last stream whose prefix is <= f
+      while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (a.wgrp[a.nsegs + mid] <= f) lo = mid; else hi = mid;
+      }
+      g = (uint32_t)(a.wgrp[lo] & 0xFFFFFFFFull) + (uint32_t)(f - a.wgrp[a.nsegs + lo]);
+      if (g >= ngroups) continue;
+    }
     const uint32_t tile = g * kScatterGroup + lane;
     uint32_t n = 0;
     if (tile < a.ntiles) {
@@ -1443,9 +1457,10 @@ __device__ __forceinline__ void scatter_body(RunArgs& a, uint32_t bid, uint32_t 
       e.seg = s;
       e.pad[0] = e.pad[1] = 0;
       s_ent[wv][lane] = e;
-      if ((ts.flags & 2u) && base < a.cap_lines) {
+      if ((ts.flags & 2u) && base < a.cap_lines && a.scatter_mode != 2) {
         // literal hit inside the line carried in from an earlier tile: that line's start
         // is the last staged start of the nearest earlier tile of the stream that has one
+        // (the window pass skips it: the pre-count pass set those bits already)
         int64_t cs = -1;
         for (uint32_t pt = tile; pt > sd.tile0;) {
           --pt;
@@ -1508,8 +1523,10 @@ __device__ __forceinline__ void scatter_body(RunArgs& a, uint32_t bid, uint32_t 
         a.line_off[li + e.seg] = e.rel_lo;
         a.meta[li] = (uint16_t)(sl[u] & 0u);
 #else
-        a.line_off[li + e.seg] = e.rel_lo + (sl[u] & kSlotOff);
-        a.meta[li] = (uint16_t)(sl[u] >> 16);
+        if (a.scatter_mode != 1) {  // (the pre-count pass: match bits only; k_mcount and
+          a.line_off[li + e.seg] = e.rel_lo + (sl[u] & kSlotOff);  // k_tailw read no more,
+          a.meta[li] = (uint16_t)(sl[u] >> 16);  // the window pass writes the lines it keeps)
+        }
         if (sl[u] & kSlotHit) atomicOr(&a.bits[li >> 5], 1u << (li & 31));
 #endif
       }
@@ -3148,10 +3165,63 @@ __device__ __forceinline__ void kbase_body(RunArgs& a) {
 // ---- the launches after the matchers (fewer kernel boundaries: each costs ~5 us) ----------
 // k_tailw: the kubelet tail rule per stream (block per stream); the last block to finish
 // (ticket) then runs the window prefix over all streams and picks the compaction path.
+// The last tile of [t0, t0 + nt) whose tile_base (the line open at its start) is <= key,
+// else t0: a block-wide search, 256 sample points per level (tile_base ascends).
+__device__ uint32_t last_tile_le(const RunArgs& a, uint32_t t0, uint32_t nt, uint64_t key) {
+  uint32_t lo = t0, span = nt;
+  while (span > 1) {
+    const uint32_t step = (span + 255u) / 256u, k = threadIdx.x * step;
+    const bool p = k < span && a.tile_base[lo + k] <= key;
+    const uint32_t c = (uint32_t)__syncthreads_count(p);  // the true samples are a prefix
+    if (c == 0) return lo;  // (first level only: sample 0 of a later level is true)
+    lo += (c - 1u) * step;
+    span = step < t0 + nt - lo ? step : t0 + nt - lo;
+  }
+  return lo;
+}
+// win_index: the scatter groups holding stream s's window lines [win_lo, win_hi] (the
+// window scatter's tiles: from the tile before the one whose base passes win_lo, to the
+// last whose base is <= win_hi), so that k_scatter's window pass visits only those.
+__device__ __forceinline__ void win_groups_body(RunArgs& a) {
+  const uint32_t s = blockIdx.x;
+  const SegDesc sd = a.segs[s];
+  const SegOut& so = a.segout[s];
+  uint64_t packed = 0;
+  if (so.win_hi > so.win_lo && sd.ntiles) {
+    uint32_t ta = last_tile_le(a, sd.tile0, sd.ntiles, so.win_lo);
+    ta = ta > sd.tile0 ? ta - 1u : ta;
+    const uint32_t tb = last_tile_le(a, sd.tile0, sd.ntiles, so.win_hi);
+    packed = (uint64_t)(ta / kScatterGroup) | (uint64_t)(tb / kScatterGroup + 1u) << 32;
+  }
+  if (threadIdx.x == 0) a.wgrp[s] = packed;
+}
+__device__ __forceinline__ void win_groups_prefix(RunArgs& a) {
+  __shared__ uint64_t s_w64[4];
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  uint64_t carry = 0;
+  for (uint32_t b = 0; b < a.nsegs; b += 256) {
+    const uint32_t s = b + t;
+    const uint64_t pk = s < a.nsegs ? a.wgrp[s] : 0;
+    const uint64_t v = (pk >> 32) - (pk & 0xFFFFFFFFull);
+    const uint64_t inc = wave_incl_scan_add(v, lane);
+    __syncthreads();
+    if (lane == 63) s_w64[wv] = inc;
+    __syncthreads();
+    uint64_t pre = 0;
+    for (int k = 0; k < wv; ++k) pre += s_w64[k];
+    if (s < a.nsegs) a.wgrp[a.nsegs + s] = carry + pre + inc - v;
+    carry += s_w64[0] + s_w64[1] + s_w64[2] + s_w64[3];
+  }
+  if (t == 0) a.wgrp[2 * a.nsegs] = carry;
+}
 __global__ __launch_bounds__(256) void k_tailw(RunArgs a) {
   __shared__ uint32_t s_last;
   tail_body(a);
   __syncthreads();
+  if (a.win_index && !a.counters[2]) {
+    win_groups_body(a);
+    __syncthreads();
+  }
   if (threadIdx.x == 0) {
     __threadfence();  // this block's stream records before its ticket
     s_last = atomicAdd(&a.counters[kCtrTailDone], 1u) == gridDim.x - 1 ? 1u : 0u;
@@ -3160,6 +3230,10 @@ __global__ __launch_bounds__(256) void k_tailw(RunArgs a) {
   if (s_last) {
     __threadfence();  // every block's records, seen through their tickets
     wprefix_body(a);
+    if (a.win_index && !a.counters[2]) {
+      __syncthreads();
+      win_groups_prefix(a);
+    }
   }
 }
 // Then three launches serve either compaction path (k_wprefix's choice, counters[kCtrDense]):

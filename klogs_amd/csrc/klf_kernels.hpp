@@ -277,6 +277,8 @@ struct RunArgs {
   uint64_t cap_lines;
   SegOut* segout;       // [nsegs]
   uint64_t* wpre;       // [nsegs + 1] exclusive prefix of window sizes
+  uint64_t* wgrp;       // win_index: [nsegs] the scatter groups [ga, gb) holding each stream's
+                        // tail window (ga | gb << 32), then [nsegs + 1] their exclusive prefix
   uint8_t* out;         // output bytes
   uint64_t out_cap;     // bytes of `out`: a copy that would pass it is skipped and flagged
                         // (counters[kCtrOutShort]); the host grows the buffer and reruns the tail stage
