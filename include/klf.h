@@ -75,7 +75,9 @@ typedef struct klf_config {
 typedef struct klf_engine klf_engine;
 
 /* Compiles the pattern set once (replaces nothing in the reference: --grep/--match are
- * new flags added at cmd/root.go:485-497). */
+ * new flags added at cmd/root.go:485-497).  Every pattern error is reported here.  A set
+ * with several literals starts one host thread that builds and uploads their Aho-Corasick
+ * automaton while the first klf_run samples the data; that run (or klf_close) joins it. */
 int klf_open(const klf_config* cfg, klf_engine** out);
 void klf_close(klf_engine* e);
 /* Human-readable detail of the last error on this engine (e.g. the pattern error). */
