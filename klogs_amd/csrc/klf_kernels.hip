@@ -3165,19 +3165,35 @@ __device__ __forceinline__ void kbase_body(RunArgs& a) {
 // ---- the launches after the matchers (fewer kernel boundaries: each costs ~5 us) ----------
 // k_tailw: the kubelet tail rule per stream (block per stream); the last block to finish
 // (ticket) then runs the window prefix over all streams and picks the compaction path.
-// The last tile of [t0, t0 + nt) whose tile_base (the line open at its start) is <= key,
-// else t0: a block-wide search, 256 sample points per level (tile_base ascends).
-__device__ uint32_t last_tile_le(const RunArgs& a, uint32_t t0, uint32_t nt, uint64_t key) {
-  uint32_t lo = t0, span = nt;
-  while (span > 1) {
-    const uint32_t step = (span + 255u) / 256u, k = threadIdx.x * step;
-    const bool p = k < span && a.tile_base[lo + k] <= key;
-    const uint32_t c = (uint32_t)__syncthreads_count(p);  // the true samples are a prefix
-    if (c == 0) return lo;  // (first level only: sample 0 of a later level is true)
-    lo += (c - 1u) * step;
-    span = step < t0 + nt - lo ? step : t0 + nt - lo;
+// The last tiles of [t0, t0 + nt) whose tile_base (the line open at its start) is <= ka /
+// <= kb, else t0: block-wide searches, 256 sample points per level (tile_base ascends),
+// both keys' loads in flight together (one memory round trip per level).
+__device__ void last_tiles_le(const RunArgs& a, uint32_t t0, uint32_t nt, uint64_t ka, uint64_t kb,
+                              uint32_t& ra, uint32_t& rb) {
+  uint32_t lo[2] = {t0, t0}, span[2] = {nt, nt};
+  const uint64_t key[2] = {ka, kb};
+  bool done[2] = {nt <= 1, nt <= 1};
+  while (!done[0] || !done[1]) {
+    uint32_t step[2];
+    bool p[2];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      step[q] = (span[q] + 255u) / 256u;
+      const uint32_t k = threadIdx.x * step[q];
+      p[q] = !done[q] && k < span[q] && a.tile_base[lo[q] + k] <= key[q];
+    }
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const uint32_t c = (uint32_t)__syncthreads_count(p[q]);  // the true samples are a prefix
+      if (done[q]) continue;
+      if (c == 0) { done[q] = true; continue; }  // (first level only: sample 0 of a later level is true)
+      lo[q] += (c - 1u) * step[q];
+      span[q] = step[q] < t0 + nt - lo[q] ? step[q] : t0 + nt - lo[q];
+      done[q] = span[q] <= 1;
+    }
   }
-  return lo;
+  ra = lo[0];
+  rb = lo[1];
 }
 // win_index: the scatter groups holding stream s's window lines [win_lo, win_hi] (the
 // window scatter's tiles: from the tile before the one whose base passes win_lo, to the
@@ -3188,9 +3204,9 @@ __device__ __forceinline__ void win_groups_body(RunArgs& a) {
   const SegOut& so = a.segout[s];
   uint64_t packed = 0;
   if (so.win_hi > so.win_lo && sd.ntiles) {
-    uint32_t ta = last_tile_le(a, sd.tile0, sd.ntiles, so.win_lo);
+    uint32_t ta, tb;
+    last_tiles_le(a, sd.tile0, sd.ntiles, so.win_lo, so.win_hi, ta, tb);
     ta = ta > sd.tile0 ? ta - 1u : ta;
-    const uint32_t tb = last_tile_le(a, sd.tile0, sd.ntiles, so.win_hi);
     packed = (uint64_t)(ta / kScatterGroup) | (uint64_t)(tb / kScatterGroup + 1u) << 32;
   }
   if (threadIdx.x == 0) a.wgrp[s] = packed;
