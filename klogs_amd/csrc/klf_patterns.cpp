@@ -1357,10 +1357,20 @@ double layout_cost(const CompiledSet& c, const DataStats& st) {
     for (uint32_t b = 0; b < c.qf_q && k + b < len; ++b) g |= (uint32_t)nb8[k + b] << (8 * b);
     grams.push_back((g | c.qf_fold) & c.qf_mask);
   }
-  std::sort(grams.begin(), grams.end());
-  grams.erase(std::unique(grams.begin(), grams.end()), grams.end());
+  // distinct grams through an open-addressing set (top bits of a product; sorting them was
+  // most of the cost's time)
+  size_t cap = 64;
+  uint32_t shift = 26;
+  while (cap < 2 * grams.size()) cap <<= 1, --shift;
+  std::vector<uint32_t> seen(cap, ~0u);
   double hit_share = 0;  // probed grams (the anchored ones only reach a bucket through an anchor)
-  for (uint32_t g : grams) hit_share += gram_share(st, g, c.qf_q);
+  for (uint32_t g : grams) {
+    uint32_t i = (g * 0x9E3779B1u) >> shift;
+    while (seen[i] != ~0u && seen[i] != g) i = (i + 1) & (uint32_t)(cap - 1);
+    if (seen[i] == g) continue;
+    seen[i] = g;
+    hit_share += gram_share(st, g, c.qf_q);
+  }
   const double samples = qf_samples_per_tile(c.qf_stride);
   double hits = samples * std::min(1.0, hit_share);
   // VALU per probe (the scan's ISA, its unrolled fast pass / 32 probes): 6.9 for a 3-byte
