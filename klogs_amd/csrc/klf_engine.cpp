@@ -979,12 +979,15 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
   hipStream_t st = e->stream;
   bool same_layout = segs.size() == e->last_segs.size() && e->d_tile_seg.cap >= ntiles * 4 &&
                      memcmp(segs.data(), e->last_segs.data(), segs.size() * sizeof(SegDesc)) == 0;
+  mark("pre-segs");
   if (!same_layout) {
     HIPCHK(e, e->d_segs.ensure(nsegs * sizeof(SegDesc)), "alloc segs");
+    mark("segs alloc");
     // (a pageable source: the runtime stages it before the call returns, so `segs` may go
     // out of scope with no stream sync, which would wait for klf_open's table uploads)
     HIPCHK(e, hipMemcpyAsync(e->d_segs.p, segs.data(), nsegs * sizeof(SegDesc), hipMemcpyHostToDevice, st),
            "H2D segs");
+    mark("segs copy");
     HIPCHK(e, e->d_tile_seg.ensure(ntiles * 4 + 16), "alloc tile_seg");  // + whole 16-B loads past the end
   }
   mark("segs");
