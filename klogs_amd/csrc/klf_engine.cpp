@@ -1165,8 +1165,6 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
     a.pairs = count ? e->d_pairs.as<uint64_t>() : nullptr;
     a.pairs_log2 = e->pairs_log2;
   };
-  if (const int rc = ensure_ac(e); rc != KLF_OK) return rc;  // (before fill_args copies dpats)
-  mark("automaton");
   bool overflow = false, pairs_over = false;
   for (int attempt = 0, line_reruns = 0, pair_reruns = 0; attempt < 4; ++attempt) {
     if (count) {
@@ -1211,7 +1209,15 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
     r->so.resize(nsegs);
     uint32_t counters[32];
     HIPCHK(e, e->h_rb.ensure(sizeof(counters) + nsegs * sizeof(SegOut)), "alloc readback");
+    // the literal automaton (klf_open's thread) is read from k_tindex on (deferred lines)
+    auto join_ac = [&]() -> int {
+      if (const int rc = ensure_ac(e); rc != KLF_OK) return rc;
+      memcpy(static_cast<void*>(&a.pats), &e->dpats, sizeof(a.pats));
+      mark("automaton");
+      return KLF_OK;
+    };
     if (two_phase) {
+      if (const int rc = join_ac(); rc != KLF_OK) return rc;
       a.cap_lines = 1ull << 40;  // phase 1 indexes no line array (k_tindex: no overflow, no bitmap)
       HIPCHK(e, klf::launch_pipeline(a, st, e->ev, e->num_cus, 1), "launch");
       uint8_t* rb1 = e->h_rb.as<uint8_t>();
@@ -1245,6 +1251,11 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
         HIPCHK(e, hipMemsetAsync(a.bits, 0, (cap / 32 + 1) * 4, st), "zero bits");
       HIPCHK(e, klf::launch_pipeline(a, st, e->ev, e->num_cus, 2), "launch");
       mark("phase 2 launched");
+    } else if (e->ac_thread.joinable()) {  // joined while the scan runs
+      HIPCHK(e, alloc_lines(a, cap), "alloc line arrays");
+      HIPCHK(e, klf::launch_pipeline(a, st, e->ev, e->num_cus, 3), "launch");
+      if (const int rc = join_ac(); rc != KLF_OK) return rc;
+      HIPCHK(e, klf::launch_pipeline(a, st, e->ev, e->num_cus, 4), "launch");
     } else {
       HIPCHK(e, alloc_lines(a, cap), "alloc line arrays");
       HIPCHK(e, klf::launch_pipeline(a, st, e->ev, e->num_cus), "launch");

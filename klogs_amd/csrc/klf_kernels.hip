@@ -3732,7 +3732,10 @@ hipError_t launch_pipeline(const RunArgs& a0, hipStream_t st, hipEvent_t* ev, in
   RunArgs a = a0;
   hipError_t e;
 #define KLF_TRY(x) do { e = (x); if (e != hipSuccess) return e; } while (0)
-  if (phase != 2) {
+  // phases: 0 all; 1 through the tile index, 2 the rest (a first run's line count between
+  // them); 3 through k_scan, 4 the rest (the host joins the literal automaton's thread while
+  // the scan runs: nothing before k_tindex reads it)
+  if (phase != 2 && phase != 4) {
   if (ev) KLF_TRY(hipEventRecord(ev[0], st));
   {
     const uint32_t nw = a.nsegs * (uint32_t)(sizeof(SegOut) / 8);
@@ -3770,6 +3773,11 @@ hipError_t launch_pipeline(const RunArgs& a0, hipStream_t st, hipEvent_t* ev, in
     else
       KLF_TRY((launch_scan<kScanPlain, 1>(a, st, num_cus)));
     t_scan_ev[0] = t_scan_ev[1] = nullptr;  // (no event record behind it: each idles the GPU ~6 us)
+  }
+  if (phase == 3) return hipSuccess;
+  }  // phase != 2, 4
+  if (phase != 2) {
+  {
     if (!a.tindex_wide) {
       hipLaunchKernelGGL((k_tindex<4, 0>), dim3((a.ntiles + 1023) / 1024), dim3(256), 0, st, a);
       KLF_TRY(hipGetLastError());
@@ -3783,7 +3791,7 @@ hipError_t launch_pipeline(const RunArgs& a0, hipStream_t st, hipEvent_t* ev, in
     KLF_TRY(hipGetLastError());
   }
   if (phase == 1) return hipSuccess;
-  }  // phase != 2
+  }  // phase != 2: the tile index
   // Regex sets: k_scatter and k_verify as one launch (k_scatter_verify; measured with two
   // streams: C5 -0.10 ms per step); a literal set's heavier verification (C4: 1,024 literals)
   // contends with the scatter instead (+0.08 ms), so literal-only sets keep the serial order.
