@@ -151,7 +151,9 @@ int klf_retail(klf_engine* e, klf_result* prev, int64_t tail, klf_result** out);
  * counts only, no D2H). */
 int klf_result_stream(klf_result* r, uint32_t stream_id, const uint8_t** bytes,
                       uint64_t* len, klf_counts* counts);
-/* Line-start offsets of one stream: n_lines+1 u64 (last = stream length). */
+/* Line-start offsets of one stream: n_lines+1 u64 (last = stream length).  Runs that did
+ * not need the whole line index (no patterns with --tail -1, or literal patterns: only the
+ * tail windows' lines were indexed) build it here on first use, on the device. */
 int klf_result_lines(klf_result* r, uint32_t stream_id, const uint64_t** off,
                      uint64_t* n_lines);
 /* Match bitmap of one stream (bit l LSB-first in byte l>>3); *nbytes = ceil(lines/8).
