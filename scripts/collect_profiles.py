@@ -74,7 +74,7 @@ def main():
              "Made by `scripts/profile_round.sh` on one MI355X (the driver's bench command under",
              "`rocprofv3 --kernel-trace --stats`, then counter passes per config) and",
              "`scripts/collect_profiles.py`.  frac = algorithmic bytes / average launch / 8 TB/s.", "",
-             "| config | kernel | alg bytes / launch | config-run trace avg (µs) | frac (rocprof) | avg w/o 1st launch (µs; C2: bench trace, others: config trace) | frac (rocprof, steady) | frac (bench HIP events) | HBM traffic / alg |",
+             "| config | kernel | alg bytes / launch | config-run trace avg (µs) | frac (rocprof) | avg w/o 1st launch (µs; bench trace, C3: its config trace) | frac (rocprof, steady) | frac (bench HIP events) | HBM traffic / alg |",
              "|---|---|---|---|---|---|---|---|---|"]
     out = {}
     # C2: the headline line
@@ -110,10 +110,13 @@ def main():
         if c in pmc and ks in pmc[c]:
             p = pmc[c][ks]
             tt = p.get("fetch_bytes_x2", 0) + p.get("write_bytes", 0)
-        # steady state from the config's own trace: in the bench command's trace one scan
-        # instantiation can serve two configs (C1 and C3 both run k_scan<0,...>)
-        st = steady_us(src / f"trace_{c}" / "run_kernel_trace.csv", ks) or \
-            steady_us(src / "trace" / "run_kernel_trace.csv", ks)
+        # steady state from the bench command's own trace (the line's numbers come from that
+        # run), except C3: its scan instantiation also serves C1 there (k_scan<0,...>), so
+        # C3's comes from its own config run
+        tr_bench = src / "trace" / "run_kernel_trace.csv"
+        tr_cfg = src / f"trace_{c}" / "run_kernel_trace.csv"
+        st = (steady_us(tr_cfg, ks) or steady_us(tr_bench, ks)) if c == "c3" else \
+            (steady_us(tr_bench, ks) or steady_us(tr_cfg, ks))
         fs = st and alg / (st * 1e-6) / 1e9 / PEAK
         out[c] = {"kernel": ks, "avg_us": ts[ks]["avg_us"], "frac_rocprof": round(fr, 4),
                   "steady_us": st and round(st, 1), "frac_rocprof_steady": fs and round(fs, 4),
