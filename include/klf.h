@@ -109,6 +109,14 @@ typedef struct klf_filter {
 #define KLF_FILTER_STAGE_TIMES 1u
 /* klf_filter.flags: count matching lines per pattern (klf_result_pattern_counts). */
 #define KLF_FILTER_PATTERN_COUNTS 2u
+/* klf_filter.flags: write every line's u64 offset inside the run (KLF_INDEX_FULL), also where
+ * the run needs only part of the index (see klf_result_index_mode). */
+#define KLF_FILTER_FULL_INDEX 4u
+
+/* klf_result_index_mode: how much of the u64 line index the run wrote itself. */
+#define KLF_INDEX_FULL 0       /* every line of every stream                                  */
+#define KLF_INDEX_WINDOWS 1    /* the lines of each stream's --tail window (literal patterns)  */
+#define KLF_INDEX_ON_DEMAND 2  /* none (no patterns, --tail -1, the dense copy path)          */
 
 typedef struct klf_counts {
   uint64_t lines;      /* all lines (a trailing fragment counts)                       */
@@ -201,6 +209,8 @@ int klf_result_write(klf_result* r, const int* fds, uint32_t n_fds, uint64_t* wr
 int klf_result_timing(const klf_result* r, double* ms, uint32_t cap, uint32_t* n);
 /* Totals across streams. */
 int klf_result_totals(const klf_result* r, klf_counts* totals);
+/* KLF_INDEX_* of the run (klf_result_lines builds the rest on demand, after the run). */
+int klf_result_index_mode(const klf_result* r);
 void klf_result_free(klf_result* r);
 
 /* ---- follow mode (-f) -------------------------------------------- */

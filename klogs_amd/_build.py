@@ -91,9 +91,9 @@ def build_oracle(force=False, quiet=True) -> Path:
     out_dir = ORACLE / "_build"
     out_dir.mkdir(parents=True, exist_ok=True)
     out = out_dir / "libklf_oracle.so"
-    src = ORACLE / "klf_oracle_c.c"
-    if force or _stale(out, [src]):
-        _run(["gcc", "-O2", "-shared", "-fPIC", src, "-o", out], quiet)
+    srcs = [ORACLE / "klf_oracle_c.c", ORACLE / "klf_oracle_rx.c"]
+    if force or _stale(out, srcs):
+        _run(["gcc", "-O2", "-Wall", "-shared", "-fPIC", *srcs, "-o", out], quiet)
     return out
 
 

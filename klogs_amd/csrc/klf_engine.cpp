@@ -219,6 +219,8 @@ struct klf_result {
   bool has_bits = false;
   uint64_t total_lines = 0, total_out = 0;
   double ms[7] = {0, 0, 0, 0, 0, 0, 0};
+  uint32_t ev_mask = 0;              // the timing events the run recorded
+  int index_mode = KLF_INDEX_FULL;   // how much of the line index the run itself wrote
   // lazily filled host copies
   bool have_out = false, have_lines = false, have_bits = false;
   std::vector<uint8_t> out;
@@ -1054,9 +1056,11 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
   uint32_t compact_mode = 0;  // tests: force either compaction path
   e->index_pending.clear();
   // lazy line index (grep none, --tail -1; KLF_LAZY_INDEX=0 turns it off)
-  const bool lazy_index = mode == klf::CompiledSet::kNone && f->tail < 0 &&
+  const bool full_index = (f->flags & KLF_FILTER_FULL_INDEX) != 0;
+  const bool lazy_index = mode == klf::CompiledSet::kNone && f->tail < 0 && !full_index &&
                           !(getenv("KLF_LAZY_INDEX") && !strcmp(getenv("KLF_LAZY_INDEX"), "0"));
-  bool win_ok = true;  // (a run that needs every line's index -- k_match's fallback -- turns it off)
+  // (a run that needs every line's index -- k_match's fallback -- turns it off)
+  bool win_ok = !full_index;
   if (const char* v = getenv("KLF_COMPACT")) compact_mode = !strcmp(v, "sparse") ? 1u : !strcmp(v, "dense") ? 2u : 0u;
   // The output buffer: sized for the whole input up front when the run keeps about as much
   // as it reads (no --tail limit: C3-like), else grown
@@ -1166,6 +1170,7 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
     a.pairs_log2 = e->pairs_log2;
   };
   bool overflow = false, pairs_over = false;
+  uint32_t ev_mask = 0;
   for (int attempt = 0, line_reruns = 0, pair_reruns = 0; attempt < 4; ++attempt) {
     if (count) {
       HIPCHK(e, e->d_pcount.ensure((size_t)nsegs * e->cs.n_cids * 4), "alloc pcount");
@@ -1206,6 +1211,7 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
     HIPCHK(e, e->d_pool.ensure(e->pool_cap * 4), "alloc pool");
     klf::RunArgs a;
     fill_args(a, attempt);
+    ev_mask = 0;  // the events this attempt records (the timing queries read only those)
     r->so.resize(nsegs);
     uint32_t counters[32];
     HIPCHK(e, e->h_rb.ensure(sizeof(counters) + nsegs * sizeof(SegOut)), "alloc readback");
@@ -1219,7 +1225,7 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
     if (two_phase) {
       if (const int rc = join_ac(); rc != KLF_OK) return rc;
       a.cap_lines = 1ull << 40;  // phase 1 indexes no line array (k_tindex: no overflow, no bitmap)
-      HIPCHK(e, klf::launch_pipeline(a, st, e->ev, e->num_cus, 1), "launch");
+      HIPCHK(e, klf::launch_pipeline(a, st, e->ev, e->num_cus, 1, &ev_mask), "launch");
       uint8_t* rb1 = e->h_rb.as<uint8_t>();
       HIPCHK(e, hipMemcpyAsync(rb1, e->d_counters.p, sizeof(counters), hipMemcpyDeviceToHost, st), "D2H counters");
       HIPCHK(e, hipMemcpyAsync(rb1 + sizeof(counters), e->d_segout.p, nsegs * sizeof(SegOut), hipMemcpyDeviceToHost, st),
@@ -1249,16 +1255,16 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
       mark("line arrays");
       if (a.grep_mode != klf::CompiledSet::kNone)  // (phase 1's k_tindex zeroes it otherwise)
         HIPCHK(e, hipMemsetAsync(a.bits, 0, (cap / 32 + 1) * 4, st), "zero bits");
-      HIPCHK(e, klf::launch_pipeline(a, st, e->ev, e->num_cus, 2), "launch");
+      HIPCHK(e, klf::launch_pipeline(a, st, e->ev, e->num_cus, 2, &ev_mask), "launch");
       mark("phase 2 launched");
     } else if (e->ac_thread.joinable()) {  // joined while the scan runs
       HIPCHK(e, alloc_lines(a, cap), "alloc line arrays");
-      HIPCHK(e, klf::launch_pipeline(a, st, e->ev, e->num_cus, 3), "launch");
+      HIPCHK(e, klf::launch_pipeline(a, st, e->ev, e->num_cus, 3, &ev_mask), "launch");
       if (const int rc = join_ac(); rc != KLF_OK) return rc;
-      HIPCHK(e, klf::launch_pipeline(a, st, e->ev, e->num_cus, 4), "launch");
+      HIPCHK(e, klf::launch_pipeline(a, st, e->ev, e->num_cus, 4, &ev_mask), "launch");
     } else {
       HIPCHK(e, alloc_lines(a, cap), "alloc line arrays");
-      HIPCHK(e, klf::launch_pipeline(a, st, e->ev, e->num_cus), "launch");
+      HIPCHK(e, klf::launch_pipeline(a, st, e->ev, e->num_cus, 0, &ev_mask), "launch");
     }
     uint8_t* rb = e->h_rb.as<uint8_t>();
     HIPCHK(e, hipMemcpyAsync(rb, e->d_counters.p, sizeof(counters), hipMemcpyDeviceToHost, st), "D2H counters");
@@ -1300,6 +1306,8 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
     }
     e->last_args = a;
     if ((a.lazy_index && counters[klf::kCtrDense]) || a.win_index) e->index_pending.push_back(a);
+    r->index_mode = (a.lazy_index && counters[klf::kCtrDense]) ? KLF_INDEX_ON_DEMAND
+                    : a.win_index ? KLF_INDEX_WINDOWS : KLF_INDEX_FULL;
     e->last_gen = r->gen;
     e->line_density = (double)(r->so[nsegs - 1].line_hi + 1) / (double)total_bytes;
     if (f->tail >= 0 && counters[klf::kCtrDense]) e->dense_tail_seen = true;
@@ -1334,15 +1342,21 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
       (void)klf::clear_timeline();
     }
   }
-  float ms;
-  if (f->flags & KLF_FILTER_STAGE_TIMES)
-    for (int k = 0; k < 4; ++k)  // scan stage, match, tail stage, compaction
-      if (hipEventElapsedTime(&ms, e->ev[k + 1], e->ev[k + 2]) == hipSuccess) r->ms[k] = ms;
-  if (hipEventElapsedTime(&ms, e->ev[0], e->ev[5]) == hipSuccess) r->ms[4] = ms;
-  if (f->flags & KLF_FILTER_STAGE_TIMES)
-    if (hipEventElapsedTime(&ms, e->ev[0], e->ev[1]) == hipSuccess) r->ms[5] = ms;
-  if (hipEventElapsedTime(&ms, e->ev[7], e->ev[8]) == hipSuccess) r->ms[6] = ms;  // k_scan's dispatch alone
-  (void)hipGetLastError();  // an event pair this run did not record: no sticky error for the next launch check
+  // only the event pairs this run recorded (ev_mask): a pair it did not record would fail
+  // the query (or time an earlier run); a recorded pair that fails to read is an error
+  static const int kPairs[6][3] = {{1, 2, 0}, {2, 3, 1}, {3, 4, 2}, {4, 5, 3}, {0, 5, 4}, {0, 1, 5}};
+  for (const auto& q : kPairs)
+    if ((ev_mask >> q[0] & 1u) && (ev_mask >> q[1] & 1u)) {
+      float ms = 0.f;
+      HIPCHK(e, hipEventElapsedTime(&ms, e->ev[q[0]], e->ev[q[1]]), "timing events");
+      r->ms[q[2]] = ms;
+    }
+  if ((ev_mask >> 7 & 1u) && (ev_mask >> 8 & 1u)) {  // k_scan's dispatch alone
+    float ms = 0.f;
+    HIPCHK(e, hipEventElapsedTime(&ms, e->ev[7], e->ev[8]), "scan timing events");
+    r->ms[6] = ms;
+  }
+  r->ev_mask = ev_mask;
   r->total_lines = r->so[nsegs - 1].line_hi;
   for (auto& s : r->so) r->total_out = std::max(r->total_out, s.out_hi);
   *out = rp.release();
@@ -1381,7 +1395,8 @@ extern "C" int klf_retail(klf_engine* e, klf_result* prev, int64_t tail, klf_res
     a.stage_times = 0;
     a.plan_runs = 0;  // (plans assume --tail -1 and are consumed by the run)
     hipStream_t st = e->stream;
-    hipError_t h = klf::launch_retail(a, st, e->ev, e->num_cus);
+    uint32_t rmask = 0;
+    hipError_t h = klf::launch_retail(a, st, e->ev, e->num_cus, &rmask);
     uint32_t short_out = 0;
     if (h == hipSuccess) h = hipMemcpyAsync(r->so.data(), e->d_segout.p, nsegs * sizeof(SegOut), hipMemcpyDeviceToHost, st);
     if (h == hipSuccess) h = hipMemcpyAsync(e->h_rb.p, e->d_counters.p, 32 * 4, hipMemcpyDeviceToHost, st);
@@ -1390,9 +1405,12 @@ extern "C" int klf_retail(klf_engine* e, klf_result* prev, int64_t tail, klf_res
     if (h == hipSuccess && short_out) h = grow_out_retail(e, a, r->so);  // a larger window than the buffer holds
     if (h == hipSuccess) e->last_args = a;
     if (h != hipSuccess) { delete r; return hip_err(e, h, "klf_retail"); }
-    float ms;
-    if (hipEventElapsedTime(&ms, e->ev[0], e->ev[5]) == hipSuccess) r->ms[4] = ms;
-    (void)hipGetLastError();
+    if ((rmask & 1u) && (rmask >> 5 & 1u)) {
+      float ms = 0.f;
+      if ((h = hipEventElapsedTime(&ms, e->ev[0], e->ev[5])) != hipSuccess) { delete r; return hip_err(e, h, "klf_retail timing"); }
+      r->ms[4] = ms;
+    }
+    r->ev_mask = rmask;
   }
   for (auto& s : r->so) r->total_out = std::max(r->total_out, s.out_hi);
   r->gen = ++e->gen;  // prev's output buffer is rewritten: prev is stale from here on
@@ -1766,6 +1784,8 @@ extern "C" int klf_result_timing(const klf_result* r, double* ms, uint32_t cap, 
   if (n) *n = k;
   return KLF_OK;
 }
+
+extern "C" int klf_result_index_mode(const klf_result* r) { return r ? r->index_mode : KLF_EINVAL; }
 
 extern "C" int klf_result_totals(const klf_result* r, klf_counts* t) {
   if (!r || !t) return KLF_EINVAL;

@@ -3196,8 +3196,11 @@ __device__ void last_tiles_le(const RunArgs& a, uint32_t t0, uint32_t nt, uint64
   rb = lo[1];
 }
 // win_index: the scatter groups holding stream s's window lines [win_lo, win_hi] (the
-// window scatter's tiles: from the tile before the one whose base passes win_lo, to the
-// last whose base is <= win_hi), so that k_scatter's window pass visits only those.
+// window scatter's tiles), so that k_scatter's window pass visits only those.  Line l > the
+// stream's first has its start slot in the tile of the newline that ends line l - 1: the
+// last tile whose base (the line open at its start) is <= l - 1.  (Not "one tile before the
+// last base <= l": a long line leaves every tile it covers with base l and no slot.)  The
+// range ends at the last tile whose base is <= win_hi.
 __device__ __forceinline__ void win_groups_body(RunArgs& a) {
   const uint32_t s = blockIdx.x;
   const SegDesc sd = a.segs[s];
@@ -3205,8 +3208,9 @@ __device__ __forceinline__ void win_groups_body(RunArgs& a) {
   uint64_t packed = 0;
   if (so.win_hi > so.win_lo && sd.ntiles) {
     uint32_t ta, tb;
-    last_tiles_le(a, sd.tile0, sd.ntiles, so.win_lo, so.win_hi, ta, tb);
-    ta = ta > sd.tile0 ? ta - 1u : ta;
+    const bool first = so.win_lo <= so.line_lo;
+    last_tiles_le(a, sd.tile0, sd.ntiles, first ? so.line_lo : so.win_lo - 1u, so.win_hi, ta, tb);
+    if (first) ta = sd.tile0;
     packed = (uint64_t)(ta / kScatterGroup) | (uint64_t)(tb / kScatterGroup + 1u) << 32;
   }
   if (threadIdx.x == 0) a.wgrp[s] = packed;
@@ -3715,7 +3719,7 @@ hipError_t launch_gen(const RunArgs& a, hipStream_t st, int num_cus) {
   return a.pats.qf_w24 ? launch_gen_q<QS, 4>(a, st, num_cus) : launch_gen_q<QS, 3>(a, st, num_cus);
 }
 
-static hipError_t launch_tail_stage(const RunArgs& a, hipStream_t st, hipEvent_t* ev, int num_cus);
+static hipError_t launch_tail_stage(const RunArgs& a, hipStream_t st, hipEvent_t* ev, int num_cus, uint32_t& m);
 
 hipError_t launch_scatter(const RunArgs& a, hipStream_t st, int num_cus) {
 #ifndef KLF_SCATTER_GRID
@@ -3728,15 +3732,19 @@ hipError_t launch_scatter(const RunArgs& a, hipStream_t st, int num_cus) {
   return hipGetLastError();
 }
 
-hipError_t launch_pipeline(const RunArgs& a0, hipStream_t st, hipEvent_t* ev, int num_cus, int phase) {
+hipError_t launch_pipeline(const RunArgs& a0, hipStream_t st, hipEvent_t* ev, int num_cus, int phase,
+                           uint32_t* ev_mask) {
   RunArgs a = a0;
   hipError_t e;
+  uint32_t m_local = 0;
+  uint32_t& m = ev_mask ? *ev_mask : m_local;
 #define KLF_TRY(x) do { e = (x); if (e != hipSuccess) return e; } while (0)
+#define KLF_REC(k) do { KLF_TRY(hipEventRecord(ev[k], st)); m |= 1u << (k); } while (0)
   // phases: 0 all; 1 through the tile index, 2 the rest (a first run's line count between
   // them); 3 through k_scan, 4 the rest (the host joins the literal automaton's thread while
   // the scan runs: nothing before k_tindex reads it)
   if (phase != 2 && phase != 4) {
-  if (ev) KLF_TRY(hipEventRecord(ev[0], st));
+  if (ev) KLF_REC(0);
   {
     const uint32_t nw = a.nsegs * (uint32_t)(sizeof(SegOut) / 8);
     uint32_t g = (nw + 255) / 256;
@@ -3752,12 +3760,13 @@ hipError_t launch_pipeline(const RunArgs& a0, hipStream_t st, hipEvent_t* ev, in
   }
   // ev[1] only with stage times: each event record idles the GPU for a few us, and the
   // scan's own time is then taken from ev[0] (k_init in front of it: ~2 us)
-  if (ev && a.stage_times) KLF_TRY(hipEventRecord(ev[1], st));
+  if (ev && a.stage_times) KLF_REC(1);
   {
     // k_scan alone (the roofline kernel): ev[7] / ev[8] carry the dispatch's own timestamps
     static const bool no_ev = getenv("KLF_SCAN_EVENTS") && !strcmp(getenv("KLF_SCAN_EVENTS"), "0");  // A/B
     t_scan_ev[0] = ev && !no_ev ? ev[7] : nullptr;
     t_scan_ev[1] = ev && !no_ev ? ev[8] : nullptr;
+    if (t_scan_ev[0]) m |= (1u << 7) | (1u << 8);
     if (a.grep_mode == kGrepLit1)
       KLF_TRY((launch_scan<kScanLit, 1>(a, st, num_cus)));
     else if (a.grep_mode == kGrepGeneral && a.pats.qf_on && a.pats.qf_stride == 4)
@@ -3809,13 +3818,13 @@ hipError_t launch_pipeline(const RunArgs& a0, hipStream_t st, hipEvent_t* ev, in
   } else if (!a.lazy_index) {
     KLF_TRY(launch_scatter(a, st, num_cus));
   }
-  if (ev && a.stage_times && !fused_sv) KLF_TRY(hipEventRecord(ev[2], st));  // ~5 us of idle GPU each
+  if (ev && a.stage_times && !fused_sv) KLF_REC(2);  // ~5 us of idle GPU each
   if (a.grep_mode == kGrepGeneral && a.pats.qf_on) {
     if (!fused_sv) {
       hipLaunchKernelGGL(k_verify, dim3(num_cus * 8), dim3(256), 0, st, a);
       KLF_TRY(hipGetLastError());
     }
-    if (ev && a.stage_times && fused_sv) KLF_TRY(hipEventRecord(ev[2], st));
+    if (ev && a.stage_times && fused_sv) KLF_REC(2);
     if (a.count_pats) {
       hipLaunchKernelGGL(k_fixcount, dim3(num_cus * 2), dim3(256), 0, st, a);
       KLF_TRY(hipGetLastError());
@@ -3840,16 +3849,17 @@ hipError_t launch_pipeline(const RunArgs& a0, hipStream_t st, hipEvent_t* ev, in
     hipLaunchKernelGGL(k_match, dim3(num_cus * 8), dim3(256), 0, st, a);
     KLF_TRY(hipGetLastError());
   }
-  if (ev && a.stage_times) KLF_TRY(hipEventRecord(ev[3], st));  // ~5 us of idle GPU each
-  KLF_TRY(launch_tail_stage(a, st, ev, num_cus));
-  if (ev) KLF_TRY(hipEventRecord(ev[5], st));
+  if (ev && a.stage_times) KLF_REC(3);  // ~5 us of idle GPU each
+  KLF_TRY(launch_tail_stage(a, st, ev, num_cus, m));
+  if (ev) KLF_REC(5);
 #undef KLF_TRY
+#undef KLF_REC
   return hipSuccess;
 }
 
 // Matched counts, kubelet tail window, window prefix, compaction + copy (the stages after
 // the matchers): shared by launch_pipeline and launch_retail.
-static hipError_t launch_tail_stage(const RunArgs& a, hipStream_t st, hipEvent_t* ev, int num_cus) {
+static hipError_t launch_tail_stage(const RunArgs& a, hipStream_t st, hipEvent_t* ev, int num_cus, uint32_t& m) {
   hipError_t e;
 #define KLF_TRY(x) do { e = (x); if (e != hipSuccess) return e; } while (0)
   if (a.grep_mode != kGrepNone) {
@@ -3866,7 +3876,10 @@ static hipError_t launch_tail_stage(const RunArgs& a, hipStream_t st, hipEvent_t
     w.scatter_mode = 2;
     KLF_TRY(launch_scatter(w, st, num_cus));
   }
-  if (ev && a.stage_times) KLF_TRY(hipEventRecord(ev[4], st));  // ~5 us of idle GPU each
+  if (ev && a.stage_times) {  // ~5 us of idle GPU each
+    KLF_TRY(hipEventRecord(ev[4], st));
+    m |= 1u << 4;
+  }
   {
     const uint32_t gt = (a.ntiles + 4 * kTkBatch - 1) / (4 * kTkBatch);
     const uint32_t gp = (uint32_t)num_cus * 8;
@@ -3899,14 +3912,18 @@ static hipError_t launch_tail_stage(const RunArgs& a, hipStream_t st, hipEvent_t
   return hipSuccess;
 }
 
-hipError_t launch_retail(const RunArgs& a, hipStream_t st, hipEvent_t* ev, int num_cus) {
+hipError_t launch_retail(const RunArgs& a, hipStream_t st, hipEvent_t* ev, int num_cus, uint32_t* ev_mask) {
+  uint32_t m_local = 0;
+  uint32_t& m = ev_mask ? *ev_mask : m_local;
   hipError_t e = hipEventRecord(ev[0], st);
   if (e != hipSuccess) return e;
+  m |= 1u;
   hipLaunchKernelGGL(k_retail_init, dim3((a.nsegs + 255) / 256 < 1024 ? (a.nsegs + 255) / 256 : 1024), dim3(256), 0,
                      st, a);
   if ((e = hipGetLastError()) != hipSuccess) return e;
-  if ((e = launch_tail_stage(a, st, ev, num_cus)) != hipSuccess) return e;
-  return hipEventRecord(ev[5], st);
+  if ((e = launch_tail_stage(a, st, ev, num_cus, m)) != hipSuccess) return e;
+  if ((e = hipEventRecord(ev[5], st)) == hipSuccess) m |= 1u << 5;
+  return e;
 }
 
 }  // namespace klf

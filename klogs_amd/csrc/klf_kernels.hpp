@@ -326,11 +326,15 @@ struct RunArgs {
 // phase: 0 the whole pipeline; 1 up to the tile index (k_init .. k_tindex: the line arrays
 // are not touched, a.bits may be null); 2 the rest (k_scatter on), after the host sized
 // the line arrays from phase 1's line count (an engine's first run).
+// ev_mask (nullable): bit k is set for every ev[k] recorded on the stream (ev[7] / ev[8]: the
+// scan's dispatch timestamps), so that the host queries only the pairs the run recorded.
 // k_scatter alone: the global line index of a run (an engine's lazy index, on demand).
 hipError_t launch_scatter(const RunArgs& a, hipStream_t stream, int num_cus);
-hipError_t launch_pipeline(const RunArgs& a, hipStream_t stream, hipEvent_t* ev, int num_cus, int phase = 0);
+hipError_t launch_pipeline(const RunArgs& a, hipStream_t stream, hipEvent_t* ev, int num_cus, int phase = 0,
+                           uint32_t* ev_mask = nullptr);
 // Re-runs matched counts, tail and compaction of the last pipeline with a.tail changed.
-hipError_t launch_retail(const RunArgs& a, hipStream_t stream, hipEvent_t* ev, int num_cus);
+hipError_t launch_retail(const RunArgs& a, hipStream_t stream, hipEvent_t* ev, int num_cus,
+                         uint32_t* ev_mask = nullptr);
 // Data statistics (kGramHistWords u32, zeroed here) of the first `sample` bytes of each of
 // up to 16 segments: byte counts, and the 2-grams at even offsets (folded like the
 // prefilter's grams).

@@ -90,6 +90,7 @@ SIGNATURES = {
     "klf_result_write": (C.c_int, [C.c_void_p, C.POINTER(C.c_int), C.c_uint32, C.POINTER(C.c_uint64)]),
     "klf_result_timing": (C.c_int, [C.c_void_p, C.POINTER(C.c_double), C.c_uint32, C.POINTER(C.c_uint32)]),
     "klf_result_totals": (C.c_int, [C.c_void_p, C.POINTER(_Counts)]),
+    "klf_result_index_mode": (C.c_int, [C.c_void_p]),
     "klf_result_free": (None, [C.c_void_p]),
     "klf_follow_open": (C.c_int, [C.c_void_p, C.POINTER(_Filter), C.POINTER(C.c_void_p)]),
     "klf_follow_feed": (C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p, C.c_size_t]),
@@ -169,15 +170,18 @@ def _patterns(grep: Sequence[bytes], match: Sequence[bytes]):
 
 KLF_FILTER_STAGE_TIMES = 1
 KLF_FILTER_PATTERN_COUNTS = 2
+KLF_FILTER_FULL_INDEX = 4
+INDEX_MODES = {0: "full", 1: "windowed", 2: "on_demand"}  # klf_result_index_mode
 
 
 def _filter(since: Optional[Tuple[int, int]], tail: int, stage_times: bool = False,
-            pattern_counts: bool = False) -> _Filter:
+            pattern_counts: bool = False, full_index: bool = False) -> _Filter:
     f = _Filter()
     s = GO_ZERO_TIME if since is None else since
     f.since.sec, f.since.nsec = int(s[0]), int(s[1])
     f.tail = int(tail)
-    f.flags = (KLF_FILTER_STAGE_TIMES if stage_times else 0) | (KLF_FILTER_PATTERN_COUNTS if pattern_counts else 0)
+    f.flags = ((KLF_FILTER_STAGE_TIMES if stage_times else 0) | (KLF_FILTER_PATTERN_COUNTS if pattern_counts else 0)
+               | (KLF_FILTER_FULL_INDEX if full_index else 0))
     return f
 
 
@@ -344,6 +348,14 @@ class Result:
         _check(_lib.klf_result_stream(self._p, i, None, C.byref(n), C.byref(c)))
         return c.as_dict()
 
+    def index_mode(self) -> str:
+        """klf_result_index_mode: "full" (the run wrote every line's u64 offset), "windowed"
+        (the --tail windows' lines only) or "on_demand" (none; klf_result_lines builds it)."""
+        m = _lib.klf_result_index_mode(self._p)
+        if m < 0:
+            _check(m)
+        return INDEX_MODES[m]
+
     def totals(self) -> dict:
         c = _Counts()
         _check(_lib.klf_result_totals(self._p, C.byref(c)))
@@ -407,18 +419,19 @@ class Engine:
         _check(_lib.klf_reset(self._h), self._h)
 
     def run(self, since=None, tail: int = -1, n_streams: Optional[int] = None, stage_times: bool = False,
-            pattern_counts: bool = False) -> Result:
-        f = _filter(since, tail, stage_times, pattern_counts)
+            pattern_counts: bool = False, full_index: bool = False) -> Result:
+        f = _filter(since, tail, stage_times, pattern_counts, full_index)
         r = C.c_void_p()
         _check(_lib.klf_run(self._h, C.byref(f), C.byref(r)), self._h)
         return Result(r.value or 0, n_streams if n_streams is not None else 0, self)
 
     def run_device(self, d_ptr: int, seg_base: Sequence[int], lens: Sequence[int], since=None,
-                   tail: int = -1, stage_times: bool = False, pattern_counts: bool = False) -> Result:
+                   tail: int = -1, stage_times: bool = False, pattern_counts: bool = False,
+                   full_index: bool = False) -> Result:
         n = len(lens)
         B = (C.c_uint64 * max(1, n))(*[int(x) for x in seg_base])
         L = (C.c_uint64 * max(1, n))(*[int(x) for x in lens])
-        f = _filter(since, tail, stage_times, pattern_counts)
+        f = _filter(since, tail, stage_times, pattern_counts, full_index)
         r = C.c_void_p()
         _check(_lib.klf_run_device(self._h, C.c_void_p(d_ptr), n, B, L, C.byref(f), C.byref(r)), self._h)
         return Result(r.value or 0, n, self)

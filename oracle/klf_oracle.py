@@ -272,6 +272,7 @@ class _GoRegexToPy:
             raise PatternError("non-ASCII pattern bytes are outside the supported subset")
         self.p = pat
         self.i = 0
+        self.quoted = []  # bytes of a \Q...\E still to push
 
     def peek(self, k=0):
         j = self.i + k
@@ -313,13 +314,35 @@ class _GoRegexToPy:
 
     def concat(self, flags) -> str:
         items = []
-        while not self.eof() and self.peek() not in (0x7C, 0x29):
+        after_none = False  # the last step pushed nothing ((?flags) or an empty \Q\E)
+        while self.quoted or (not self.eof() and self.peek() not in (0x7C, 0x29)):
+            if self.quoted:  # \Q...\E: one literal per byte; a repetition after \E takes the last
+                b = self.quoted.pop(0)
+                atom = self.emit_set(_fold({b}) if flags["i"] else {b})
+                items.append(self.repeat(atom) if not self.quoted else atom)
+                after_none = False
+                continue
+            if after_none and items and self.at_repeat():
+                # Go parse.go: (?flags) pushes nothing, so a repetition right after it
+                # applies to the item before it (and is not a nested repetition)
+                items[-1] = self.repeat(items[-1])
+                after_none = False
+                continue
             atom = self.atom(flags)
             if atom is None:  # flag group that only changed flags
+                after_none = True
+                continue
+            after_none = False
+            if self.quoted:  # (the \Q text's first byte came back as this atom)
+                items.append(atom)
                 continue
             atom = self.repeat(atom)
             items.append(atom)
         return "".join(items)
+
+    def at_repeat(self) -> bool:
+        c = self.peek()
+        return c in (0x2A, 0x2B, 0x3F) or (c == 0x7B and _BRACES.match(self.p, self.i) is not None)
 
     def repeat(self, atom: str) -> str:
         seen = False
@@ -345,19 +368,19 @@ class _GoRegexToPy:
                 self.i += 1
 
     def try_braces(self):
-        m = re.match(rb"\{(\d+)(,(\d*))?\}", self.p[self.i:])
+        m = _BRACES.match(self.p, self.i)
         if not m:
-            return None  # Go: literal '{'
+            return None  # Go: literal '{' (parseInt takes no leading zeros)
         lo = int(m.group(1))
-        hi = lo if m.group(2) is None else (None if m.group(3) == b"" else int(m.group(3)))
+        hi = lo if m.group(2) is None else (None if m.group(3) is None else int(m.group(3)))
         if lo > 1000 or (hi is not None and (hi > 1000 or hi < lo)):
             raise PatternError("invalid repeat count")
-        self.i += m.end()
+        self.i = m.end()
         return lo, hi
 
     def atom(self, flags):
         c = self.peek()
-        if c in (0x2A, 0x2B, 0x3F) or (c == 0x7B and re.match(rb"\{\d+(,\d*)?\}", self.p[self.i:])):
+        if c in (0x2A, 0x2B, 0x3F) or (c == 0x7B and _BRACES.match(self.p, self.i)):
             raise PatternError("missing argument to repetition operator")
         if c == 0x28:  # (
             return self.group(flags)
@@ -474,7 +497,10 @@ class _GoRegexToPy:
             end = self.p.find(b"\\E", self.i + 2)
             lit = self.p[self.i + 2:] if end < 0 else self.p[self.i + 2:end]
             self.i = len(self.p) if end < 0 else end + 2
-            return "".join(self.emit_set(_fold({b}) if flags["i"] else {b}) for b in lit) or ""
+            if not lit:
+                return None
+            self.quoted = list(lit[1:])
+            return self.emit_set(_fold({lit[0]}) if flags["i"] else {lit[0]})
         kind, v = self.escape_byte(False)
         if kind == "assert":
             return v
@@ -500,8 +526,12 @@ class _GoRegexToPy:
             first = False
             if c == 0x5B and self.peek(1) == 0x3A:  # [:name:]
                 m = re.match(rb"\[:(\^?)([a-z]+):\]", self.p[self.i:])
-                if m and m.group(2).decode() in _POSIX:
+                if m:
+                    if m.group(2).decode() not in _POSIX:
+                        raise PatternError("invalid character class range")
                     cls = _POSIX[m.group(2).decode()]
+                    if flags["i"]:  # appendGroup: fold the group, then negate it
+                        cls = _fold(cls)
                     s |= (_ALL - cls) if m.group(1) else cls
                     self.i += m.end()
                     continue
@@ -532,6 +562,9 @@ class _GoRegexToPy:
             return v  # int for a single byte, set for \d \w \s \D \W \S
         self.i += 1
         return c
+
+
+_BRACES = re.compile(rb"\{(0|[1-9][0-9]*)(,(0|[1-9][0-9]*)?)?\}")
 
 
 def go_regex_to_python(pat: bytes) -> bytes:

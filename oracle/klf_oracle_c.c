@@ -13,17 +13,10 @@
  *                    + logWriter.write (drop ts.Before(since));
  *   - grep:          Go bytes.Contains via memmem over the content without its '\n'
  *                    (sets of more than 8 literals: an Aho-Corasick DFA, same answer);
- *   - match (ko_filter_rx, the CPU baseline of regex sets): Go regexp.Match restated as
- *                    glibc POSIX ERE (regcomp REG_EXTENDED | REG_NOSUB [| REG_ICASE],
- *                    regexec REG_STARTEND over the content), translated from the SPEC.md S5
- *                    subset by oracle/posix_re.py, behind an Aho-Corasick pass over every
- *                    pattern's required literal (a content holding none of them cannot
- *                    match).  The regex parity checker stays the Python oracle (Python `re`);
- *                    this one is validated against it (tests/test_oracle.py).
+ *   - match:         Go regexp.Match, in klf_oracle_rx.c (ko_filter_rx: its own parser of the
+ *                    SPEC.md S5 subset, Thompson NFA, lazy DFA), through ko_filter_impl below.
  */
 #define _GNU_SOURCE
-#include <locale.h>
-#include <regex.h>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
@@ -262,10 +255,12 @@ static int content_matches(const uint8_t* c, size_t cn, uint32_t n_lit, const ui
   return 0;
 }
 
-/* The line matcher of one filter call: content (its '\n' included or not) -> match. */
+/* The line matcher of one filter call: content (its '\n' included or not) -> match.
+ * ko_filter_impl is the kubelet read loop every matcher shares (exported for
+ * klf_oracle_rx.c). */
 typedef int (*ko_match_fn)(void* ctx, const uint8_t* c, size_t cn);
 
-static int64_t filter_impl(const uint8_t* data, uint64_t n, int64_t since_sec, int32_t since_nsec, int64_t tail,
+int64_t ko_filter_impl(const uint8_t* data, uint64_t n, int64_t since_sec, int32_t since_nsec, int64_t tail,
                            int grep_active, ko_match_fn match, void* mctx, uint8_t* out, uint64_t* line_off,
                            uint64_t line_cap, uint8_t* match_bits, ko_counts* cnt) {
   ko_counts c;
@@ -363,108 +358,8 @@ int64_t ko_filter(const uint8_t* data, uint64_t n, int64_t since_sec, int32_t si
   memset(&ac, 0, sizeof ac);
   if (grep_active && n_lit > 8 && ac_build(&ac, n_lit, lits, lit_lens) != 0) return -1;
   lit_ctx x = {n_lit, lits, lit_lens, &ac};
-  const int64_t r = filter_impl(data, n, since_sec, since_nsec, tail, grep_active, lit_match, &x, out, line_off,
+  const int64_t r = ko_filter_impl(data, n, since_sec, since_nsec, tail, grep_active, lit_match, &x, out, line_off,
                                 line_cap, match_bits, cnt);
   ac_free(&ac);
-  return r;
-}
-
-/* ---- regex sets: glibc POSIX ERE behind a required-literal Aho-Corasick pass ----------- */
-typedef struct {
-  uint32_t n;
-  regex_t* re;
-  const int32_t* icase;        /* [n] pattern compiled REG_ICASE; its required literal is lower case */
-  const uint8_t* const* req;   /* [n] required literal (len 0: none, the pattern is always run) */
-  const uint64_t* req_len;
-  ko_ac ac;                    /* every required literal, lower-cased, matched case-insensitively:
-                                  a line holding none of them skips the patterns */
-  int always;                  /* some pattern has no required literal */
-  int any_ci;                  /* some pattern is REG_ICASE */
-  uint8_t* low;                /* the content lower-cased (REG_ICASE literals) */
-  size_t low_cap;
-} rx_ctx;
-
-static int ac_any(const ko_ac* ac, const uint8_t* c, size_t cn) {
-  return ac->next ? ac_scan(ac, c, cn) : 0;
-}
-
-static int rx_match(void* ctx, const uint8_t* c, size_t cn) {
-  rx_ctx* x = (rx_ctx*)ctx;
-  if (cn && c[cn - 1] == '\n') --cn;
-  if (!x->always && !ac_any(&x->ac, c, cn)) return 0;
-  const uint8_t* low = NULL;
-  if (x->any_ci) {
-    if (cn > x->low_cap) {
-      free(x->low);
-      x->low_cap = cn * 2;
-      x->low = (uint8_t*)malloc(x->low_cap);
-      if (!x->low) { x->low_cap = 0; return 0; }
-    }
-    for (size_t i = 0; i < cn; ++i) x->low[i] = (uint8_t)(c[i] >= 'A' && c[i] <= 'Z' ? c[i] | 0x20 : c[i]);
-    low = x->low;
-  }
-  for (uint32_t k = 0; k < x->n; ++k) {
-    if (x->req_len[k]) {
-      const uint8_t* src = x->icase[k] ? low : c;
-      if (x->req_len[k] > cn || !memmem(src, cn, x->req[k], x->req_len[k])) continue;
-    }
-    regmatch_t m;
-    m.rm_so = 0;
-    m.rm_eo = (regoff_t)cn;
-    if (regexec(&x->re[k], (const char*)c, 1, &m, REG_STARTEND) == 0) return 1;
-  }
-  return 0;
-}
-
-/* As ko_filter with n_rx regexes (POSIX ERE, NUL-terminated, translated from the Go
- * subset) in place of literals.  Returns -1 on allocation failure, -2 - k when pattern k
- * does not compile. */
-int64_t ko_filter_rx(const uint8_t* data, uint64_t n, int64_t since_sec, int32_t since_nsec, int64_t tail,
-                     uint32_t n_rx, const char* const* ere, const int32_t* icase, const uint8_t* const* req,
-                     const uint64_t* req_len, uint8_t* out, uint64_t* line_off, uint64_t line_cap, uint8_t* match_bits,
-                     ko_counts* cnt) {
-  rx_ctx x;
-  memset(&x, 0, sizeof x);
-  x.n = n_rx;
-  x.icase = icase;
-  x.req = req;
-  x.req_len = req_len;
-  x.re = (regex_t*)calloc(n_rx ? n_rx : 1, sizeof(regex_t));
-  uint8_t** lw = (uint8_t**)calloc(n_rx ? n_rx : 1, sizeof(void*));
-  uint64_t* lwl = (uint64_t*)calloc(n_rx ? n_rx : 1, sizeof(uint64_t));
-  int64_t r = -1;
-  uint32_t ok = 0, nl = 0;
-  /* byte semantics whatever the process locale (a UTF-8 LC_CTYPE would read the classes'
-   * high bytes as broken multibyte characters): the C locale for this thread */
-  locale_t cloc = newlocale(LC_ALL_MASK, "C", (locale_t)0);
-  locale_t prev = cloc ? uselocale(cloc) : (locale_t)0;
-  if (!cloc || !x.re || !lw || !lwl) goto done;
-  for (; ok < n_rx; ++ok) {
-    if (regcomp(&x.re[ok], ere[ok], REG_EXTENDED | REG_NOSUB | (icase[ok] ? REG_ICASE : 0)) != 0) {
-      r = -2 - (int64_t)ok;
-      goto done;
-    }
-    x.any_ci |= icase[ok] != 0;
-    if (!req_len[ok]) { x.always = 1; continue; }
-    if (!(lw[nl] = (uint8_t*)malloc(req_len[ok]))) goto done;
-    for (uint64_t j = 0; j < req_len[ok]; ++j)
-      lw[nl][j] = (uint8_t)(req[ok][j] >= 'A' && req[ok][j] <= 'Z' ? req[ok][j] | 0x20 : req[ok][j]);
-    lwl[nl++] = req_len[ok];
-  }
-  if (!x.always && ac_build_fold(&x.ac, nl, (const uint8_t* const*)lw, lwl, 1) != 0) goto done;
-  r = filter_impl(data, n, since_sec, since_nsec, tail, n_rx != 0, rx_match, &x, out, line_off, line_cap, match_bits,
-                  cnt);
-done:
-  for (uint32_t k = 0; k < ok; ++k) regfree(&x.re[k]);
-  free(x.re);
-  for (uint32_t k = 0; lw && k < nl; ++k) free(lw[k]);
-  free(lw);
-  free(lwl);
-  ac_free(&x.ac);
-  free(x.low);
-  if (cloc) {
-    uselocale(prev);
-    freelocale(cloc);
-  }
   return r;
 }

@@ -424,6 +424,41 @@ def test_windowed_line_index(gpu, monkeypatch, win):
     check_against_c(streams, None, 50, lits)
 
 
+def _long_window_stream(pre_bytes, long_len, after, lit=b"ms"):
+    """Short lines up to `pre_bytes`, then one line of `long_len` content bytes holding `lit`,
+    then `after` short lines holding it: a --tail after+1 window starts at the long line."""
+    ts = b"2024-10-22T00:59:00.000000000Z "
+    parts, n, i = [], 0, 0
+    while n < pre_bytes:
+        ln = ts + b"short line %d %s\n" % (i, lit if i % 3 == 0 else b"--")
+        parts.append(ln)
+        n += len(ln)
+        i += 1
+    parts.append(ts + b"L" * (long_len // 2) + lit + b"x" * (long_len - long_len // 2 - len(lit)) + b"\n")
+    for j in range(after):
+        parts.append(ts + b"after %d %s\n" % (j, lit))
+    return b"".join(parts)
+
+
+@pytest.mark.parametrize("win", ["1", "0"])
+def test_windowed_index_long_first_line(gpu, monkeypatch, win):
+    """The first line of a tail window is longer than 16 KiB and straddles a 64-tile
+    (512 KiB) scatter-group boundary: the window pass must visit the tile that holds that
+    line's start slot (the tile of the newline before it), not a tile found from the
+    window's line index minus one tile.  Several tiles after that
+    one carry no line start at all."""
+    monkeypatch.setenv("KLF_WIN_INDEX", win)
+    lits = synth.c4_literals(1024)[:200] + [b"ms"]
+    for pre, long_len in ((500_000, 40_000), (520_000, 20_000), (300_000, 600_000), (0, 70_000)):
+        d = _long_window_stream(pre, long_len, 20)
+        lead = synth.generate(synth.TEXT, 3, 0, 200_000)  # moves the global tile numbering
+        for grep in ([b"ms"], lits):
+            for tail in (21, 22, 20, 1):
+                check_against_c([d], None, tail, grep)
+                check_against_c([lead, d], None, tail, grep)
+            check_against_c([d, lead], (synth.T0 + 1800, 0), 21, grep)
+
+
 def test_literal_automaton_thread(gpu, monkeypatch):
     """A literal set's Aho-Corasick automaton is built and uploaded by a host thread that
     klf_open starts and the first run joins: engines closed before any run (the thread

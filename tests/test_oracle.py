@@ -139,7 +139,23 @@ def test_duration_seconds_trunc():
     assert po.duration_seconds_trunc((1 << 33) * 10**9 + 999999999) == (1 << 33) + 1
 
 
-# ---- Go regexp subset (Python re translation) -----------------------------------------
+# ---- Go regexp subset: the Python re translation and the C leg ------------------------
+RX_KAT_GO = [  # regexp/syntax parse.go rules the two legs were written to (round 5)
+    (rb"a{01}", b"a{01}", True), (rb"a{01}", b"a", False),          # parseInt: no leading zeros -> literal '{'
+    (rb"a{1,02}", b"a{1,02}", True), (rb"x{0}y", b"y", True),
+    (rb"\Qab\E*", b"a", True), (rb"^\Qab\E*$", b"abbb", True),   # the repetition takes the last byte
+    (rb"^\Qab\E*$", b"abab", False), (rb"\Q(a|b\E", b"x(a|b", True), (rb"\Qa.b", b"a.b", True),
+    (rb"^a(?i)*$", b"aaa", True), (rb"^a*(?i)*$", b"aaa", True),    # (?flags) pushes nothing
+    (rb"(?i)[[:^upper:]]", b"aB", False), (rb"(?i)[[:^upper:]]", b"a1", True),  # fold, then negate
+    (rb"(?i)[^A-Z]", b"q", False), (rb"(?i)\W", b"K", False), (rb"[[:word:]]", b"_", True),
+    (rb"a(?i)b|c", b"C", True), (rb"(?i:a)b", b"AB", False), (rb"(?i)a(?-i)b", b"AB", False),
+    (rb"(?s).", b"\n", True), (rb".", b"\n", False), (rb"[^a]", b"\n", True),
+    (rb"(?P<x>ab)+$", b"abab", True), (rb"(?<x>a)", b"a", True), (rb"\x{41}", b"A", True),
+    (rb"\0", b"\x00", True), (rb"\x7f", b"\x7f", True), (rb"[]a]", b"]", True), (rb"[^]a]", b"]", False),
+    (rb"[a-]", b"-", True), (rb"[]-a]", b"^", True), (rb"\_", b"_", True), (rb"x{2}{", b"xx{", True),
+    (rb"^$", b"", True), (rb"$^", b"", True), (rb"a$^", b"a", False), (rb"(a|)+b", b"b", True),
+    (rb"(a*)*$", b"bbb", True), (rb"((a*)*|b)+c", b"abac", True), (rb"[[:alpha:]-]{3}", b"a-b", True), (rb"[\d-z]", b"-", True),
+]
 RX_KAT = [
     (rb"a.c", b"xabc", True), (rb"a.c", b"ac", False), (rb"^abc", b"abcd", True), (rb"^abc", b"xabc", False),
     (rb"abc$", b"xabc", True), (rb"abc$", b"abcx", False), (rb"(?i)error", b"an ERROR here", True),
@@ -151,9 +167,11 @@ RX_KAT = [
 ]
 
 
-@pytest.mark.parametrize("pat,s,want", RX_KAT)
+@pytest.mark.parametrize("pat,s,want", RX_KAT + RX_KAT_GO)
 def test_regex_known_answers(pat, s, want):
+    """Both regex legs: the Python oracle (Python re) and the C oracle's own parser + lazy DFA."""
     assert po.Pattern("regex", pat).matches(s) is want
+    assert co.rx_match(pat, s) is want
 
 
 @pytest.mark.parametrize("pat", [rb"a**", rb"(", rb"a)", rb"[a", rb"\b", rb"\pL", rb"\1", rb"*a", rb"a{2,1}",
@@ -161,6 +179,60 @@ def test_regex_known_answers(pat, s, want):
 def test_regex_rejects(pat):
     with pytest.raises((po.PatternError, re.error)):
         po.Pattern("regex", pat)
+    assert co.rx_error(pat) is not None
+
+
+@pytest.mark.parametrize("pat", [rb"[[:foo:]]", rb"a{2}{3}", rb"a*?+", rb"(?i)*", rb"\Q\E*", rb"[z-a]",
+                                 rb"\C", rb"a{1001,}", rb"(?P=x)", rb"(?x)", rb"\x{}", rb"\xg1"])
+def test_regex_rejects_go_rules(pat):
+    with pytest.raises((po.PatternError, re.error)):
+        po.Pattern("regex", pat)
+    assert co.rx_error(pat) is not None
+
+
+def _random_regex(rng, depth=0):
+    """A random pattern of the SPEC.md S5 subset over a small alphabet."""
+    atoms = ["a", "b", "B", "-", ".", r"\d", r"\w", r"\s", r"\W", "[a-c]", "[^ab]", "[[:upper:]]", "[[:^alpha:]]",
+             r"\.", r"\x41", "[-b]", "^", "$"]
+    out = []
+    for _ in range(rng.randint(1, 4)):
+        k = rng.random()
+        if k < 0.15 and depth < 2:
+            inner = "|".join(_random_regex(rng, depth + 1) for _ in range(rng.randint(1, 3)))
+            a = rng.choice(["(", "(?:", "(?i:", "(?P<g>"]) + inner + ")"
+        elif k < 0.2:
+            a = r"\Q" + rng.choice(["a.", "b*", "ab"]) + r"\E"
+        else:
+            a = rng.choice(atoms)
+        if a not in ("^", "$") or rng.random() < 0.3:
+            a += rng.choice(["", "", "", "*", "+", "?", "{2}", "{1,3}", "{0,}", "*?", "{01}"])
+        out.append(a)
+        if rng.random() < 0.1:
+            out.append(rng.choice(["(?i)", "(?-i)", "(?s)"]))
+    return "".join(out)
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_regex_legs_agree_random(seed):
+    """The two regex legs (Python re over the Python oracle's translation; the C leg's own
+    parser, Thompson NFA and lazy DFA) decide random subset patterns the same way, and
+    accept / reject the same patterns."""
+    rng = random.Random(1000 + seed)
+    alphabet = "abAB-.1 _\tzC"
+    n_ok = 0
+    for _ in range(400):
+        pat = _random_regex(rng).encode()
+        try:
+            py = po.Pattern("regex", pat)
+        except (po.PatternError, re.error):
+            assert co.rx_error(pat) is not None, pat
+            continue
+        assert co.rx_error(pat) is None, pat
+        n_ok += 1
+        for _ in range(12):
+            s = "".join(rng.choice(alphabet) for _ in range(rng.randint(0, 9))).encode()
+            assert co.rx_match(pat, s) is py.matches(s), (pat, s)
+    assert n_ok > 250
 
 
 # ---- the two restatements agree -----------------------------------------------------
@@ -272,7 +344,7 @@ def test_c_oracle_aho_corasick_every_byte_value():
     assert whole[3]["matched"] == int(np.unpackbits(bits).sum()) > 0
 
 
-# ---- the compiled CPU baseline of regex sets (glibc POSIX ERE) equals the oracle ------
+# ---- the C regex leg over whole streams equals the Python oracle ---------------------------
 RX_SETS = [
     synth.c5_regexes(),
     [rb"ms$", rb"^\S+ \d", rb"(?i)POD", rb"a.b|c[^x]d", rb"\w{3,5}-\d+", rb"x*", rb"\.\*"],
