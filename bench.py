@@ -1,19 +1,21 @@
 #!/usr/bin/env python3
-"""klogs filter-path benchmark (BASELINE.json configs[1], "C2"):
+"""klogs filter-path benchmark.  Headline: BASELINE.json's north-star workload, config 5 ("C5"):
 
-    one 4 GiB synthetic JSON log stream per GPU, --since 5m --tail 100 --grep <literal>
+    32 GiB of 1-32 KiB JSON log lines per GPU in 28 pod/container streams (8 pods, each with
+    1-2 init containers and 2 containers, the -i stream table of getPodLogs), 64 --match
+    RE2-subset regexes, --since 5m --tail 100
 
-A step = one full klf_run_device pass (memsets, scan kernel, counts/tail, compaction)
-over the device-resident batch plus the per-stream count gather across ranks.  Weak
-scaling: every rank owns its own stream (streams shard across GPUs; no data-path
-collective).  value = total input bytes of all ranks / max-over-ranks wall time.
+A step = one full klf_run_device pass over the device-resident batch (memsets, scan with the
+fused q-gram prefilter, tile index, factor verification, Glushkov NFA windows, counts, tail,
+compaction), plus, at N > 1, the all-gather of the per-stream count records (+ the 64
+per-pattern counts) over RCCL.  Weak scaling: every rank owns 32 GiB (8 pods x N, the stream
+table LPT-sharded, shard.assign); value = all ranks' input bytes / max-over-ranks wall time.
 
-At N = 1 the same line also carries BASELINE configs 4 and 5 under "extra.configs" (the
-general matcher: the scan with the fused q-gram prefilter, then the per-candidate NFA):
-  C4: 32 GiB of mixed-length lines (8 streams), 1,024 --grep literals, --since 5m --tail 100
-  C5: 32 GiB of 1-32 KiB JSON lines, 8 pods with 1-2 init containers (-i stream table),
-      64 --match regexes, --since 5m --tail 100
-each measured the same way (device-resident, HIP events on the launch stream).
+The same line carries the other BASELINE configs under "extra.configs" (N = 1: C2, C1, C3,
+C4; N > 1: C2 and C3 sharded), each measured the same way, and per config the honest step
+bytes: the u64 line index counts only when the run wrote it (klf_result_index_mode "full");
+runs that index only their tail windows (literal sets) or nothing (-l only) report a second
+timing with KLF_FILTER_FULL_INDEX beside it.
 
 Launch: python bench.py [--gpus 1 --steps K --warmup W]; for N > 1 the driver runs
 `python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...`.
@@ -23,9 +25,11 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import subprocess
 import sys
 import tempfile
 import time
+from concurrent.futures import ThreadPoolExecutor
 from pathlib import Path
 
 import numpy as np
@@ -40,51 +44,600 @@ from klogs_amd import shard, synth  # noqa: E402
 
 METRIC = "filtered log GB/s (whole node) at 1/2/4/8 MI355X; % of HBM peak"
 HBM_PEAK_GBS = 8000.0  # MI355X spec, /opt/skills/guides/MI355X_MICROARCH.md
-STREAM_BYTES = 4 << 30
+HEADLINE = "c5"
 SINCE_S = 300  # --since 5m
 TAIL = 100
-
-
-def pmc_traffic():
-    """Per-launch HBM bytes of k_scan<literal> from the newest committed rocprofv3 --pmc
-    summary (profiles/<round>/traffic.json, written by scripts/collect_profiles.py from
-    FETCH_SIZE / WRITE_SIZE passes over this same command), or None."""
-    files = sorted(ROOT.glob("profiles/r*/traffic.json"))
-    if not files:
-        return None, None
-    t = json.loads(files[-1].read_text())
-    return int(t["traffic_bytes"]), str(files[-1].relative_to(ROOT))
-
-
-def committed_trace_frac(cfg: str = "c2"):
-    """The same roofline fraction from the newest committed kernel trace
-    (profiles/<round>/summary.json, scripts/collect_profiles.py): bytes / rocprofv3's average
-    launch / peak, measured on the profiling box -- reported beside the live HIP-event one."""
-    files = sorted(ROOT.glob("profiles/r*/summary.json"))
-    if not files:
-        return None, None
-    s = json.loads(files[-1].read_text()).get(cfg)
-    return (s and s["frac_rocprof"]), str(files[-1].relative_to(ROOT))
+PER_GPU = 32 << 30  # C4 / C5 bytes per GPU
 
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+def oracle():
+    """The C oracle (test infrastructure): only ever the checker / the CPU baseline leg,
+    imported after the timed regions."""
+    sys.path.insert(0, str(ROOT / "oracle"))
+    import c_oracle as co
+    return co
+
+
+def host_threads() -> int:
+    return max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", "16") or 16)))
+
+
+# ---------------------------------------------------------------- configs -----------
+def c5_pods(n_pods: int):
+    return [(f"synthetic-{p}", [f"init-{k}" for k in range(1 + p % 2)], ["app", "sidecar"]) for p in range(n_pods)]
+
+
+def config_table(name: str, world: int = 1):
+    """(stream sizes, generator kind, patterns, permille, mode, description) of BASELINE
+    config `name`; at N ranks the per-GPU share times N (weak scaling)."""
+    if name == "c1":  # the reference's own CPU-runnable case (BASELINE configs[0])
+        return [64 << 20], synth.TEXT, {}, 10, "since+tail", \
+            "C1: one 64 MiB stream (lognormal line lengths, median 96 B), --since 5m --tail 100"
+    if name == "c2":
+        return [4 << 30] * world, synth.JSON, dict(grep=[synth.NEEDLE]), 10, "since+tail", \
+            (f"C2: one 4 GiB JSON log stream per GPU (x {world}), --since 5m --tail 100 --grep "
+             + synth.NEEDLE.decode())
+    if name == "c3":  # one GPU's share of C3 at 8 GPUs: 256 pods x 4 containers / 8
+        return [64 << 20] * (128 * world), synth.TEXT, {}, 10, "-l", \
+            (f"C3: 128 x 64 MiB streams per GPU (x {world}; 256 pods x 4 containers over 8 GPUs), -l selection "
+             "only: no --since, no --tail, no grep (every line out, prefix stripped)")
+    if name == "c4":
+        n = 8 * world
+        return [PER_GPU // 8] * n, synth.MIXED, dict(grep=synth.c4_literals(1024)), 5, "since+tail", \
+            (f"C4: 8 streams per GPU (x {world}) of mixed-length lines (16 B-8 KiB, lognormal), 1,024 --grep "
+             "literals (6-24 B, 0.5% of lines hold one), --since 5m --tail 100")
+    if name == "c5":
+        from klogs_amd import host as H
+        table = H.stream_table(c5_pods(8 * world), init=True)  # getPodLogs order with -i (cmd/root.go:240-262)
+        w = [1 if is_init else 4 for _, _, is_init in table]
+        sizes = [PER_GPU * world * x // sum(w) for x in w]
+        return sizes, synth.LONGJSON, dict(match=synth.c5_regexes()), 5, "since+tail", \
+            (f"C5: {len(table)} streams (8 pods per GPU x {world}, 1-2 init containers + 2 containers each, -i), "
+             "32 GiB per GPU of 1-32 KiB JSON lines, 64 --match RE2-subset regexes (0.5% of lines match one, "
+             "1% hold a factor but no match), --since 5m --tail 100")
+    raise ValueError(name)
+
+
+def scan_kernel_name(name: str, pats: dict) -> str:
+    if name == "c2":
+        return "k_scan<literal>"
+    if not pats:
+        return "k_scan<plain>"
+    return "k_scan<general: fused q-gram prefilter>"
+
+
+def load_batch(sizes, kind, permille, ids, local):
+    """Streams `ids` of the config generated on the host and copied into one device batch."""
+    lens = [synth.size(kind, 42, i, sizes[i], permille=permille) for i in ids]
+    seg_base, total = E.layout(lens)
+    dev = torch.empty(total, dtype=torch.uint8, device=f"cuda:{local}")
+    h = np.empty(max(lens) + 1, dtype=np.uint8)
+    for j, i in enumerate(ids):
+        synth.generate_into(h, kind, 42, i, sizes[i], permille=permille)
+        dev[int(seg_base[j]):int(seg_base[j]) + lens[j]].copy_(torch.from_numpy(h[:lens[j]]))
+    torch.cuda.synchronize()
+    return dev, seg_base, lens
+
+
+# ---------------------------------------------------------------- GPU state ---------
+def gpu_state(local: int) -> dict:
+    """sclk / mclk / power / temperature / perf level of this rank's card (rocm-smi), so a
+    box-to-box spread can be attributed; {"error": ...} when rocm-smi cannot say."""
+    try:
+        bus = None
+        try:
+            p = torch.cuda.get_device_properties(local)
+            bus = getattr(p, "pci_bus_id", None)
+        except Exception:
+            pass
+        out = subprocess.run(["rocm-smi", "--showbus", "-c", "-P", "-t", "-p", "--json"], capture_output=True,
+                             text=True, timeout=30)
+        txt = out.stdout[out.stdout.find("{"):]
+        d = json.loads(txt)
+        cards = {k: v for k, v in d.items() if k.startswith("card")}
+        mine = {k: v for k, v in cards.items()
+                if bus is not None and any(str(x).lower().endswith(f"{bus:02x}:00.0") for x in v.values())}
+        pick = mine or cards
+        keep = ("sclk", "mclk", "fclk", "socclk", "power", "temperature", "perf", "pci bus")
+        return {k: {f: x for f, x in v.items() if any(s in f.lower() for s in keep)} for k, v in pick.items()} | \
+            {"matched_card": bool(mine)}
+    except Exception as ex:  # noqa: BLE001 (diagnostic only)
+        return {"error": f"{type(ex).__name__}: {ex}"[:200]}
+
+
+# ---------------------------------------------------------------- bytes -------------
+def step_bytes(n_in: int, tot: dict, n_streams: int, has_patterns: bool, index_full: bool) -> int:
+    """SURVEY.md §8d B_alg = B_in + B_out + 8 (L + S) + ceil(L / 8), with the u64 line index
+    counted only when the run wrote it, and the match bitmap only when the run has patterns."""
+    b = n_in + tot["out_bytes"]
+    if has_patterns:
+        b += (tot["lines"] + 7) // 8
+    if index_full:
+        b += 8 * (tot["lines"] + n_streams)
+    return b
+
+
+# ---------------------------------------------------------------- one config (N = 1) -
+def run_config(name: str, args, local: int, now: int, headline: bool = False) -> dict:
+    sizes, kind, pats, permille, mode, desc = config_table(name)
+    t = time.time()
+    dev, seg_base, lens = load_batch(sizes, kind, permille, list(range(len(sizes))), local)
+    log(f"[{name}] generated + uploaded {sum(lens)} B in {time.time() - t:.1f}s")
+    since, tail = ((None, -1) if mode == "-l" else ((now - SINCE_S, 0), TAIL))
+    stream = torch.cuda.current_stream()
+    state0 = gpu_state(local)
+    eng = E.Engine(local, hip_stream=stream.cuda_stream, **pats)
+    ptr = dev.data_ptr()
+    n = sum(lens)
+
+    def timed(steps, warmup, **kw):
+        for _ in range(warmup):
+            eng.run_device(ptr, seg_base, lens, since=since, tail=tail, **kw).free()
+        torch.cuda.synchronize()
+        scan, copy, dev_ms = [], [], []
+        t0 = time.perf_counter()
+        last = None
+        for i in range(steps):
+            r = eng.run_device(ptr, seg_base, lens, since=since, tail=tail, **kw)
+            tm = r.timing()
+            scan.append(tm[6])
+            copy.append(tm[7])
+            dev_ms.append(tm[4])
+            if i + 1 < steps:
+                r.free()
+            else:
+                last = r
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t0), last, float(np.mean(scan)), float(np.mean(copy)), float(np.mean(dev_ms))
+
+    dt, last, scan_ms, copy_ms, dev_ms = timed(args.steps, args.warmup)
+    tot = last.totals()
+    index_mode = last.index_mode()
+    has_pats = bool(pats)
+    alg = step_bytes(n, tot, len(lens), has_pats, index_mode == "full")
+    ms_step = dt / args.steps * 1e3
+    out = {"workload": desc, "streams": len(lens), "bytes": n, "lines": tot["lines"],
+           "value_GBps": round(n * args.steps / dt / 1e9, 1), "ms_per_step": round(ms_step, 4),
+           "device_ms_per_step": round(dev_ms, 4), "line_index": index_mode}
+    # the dominant kernel: the scan, except C3 (-l only, every line out) where the dense copy
+    # k_tcopy takes ~60 % of the step; its algorithmic bytes are the bytes it must move, the
+    # selected content read once and written once (2 B_out)
+    if mode == "-l":
+        k_alg, k_ms, k_name = 2 * tot["out_bytes"], copy_ms, "k_tcopy"
+    else:
+        k_alg, k_ms, k_name = n, scan_ms, scan_kernel_name(name, pats)
+    k_ms = max(k_ms, 1e-9)  # (0: a build without the dispatch events, KLF_SCAN_EVENTS=0)
+    out["roofline"] = {"bound": "hbm", "kernel": k_name, "achieved": round(k_alg / k_ms / 1e6, 1),
+                       "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(k_alg / k_ms / 1e6 / HBM_PEAK_GBS, 4),
+                       "alg_bytes_per_launch": k_alg, "avg_launch_ms": round(k_ms, 4),
+                       "frac_source": "HIP events carrying the kernel dispatch's own start / end timestamps "
+                                      "(hipExtLaunchKernel on the launch stream), this run's timed steps"}
+    if mode == "-l":
+        out["roofline"]["alg_bytes_note"] = ("k_tcopy moves the selected contents: B_out read + B_out written "
+                                             "(the input's 31-B prefixes are skipped in place)")
+        out["scan"] = {"kernel": "k_scan<plain>", "avg_launch_ms": round(scan_ms, 4),
+                       "frac": round(n / max(scan_ms, 1e-9) / 1e6 / HBM_PEAK_GBS, 4)}
+    out["step_alg_bytes"] = alg
+    out["step_alg_frac_of_peak"] = round(alg / (ms_step / 1e3) / 1e9 / HBM_PEAK_GBS, 4)
+    out["step_alg_frac_of_peak_device"] = round(alg / (dev_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4)
+    out["step_bytes_rule"] = ("B_in + B_out" + (" + ceil(L/8) match bitmap" if has_pats else "")
+                              + (" + 8 (L + S) u64 line index (written by the run)" if index_mode == "full" else
+                                 " (the u64 line index is not written by this run: see full_index)"))
+    out["matched_lines"], out["selected_lines"], out["out_bytes"] = tot["matched"], tot["selected"], tot["out_bytes"]
+    # the step that writes every line's u64 offset too (KLF_FILTER_FULL_INDEX), beside it
+    if index_mode != "full":
+        last.free()
+        last = None
+        fsteps = max(3, args.steps // 2)
+        fdt, flast, _, _, fdev = timed(fsteps, 1, full_index=True)
+        ftot = flast.totals()
+        assert flast.index_mode() == "full" and ftot == tot, (flast.index_mode(), ftot, tot)
+        falg = step_bytes(n, ftot, len(lens), has_pats, True)
+        out["full_index"] = {"ms_per_step": round(fdt / fsteps * 1e3, 4), "steps": fsteps,
+                             "value_GBps": round(n * fsteps / fdt / 1e9, 1), "step_alg_bytes": falg,
+                             "step_alg_frac_of_peak": round(falg / (fdt / fsteps) / 1e9 / HBM_PEAK_GBS, 4),
+                             "device_ms_per_step": round(fdev, 4)}
+        last = flast
+    out["cold"] = cold_run(local, pats, ptr, seg_base, lens, since, tail)
+    # checks after the timed regions
+    co = None
+    if not args.no_verify:
+        co = oracle()
+    if name in ("c1", "c2") and co is not None:  # the whole stream: bytes, counts, every line offset
+        h = np.empty(lens[0] + 1, dtype=np.uint8)
+        synth.generate_into(h, kind, 42, 0, sizes[0], permille=permille)
+        ref_out, ref_lo, _, ref_c = co.filter_stream(h[:lens[0]], since, tail, pats.get("grep", []), want_bits=False)
+        so = last.stream(0)
+        out["verified_vs_oracle"] = bool(so.out == ref_out and all(so.counts[k] == ref_c[k] for k in ref_c)
+                                         and np.array_equal(last.lines(0), ref_lo))
+        out["verify"] = {"scope": "the whole stream: output bytes, all counts, every u64 line offset (C oracle)"}
+        if name == "c2" and not args.no_capture:
+            out["capture_path"] = capture_path(local, pats, h[:lens[0]], since, tail, so.out, args.capture_piece)
+        del h
+    write = None
+    if name == "c3" and not args.no_write:
+        write = write_path(last, lens, sizes, kind, permille, co)
+        out["write_path"] = write
+        if co is not None and "verified_vs_c_oracle" in write:
+            out["verified_vs_oracle"] = write["verified_vs_c_oracle"]
+            out["verify"] = {"scope": "first and last stream as written to their files (C oracle)"}
+    if name in ("c4", "c5") and co is not None:
+        del dev  # the checks regenerate the streams on the host
+        torch.cuda.empty_cache()
+        dev = None
+        v = verify_large(name, sizes, lens, kind, permille, pats, since, tail, last, co)
+        out["verified_vs_oracle"] = v.pop("ok")
+        out["verify"] = v
+    if dev is not None:
+        last.free()
+        last = None
+        staged = eng.run_device(ptr, seg_base, lens, since=since, tail=tail, stage_times=True)
+        stage = staged.timing()
+        staged.free()
+    else:  # the batch was dropped for the checks: the stage split of the timed runs' last
+        stage = last.timing()
+    out["stage_ms"] = [round(x, 4) for x in stage]
+    out["stage_names"] = ["scan stage", "matchers", "counts+tail", "compaction", "total", "memsets", "k_scan",
+                          "k_tcopy"]
+    if last is not None:
+        last.free()
+    eng.close()
+    del dev
+    torch.cuda.empty_cache()
+    out["gpu_state"] = {"before": state0, "after": gpu_state(local)}
+    if not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(name, kind, pats, permille, since, tail, headline)
+    return out
+
+
+def capture_path(local, pats, host, since, tail, want, piece) -> dict:
+    """§8f-2, C2 at N = 1: the product's host entry points on this run's bytes -- klf_stage in
+    pieces (io.Copy's role) into pinned chunks, then klf_run (DMA H2D from the pinned chunks
+    + the whole filter) and the output D2H.  Reported beside `value`, never as it."""
+    n = len(host)
+    ceng = E.Engine(local, **pats)
+    runs = []
+    for _ in range(2):  # the first pays the pinned-chunk allocation
+        ceng.reset()
+        ceng.set_streams(1)
+        t0 = time.perf_counter()
+        for off in range(0, n, piece):
+            ceng.stage_array(0, host[off:off + piece])
+        t1 = time.perf_counter()
+        r = ceng.run(since=since, tail=tail, n_streams=1)
+        got = r.stream(0).out
+        t2 = time.perf_counter()
+        r.free()
+        runs.append((t1 - t0, t2 - t1, got == want))
+    ceng.close()
+    st_s, run_s, same = runs[-1]
+    return {"stage_GBps": round(n / st_s / 1e9, 2), "h2d_filter_d2h_GBps": round(n / run_s / 1e9, 2),
+            "end_to_end_GBps": round(n / (st_s + run_s) / 1e9, 2), "piece_bytes": piece,
+            "staging": "pinned 64 MiB chunks (hipHostMalloc, reused across runs)",
+            "output_matches_device_run": bool(same and runs[0][2])}
+
+
+def write_path(last, lens, sizes, kind, permille, co) -> dict:
+    """§8f-3 output write path (C3): every stream into its own file (klf_result_write); the
+    first and last file checked against the C oracle."""
+    wdir = tempfile.TemporaryDirectory(prefix="klf_c3_")
+    paths = [os.path.join(wdir.name, f"pod{i // 4}__c{i % 4}.log") for i in range(len(lens))]
+    tw = time.perf_counter()
+    try:
+        wbytes = last.write_files(paths)
+    except E.KlfError as ex:  # e.g. no room for 6.9 GB in the temp dir: reported, not fatal
+        wdir.cleanup()
+        return {"error": str(ex)}
+    wdt = time.perf_counter() - tw
+    write = {"GBps": round(wbytes / wdt / 1e9, 2), "bytes": wbytes, "files": len(paths), "s": round(wdt, 3),
+             "how": "klf_result_write: 64 MiB pinned D2H chunks, double-buffered, 8 writer threads each owning "
+                    "whole files, into page-cache files under " + os.path.dirname(wdir.name)}
+    if co is not None:
+        ok = True
+        for i in (0, len(lens) - 1):
+            h = np.empty(lens[i] + 1, dtype=np.uint8)
+            synth.generate_into(h, kind, 42, i, sizes[i], permille=permille)
+            want = co.filter_stream(h[:lens[i]], co.GO_ZERO_TIME, -1, [], want_lines=False, want_bits=False)[0]
+            with open(paths[i], "rb") as f:  # the written file, i.e. the D2H + write path too
+                ok = ok and f.read() == want
+        write["verified_vs_c_oracle"] = bool(ok)
+    wdir.cleanup()
+    return write
+
+
+def verify_large(name, sizes, lens, kind, permille, pats, since, tail, r, co) -> dict:
+    """Checks the last timed run of C4 / C5 against the C oracle, every stream in full, one
+    host thread per stream: output bytes, all counts and the match bitmap.  C4: Aho-Corasick
+    over the 1,024 literals.  C5: the oracle's own Go-regexp restatement (ko_filter_rx:
+    oracle/klf_oracle_rx.c, its own parser, Thompson NFA + lazy DFA behind a required-literal
+    pass; tests/test_oracle.py checks it against the Python oracle)."""
+    t = time.perf_counter()
+    got = [(r.stream(i), r.match_bits(i)) for i in range(len(lens))]
+    sn = since if since is not None else co.GO_ZERO_TIME
+    rs = co.RegexSet(pats["match"]) if "match" in pats else None
+
+    def check(i):
+        h = np.empty(lens[i] + 1, dtype=np.uint8)
+        synth.generate_into(h, kind, 42, i, sizes[i], permille=permille, threads=1)
+        if rs is not None:
+            out, _, bits, c = co.filter_stream_rx(h[:lens[i]], sn, tail, rs, want_lines=False)
+        else:
+            out, _, bits, c = co.filter_stream(h[:lens[i]], sn, tail, pats["grep"], want_lines=False)
+        so, gbits = got[i]
+        return so.out == out and gbits == bits and all(so.counts[k] == c[k] for k in c)
+    with ThreadPoolExecutor(min(host_threads(), len(lens))) as ex:
+        ok = list(ex.map(check, range(len(lens))))
+    bad = [i for i, x in enumerate(ok) if not x]
+    scope = ("every stream in full: output bytes, all counts, match bitmap ("
+             + ("C oracle ko_filter_rx: own Go-regexp restatement" if rs is not None else "C oracle, Aho-Corasick")
+             + ")")
+    return {"ok": not bad, "streams": len(lens), "failed_streams": bad, "scope": scope,
+            "s": round(time.perf_counter() - t, 1)}
+
+
+def cold_run(local: int, pats: dict, ptr: int, seg_base, lens, since, tail: int) -> dict:
+    """One-shot cost, as one klogs invocation pays it (INTEGRATION.md: klf_run once per
+    run): a fresh engine (klf_open: pattern compile + table uploads) and its first run on
+    the device-resident batch, host wall clock; beside it the same engine's second run."""
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    eng = E.Engine(local, hip_stream=torch.cuda.current_stream().cuda_stream, **pats)
+    t1 = time.perf_counter()
+    r = eng.run_device(ptr, seg_base, lens, since=since, tail=tail)
+    t2 = time.perf_counter()
+    r.free()
+    t3 = time.perf_counter()
+    r = eng.run_device(ptr, seg_base, lens, since=since, tail=tail)
+    t4 = time.perf_counter()
+    r.free()
+    eng.close()
+    return {"open_ms": round((t1 - t0) * 1e3, 3), "first_run_ms": round((t2 - t1) * 1e3, 3),
+            "cold_ms": round((t2 - t0) * 1e3, 3), "second_run_ms": round((t4 - t3) * 1e3, 3),
+            "ratio": round((t2 - t0) / max(t4 - t3, 1e-9), 3)}
+
+
+# ---------------------------------------------------------------- CPU baseline ------
+def cpu_baseline(name, kind, pats, permille, since, tail, headline: bool) -> dict:
+    """The C restatement (oracle/klf_oracle_c.c, klf_oracle_rx.c) timed on this box's host
+    cores over a bounded sample of the same generator and shape (rank 0, N = 1): one core
+    (the baseline object itself), and T threads with one stream each (the reference runs one
+    goroutine per stream).  The headline's sample is ~10 s of single-core work.  Literal
+    paths: ko_filter (memmem / Aho-Corasick).  C5: ko_filter_rx, the C leg's own Go-regexp
+    restatement behind a required-literal pass."""
+    co = oracle()
+    threads = host_threads()
+    sample = {"c1": 64 << 20, "c2": 64 << 20, "c3": 64 << 20, "c4": 4 << 20, "c5": 16 << 20}[name]
+    nstreams = 1 if name == "c1" else threads
+    streams = [synth.generate(kind, 7, i, sample, permille=permille) for i in range(nstreams)]
+    grep = pats.get("grep", [])
+    sn = since if since is not None else co.GO_ZERO_TIME
+    if "match" in pats:
+        rs = co.RegexSet(pats["match"])
+
+        def one(b):
+            return co.filter_stream_rx(b, sn, tail, rs, want_lines=False, want_bits=False)
+        impl = "oracle/klf_oracle_rx.c ko_filter_rx (own Go-regexp restatement: Thompson NFA + lazy DFA behind " \
+               "a required-literal Aho-Corasick pass)"
+    else:
+        def one(b):
+            return co.filter_stream(b, sn, tail, grep, want_lines=False, want_bits=False)
+        impl = "oracle/klf_oracle_c.c ko_filter (memchr line split, Go time.Parse restated, memmem / Aho-Corasick, " \
+               "kubelet tail + since)"
+
+    def timed(f, budget):
+        k, tt = 0, 0.0
+        while tt < budget and k < 2048:
+            t0 = time.perf_counter()
+            f()
+            tt += time.perf_counter() - t0
+            k += 1
+        return k, tt
+    k, tt = timed(lambda: one(streams[0]), 10.0 if headline else 3.0)
+    res = {"value": round(sample * k / tt / 1e9, 4), "unit": "GB/s", "cores": 1, "kind": "port",
+           "sample": f"{k} passes over one {sample >> 20} MiB stream of the {name.upper()} generator, {impl}, "
+                     f"1 host thread, {tt:.1f} s",
+           "host_cpus": os.cpu_count(), "host_cpus_affinity": len(os.sched_getaffinity(0))}
+    if nstreams > 1:
+        with ThreadPoolExecutor(threads) as ex:
+            k, tt = timed(lambda: list(ex.map(one, streams)), 4.0 if headline else 3.0)
+        res["threads"] = {"value": round(sample * threads * k / tt / 1e9, 4), "unit": "GB/s", "cores": threads,
+                          "kind": "port", "sample": f"{k} passes over {threads} streams of {sample >> 20} MiB, one "
+                                                    f"host thread per stream, {tt:.1f} s",
+                          "note": f"threads = min(16, OMP_NUM_THREADS) of the box's {os.cpu_count()} CPUs "
+                                  "(the GPU box's CPU share is 16)"}
+    if headline:  # the reference client's own work: io.Copy of each body into its file
+        res["copy_bound"] = copy_bound(streams[0])
+    return res
+
+
+def copy_bound(host: bytes) -> dict:
+    """klogs itself only io.Copy's each body into its file (cmd/root.go:359-374): a host
+    memcpy and a page-cache file write of the sample bound that from above."""
+    src = np.frombuffer(host, dtype=np.uint8)
+    dst = np.empty_like(src)
+    t = time.perf_counter()
+    for _ in range(8):
+        np.copyto(dst, src)
+    t_cp = (time.perf_counter() - t) / 8
+    with tempfile.NamedTemporaryFile(prefix="klf_cpy_") as f:
+        t = time.perf_counter()
+        mv = memoryview(src)
+        off = 0
+        while off < len(src):
+            off += os.write(f.fileno(), mv[off:off + (64 << 20)])
+        t_w = time.perf_counter() - t
+    return {"memcpy_1t_GBps": round(len(src) / t_cp / 1e9, 2), "file_write_GBps": round(len(src) / t_w / 1e9, 2)}
+
+
+# ---------------------------------------------------------------- N > 1 -------------
+def run_sharded(name: str, args, world: int, rank: int, local: int, coll_dev, now: int) -> dict:
+    """BASELINE config `name` across ranks: the stream table LPT-assigned
+    (shard.assign), each rank one device batch of its own streams, then the one all-gather
+    of per-stream count records (+ per-pattern counts) per step over RCCL.  value = all
+    ranks' bytes / max-over-ranks time.  After the timed region every rank checks its own
+    rows of the gathered table and verifies its first and last stream in full against the C
+    oracle; the flags are all-reduced (MIN)."""
+    sizes, kind, pats, permille, mode, desc = config_table(name, world)
+    since, tail = ((None, -1) if mode == "-l" else ((now - SINCE_S, 0), TAIL))
+    lens_all = [synth.size(kind, 42, i, sz, permille=permille) for i, sz in enumerate(sizes)]
+    mine = shard.local_streams(lens_all, world, rank)
+    t = time.time()
+    dev, seg_base, lens = load_batch(sizes, kind, permille, mine, local)
+    log(f"[rank {rank}] {name} share: {len(mine)} streams, {sum(lens)} B in {time.time() - t:.1f}s")
+    eng = E.Engine(local, hip_stream=torch.cuda.current_stream().cuda_stream, **pats)
+    ptr = dev.data_ptr()
+    npat = len(pats.get("match", [])) + len(pats.get("grep", []))
+    pending = []
+
+    def records(r):
+        recs = {}
+        for j, sid in enumerate(mine):
+            c = r.stream_counts(j)
+            if npat:
+                c = dict(c, patterns=r.pattern_counts(j))
+            recs[sid] = c
+        return recs
+
+    def step():
+        r = eng.run_device(ptr, seg_base, lens, since=since, tail=tail, pattern_counts=bool(npat))
+        # the records go out while the next step filters; every gather is waited for before
+        # the timed region closes
+        pending.append(shard.gather_counts_async(records(r), lens_all, world, device=coll_dev, n_patterns=npat))
+        if len(pending) > 1:
+            pending.pop(0).wait()
+        return r
+
+    def finish():
+        while pending:
+            step.table = pending.pop(0).wait()
+    for _ in range(args.warmup):
+        step().free()
+    finish()
+    torch.cuda.synchronize()
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    last = None
+    scan_ms = []
+    for i in range(args.steps):
+        r = step()
+        scan_ms.append(r.timing()[6])
+        if i + 1 < args.steps:
+            r.free()
+        else:
+            last = r
+    finish()
+    torch.cuda.synchronize()
+    dist.barrier()
+    dt = time.perf_counter() - t0
+    tt = torch.tensor([dt], dtype=torch.float64, device=coll_dev)
+    dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+    dt = float(tt.item())
+    mine_rec = records(last)
+    fields = shard.RECORD_FIELDS[1:]
+    rec_ok = all(step.table[sid].tolist() == [mine_rec[sid][k] for k in fields] + list(mine_rec[sid].get("patterns", []))
+                 for sid in mine)
+    rec_ok = rec_ok and int(step.table[:, 0].sum()) > 0 and int(step.table[:, 5].sum()) > 0
+    tot = last.totals()
+    index_mode = last.index_mode()
+    n_mine = sum(lens)
+    scan_avg = max(float(np.mean(scan_ms)), 1e-9)
+    ver = None
+    if not args.no_verify:
+        co = oracle()
+        rs = co.RegexSet(pats["match"]) if "match" in pats else None
+        sn = since if since is not None else co.GO_ZERO_TIME
+        got = {j: (last.stream(j), last.match_bits(j) if npat else None) for j in sorted({0, len(mine) - 1})}
+        del dev
+        torch.cuda.empty_cache()
+        dev = None
+
+        def check(j):
+            i = mine[j]
+            hh = np.empty(lens[j] + 1, dtype=np.uint8)
+            synth.generate_into(hh, kind, 42, i, sizes[i], permille=permille)
+            if rs is not None:
+                out, _, bits, c = co.filter_stream_rx(hh[:lens[j]], sn, tail, rs, want_lines=False)
+            else:
+                out, _, bits, c = co.filter_stream(hh[:lens[j]], sn, tail, pats.get("grep", []), want_lines=False,
+                                                   want_bits=bool(npat))
+            so, gb = got[j]
+            return so.out == out and all(so.counts[k] == c[k] for k in c) and (gb is None or gb == bits)
+        tv = time.perf_counter()
+        with ThreadPoolExecutor(len(got)) as ex:
+            ver = all(ex.map(check, list(got)))
+        log(f"[rank {rank}] {name} verified={ver} ({time.perf_counter() - tv:.1f}s)")
+    # every rank's scan fraction and step bytes, reduced: MIN fraction, SUM bytes
+    alg_mine = step_bytes(n_mine, tot, len(lens), bool(npat), index_mode == "full")
+    red = torch.tensor([alg_mine, n_mine], dtype=torch.float64, device=coll_dev)
+    dist.all_reduce(red, op=dist.ReduceOp.SUM)
+    fmin = torch.tensor([n_mine / scan_avg / 1e6 / HBM_PEAK_GBS], dtype=torch.float64, device=coll_dev)
+    dist.all_reduce(fmin, op=dist.ReduceOp.MIN)
+    flags = torch.tensor([int(rec_ok), -1 if ver is None else int(ver)], dtype=torch.int64, device=coll_dev)
+    dist.all_reduce(flags, op=dist.ReduceOp.MIN)
+    last.free()
+    eng.close()
+    del dev
+    torch.cuda.empty_cache()
+    total_in = int(sum(lens_all))
+    out = {"workload": desc, "streams": len(lens_all), "bytes": total_in,
+           "value_GBps": round(total_in * args.steps / dt / 1e9, 1), "ms_per_step": round(dt / args.steps * 1e3, 4),
+           "line_index": index_mode,
+           "rank0": {"streams": len(mine), "bytes": n_mine,
+                     "scan": {"kernel": scan_kernel_name(name, pats), "avg_launch_ms": round(scan_avg, 4),
+                              "alg_bytes_per_launch": n_mine,
+                              "frac": round(n_mine / scan_avg / 1e6 / HBM_PEAK_GBS, 4)}},
+           "scan_frac_min_over_ranks": round(float(fmin.item()), 4),
+           "step_alg_bytes_all_ranks": int(red[0].item()),
+           "step_alg_frac_of_peak_per_gpu": round(float(red[0].item()) / (dt / args.steps) / 1e9 / HBM_PEAK_GBS
+                                                  / world, 4),
+           "records_consistent": bool(flags[0].item()),
+           "collective": f"one all-gather per step of {len(lens_all)} x {shard.NREC + npat} int64 records "
+                         f"({'RCCL' if coll_dev != 'cpu' else 'gloo'})"}
+    if ver is not None:
+        out["verified_vs_oracle"] = bool(flags[1].item() == 1)
+        out["verify_scope"] = ("on every rank: its first and last stream in full (output bytes, all counts"
+                               + (", match bitmap" if npat else "") + ") against the C oracle")
+    return out
+
+
+# ---------------------------------------------------------------- profiles ----------
+def committed(cfg: str):
+    """(per-launch HBM traffic of cfg's roofline kernel from the newest rocprofv3 --pmc
+    summary, its source; the rocprof-trace fraction, its source) -- profiles/<round>/
+    traffic.json and summary.json, written by scripts/collect_profiles.py."""
+    tr = sorted(ROOT.glob("profiles/r*/traffic.json"))
+    traffic = src_t = None
+    if tr:
+        t = json.loads(tr[-1].read_text())
+        if cfg in t:
+            traffic, src_t = int(t[cfg]["traffic_bytes"]), str(tr[-1].relative_to(ROOT))
+    sm = sorted(ROOT.glob("profiles/r*/summary.json"))
+    frac = src_f = None
+    if sm:
+        s = json.loads(sm[-1].read_text()).get(cfg)
+        if s:
+            frac, src_f = s.get("frac_rocprof_steady") or s.get("frac_rocprof"), str(sm[-1].relative_to(ROOT))
+    return traffic, src_t, frac, src_f
+
+
+# ---------------------------------------------------------------- main --------------
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--bytes", type=int, default=STREAM_BYTES, help="stream bytes per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--no-write", action="store_true", help="skip C3's file write path")
-    ap.add_argument("--no-capture", action="store_true", help="skip the host-staged capture-path timing")
+    ap.add_argument("--no-capture", action="store_true", help="skip C2's host-staged capture-path timing")
     ap.add_argument("--capture-piece", type=int, default=4 << 20, help="klf_stage piece size of the capture path")
-    ap.add_argument("--extra-configs", default="c1,c3,c4,c5",
-                    help="comma list of c1,c3,c4,c5 ('' = none); at N > 1: c3 and c5 run sharded")
-    ap.add_argument("--extra-bytes", type=int, default=32 << 30, help="total bytes of each extra config")
+    ap.add_argument("--extra-configs", default=None,
+                    help="comma list ('' = none); default c2,c1,c3,c4 at N = 1, c2,c3 (sharded) at N > 1")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -102,696 +655,69 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
             dist.init_process_group(backend)
+    now = synth.T0 + synth.SPAN + 1  # "now" = end of the streams + 1 s
+    extras = args.extra_configs
+    if extras is None:
+        extras = "c2,c1,c3,c4" if world == 1 else "c2,c3"
+    extras = [x for x in extras.split(",") if x and x != HEADLINE]
 
-    # ---- synthetic input: stream `rank` of the C2 family, generated on the host ----
-    assert shard.local_streams([args.bytes] * world, world, rank) == [rank]  # LPT: equal streams 1:1
-    t = time.time()
-    n = synth.size(synth.JSON, 42, rank, args.bytes, permille=10)
-    host = np.empty(n + 1, dtype=np.uint8)
-    synth.generate_into(host, synth.JSON, 42, rank, args.bytes, permille=10)
-    host = host[:n]
-    seg_base, total = E.layout([n])
-    dev = torch.empty(total, dtype=torch.uint8, device=f"cuda:{local}")
-    torch.cuda.synchronize()
-    t_h2d = time.time()
-    dev[:n].copy_(torch.from_numpy(host), non_blocking=False)
-    torch.cuda.synchronize()
-    h2d_s = time.time() - t_h2d
-    log(f"[rank {rank}] generated {n} B in {time.time() - t:.1f}s, H2D {n / h2d_s / 1e9:.1f} GB/s")
-
-    now = synth.T0 + synth.SPAN + 1  # "now" = end of the stream + 1 s
-    since = (now - SINCE_S, 0)
-    stream = torch.cuda.current_stream()
-    eng = E.Engine(local, grep=[synth.NEEDLE], hip_stream=stream.cuda_stream)
-    ptr = dev.data_ptr()
-
-    step_pending = []
-
-    def step():
-        # per-pattern counts ride along (one literal: no extra kernel work, SPEC.md S6)
-        r = eng.run_device(ptr, seg_base, [n], since=since, tail=TAIL, pattern_counts=True)
-        if world > 1:  # per-stream count records -> every rank (one all-gather, RCCL over xGMI),
-            # left in flight while the next step filters; every gather is waited for before
-            # the timed region closes (finish_gathers)
-            rec = dict(r.totals(), patterns=r.pattern_counts(0))
-            step_pending.append(shard.gather_counts_async({rank: rec}, [n] * world, world, device=coll_dev,
-                                                          n_patterns=1))
-            if len(step_pending) > 1:
-                step_pending.pop(0).wait()
-        return r
-
-    def finish_gathers():
-        while step_pending:
-            step.table = step_pending.pop(0).wait()
-
-    for _ in range(args.warmup):
-        step().free()
-    finish_gathers()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    scan_ms, total_ms = [], []
-    t0 = time.perf_counter()
-    last = None
-    for i in range(args.steps):
-        r = step()
-        tm = r.timing()
-        scan_ms.append(tm[6])  # the k_scan kernel alone
-        total_ms.append(tm[4])
-        if i + 1 < args.steps:
-            r.free()
-        else:
-            last = r
-    finish_gathers()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    dt = time.perf_counter() - t0
-    if world > 1:
-        tt = torch.tensor([dt], dtype=torch.float64, device=coll_dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        dt = float(tt.item())
-
-    tot = last.totals()
-    lines = tot["lines"]
-    out_bytes = tot["out_bytes"]
-    # algorithmic bytes.  k_scan, the dominant kernel, reads every input
-    # byte once; its staged per-line slots are intermediate (not counted).  The K1 stage
-    # adds the u64 line-offset index (L + 1 per stream) and the match bitmap, written once.
-    scan_alg = n
-    k1_alg = n + 8 * (lines + 1) + 4 * (lines // 32 + 1)
-    step_alg = k1_alg + out_bytes
-    scan_avg_s = float(np.mean(scan_ms)) / 1e3
-
-    dev_avg_s = float(np.mean(total_ms)) / 1e3
-    achieved = scan_alg / scan_avg_s / 1e9
-
-    log(f"[rank {rank}] timed {args.steps} steps: {dt / args.steps * 1e3:.3f} ms/step")
-    cold = cold_run(local, dict(grep=[synth.NEEDLE]), ptr, seg_base, [n], since, TAIL) if world == 1 else None
-    verified = None
-    if not args.no_verify:  # every rank: its own stream in full against the C oracle
-        sys.path.insert(0, str(ROOT / "oracle"))
-        import c_oracle as co
-        so = last.stream(0)
-        t = time.perf_counter()
-        ref_out, _, _, ref_c = co.filter_stream(host, since, TAIL, [synth.NEEDLE], want_lines=False,
-                                                want_bits=False)
-        cpu_s = time.perf_counter() - t
-        verified = ref_out == so.out and ref_c["selected"] == tot["selected"] and ref_c["lines"] == lines
-        lo = last.lines(0)
-        verified = bool(verified and lo.shape[0] == lines + 1 and int(lo[-1]) == n)
-        if world > 1:  # every rank's verdict (MIN)
-            vt = torch.tensor([int(verified)], dtype=torch.int64, device=coll_dev)
-            dist.all_reduce(vt, op=dist.ReduceOp.MIN)
-            verified = bool(vt.item())
-    records_ok = None
-    if world > 1:  # the gathered table: every rank's row equals what that rank computed
-        mine = step.table[rank].tolist()
-        records_ok = mine == [tot[k] for k in shard.RECORD_FIELDS[1:]] + last.pattern_counts(0)
-    cpu = None
-    cpu_more = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        sys.path.insert(0, str(ROOT / "oracle"))
-        import c_oracle as co
-        # repeat whole passes over this run's stream until >= 10 s of CPU work
-        passes, cpu_t = 0, 0.0
-        while cpu_t < 10.0 and passes < 64:
-            t = time.perf_counter()
-            co.filter_stream(host, since, TAIL, [synth.NEEDLE], want_lines=False, want_bits=False)
-            cpu_t += time.perf_counter() - t
-            passes += 1
-        cpu = {"value": round(n * passes / cpu_t / 1e9, 4), "unit": "GB/s", "cores": 1, "kind": "port",
-               "sample": f"{passes} full passes over this run's {n} B stream with oracle/klf_oracle_c.c "
-                         f"(memchr line split, Go time.Parse restated, memmem grep, kubelet tail+since) "
-                         f"on 1 host core, {cpu_t:.1f} s"}
-        cpu_more = cpu_variants(host, since)
-
-    # Capture path, N = 1 only: the product's host entry points on this
-    # run's bytes -- klf_stage in 1 MiB pieces (io.Copy's role) into pinned chunks, then
-    # klf_run (DMA H2D from the pinned chunks + the whole filter) and the output D2H.
-    # Reported beside `value`, never as it (device-resident is the metric).
-    capture = None
-    log(f"[rank {rank}] verified={verified} cpu_baseline={cpu and cpu['value']}")
-    if rank == 0 and world == 1 and not args.no_capture:
-        ceng = E.Engine(local, grep=[synth.NEEDLE])
-        want = last.stream(0).out
-        piece = args.capture_piece
-        runs = []
-        for _ in range(2):  # the first pays the pinned-chunk allocation
-            ceng.reset()
-            ceng.set_streams(1)
-            t0 = time.perf_counter()
-            for off in range(0, n, piece):
-                ceng.stage_array(0, host[off:off + piece])
-            t1 = time.perf_counter()
-            r = ceng.run(since=since, tail=TAIL, n_streams=1)
-            got = r.stream(0).out
-            t2 = time.perf_counter()
-            r.free()
-            runs.append((t1 - t0, t2 - t1, got == want))
-        ceng.close()
-        st_s, run_s, same = runs[-1]
-        capture = {"stage_GBps": round(n / st_s / 1e9, 2), "h2d_filter_d2h_GBps": round(n / run_s / 1e9, 2),
-                   "end_to_end_GBps": round(n / (st_s + run_s) / 1e9, 2), "piece_bytes": piece,
-                   "staging": "pinned 64 MiB chunks (hipHostMalloc, reused across runs)",
-                   "output_matches_device_run": bool(same and runs[0][2])}
-        log(f"[rank 0] capture path: {capture}")
-
-    # stage breakdown (after the checks: a later run invalidates `last`); outside the timed region (the stage events idle the GPU ~5 us each)
-    k1_ms, staged = [], None
-    for _ in range(3):
-        if staged is not None:
-            staged.free()
-        staged = eng.run_device(ptr, seg_base, [n], since=since, tail=TAIL, stage_times=True)
-        k1_ms.append(staged.timing()[0])  # K1 stage: k_scan + k_fixup + tile-base scan + scatter
-    stage_last = staged.timing()
-    staged.free()
-    k1_avg_s = float(np.mean(k1_ms)) / 1e3
-    traffic, traffic_src = pmc_traffic()
-    trace_frac, trace_src = committed_trace_frac("c2")
-    value = world * n * args.steps / dt / 1e9
+    if world == 1:
+        head = run_config(HEADLINE, args, local, now, headline=True)
+        value, ms = head["value_GBps"], head["ms_per_step"]
+        roof = dict(head.pop("roofline"))
+        cpu = head.pop("cpu_baseline", None)
+    else:
+        head = run_sharded(HEADLINE, args, world, rank, local, coll_dev, now)
+        value, ms = head["value_GBps"], head["ms_per_step"]
+        sc = head["rank0"]["scan"]
+        roof = {"bound": "hbm", "kernel": sc["kernel"], "achieved": round(sc["alg_bytes_per_launch"]
+                                                                           / sc["avg_launch_ms"] / 1e6, 1),
+                "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": sc["frac"],
+                "alg_bytes_per_launch": sc["alg_bytes_per_launch"], "avg_launch_ms": sc["avg_launch_ms"],
+                "frac_min_over_ranks": head["scan_frac_min_over_ranks"],
+                "frac_source": "rank 0's k_scan dispatch events (hipExtLaunchKernel), this run"}
+        cpu = None  # (rank 0 at N = 1 only)
+    traffic, src_t, frac_rp, src_f = committed(HEADLINE)
+    roof["traffic"] = traffic
+    roof["traffic_source"] = src_t
+    roof["frac_rocprof_committed"] = frac_rp
+    roof["rocprof_source"] = src_f
     res = {
         "metric": METRIC,
-        "value": round(value, 3),
+        "value": value,
         "unit": "GB/s",
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": round(dt / args.steps * 1e3, 4),
+        "ms_per_step": ms,
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "u8",
-        "data": "synthetic: seeded JSON kubelet log lines (200-599 B content, 31-B RFC3339Nano prefix, "
-                "1% carry the grep literal), monotonic timestamps over 60 min",
-        "config": {"workload": "C2: one 4 GiB JSON log stream per GPU, --since 5m --tail 100 --grep "
-                               + synth.NEEDLE.decode(),
-                   "stream_bytes": n, "lines_per_stream": lines, "global_bytes": world * n,
-                   "parallelism": f"streams sharded, 1 stream per GPU x {world}"},
-        "roofline": {"bound": "hbm", "kernel": "k_scan<literal>", "achieved": round(achieved, 1),
-                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                     "traffic": traffic, "traffic_source": traffic_src, "alg_bytes_per_launch": scan_alg,
-                     "avg_launch_ms": round(scan_avg_s * 1e3, 4),
-                     "frac_source": "HIP events carrying the k_scan dispatch's own start / end timestamps (hipExtLaunchKernel), this run",
-                     "frac_rocprof_committed": trace_frac, "rocprof_source": trace_src},
+        "data": "synthetic: seeded kubelet log streams (31-B RFC3339Nano prefix, monotonic timestamps over "
+                "60 min); C5: 1-32 KiB JSON lines",
+        "config": {"workload": head["workload"], "streams": head["streams"], "global_bytes": head["bytes"],
+                   "parallelism": f"stream table LPT-sharded over {world} GPU(s), one process per GPU"},
+        "roofline": roof,
         "cpu_baseline": cpu,
-        "extra": {"device_ms_per_step": round(dev_avg_s * 1e3, 4),
-                  "k1_stage": {"kernels": "k_scan+k_fixup+k_tsum+k_tbase+k_scatter", "alg_bytes": k1_alg,
-                               "avg_ms": round(k1_avg_s * 1e3, 4),
-                               "achieved_GBps": round(k1_alg / k1_avg_s / 1e9, 1)},
-                  "step_alg_frac_of_peak": round(step_alg / dev_avg_s / 1e9 / HBM_PEAK_GBS, 4),
-                  "stage_ms": [round(x, 4) for x in stage_last],
-                  "selected_lines": tot["selected"], "matched_lines": tot["matched"], "out_bytes": out_bytes,
-                  "h2d_inclusive_GBps": round(n / (h2d_s + dev_avg_s) / 1e9, 3),
-                  "capture_path": capture,
-                  "cold": cold,
-                  "cpu_baseline_variants": cpu_more,
-                  "gathered_records_consistent": records_ok,
-                  "verified_vs_c_oracle": verified},
+        "extra": {"headline": head, "configs": {}},
     }
-    last.free()
-    eng.close()
-    del dev, host
-    torch.cuda.empty_cache()
-    if world == 1 and args.extra_configs:
-        res["extra"]["configs"] = {}
-        for name in [x for x in args.extra_configs.split(",") if x]:
-            res["extra"]["configs"][name] = run_extra(name, args, local, now)
-            torch.cuda.empty_cache()
-    if world > 1:
-        res["extra"]["configs"] = {}
-        for name in [x for x in args.extra_configs.split(",") if x in ("c3", "c5")]:
-            res["extra"]["configs"][name + "_sharded"] = run_sharded(name, args, world, rank, local, coll_dev, now)
-            torch.cuda.empty_cache()
+    for name in extras:
+        try:
+            if world == 1:
+                res["extra"]["configs"][name] = run_config(name, args, local, now)
+            else:
+                res["extra"]["configs"][name + "_sharded"] = run_sharded(name, args, world, rank, local, coll_dev, now)
+        except Exception as ex:  # noqa: BLE001 -- an extra config's failure is reported, not fatal
+            if world > 1:
+                raise
+            res["extra"]["configs"][name] = {"error": f"{type(ex).__name__}: {ex}"[:400]}
+            log(f"[{name}] failed: {ex}")
+        torch.cuda.empty_cache()
     if rank == 0:
         print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()
-
-
-def cpu_variants(host: np.ndarray, since) -> dict:
-    """More CPU reference points on the same stream, rank 0 at N = 1 (bounded, ~10 s):
-    the C restatement on T host threads over line-aligned pieces (each piece with the run's
-    --tail: the same per-line work; the split-tail exchange is O(1)), and the reference
-    client's own ceiling -- klogs only io.Copy's each body into its file (cmd/root.go:359-374)
-    -- as a host memcpy bound (1 and T threads) and a page-cache file write of the stream."""
-    from concurrent.futures import ThreadPoolExecutor
-    sys.path.insert(0, str(ROOT / "oracle"))
-    import c_oracle as co
-    threads = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", "16") or 16)))
-    n = len(host)
-    cuts = [0]
-    for k in range(1, threads):
-        j = int(np.flatnonzero(host[k * n // threads:k * n // threads + (1 << 20)] == 10)[0]) + 1
-        cuts.append(k * n // threads + j)
-    cuts.append(n)
-    pieces = [host[a:b] for a, b in zip(cuts, cuts[1:])]
-    with ThreadPoolExecutor(threads) as ex:
-        passes, t_mt = 0, 0.0
-        while t_mt < 4.0 and passes < 64:
-            t = time.perf_counter()
-            list(ex.map(lambda p: co.filter_stream(p, since, TAIL, [synth.NEEDLE], want_lines=False,
-                                                   want_bits=False), pieces))
-            t_mt += time.perf_counter() - t
-            passes += 1
-        dst = np.empty_like(host)
-        t = time.perf_counter()
-        np.copyto(dst, host)
-        t_cp1 = time.perf_counter() - t
-        t = time.perf_counter()
-        list(ex.map(lambda ab: np.copyto(dst[ab[0]:ab[1]], host[ab[0]:ab[1]]), zip(cuts, cuts[1:])))
-        t_cpn = time.perf_counter() - t
-    del dst
-    wn = min(n, 1 << 30)
-    with tempfile.NamedTemporaryFile(prefix="klf_cpy_") as f:
-        t = time.perf_counter()
-        mv = memoryview(host[:wn])
-        off = 0
-        while off < wn:
-            off += os.write(f.fileno(), mv[off:off + (64 << 20)])
-        t_w = time.perf_counter() - t
-    return {
-        "port_threads": {"value": round(n * passes / t_mt / 1e9, 3), "unit": "GB/s", "cores": threads,
-                         "kind": "port", "sample": f"{passes} passes, {threads} line-aligned pieces of this run's "
-                                                   f"stream, one host thread each, {t_mt:.1f} s"},
-        "copy_bound_1t_GBps": round(n / t_cp1 / 1e9, 2),
-        "copy_bound_threads_GBps": round(n / t_cpn / 1e9, 2),
-        "file_write_GBps": round(wn / t_w / 1e9, 2),
-        "copy_note": "the reference client's own work is io.Copy of each body into a file; host memcpy and "
-                     "a page-cache write of the stream bound it from above",
-    }
-
-
-def sharded_table(name: str, world: int):
-    """(stream sizes, kind, patterns, permille, since_tail, description) of config `name`
-    at N ranks, weak scaling: each rank's share is the config's per-GPU workload.
-      c3: 128 x 64 MiB TEXT streams per rank (256 pods x 4 containers over 8 GPUs), -l only;
-      c5: 8 x N pods with 1-2 init containers + 2 containers (-i stream table, getPodLogs
-          order), 32 GiB per rank of 1-32 KiB JSON lines, 64 --match regexes, since + tail."""
-    if name == "c3":
-        return [64 << 20] * (128 * world), synth.TEXT, {}, 10, "-l", \
-            "C3 at N GPUs: 128 x 64 MiB TEXT streams per GPU, LPT-sharded, -l only (every line out)"
-    from klogs_amd import host as H
-    pods = [(f"synthetic-{p}", [f"init-{k}" for k in range(1 + p % 2)], ["app", "sidecar"]) for p in range(8 * world)]
-    table = H.stream_table(pods, init=True)  # getPodLogs order with -i (cmd/root.go:240-262)
-    w = [1 if is_init else 4 for _, _, is_init in table]
-    per_rank = 32 << 30
-    sizes = [per_rank * world * x // sum(w) for x in w]
-    return sizes, synth.LONGJSON, dict(match=synth.c5_regexes()), 5, "since+tail", \
-        (f"C5 at N GPUs: {len(table)} streams (8 pods per GPU, 1-2 init containers + 2 containers each, -i), "
-         "32 GiB per GPU of 1-32 KiB JSON lines, 64 --match regexes, --since 5m --tail 100, LPT-sharded")
-
-
-def run_sharded(name: str, args, world: int, rank: int, local: int, coll_dev, now: int) -> dict:
-    """BASELINE config 3 or 5 across ranks: the stream table LPT-assigned
-    (shard.assign), each rank one device batch of its own streams, then the one all-gather
-    of per-stream count records (+ per-pattern counts for C5) per step over RCCL.  value =
-    all ranks' bytes / max-over-ranks time.  After the timed region every rank checks its
-    own rows of the gathered table and verifies its first and last stream in full against
-    the C oracle (C5: the glibc-regex leg, ko_filter_rx); the flags are all-reduced (MIN)."""
-    sizes, kind, pats, permille, mode, desc = sharded_table(name, world)
-    since, tail = ((None, -1) if mode == "-l" else ((now - SINCE_S, 0), TAIL))
-    lens_all = [synth.size(kind, 42, i, sz, permille=permille) for i, sz in enumerate(sizes)]
-    mine = shard.local_streams(lens_all, world, rank)
-    lens = [lens_all[i] for i in mine]
-    seg_base, total = E.layout(lens)
-    dev = torch.empty(total, dtype=torch.uint8, device=f"cuda:{local}")
-    h = np.empty(max(lens) + 1, dtype=np.uint8)
-    t = time.time()
-    for j, i in enumerate(mine):
-        synth.generate_into(h, kind, 42, i, sizes[i], permille=permille)
-        dev[int(seg_base[j]):int(seg_base[j]) + lens[j]].copy_(torch.from_numpy(h[:lens[j]]))
-    torch.cuda.synchronize()
-    del h
-    log(f"[rank {rank}] {name} share: {len(mine)} streams, {sum(lens)} B in {time.time() - t:.1f}s")
-    eng = E.Engine(local, hip_stream=torch.cuda.current_stream().cuda_stream, **pats)
-    ptr = dev.data_ptr()
-    npat = len(pats.get("match", [])) + len(pats.get("grep", []))
-
-    pending = []
-
-    def records(r):
-        recs = {}
-        for j, sid in enumerate(mine):
-            c = r.stream_counts(j)
-            if npat:
-                c = dict(c, patterns=r.pattern_counts(j))
-            recs[sid] = c
-        return recs
-
-    def step():
-        r = eng.run_device(ptr, seg_base, lens, since=since, tail=tail, pattern_counts=bool(npat))
-        pending.append(shard.gather_counts_async(records(r), lens_all, world, device=coll_dev, n_patterns=npat))
-        if len(pending) > 1:
-            pending.pop(0).wait()
-        return r
-
-    def finish():
-        while pending:
-            step.table = pending.pop(0).wait()
-    for _ in range(args.warmup):
-        step().free()
-    finish()
-    torch.cuda.synchronize()
-    dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    last = None
-    for i in range(args.steps):
-        r = step()
-        if i + 1 < args.steps:
-            r.free()
-        else:
-            last = r
-    finish()
-    torch.cuda.synchronize()
-    dist.barrier()
-    dt = time.perf_counter() - t0
-    tt = torch.tensor([dt], dtype=torch.float64, device=coll_dev)
-    dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-    dt = float(tt.item())
-    # every rank's own rows of the gathered table equal its own counts; totals add up
-    mine_rec = records(last)
-    fields = shard.RECORD_FIELDS[1:]
-    rec_ok = all(step.table[sid].tolist() == [mine_rec[sid][k] for k in fields] + list(mine_rec[sid].get("patterns", []))
-                 for sid in mine)
-    rec_ok = rec_ok and int(step.table[:, 0].sum()) > 0 and int(step.table[:, 5].sum()) > 0
-    ver = None
-    if not args.no_verify:  # the rank's first and last stream in full vs the C oracle
-        sys.path.insert(0, str(ROOT / "oracle"))
-        import c_oracle as co
-        rs = co.RegexSet(pats["match"]) if "match" in pats else None
-        sn = since if since is not None else co.GO_ZERO_TIME
-        got = {j: (last.stream(j), last.match_bits(j) if npat else None) for j in sorted({0, len(mine) - 1})}
-        del dev
-        torch.cuda.empty_cache()
-        dev = None
-
-        def check(j):
-            i = mine[j]
-            hh = np.empty(lens[j] + 1, dtype=np.uint8)
-            synth.generate_into(hh, kind, 42, i, sizes[i], permille=permille)
-            if rs is not None:
-                out, _, bits, c = co.filter_stream_rx(hh[:lens[j]], sn, tail, rs, want_lines=False)
-            else:
-                out, _, bits, c = co.filter_stream(hh[:lens[j]], sn, tail, [], want_lines=False, want_bits=False)
-            so, gb = got[j]
-            return so.out == out and all(so.counts[k] == c[k] for k in c) and (gb is None or gb == bits)
-        from concurrent.futures import ThreadPoolExecutor
-        tv = time.perf_counter()
-        with ThreadPoolExecutor(len(got)) as ex:
-            ver = all(ex.map(check, list(got)))
-        log(f"[rank {rank}] {name} verified={ver} ({time.perf_counter() - tv:.1f}s)")
-    flags = torch.tensor([int(rec_ok), -1 if ver is None else int(ver)], dtype=torch.int64, device=coll_dev)
-    dist.all_reduce(flags, op=dist.ReduceOp.MIN)
-    last.free()
-    eng.close()
-    del dev
-    out = {"workload": desc, "streams": len(lens_all), "bytes": int(sum(lens_all)),
-           "value_GBps": round(sum(lens_all) * args.steps / dt / 1e9, 1),
-           "ms_per_step": round(dt / args.steps * 1e3, 3),
-           "records_consistent": bool(flags[0].item()),
-           "collective": f"one all-gather per step of {len(lens_all)} x {shard.NREC + npat} int64 records "
-                         f"({'RCCL' if coll_dev != 'cpu' else 'gloo'})"}
-    if ver is not None:
-        out["verified_vs_oracle"] = bool(flags[1].item() == 1)
-        out["verify_scope"] = ("on every rank: its first and last stream in full (output bytes, all counts"
-                               + (", match bitmap" if npat else "") + ") against "
-                               + ("the C oracle's glibc-regex leg (ko_filter_rx)" if npat else "the C oracle"))
-    return out
-
-
-def extra_streams(name: str, total: int):
-    """(stream sizes, generator kind, patterns, permille, description) of BASELINE configs
-    3 / 4 / 5."""
-    if name == "c2":  # the headline workload, for scripts/run_config.py
-        return [STREAM_BYTES], synth.JSON, dict(grep=[synth.NEEDLE]), 10, \
-            "C2: one 4 GiB JSON log stream, --since 5m --tail 100 --grep " + synth.NEEDLE.decode()
-    if name == "c1":  # the reference's own CPU-runnable case (BASELINE configs[0])
-        return [64 << 20], synth.TEXT, {}, 10, \
-            "C1: one 64 MiB stream (lognormal line lengths, median 96 B), --since 5m --tail 100"
-    if name == "c3":  # one GPU's share of C3 at 8 GPUs (fixed size: --extra-bytes is for C4/C5)
-        n = 128
-        return [64 << 20] * n, synth.TEXT, {}, 10, \
-            "C3 per-GPU share at 8 GPUs: 128 streams x 64 MiB (256 pods x 4 containers / 8), -l selection " \
-            "only: no --since, no --tail, no grep (every line out, prefix stripped)"
-    if name == "c4":
-        n = 8
-        return [total // n] * n, synth.MIXED, dict(grep=synth.c4_literals(1024)), 5, \
-            "C4: 8 streams of mixed-length lines (16 B-8 KiB, lognormal), 1,024 --grep literals (6-24 B, " \
-            "0.5% of lines hold one), --since 5m --tail 100"
-    if name == "c5":
-        from klogs_amd import host as H
-        pods = [(f"synthetic-{p}", [f"init-{k}" for k in range(1 + p % 2)], ["app", "sidecar"]) for p in range(8)]
-        table = H.stream_table(pods, init=True)  # getPodLogs order with -i (cmd/root.go:240-262)
-        w = [1 if is_init else 4 for _, _, is_init in table]
-        sizes = [total * x // sum(w) for x in w]
-        return sizes, synth.LONGJSON, dict(match=synth.c5_regexes()), 5, \
-            f"C5: {len(table)} streams (8 pods x 1-2 init containers + 2 containers, -i), 1-32 KiB JSON " \
-            "lines, 64 --match regexes (0.5% of lines match one, 1% hold a factor but no match), " \
-            "--since 5m --tail 100"
-    raise ValueError(name)
-
-
-def cpu_extra(name: str, kind: int, pats: dict, permille: int, since, tail: int) -> dict:
-    """CPU reference points for configs 1 and 3-5 (rank 0, N = 1; bounded, a few seconds
-    each) on samples of the same generator and shape: the C restatement on 1 and on T host
-    threads (one stream per thread, as the reference runs one goroutine per stream).  Literal
-    paths: oracle/klf_oracle_c.c ko_filter (memmem / Aho-Corasick).  The regex set (C5):
-    ko_filter_rx, glibc POSIX ERE translated from the Go subset (oracle/posix_re.py) behind an
-    Aho-Corasick pass over each pattern's required literal, first checked against the Python
-    oracle on one sample stream; the Python oracle's own rate (one core, Python `re`) beside it.
-    C1 is one 64 MiB stream: one core only."""
-    from concurrent.futures import ThreadPoolExecutor
-    sys.path.insert(0, str(ROOT / "oracle"))
-    import c_oracle as co
-    threads = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", "16") or 16)))
-    sample = {"c1": 64 << 20, "c3": 64 << 20, "c4": 2 << 20, "c5": 8 << 20}[name]
-    nstreams = 1 if name == "c1" else threads
-    streams = [synth.generate(kind, 7, i, sample, permille=permille) for i in range(nstreams)]
-    grep = pats.get("grep", [])
-    sn = since if since is not None else co.GO_ZERO_TIME
-
-    if name == "c5":
-        rs = co.RegexSet(pats["match"])
-
-        def one(b):
-            return co.filter_stream_rx(b, sn, tail, rs, want_lines=False, want_bits=False)
-    else:
-        def one(b):
-            return co.filter_stream(b, sn, tail, grep, want_lines=False, want_bits=False)
-
-    def timed(f, budget):
-        n, t = 0, 0.0
-        while t < budget and n < 64:
-            t0 = time.perf_counter()
-            f()
-            t += time.perf_counter() - t0
-            n += 1
-        return n, t
-    what = {"c5": "oracle/klf_oracle_c.c ko_filter_rx (glibc regexec behind the required-literal Aho-Corasick pass)"}
-    impl = what.get(name, "oracle/klf_oracle_c.c")
-    res = {}
-    if name == "c5":  # the C leg decides every line as the Python oracle does (one sample stream)
-        from oracle import klf_oracle as ko
-        cp = ko.compile_patterns(match=pats["match"])
-        probe = streams[0][:2 << 20]
-        probe = probe[:probe.rfind(b"\n") + 1]
-        ref = ko.filter_stream(probe, sn, tail, cp)
-        got = co.filter_stream_rx(probe, sn, tail, rs, want_lines=False)
-        res["c_leg_equals_python_oracle"] = bool(got[0] == ref.out and got[2] == ref.match_bits)
-        n, t = timed(lambda: ko.filter_stream(probe, sn, tail, cp), 3.0)
-        res["python_1_core"] = {"value": round(len(probe) * n / t / 1e9, 4), "unit": "GB/s", "cores": 1,
-                                "kind": "port", "sample": f"{n} passes over {len(probe)} B of the C5 generator, "
-                                                          f"oracle/klf_oracle.py (Python re), {t:.1f} s"}
-    n, t = timed(lambda: one(streams[0]), 3.0)
-    res["port_1_core"] = {"value": round(sample * n / t / 1e9, 4), "unit": "GB/s", "cores": 1, "kind": "port",
-                          "sample": f"{n} passes over one {sample >> 20} MiB stream of the {name.upper()} generator, "
-                                    f"{impl}, {t:.1f} s"}
-    if nstreams > 1:
-        with ThreadPoolExecutor(threads) as ex:
-            n, t = timed(lambda: list(ex.map(one, streams)), 3.0)
-        res["port_threads"] = {"value": round(sample * threads * n / t / 1e9, 4), "unit": "GB/s",
-                               "cores": threads, "kind": "port",
-                               "sample": f"{n} passes over {threads} streams of {sample >> 20} MiB, one host thread "
-                                         f"per stream, {impl}, {t:.1f} s"}
-    return res
-
-
-def cold_run(local: int, pats: dict, ptr: int, seg_base, lens, since, tail: int) -> dict:
-    """One-shot cost, as one klogs invocation pays it (INTEGRATION.md: klf_run once per
-    run): a fresh engine (klf_open: pattern compile + table uploads) and its first run on
-    the device-resident batch (first-batch statistics + layout choice + uploads, the
-    pipeline, the readback), host wall clock; beside it the steady step of the same
-    engine's second run."""
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    eng = E.Engine(local, hip_stream=torch.cuda.current_stream().cuda_stream, **pats)
-    t1 = time.perf_counter()
-    r = eng.run_device(ptr, seg_base, lens, since=since, tail=tail)
-    t2 = time.perf_counter()
-    r.free()
-    t3 = time.perf_counter()
-    r = eng.run_device(ptr, seg_base, lens, since=since, tail=tail)
-    t4 = time.perf_counter()
-    r.free()
-    eng.close()
-    return {"open_ms": round((t1 - t0) * 1e3, 3), "first_run_ms": round((t2 - t1) * 1e3, 3),
-            "cold_ms": round((t2 - t0) * 1e3, 3), "second_run_ms": round((t4 - t3) * 1e3, 3)}
-
-
-def verify_large(name, sizes, lens, kind, permille, pats, since, tail, r) -> dict:
-    """Checks the last timed run of C4 / C5 against the oracles (after the timed region),
-    every stream in full, one host thread per stream: output bytes, all counts and the match
-    bitmap.  C4: the C oracle (Aho-Corasick over the 1,024 literals).  C5: the C oracle's
-    regex leg (ko_filter_rx: the 64 regexes as glibc POSIX ERE behind a required-literal
-    pass, itself checked against the Python oracle in tests/test_oracle.py and, on a sample
-    of this run's generator, in cpu_baseline.c_leg_equals_python_oracle)."""
-    from concurrent.futures import ThreadPoolExecutor
-    sys.path.insert(0, str(ROOT / "oracle"))
-    import c_oracle as co
-    t = time.perf_counter()
-    got = [(r.stream(i), r.match_bits(i)) for i in range(len(lens))]
-    sn = since if since is not None else co.GO_ZERO_TIME
-    threads = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", "16") or 16)))
-    rs = co.RegexSet(pats["match"]) if name == "c5" else None
-
-    def check(i):
-        h = np.empty(lens[i] + 1, dtype=np.uint8)
-        synth.generate_into(h, kind, 42, i, sizes[i], permille=permille, threads=1)
-        if rs is not None:
-            out, _, bits, c = co.filter_stream_rx(h[:lens[i]], sn, tail, rs, want_lines=False)
-        else:
-            out, _, bits, c = co.filter_stream(h[:lens[i]], sn, tail, pats["grep"], want_lines=False)
-        so, gbits = got[i]
-        return so.out == out and gbits == bits and all(so.counts[k] == c[k] for k in c)
-    with ThreadPoolExecutor(min(threads, len(lens))) as ex:
-        ok = list(ex.map(check, range(len(lens))))
-    bad = [i for i, x in enumerate(ok) if not x]
-    scope = ("every stream in full: output bytes, all counts, match bitmap ("
-             + ("C oracle regex leg: glibc POSIX ERE behind the required-literal pass" if rs is not None
-                else "C oracle, Aho-Corasick") + ")")
-    return {"ok": not bad, "streams": len(lens), "failed_streams": bad, "scope": scope,
-            "s": round(time.perf_counter() - t, 1)}
-
-
-def run_extra(name: str, args, local: int, now: int) -> dict:
-    sizes, kind, pats, permille, desc = extra_streams(name, args.extra_bytes)
-    t = time.time()
-    lens = [synth.size(kind, 42, i, sz, permille=permille) for i, sz in enumerate(sizes)]
-    seg_base, total = E.layout(lens)
-    dev = torch.empty(total, dtype=torch.uint8, device=f"cuda:{local}")
-    for i, (sz, n) in enumerate(zip(sizes, lens)):  # one stream at a time through host memory
-        h = np.empty(n + 1, dtype=np.uint8)
-        synth.generate_into(h, kind, 42, i, sz, permille=permille)
-        dev[int(seg_base[i]):int(seg_base[i]) + n].copy_(torch.from_numpy(h[:n]))
-        del h
-    torch.cuda.synchronize()
-    log(f"[{name}] generated + uploaded {sum(lens)} B in {time.time() - t:.1f}s")
-    since, tail = ((None, -1) if name == "c3" else ((now - SINCE_S, 0), TAIL))
-    stream = torch.cuda.current_stream()
-    eng = E.Engine(local, hip_stream=stream.cuda_stream, **pats)
-    ptr = dev.data_ptr()
-    for _ in range(args.warmup):
-        eng.run_device(ptr, seg_base, lens, since=since, tail=tail).free()
-    torch.cuda.synchronize()
-    scan_ms, total_ms = [], []
-    t0 = time.perf_counter()
-    last = None
-    for i in range(args.steps):
-        r = eng.run_device(ptr, seg_base, lens, since=since, tail=tail)
-        tm = r.timing()
-        scan_ms.append(tm[6])
-        total_ms.append(tm[4])
-        if i + 1 < args.steps:
-            r.free()
-        else:
-            last = r
-    torch.cuda.synchronize()
-    dt = time.perf_counter() - t0
-    cold = cold_run(local, pats, ptr, seg_base, lens, since, tail)
-    verified = None
-    write = None
-    wdir = None
-    if name == "c3" and not args.no_write:  # §8f-3 output write path: every stream into its own file (klf_result_write)
-        wdir = tempfile.TemporaryDirectory(prefix="klf_c3_")
-        paths = [os.path.join(wdir.name, f"pod{i // 4}__c{i % 4}.log") for i in range(len(lens))]
-        tw = time.perf_counter()
-        try:
-            wbytes = last.write_files(paths)
-        except E.KlfError as ex:  # e.g. no room for 6.9 GB in the temp dir: reported, not fatal
-            wbytes, write = None, {"error": str(ex), "dir": wdir.name}
-        wdt = time.perf_counter() - tw
-    if write is None and wdir is not None:
-        write = {"GBps": round(wbytes / wdt / 1e9, 2), "bytes": wbytes, "files": len(paths), "s": round(wdt, 3),
-                 "how": "klf_result_write: 64 MiB pinned D2H chunks, double-buffered, 8 writer threads each owning whole files (own HIP stream + 2x32 MiB pinned halves), "
-                        "into page-cache files under " + os.path.dirname(wdir.name)}
-    if name == "c3" and not args.no_verify and write is not None and wbytes is not None:  # first and last stream vs the C oracle
-        sys.path.insert(0, str(ROOT / "oracle"))
-        import c_oracle as co
-        verified = True
-        for i in (0, len(lens) - 1):
-            h = np.empty(lens[i] + 1, dtype=np.uint8)
-            synth.generate_into(h, kind, 42, i, sizes[i], permille=permille)
-            want = co.filter_stream(h[:lens[i]], co.GO_ZERO_TIME, -1, [], want_lines=False, want_bits=False)[0]
-            with open(paths[i], "rb") as f:  # the written file, i.e. the D2H + write path too
-                verified = verified and f.read() == want
-        write["verified_vs_c_oracle"] = bool(verified)
-    if wdir is not None:
-        wdir.cleanup()
-    if name == "c1" and not args.no_verify:  # the whole stream vs the C oracle
-        sys.path.insert(0, str(ROOT / "oracle"))
-        import c_oracle as co
-        h = np.empty(lens[0] + 1, dtype=np.uint8)
-        synth.generate_into(h, kind, 42, 0, sizes[0], permille=permille)
-        ref_out, ref_lo, _, ref_c = co.filter_stream(h[:lens[0]], since, tail, [], want_bits=False)
-        so = last.stream(0)
-        verified = bool(so.out == ref_out and all(so.counts[k] == ref_c[k] for k in ref_c)
-                        and np.array_equal(last.lines(0), ref_lo))
-    vlarge = None
-    if name in ("c4", "c5") and not args.no_verify:
-        del dev  # the checks regenerate the streams on the host
-        torch.cuda.empty_cache()
-        dev = None
-        vlarge = verify_large(name, sizes, lens, kind, permille, pats, since, tail, last)
-    tot = last.totals()
-    if dev is not None:
-        staged = eng.run_device(ptr, seg_base, lens, since=since, tail=tail, stage_times=True)
-        stage = staged.timing()
-        staged.free()
-    else:  # the batch was dropped for the checks: the stage split of the timed runs' last
-        stage = last.timing()
-    n = sum(lens)
-    scan_s = max(float(np.mean(scan_ms)) / 1e3, 1e-12)  # (0: a build without the scan's events)
-    dev_s = float(np.mean(total_ms)) / 1e3
-    step_alg = n + 8 * (tot["lines"] + len(lens)) + 4 * (tot["lines"] // 32 + 1) + tot["out_bytes"]
-    out = {
-        "workload": desc, "streams": len(lens), "bytes": n, "lines": tot["lines"],
-        "value_GBps": round(n * args.steps / dt / 1e9, 1), "ms_per_step": round(dt / args.steps * 1e3, 3),
-        "device_ms_per_step": round(dev_s * 1e3, 3),
-        "roofline": {"bound": "hbm", "kernel": "k_scan<plain>" if not pats else "k_scan<general, q-gram prefilter>",
-                     "achieved": round(n / scan_s / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(n / scan_s / 1e9 / HBM_PEAK_GBS, 4), "avg_launch_ms": round(scan_s * 1e3, 4)},
-        "cold": cold,
-        "matcher_ms": round(stage[1], 4),
-        "step_alg_frac_of_peak": round(step_alg / dev_s / 1e9 / HBM_PEAK_GBS, 4),
-        "matched_lines": tot["matched"], "selected_lines": tot["selected"], "out_bytes": tot["out_bytes"],
-        "stage_ms": [round(x, 4) for x in stage],
-    }
-    if not getattr(args, "no_cpu_baseline", True):
-        out["cpu_baseline"] = cpu_extra(name, kind, pats, permille, since, tail)
-    if verified is not None:
-        out["verified_vs_c_oracle"] = bool(verified)
-    if vlarge is not None:
-        out["verified_vs_oracle"] = vlarge.pop("ok")
-        out["verify"] = vlarge
-    if write is not None:
-        out["write_path"] = write
-    last.free()
-    eng.close()
-    del dev
-    return out
 
 
 if __name__ == "__main__":

@@ -205,7 +205,8 @@ int klf_result_write(klf_result* r, const int* fds, uint32_t n_fds, uint64_t* wr
  * (these four only with KLF_FILTER_STAGE_TIMES, else 0), [4] total device time,
  * [5] workspace memsets (KLF_FILTER_STAGE_TIMES, else 0), [6] the k_scan kernel alone
  * (part of [0]): the start / end timestamps of its own dispatch (hipExtLaunchKernel
- * events, no event record beside it).  n = entries written. */
+ * events, no event record beside it), [7] the dense copy kernel k_tcopy alone, the same way
+ * (part of [3]; it exits at once when the run takes the sparse gather path).  n = entries written. */
 int klf_result_timing(const klf_result* r, double* ms, uint32_t cap, uint32_t* n);
 /* Totals across streams. */
 int klf_result_totals(const klf_result* r, klf_counts* totals);

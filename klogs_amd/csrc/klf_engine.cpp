@@ -201,7 +201,7 @@ struct klf_engine {
   DevBuf d_acblk;
   hipEvent_t stage_ev = nullptr;  // the staged copies have drained
   bool stage_ev_pending = false;
-  hipEvent_t ev[9] = {};  // [7], [8]: k_scan's dispatch (hipExtLaunchKernel start / stop); [6] unused
+  hipEvent_t ev[11] = {};  // [7], [8]: k_scan's dispatch (hipExtLaunchKernel start / stop); [9], [10]: k_tcopy's; [6] unused
   klf::RunArgs last_args{};  // arguments of the latest completed run (klf_retail)
   // the latest run's global line index is still to be built (lazy index, dense path): the
   // k_scatter launch that builds it
@@ -218,7 +218,7 @@ struct klf_result {
   std::vector<uint64_t> seg_base;    // per segment (device byte offset)
   bool has_bits = false;
   uint64_t total_lines = 0, total_out = 0;
-  double ms[7] = {0, 0, 0, 0, 0, 0, 0};
+  double ms[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   uint32_t ev_mask = 0;              // the timing events the run recorded
   int index_mode = KLF_INDEX_FULL;   // how much of the line index the run itself wrote
   // lazily filled host copies
@@ -1356,6 +1356,11 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
     HIPCHK(e, hipEventElapsedTime(&ms, e->ev[7], e->ev[8]), "scan timing events");
     r->ms[6] = ms;
   }
+  if ((ev_mask >> 9 & 1u) && (ev_mask >> 10 & 1u)) {  // k_tcopy's dispatch alone (dense copy)
+    float ms = 0.f;
+    HIPCHK(e, hipEventElapsedTime(&ms, e->ev[9], e->ev[10]), "copy timing events");
+    r->ms[7] = ms;
+  }
   r->ev_mask = ev_mask;
   r->total_lines = r->so[nsegs - 1].line_hi;
   for (auto& s : r->so) r->total_out = std::max(r->total_out, s.out_hi);
@@ -1409,6 +1414,11 @@ extern "C" int klf_retail(klf_engine* e, klf_result* prev, int64_t tail, klf_res
       float ms = 0.f;
       if ((h = hipEventElapsedTime(&ms, e->ev[0], e->ev[5])) != hipSuccess) { delete r; return hip_err(e, h, "klf_retail timing"); }
       r->ms[4] = ms;
+    }
+    if ((rmask >> 9 & 1u) && (rmask >> 10 & 1u)) {
+      float ms = 0.f;
+      if ((h = hipEventElapsedTime(&ms, e->ev[9], e->ev[10])) != hipSuccess) { delete r; return hip_err(e, h, "klf_retail timing"); }
+      r->ms[7] = ms;
     }
     r->ev_mask = rmask;
   }
@@ -1779,7 +1789,7 @@ extern "C" int klf_result_device_out(klf_result* r, uint32_t id, const uint8_t**
 
 extern "C" int klf_result_timing(const klf_result* r, double* ms, uint32_t cap, uint32_t* n) {
   if (!r || (cap && !ms)) return KLF_EINVAL;
-  const uint32_t k = std::min<uint32_t>(cap, 7);
+  const uint32_t k = std::min<uint32_t>(cap, 8);
   for (uint32_t i = 0; i < k; ++i) ms[i] = r->ms[i];
   if (n) *n = k;
   return KLF_OK;

@@ -3682,6 +3682,12 @@ size_t nfa_lds_bytes(const DevPatterns& P) {
   return 8ull * P.rx_count * (P.rx_classes + P.rx_maxpos + 4) + 256;
 }
 
+// KLF_SCAN_EVENTS=0 (A/B builds): no dispatch timestamps on k_scan / k_tcopy
+static bool env_off(const char* name) {
+  const char* v = getenv(name);
+  return v && !strcmp(v, "0");
+}
+
 // the scan's timing events for the current launch_pipeline call (ev[7], ev[8]), else null
 thread_local hipEvent_t t_scan_ev[2] = {nullptr, nullptr};
 
@@ -3763,7 +3769,7 @@ hipError_t launch_pipeline(const RunArgs& a0, hipStream_t st, hipEvent_t* ev, in
   if (ev && a.stage_times) KLF_REC(1);
   {
     // k_scan alone (the roofline kernel): ev[7] / ev[8] carry the dispatch's own timestamps
-    static const bool no_ev = getenv("KLF_SCAN_EVENTS") && !strcmp(getenv("KLF_SCAN_EVENTS"), "0");  // A/B
+    const bool no_ev = env_off("KLF_SCAN_EVENTS");  // A/B (read per launch: tests toggle it)
     t_scan_ev[0] = ev && !no_ev ? ev[7] : nullptr;
     t_scan_ev[1] = ev && !no_ev ? ev[8] : nullptr;
     if (t_scan_ev[0]) m |= (1u << 7) | (1u << 8);
@@ -3904,8 +3910,14 @@ static hipError_t launch_tail_stage(const RunArgs& a, hipStream_t st, hipEvent_t
       if (getenv("KLF_DIAG")) fprintf(stderr, "[klf] k_tcopy: %d blocks of %d waves per CU\n", occ, kTcWaves);
     }
     const uint32_t gc = (uint32_t)num_cus * (uint32_t)occ;
-    hipLaunchKernelGGL(k_tcopy, dim3(gk < gc ? gk : gc), dim3(64 * kTcWaves), 0, st, a,
-                       reinterpret_cast<const uint4*>(a.trec), a.kbase, a.truns);
+    if (ev && !env_off("KLF_SCAN_EVENTS")) {  // ev[9] / ev[10]: the dispatch's own timestamps
+      hipExtLaunchKernelGGL(k_tcopy, dim3(gk < gc ? gk : gc), dim3(64 * kTcWaves), 0, st, ev[9], ev[10], 0, a,
+                            reinterpret_cast<const uint4*>(a.trec), a.kbase, a.truns);
+      m |= (1u << 9) | (1u << 10);
+    } else {
+      hipLaunchKernelGGL(k_tcopy, dim3(gk < gc ? gk : gc), dim3(64 * kTcWaves), 0, st, a,
+                         reinterpret_cast<const uint4*>(a.trec), a.kbase, a.truns);
+    }
     KLF_TRY(hipGetLastError());
   }
 #undef KLF_TRY

@@ -336,9 +336,9 @@ class Result:
                     os.close(f)
 
     def timing(self) -> List[float]:
-        ms = (C.c_double * 7)()
+        ms = (C.c_double * 8)()
         k = C.c_uint32()
-        _check(_lib.klf_result_timing(self._p, ms, 7, C.byref(k)))
+        _check(_lib.klf_result_timing(self._p, ms, 8, C.byref(k)))
         return list(ms[: k.value])
 
     def stream_counts(self, i: int) -> dict:

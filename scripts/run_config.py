@@ -1,10 +1,10 @@
 #!/usr/bin/env python3
 """Runs one BASELINE config's device-resident filter a few times (profiling driver).
 
-    python scripts/run_config.py c2|c3|c4|c5 [--steps K] [--bytes B]
+    python scripts/run_config.py c1|c2|c3|c4|c5 [--steps K] [--warmup W]
 
-c2 is bench.py's headline workload (one 4 GiB JSON stream, --since 5m --tail 100 --grep);
-c3/c4/c5 are bench.run_extra's.  Prints the result dict as one JSON line."""
+bench.run_config without the checks, the CPU baseline, the write and capture paths.
+Prints the result dict as one JSON line."""
 import argparse
 import json
 import sys
@@ -21,11 +21,11 @@ def main():
     ap.add_argument("config")
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--bytes", type=int, default=32 << 30, help="total bytes of c4 / c5")
     a = ap.parse_args()
-    ns = argparse.Namespace(steps=a.steps, warmup=a.warmup, extra_bytes=a.bytes, no_verify=True, no_write=True)
+    ns = argparse.Namespace(steps=a.steps, warmup=a.warmup, no_verify=True, no_write=True, no_capture=True,
+                            no_cpu_baseline=True, capture_piece=4 << 20)
     now = bench.synth.T0 + bench.synth.SPAN + 1
-    out = bench.run_extra(a.config, ns, 0, now)
+    out = bench.run_config(a.config, ns, 0, now)
     print(json.dumps(out))
 
 
