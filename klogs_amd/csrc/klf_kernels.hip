@@ -403,6 +403,21 @@ __device__ __forceinline__ bool parse_fast(const uint8_t* lds, uint32_t o, const
 #ifndef KLF_ABL
 #define KLF_ABL 0
 #endif
+#ifndef KLF_SCAN_NT
+// the scan's prefetch rows as non-temporal loads (read once; L1 bypassed): C5 k_scan
+// 6.33 -> 6.09-6.12 ms, C2 0.92-0.93 -> 0.89-0.92, C4 7.72 -> 7.64 (same box, two rounds
+// each, gpurun_out/r5d, r5e)
+#define KLF_SCAN_NT 1
+#endif
+#ifndef KLF_SCAN_SUMSKIP
+// no count reductions on tiles where no line starts (C5: ~half its tiles): 6.33 -> 6.29 ms
+#define KLF_SCAN_SUMSKIP 1
+#endif
+typedef uint32_t klf_v4u __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint4 ld_nt(const uint4* p) {
+  const klf_v4u v = __builtin_nontemporal_load(reinterpret_cast<const klf_v4u*>(p));
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
 #ifndef KLF_CG_NT
 #define KLF_CG_NT 0
 #endif
@@ -480,7 +495,9 @@ __global__ __launch_bounds__(kThreads, MODE == kScanGen ? 3 : KLF_SCAN_OCC) void
 #define KLF_DECL(r) uint4 pf##r;
   KLF_ROWS(KLF_DECL)
 #undef KLF_DECL
-#define KLF_LOAD(r) pf##r = gp[r * 64 + lane];
+// non-temporal prefetch loads in the literal / general scans (not the plain one: C3's
+// k_tcopy re-reads the input, 5.15 -> 5.18 ms with them)
+#define KLF_LOAD(r) pf##r = (KLF_SCAN_NT && MODE != kScanPlain) ? ld_nt(&gp[r * 64 + lane]) : gp[r * 64 + lane];
 #define KLF_STORE(r) l[r * 64 + lane] = pf##r;
   uint4 pfh = make_uint4(0, 0, 0, 0);
   // A wave takes groups of kScanGroup consecutive tiles (group g, g + nwaves, ...): their
@@ -501,7 +518,7 @@ __global__ __launch_bounds__(kThreads, MODE == kScanGen ? 3 : KLF_SCAN_OCC) void
     pf_sd = segs[pf_s];
     const uint4* gp = reinterpret_cast<const uint4*>(a.bytes + pf_sd.base + (uint64_t)(tile - pf_sd.tile0) * kTile);
     KLF_ROWS(KLF_LOAD)
-    if (lane < kHalo / 16) pfh = gp[kTile / 16 + lane];
+    if (lane < kHalo / 16) pfh = (KLF_SCAN_NT && MODE != kScanPlain) ? ld_nt(&gp[kTile / 16 + lane]) : gp[kTile / 16 + lane];
   }
   // Each tile ends with exactly one unconditional store instruction (the first two 128-B
   // lines of its record region, through a buffer descriptor so that an ablated launch can
@@ -536,7 +553,7 @@ __global__ __launch_bounds__(kThreads, MODE == kScanGen ? 3 : KLF_SCAN_OCC) void
         }
         const uint4* gp = reinterpret_cast<const uint4*>(a.bytes + pf_sd.base + (uint64_t)(nx - pf_sd.tile0) * kTile);
         KLF_ROWS(KLF_LOAD)
-        if (lane < kHalo / 16) pfh = gp[kTile / 16 + lane];
+        if (lane < kHalo / 16) pfh = (KLF_SCAN_NT && MODE != kScanPlain) ? ld_nt(&gp[kTile / 16 + lane]) : gp[kTile / 16 + lane];
       }
     }
     wave_lds_sync();
@@ -1040,7 +1057,12 @@ __global__ __launch_bounds__(kThreads, MODE == kScanGen ? 3 : KLF_SCAN_OCC) void
 
     // ---- per-tile record: the first 64 slots and the TileStat, two store instructions
     // on every path (see the loop entry) ----
+#if KLF_SCAN_SUMSKIP  // A/B: no reductions on tiles where no line starts (wave-uniform)
+    uint32_t pp = 0, qq = 0, dd = 0;
+    if (nlines) { pp = wave_sum(n_parsed); qq = wave_sum(n_since); dd = wave_sum(n_defer); }
+#else
     const uint32_t pp = wave_sum(n_parsed), qq = wave_sum(n_since), dd = wave_sum(n_defer);
+#endif
     any_defer |= dd != 0;
     {  // the record region in 16-B units, whole 128-B lines: unit 0 the TileStat, unit u
        // slots 4u - 4 .. 4u - 1 (garbage past the last slot; a dense tile's slots are in
