@@ -2,16 +2,18 @@
 """Copies one scripts/profile_round.sh result into profiles/<round> and derives what the
 bench line cites from it:
 
-    python3 scripts/collect_profiles.py gpurun_out/<tag> profiles/r02
+    python3 scripts/collect_profiles.py gpurun_out/<tag> profiles/r05
 
   bench.json / bench_kernel_stats.csv    the driver's bench command and its kernel trace
-  <cfg>_kernel_stats.csv                 per-config kernel traces (C3, C5)
+  <cfg>_kernel_stats.csv                 per-config kernel traces (scripts/run_config.py)
   pmc_<cfg>.json                         per-kernel counter means (FETCH_SIZE x2, KiB -> B)
-  traffic.json                           per-launch HBM bytes of C2's k_scan<1, ...> (bench.py
-                                         reads it as roofline.traffic)
-  summary.md                             per config: dominant kernel, trace average, the
-                                         rocprof-derived roofline fraction beside the bench's
-                                         HIP-event one, traffic / algorithmic bytes
+  traffic.json                           per config: per-launch HBM bytes of the roofline
+                                         kernel (bench.py reads the headline's as
+                                         roofline.traffic)
+  summary.md / summary.json              per config: the roofline kernel (k_scan, C3:
+                                         k_tcopy), its steady trace average, the rocprof
+                                         roofline fraction beside the bench's HIP-event one,
+                                         traffic / algorithmic bytes, the kernel split
 """
 import csv
 import json
@@ -23,6 +25,7 @@ from pathlib import Path
 
 ROOT = Path(__file__).resolve().parent.parent
 PEAK = 8000.0  # GB/s
+CONFIGS = ("c5", "c2", "c3", "c4")
 
 
 def short(name):
@@ -52,83 +55,90 @@ def last_json(path):
     return json.loads(lines[-1])
 
 
+def bench_entry(b, c):
+    """(roofline dict, bytes of the config) of config c in a bench line."""
+    if c == "c5":
+        return b["roofline"], b["extra"]["headline"]
+    ex = b.get("extra", {}).get("configs", {}).get(c)
+    return (ex["roofline"], ex) if ex and "roofline" in ex else (None, None)
+
+
 def main():
     src, dst = Path(sys.argv[1]), Path(sys.argv[2])
     dst.mkdir(parents=True, exist_ok=True)
     shutil.copy(src / "bench.json", dst / "bench.json")
     shutil.copy(src / "trace" / "run_kernel_stats.csv", dst / "bench_kernel_stats.csv")
-    for c in ("c3", "c4", "c5"):
+    for c in CONFIGS:
         f = src / f"trace_{c}" / "run_kernel_stats.csv"
         if f.exists():
             shutil.copy(f, dst / f"{c}_kernel_stats.csv")
     pmc = {}
-    for c in ("c2", "c3", "c4", "c5"):
+    for c in CONFIGS:
         d = src / f"pmc_{c}"
         if d.exists():
             subprocess.run([sys.executable, str(ROOT / "scripts/pmc_summary.py"), str(d), "--json",
                             str(dst / f"pmc_{c}.json")], check=True, stdout=subprocess.DEVNULL)
             pmc[c] = json.loads((dst / f"pmc_{c}.json").read_text())
     b = last_json(dst / "bench.json")
-    tr = stats(dst / "bench_kernel_stats.csv")
     lines = ["# Profiles of this round", "",
              "Made by `scripts/profile_round.sh` on one MI355X (the driver's bench command under",
-             "`rocprofv3 --kernel-trace --stats`, then counter passes per config) and",
-             "`scripts/collect_profiles.py`.  frac = algorithmic bytes / average launch / 8 TB/s.", "",
-             "| config | kernel | alg bytes / launch | config-run trace avg (µs) | frac (rocprof) | avg w/o 1st launch (µs; bench trace, C3: its config trace) | frac (rocprof, steady) | frac (bench HIP events) | HBM traffic / alg |",
+             "`rocprofv3 --kernel-trace --stats`, per-config traces of `scripts/run_config.py`, then counter",
+             "passes per config) and `scripts/collect_profiles.py`.  frac = algorithmic bytes per launch /",
+             "average launch / 8 TB/s; the steady average leaves each config run's first launch out.", "",
+             "| config | roofline kernel | alg bytes / launch | trace avg (µs) | steady avg (µs) | frac (rocprof, steady) "
+             "| frac (bench HIP events) | HBM traffic / launch | traffic / alg |",
              "|---|---|---|---|---|---|---|---|---|"]
-    out = {}
-    # C2: the headline line
-    k2 = next(k for k in tr if k.startswith("k_scan<1"))
-    alg2 = b["roofline"]["alg_bytes_per_launch"]
-    fr2 = alg2 / (tr[k2]["avg_us"] * 1e-6) / 1e9 / PEAK
-    t2 = None
-    if "c2" in pmc and k2 in pmc["c2"]:
-        p = pmc["c2"][k2]
-        t2 = p.get("fetch_bytes_x2", 0) + p.get("write_bytes", 0)
-        json.dump({"kernel": k2, "fetch_bytes": round(p.get("fetch_bytes_x2", 0)),
-                   "write_bytes": round(p.get("write_bytes", 0)), "traffic_bytes": round(t2),
-                   "correction": "FETCH_SIZE x2 (gfx950 wide streaming reads), WRITE_SIZE x1; KiB -> B",
-                   "sources": [str(src / "pmc_c2")]}, open(dst / "traffic.json", "w"), indent=1)
-    st2 = steady_us(src / "trace" / "run_kernel_trace.csv", k2)
-    fs2 = st2 and alg2 / (st2 * 1e-6) / 1e9 / PEAK
-    out["c2"] = {"kernel": k2, "avg_us": tr[k2]["avg_us"], "frac_rocprof": round(fr2, 4),
-                 "steady_us": st2 and round(st2, 1), "frac_rocprof_steady": fs2 and round(fs2, 4),
-                 "frac_hip": b["roofline"]["frac"], "traffic_over_alg": t2 and round(t2 / alg2, 3)}
-    lines.append(f"| C2 | `{k2}` | {alg2} | {tr[k2]['avg_us']:.1f} | {fr2:.4f} | "
-                 f"{'%.1f' % st2 if st2 else '—'} | {'%.4f' % fs2 if fs2 else '—'} | {b['roofline']['frac']} | "
-                 f"{'%.3f' % (t2 / alg2) if t2 else '—'} |")
-    for c in ("c3", "c4", "c5"):
+    out, traffic = {}, {}
+    for c in CONFIGS:
         f = dst / f"{c}_kernel_stats.csv"
-        ex = b.get("extra", {}).get("configs", {}).get(c)
-        if not f.exists() or not ex:
+        roof, ex = bench_entry(b, c)
+        if not f.exists() or roof is None:
             continue
         ts = stats(f)
-        ks = next(k for k in ts if k.startswith("k_scan<"))
-        alg = ex["bytes"]
-        fr = alg / (ts[ks]["avg_us"] * 1e-6) / 1e9 / PEAK
+        want = "k_tcopy" if roof["kernel"] == "k_tcopy" else "k_scan<"
+        ks = next((k for k in ts if k.startswith(want)), None)
+        if ks is None:
+            continue
+        alg = roof["alg_bytes_per_launch"]
+        st = steady_us(src / f"trace_{c}" / "run_kernel_trace.csv", ks)
+        fs = st and alg / (st * 1e-6) / 1e9 / PEAK
         tt = None
         if c in pmc and ks in pmc[c]:
             p = pmc[c][ks]
             tt = p.get("fetch_bytes_x2", 0) + p.get("write_bytes", 0)
-        # steady state from the bench command's own trace (the line's numbers come from that
-        # run), except C3: its scan instantiation also serves C1 there (k_scan<0,...>), so
-        # C3's comes from its own config run
-        tr_bench = src / "trace" / "run_kernel_trace.csv"
-        tr_cfg = src / f"trace_{c}" / "run_kernel_trace.csv"
-        st = (steady_us(tr_cfg, ks) or steady_us(tr_bench, ks)) if c == "c3" else \
-            (steady_us(tr_bench, ks) or steady_us(tr_cfg, ks))
-        fs = st and alg / (st * 1e-6) / 1e9 / PEAK
-        out[c] = {"kernel": ks, "avg_us": ts[ks]["avg_us"], "frac_rocprof": round(fr, 4),
+            traffic[c] = {"kernel": ks, "fetch_bytes": round(p.get("fetch_bytes_x2", 0)),
+                          "write_bytes": round(p.get("write_bytes", 0)), "traffic_bytes": round(tt),
+                          "alg_bytes": alg,
+                          "correction": "FETCH_SIZE x2 (gfx950 wide streaming reads), WRITE_SIZE x1; KiB -> B",
+                          "source": str(src / f"pmc_{c}")}
+        out[c] = {"kernel": ks, "alg_bytes": alg, "avg_us": round(ts[ks]["avg_us"], 1),
                   "steady_us": st and round(st, 1), "frac_rocprof_steady": fs and round(fs, 4),
-                  "frac_hip": ex["roofline"]["frac"], "traffic_over_alg": tt and round(tt / alg, 3),
-                  "kernels": {k: round(v["avg_us"], 1) for k, v in sorted(ts.items(), key=lambda kv: -kv[1]["pct"])[:8]}}
-        lines.append(f"| {c.upper()} | `{ks}` | {alg} | {ts[ks]['avg_us']:.1f} | {fr:.4f} | "
-                     f"{'%.1f' % st if st else '—'} | {'%.4f' % fs if fs else '—'} | {ex['roofline']['frac']} | "
+                  "frac_hip": roof["frac"], "traffic_bytes": tt and round(tt),
+                  "traffic_over_alg": tt and round(tt / alg, 3),
+                  "kernels": {k: round(v["avg_us"], 1) for k, v in sorted(ts.items(), key=lambda kv: -kv[1]["pct"])[:10]}}
+        lines.append(f"| {c.upper()} | `{ks}` | {alg} | {ts[ks]['avg_us']:.1f} | {'%.1f' % st if st else '—'} | "
+                     f"{'%.4f' % fs if fs else '—'} | {roof['frac']} | {'%.4g' % tt if tt else '—'} | "
                      f"{'%.3f' % (tt / alg) if tt else '—'} |")
-    lines += ["", "Per-config kernel split (trace averages, µs):", ""]
+    if traffic:
+        json.dump(traffic, open(dst / "traffic.json", "w"), indent=1)
+    lines += ["", "Per-config kernel split (trace averages over the config run, µs):", ""]
     for c, v in out.items():
-        if "kernels" in v:
-            lines.append(f"* {c.upper()}: " + ", ".join(f"`{k}` {t}" for k, t in v["kernels"].items()))
+        lines.append(f"* {c.upper()}: " + ", ".join(f"`{k}` {t}" for k, t in v["kernels"].items()))
+    # counters of the roofline kernels: VALU per 8 KiB tile, LDS bank conflicts / LDS-active
+    lines += ["", "Counters of the scans (per launch):", "",
+              "| config | kernel | SQ_INSTS_VALU / 8 KiB tile | SQ_LDS_BANK_CONFLICT / SQ_ACTIVE_INST_LDS |", "|---|---|---|---|"]
+    for c in CONFIGS:
+        if c not in pmc or c not in out:
+            continue
+        ex = bench_entry(b, c)[1]
+        tiles = ex["bytes"] / 8192 if ex else None
+        for k, p in pmc[c].items():
+            if not k.startswith("k_scan") or "SQ_INSTS_VALU" not in p:
+                continue
+            v = p["SQ_INSTS_VALU"] / tiles if tiles else None  # (summed over the dispatch's rows)
+            bc = p.get("SQ_LDS_BANK_CONFLICT"), p.get("SQ_ACTIVE_INST_LDS")
+            r = bc[0] / bc[1] if bc[0] is not None and bc[1] else None
+            lines.append(f"| {c.upper()} | `{k}` | {'%.0f' % v if v else '—'} | {'%.2f' % r if r else '—'} |")
     (dst / "summary.md").write_text("\n".join(lines) + "\n")
     json.dump(out, open(dst / "summary.json", "w"), indent=1)
     print("\n".join(lines))

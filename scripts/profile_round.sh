@@ -16,7 +16,7 @@ if [ "$what" != pmc ]; then
   timeout -k 10 700 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/trace" -o run \
     -- python3 bench.py > "$out/bench.json" 2> "$out/bench.err"
   echo "trace done"
-  for c in c3 c4 c5; do  # per-config kernel splits (the bench trace mixes C2 with the extras)
+  for c in c5 c2 c3 c4; do  # per-config kernel splits (the bench trace mixes every config)
     timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/trace_$c" -o run \
       -- python3 scripts/run_config.py "$c" --steps 8 > "$out/run_$c.json" 2> "$out/run_$c.err"
     echo "trace $c done"
