@@ -84,7 +84,8 @@ def main():
              "Made by `scripts/profile_round.sh` on one MI355X (the driver's bench command under",
              "`rocprofv3 --kernel-trace --stats`, per-config traces of `scripts/run_config.py`, then counter",
              "passes per config) and `scripts/collect_profiles.py`.  frac = algorithmic bytes per launch /",
-             "average launch / 8 TB/s; the steady average leaves each config run's first launch out.", "",
+             "average launch / 8 TB/s; the steady average leaves the kernel's first launch out (C5, C2, C4: in the",
+             "bench trace; C3: in its config run).", "",
              "| config | roofline kernel | alg bytes / launch | trace avg (µs) | steady avg (µs) | frac (rocprof, steady) "
              "| frac (bench HIP events) | HBM traffic / launch | traffic / alg |",
              "|---|---|---|---|---|---|---|---|---|"]
@@ -100,7 +101,11 @@ def main():
         if ks is None:
             continue
         alg = roof["alg_bytes_per_launch"]
-        st = steady_us(src / f"trace_{c}" / "run_kernel_trace.csv", ks)
+        # steady state from the bench command's own trace (the line's numbers come from that
+        # run) where the kernel is the config's alone there; C3's k_tcopy / plain scan also
+        # run for other configs in that trace: its config run's
+        st = steady_us(src / "trace" / "run_kernel_trace.csv", ks) if c != "c3" else None
+        st = st or steady_us(src / f"trace_{c}" / "run_kernel_trace.csv", ks)
         fs = st and alg / (st * 1e-6) / 1e9 / PEAK
         tt = None
         if c in pmc and ks in pmc[c]:
