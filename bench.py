@@ -206,7 +206,11 @@ def run_config(name: str, args, local: int, now: int, headline: bool = False) ->
     # the dominant kernel: the scan, except C3 (-l only, every line out) where the dense copy
     # k_tcopy takes ~60 % of the step; its algorithmic bytes are the bytes it must move, the
     # selected content read once and written once (2 B_out)
-    if mode == "-l":
+    compaction = last.compaction()
+    out["compaction"] = compaction
+    if mode == "-l" and compaction == "one_pass":  # the scan compacts in place: it reads and writes
+        k_alg, k_ms, k_name = n + tot["out_bytes"], scan_ms, "k_scan<plain, one-pass compaction>"
+    elif mode == "-l":
         k_alg, k_ms, k_name = 2 * tot["out_bytes"], copy_ms, "k_tcopy"
     else:
         k_alg, k_ms, k_name = n, scan_ms, scan_kernel_name(name, pats)
@@ -216,7 +220,9 @@ def run_config(name: str, args, local: int, now: int, headline: bool = False) ->
                        "alg_bytes_per_launch": k_alg, "avg_launch_ms": round(k_ms, 4),
                        "frac_source": "HIP events carrying the kernel dispatch's own start / end timestamps "
                                       "(hipExtLaunchKernel on the launch stream), this run's timed steps"}
-    if mode == "-l":
+    if mode == "-l" and compaction == "one_pass":
+        out["roofline"]["alg_bytes_note"] = "the one-pass scan reads the input once and writes the output once"
+    elif mode == "-l":
         out["roofline"]["alg_bytes_note"] = ("k_tcopy moves the selected contents: B_out read + B_out written "
                                              "(the input's 31-B prefixes are skipped in place)")
         out["scan"] = {"kernel": "k_scan<plain>", "avg_launch_ms": round(scan_ms, 4),

@@ -212,6 +212,14 @@ int klf_result_timing(const klf_result* r, double* ms, uint32_t cap, uint32_t* n
 int klf_result_totals(const klf_result* r, klf_counts* totals);
 /* KLF_INDEX_* of the run (klf_result_lines builds the rest on demand, after the run). */
 int klf_result_index_mode(const klf_result* r);
+/* klf_result_compaction: how the run put the selected bytes together in HBM. */
+#define KLF_COMPACT_GATHER 0   /* line gather of the selected lines (--tail windows, sparse)   */
+#define KLF_COMPACT_TILES 1    /* tile copy after the scan (most lines selected)               */
+#define KLF_COMPACT_ONEPASS 2  /* in the scan itself, each tile range in place (no patterns,   */
+                               /* --tail -1): a stream's output is a few extents in HBM, the   */
+                               /* host views / klf_result_write join them, klf_result_device_out */
+                               /* makes one contiguous copy on demand                          */
+int klf_result_compaction(const klf_result* r);
 void klf_result_free(klf_result* r);
 
 /* ---- follow mode (-f) -------------------------------------------- */

@@ -183,6 +183,11 @@ struct klf_engine {
   DevBuf d_block;  // the first run's workspace buffers (ensure_all), freed last
   DevBuf d_batch, d_segs, d_tstat, d_slots, d_pool, d_tile_base, d_bsum, d_cstatus, d_counters, d_line_off,
       d_meta, d_bits, d_segout, d_wpre, d_out, d_mpart, d_trec, d_truns, d_kbase;
+  // one-pass compaction (RunArgs::fuse): range table, extents, range states; d_out2 the
+  // contiguous device copy klf_result_device_out makes of a fused result on demand
+  DevBuf d_fext0, d_fext, d_frinfo, d_out2;
+  uint32_t fuse_range = 0, fuse_nranges = 0, fuse_next = 0;  // the layout d_fext0 was made for
+  std::vector<uint32_t> fuse_ext0;
   uint64_t pool_cap = 1 << 20;
   // lines per input byte of the last run (0: no run yet): sizes the line arrays of the next
   // runs (the first run sizes them from its own tile index, between two launch phases)
@@ -231,6 +236,13 @@ struct klf_result {
   // per-pattern counts (KLF_FILTER_PATTERN_COUNTS): [segment][compiled id]
   bool counted = false, pcount_ok = false;
   std::vector<uint32_t> pcount;
+  // a one-pass compaction run: each segment's output is the extents fx[2 k], fx[2 k + 1]
+  // (d_out offset, length) for k in [fx_first[s], fx_first[s + 1]); so[s].out_lo / out_hi
+  // are then the segment's place in the concatenated (host) output
+  bool fused = false, have_dev = false;
+  int compaction = KLF_COMPACT_GATHER;
+  std::vector<uint64_t> fx;
+  std::vector<uint32_t> fx_first;
 };
 
 static int set_err(klf_engine* e, int code, const std::string& m) {
@@ -612,7 +624,8 @@ extern "C" void klf_close(klf_engine* e) {
                     &e->d_rx_follow, &e->d_rx_vec, &e->d_rx_flags, &e->d_rx_pre, &e->d_qf_bitmap, &e->d_qf_head,
                     &e->d_qf_ent, &e->d_qf_nbytes, &e->d_qf_anc, &e->d_rx_vec4, &e->d_qhits, &e->d_hslots, &e->d_hist, &e->d_hflat, &e->d_cand, &e->d_batch, &e->d_segs, &e->d_tstat,
                     &e->d_slots, &e->d_pool, &e->d_tile_base, &e->d_bsum, &e->d_cstatus, &e->d_counters, &e->d_cmap, &e->d_cseg,
-                    &e->d_line_off, &e->d_meta, &e->d_bits, &e->d_segout, &e->d_wpre, &e->d_out, &e->d_tile_seg, &e->d_mpart, &e->d_trec, &e->d_truns, &e->d_kbase})
+                    &e->d_line_off, &e->d_meta, &e->d_bits, &e->d_segout, &e->d_wpre, &e->d_out, &e->d_tile_seg, &e->d_mpart, &e->d_trec, &e->d_truns, &e->d_kbase,
+                    &e->d_fext0, &e->d_fext, &e->d_frinfo, &e->d_out2})
     b->release();
   e->d_asm.release();
   e->d_scratch.release();
@@ -1054,6 +1067,46 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
   const bool want_truns = f->tail < 0 || e->dense_tail_seen;
   if (want_truns) ws.push_back({&e->d_truns, ntiles * klf::kRunSlots * 4});
   uint32_t compact_mode = 0;  // tests: force either compaction path
+  if (const char* v = getenv("KLF_COMPACT")) compact_mode = !strcmp(v, "sparse") ? 1u : !strcmp(v, "dense") ? 2u : 0u;
+  // One-pass compaction (no patterns, --tail -1): the fused scan compacts each wave's tile
+  // range in place.  The ranges (a multiple of kScanGroup tiles each, one per wave of a
+  // full-occupancy launch) and each range's first extent (one extent per stream it touches).
+  const bool fuse_try = mode == klf::CompiledSet::kNone && f->tail < 0 && compact_mode == 0 &&
+                        !(getenv("KLF_FUSE") && !strcmp(getenv("KLF_FUSE"), "0"));
+  bool fuse_ok = fuse_try;
+  uint64_t seg_end = 0;  // past the last input byte (the fused output is laid out like the input)
+  for (const auto& d : segs) seg_end = std::max<uint64_t>(seg_end, d.base + d.len);
+  auto seg_of_tile = [&](uint64_t t) -> uint32_t {
+    uint32_t lo = 0, hi = nsegs;  // the last segment whose tile0 <= t
+    while (hi - lo > 1) {
+      const uint32_t mid = (lo + hi) / 2;
+      if (segs[mid].tile0 <= t) lo = mid; else hi = mid;
+    }
+    return lo;
+  };
+  if (fuse_try) {
+    const uint64_t waves = (uint64_t)std::max(1, klf::fuse_waves(e->num_cus));
+    uint64_t R = (ntiles + waves - 1) / waves;
+    R = (R + klf::kScanGroup - 1) / klf::kScanGroup * klf::kScanGroup;
+    if (const char* v = getenv("KLF_DEBUG_FUSE_RANGE"))  // tests: short ranges (many range seams)
+      R = std::max<uint64_t>(klf::kScanGroup, (uint64_t)atol(v) / klf::kScanGroup * klf::kScanGroup);
+    const uint32_t nr = (uint32_t)((ntiles + R - 1) / R);
+    if (!same_layout || e->fuse_range != (uint32_t)R || e->fuse_nranges != nr) {
+      e->fuse_ext0.assign(nr + 1, 0);
+      for (uint32_t q = 0; q < nr; ++q) {
+        const uint64_t t0 = (uint64_t)q * R, t1 = std::min<uint64_t>(t0 + R, ntiles) - 1;
+        e->fuse_ext0[q + 1] = e->fuse_ext0[q] + (seg_of_tile(t1) - seg_of_tile(t0) + 1);
+      }
+      HIPCHK(e, e->d_fext0.ensure((nr + 1) * 4), "alloc fuse ranges");
+      HIPCHK(e, hipMemcpyAsync(e->d_fext0.p, e->fuse_ext0.data(), (nr + 1) * 4, hipMemcpyHostToDevice, st),
+             "H2D fuse ranges");
+      e->fuse_range = (uint32_t)R;
+      e->fuse_nranges = nr;
+      e->fuse_next = e->fuse_ext0[nr];
+    }
+    HIPCHK(e, e->d_fext.ensure((size_t)e->fuse_next * 16), "alloc fuse extents");
+    HIPCHK(e, e->d_frinfo.ensure((size_t)e->fuse_nranges * 32), "alloc fuse range states");
+  }
   e->index_pending.clear();
   // lazy line index (grep none, --tail -1; KLF_LAZY_INDEX=0 turns it off)
   const bool full_index = (f->flags & KLF_FILTER_FULL_INDEX) != 0;
@@ -1061,13 +1114,12 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
                           !(getenv("KLF_LAZY_INDEX") && !strcmp(getenv("KLF_LAZY_INDEX"), "0"));
   // (a run that needs every line's index -- k_match's fallback -- turns it off)
   bool win_ok = !full_index;
-  if (const char* v = getenv("KLF_COMPACT")) compact_mode = !strcmp(v, "sparse") ? 1u : !strcmp(v, "dense") ? 2u : 0u;
   // The output buffer: sized for the whole input up front when the run keeps about as much
   // as it reads (no --tail limit: C3-like), else grown
   // on demand -- the compaction skips a copy that would not fit, the host grows the buffer
   // to the run's output and reruns the tail stage (first runs only: the buffer is kept).
   // A --tail run then never maps an input-sized buffer (34 GB for C4 / C5).
-  if (f->tail < 0) HIPCHK(e, e->d_out.ensure(total_bytes + 64), "alloc out");
+  if (f->tail < 0) HIPCHK(e, e->d_out.ensure(std::max<uint64_t>(total_bytes, fuse_try ? seg_end : 0) + 64), "alloc out");
   else if (!e->d_out.p) {  // a first --tail run: room for a typical tail window (no rerun to grow)
     uint64_t first = 64ull << 20;
     if (const char* v = getenv("KLF_DEBUG_OUT_INIT")) first = (uint64_t)std::max(1L, atol(v));  // tests: force growth
@@ -1168,6 +1220,15 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
     a.pcount = count ? e->d_pcount.as<uint32_t>() : nullptr;
     a.pairs = count ? e->d_pairs.as<uint64_t>() : nullptr;
     a.pairs_log2 = e->pairs_log2;
+    if (fuse_ok) {
+      a.fuse = 1;
+      a.plan_runs = 0;
+      a.fuse_range = e->fuse_range;
+      a.fuse_nranges = e->fuse_nranges;
+      a.fuse_ext0 = e->d_fext0.as<uint32_t>();
+      a.fuse_ext = e->d_fext.as<uint64_t>();
+      a.fuse_rinfo = e->d_frinfo.as<uint64_t>();
+    }
   };
   bool overflow = false, pairs_over = false;
   uint32_t ev_mask = 0;
@@ -1286,6 +1347,10 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
       e->pool_cap = std::max<uint64_t>(e->pool_cap, (uint64_t)counters[klf::kCtrPool] + 1024);
       continue;
     }
+    if (a.fuse && counters[klf::kCtrFuseBad]) {  // a deferred line or a dense tile: the two-pass rerun
+      fuse_ok = false;
+      continue;
+    }
     if (a.win_index && counters[klf::kCtrRedo]) {  // k_match needed the whole index: rerun with it
       win_ok = false;
       continue;
@@ -1304,10 +1369,29 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
       HIPCHK(e, grow_out_retail(e, a, r->so), "grow output");
       if (getenv("KLF_DIAG")) fprintf(stderr, "[klf] output buffer grown to %zu B\n", e->d_out.cap);
     }
+    if (a.fuse) {  // the extents, in stream order (ranges ascend, and so do a range's streams)
+      r->fused = true;
+      r->fx.resize((size_t)e->fuse_next * 2);
+      HIPCHK(e, hipMemcpy(r->fx.data(), e->d_fext.p, (size_t)e->fuse_next * 16, hipMemcpyDeviceToHost), "D2H extents");
+      r->fx_first.assign(nsegs + 1, e->fuse_next);
+      for (uint32_t q = e->fuse_nranges; q-- > 0;) {
+        const uint32_t s0 = seg_of_tile((uint64_t)q * e->fuse_range);
+        for (uint32_t k = e->fuse_ext0[q]; k < e->fuse_ext0[q + 1]; ++k) r->fx_first[s0 + (k - e->fuse_ext0[q])] = k;
+      }
+      uint64_t acc = 0;
+      for (uint32_t sg = 0; sg < nsegs; ++sg) {
+        r->so[sg].sel_lo = 0;  // --tail -1, no patterns: every parsed line since the cutoff
+        r->so[sg].sel_hi = r->so[sg].since_ok;
+        r->so[sg].out_lo = acc;
+        for (uint32_t k = r->fx_first[sg]; k < r->fx_first[sg + 1]; ++k) acc += r->fx[2 * (size_t)k + 1];
+        r->so[sg].out_hi = acc;
+      }
+    }
     e->last_args = a;
-    if ((a.lazy_index && counters[klf::kCtrDense]) || a.win_index) e->index_pending.push_back(a);
-    r->index_mode = (a.lazy_index && counters[klf::kCtrDense]) ? KLF_INDEX_ON_DEMAND
-                    : a.win_index ? KLF_INDEX_WINDOWS : KLF_INDEX_FULL;
+    const bool on_demand = a.lazy_index && (counters[klf::kCtrDense] || a.fuse);
+    if (on_demand || a.win_index) e->index_pending.push_back(a);
+    r->index_mode = on_demand ? KLF_INDEX_ON_DEMAND : a.win_index ? KLF_INDEX_WINDOWS : KLF_INDEX_FULL;
+    r->compaction = a.fuse ? KLF_COMPACT_ONEPASS : counters[klf::kCtrDense] ? KLF_COMPACT_TILES : KLF_COMPACT_GATHER;
     e->last_gen = r->gen;
     e->line_density = (double)(r->so[nsegs - 1].line_hi + 1) / (double)total_bytes;
     if (f->tail >= 0 && counters[klf::kCtrDense]) e->dense_tail_seen = true;
@@ -1398,6 +1482,7 @@ extern "C" int klf_retail(klf_engine* e, klf_result* prev, int64_t tail, klf_res
     klf::RunArgs a = e->last_args;
     a.tail = tail;
     a.stage_times = 0;
+    a.fuse = 0;  // (the two-pass compaction, over the line index)
     a.plan_runs = 0;  // (plans assume --tail -1 and are consumed by the run)
     hipStream_t st = e->stream;
     uint32_t rmask = 0;
@@ -1406,7 +1491,10 @@ extern "C" int klf_retail(klf_engine* e, klf_result* prev, int64_t tail, klf_res
     if (h == hipSuccess) h = hipMemcpyAsync(r->so.data(), e->d_segout.p, nsegs * sizeof(SegOut), hipMemcpyDeviceToHost, st);
     if (h == hipSuccess) h = hipMemcpyAsync(e->h_rb.p, e->d_counters.p, 32 * 4, hipMemcpyDeviceToHost, st);
     if (h == hipSuccess) h = hipStreamSynchronize(st);
-    if (h == hipSuccess) short_out = static_cast<uint32_t*>(e->h_rb.p)[klf::kCtrOutShort];
+    if (h == hipSuccess) {
+      short_out = static_cast<uint32_t*>(e->h_rb.p)[klf::kCtrOutShort];
+      r->compaction = static_cast<uint32_t*>(e->h_rb.p)[klf::kCtrDense] ? KLF_COMPACT_TILES : KLF_COMPACT_GATHER;
+    }
     if (h == hipSuccess && short_out) h = grow_out_retail(e, a, r->so);  // a larger window than the buffer holds
     if (h == hipSuccess) e->last_args = a;
     if (h != hipSuccess) { delete r; return hip_err(e, h, "klf_retail"); }
@@ -1514,8 +1602,20 @@ extern "C" int klf_result_stream(klf_result* r, uint32_t id, const uint8_t** byt
   klf_engine* e = r->e;
   if (bytes && !r->have_out) {  // counts only: no D2H
     r->out.resize(r->total_out + 1);
-    if (r->total_out) {
+    if (r->total_out && !r->fused) {
       HIPCHK(e, hipMemcpyAsync(r->out.data(), e->d_out.p, r->total_out, hipMemcpyDeviceToHost, e->stream), "D2H out");
+      HIPCHK(e, hipStreamSynchronize(e->stream), "sync");
+    } else if (r->total_out) {  // one copy per extent, into the stream's place
+      const uint8_t* d = e->d_out.as<uint8_t>();
+      for (size_t sg = 0; sg < r->so.size(); ++sg) {
+        uint64_t o = r->so[sg].out_lo;
+        for (uint32_t k = r->fx_first[sg]; k < r->fx_first[sg + 1]; ++k) {
+          const uint64_t n = r->fx[2 * (size_t)k + 1];
+          if (n) HIPCHK(e, hipMemcpyAsync(r->out.data() + o, d + r->fx[2 * (size_t)k], n, hipMemcpyDeviceToHost, e->stream),
+                        "D2H out");
+          o += n;
+        }
+      }
       HIPCHK(e, hipStreamSynchronize(e->stream), "sync");
     }
     r->have_out = true;
@@ -1557,23 +1657,38 @@ static bool write_all(int fd, const uint8_t* p, uint64_t n) {  // io.Copy's writ
 // shared by several streams must see them in stream order: that case (and small outputs)
 // runs on the calling thread alone.
 namespace {
-struct WPiece { uint64_t lo, hi; int fd; uint32_t id; };
+// a stream's output: [lo, hi) of the concatenated output, in d_out as `parts` ({offset,
+// length}: one part, or a fused run's extents)
+struct WPiece {
+  uint64_t lo, hi;
+  int fd;
+  uint32_t id;
+  std::vector<std::pair<uint64_t, uint64_t>> parts;
+};
 
 struct WErr { std::atomic<int> id{-1}; int err = 0; std::string what; std::mutex mu; };
 
-// D2H [lo, hi) of d_out in two halves of `buf` (double-buffered on `st`) and write(2) each
-// half to fd.  Returns false with `werr` set on the first failure.
+// D2H each part of the stream's output in two halves of `buf` (double-buffered on `st`) and
+// write(2) each half to fd.  Returns false with `werr` set on the first failure.
+bool copy_part(klf_engine* e, const uint8_t* d_out, const WPiece& q, uint64_t dlo, uint64_t n, uint8_t* buf,
+               uint64_t half, hipStream_t st, hipEvent_t ev[2], WErr& werr, uint64_t& total);
 bool copy_piece(klf_engine* e, const uint8_t* d_out, const WPiece& q, uint8_t* buf, uint64_t half,
                 hipStream_t st, hipEvent_t ev[2], WErr& werr, uint64_t& total) {
+  for (const auto& pt : q.parts)
+    if (pt.second && !copy_part(e, d_out, q, pt.first, pt.second, buf, half, st, ev, werr, total)) return false;
+  return true;
+}
+bool copy_part(klf_engine* e, const uint8_t* d_out, const WPiece& q, uint64_t dlo, uint64_t n, uint8_t* buf,
+               uint64_t half, hipStream_t st, hipEvent_t ev[2], WErr& werr, uint64_t& total) {
   auto fail = [&](int err, const std::string& what) {
     int exp = -1;
     if (werr.id.compare_exchange_strong(exp, (int)q.id)) { werr.err = err; werr.what = what; }
     return false;
   };
-  const uint64_t n = q.hi - q.lo, nk = (n + half - 1) / half;
+  const uint64_t nk = (n + half - 1) / half;
   auto issue = [&](uint64_t k) {
     const uint64_t o = k * half, m = std::min(half, n - o);
-    return hipMemcpyAsync(buf + (k & 1) * half, d_out + q.lo + o, m, hipMemcpyDeviceToHost, st) == hipSuccess &&
+    return hipMemcpyAsync(buf + (k & 1) * half, d_out + dlo + o, m, hipMemcpyDeviceToHost, st) == hipSuccess &&
            hipEventRecord(ev[k & 1], st) == hipSuccess;
   };
   if (!issue(0)) return fail(0, "D2H");
@@ -1599,7 +1714,13 @@ extern "C" int klf_result_write(klf_result* r, const int* fds, uint32_t n_fds, u
   for (uint32_t i = 0; i < n_fds; ++i) {
     const int64_t s = r->seg_of[i];
     if (fds[i] < 0 || s < 0 || r->so[s].out_hi == r->so[s].out_lo) continue;
-    pcs.push_back({r->so[s].out_lo, r->so[s].out_hi, fds[i], i});
+    WPiece q{r->so[s].out_lo, r->so[s].out_hi, fds[i], i, {}};
+    if (r->fused) {
+      for (uint32_t k = r->fx_first[s]; k < r->fx_first[s + 1]; ++k) q.parts.emplace_back(r->fx[2 * (size_t)k], r->fx[2 * (size_t)k + 1]);
+    } else {
+      q.parts.emplace_back(q.lo, q.hi - q.lo);
+    }
+    pcs.push_back(std::move(q));
   }
   if (pcs.empty()) return KLF_OK;
   std::sort(pcs.begin(), pcs.end(), [](const WPiece& a, const WPiece& b) { return a.lo < b.lo; });
@@ -1778,10 +1899,27 @@ extern "C" int klf_result_last_unparsed(klf_result* r, uint32_t id, uint64_t* ra
 }
 
 extern "C" int klf_result_device_out(klf_result* r, uint32_t id, const uint8_t** d_out, uint64_t* off, uint64_t* len) {
+  if (r && r->fused && !r->have_dev && check_result(r, id) == KLF_OK) {  // one contiguous copy, on demand
+    klf_engine* e = r->e;
+    HIPCHK(e, hipSetDevice(e->device), "hipSetDevice");
+    HIPCHK(e, e->d_out2.ensure(r->total_out + 64), "alloc contiguous output");
+    const uint8_t* d = e->d_out.as<uint8_t>();
+    for (size_t sg = 0; sg < r->so.size(); ++sg) {
+      uint64_t o = r->so[sg].out_lo;
+      for (uint32_t k = r->fx_first[sg]; k < r->fx_first[sg + 1]; ++k) {
+        const uint64_t n = r->fx[2 * (size_t)k + 1];
+        if (n) HIPCHK(e, hipMemcpyAsync(e->d_out2.as<uint8_t>() + o, d + r->fx[2 * (size_t)k], n, hipMemcpyDeviceToDevice,
+                                        e->stream), "D2D contiguous output");
+        o += n;
+      }
+    }
+    HIPCHK(e, hipStreamSynchronize(e->stream), "sync");
+    r->have_dev = true;
+  }
   int rc = check_result(r, id);
   if (rc) return rc;
   const int64_t s = r->seg_of[id];
-  if (d_out) *d_out = r->e->d_out.as<uint8_t>();
+  if (d_out) *d_out = r->fused ? r->e->d_out2.as<uint8_t>() : r->e->d_out.as<uint8_t>();
   if (off) *off = s >= 0 ? r->so[s].out_lo : 0;
   if (len) *len = s >= 0 ? r->so[s].out_hi - r->so[s].out_lo : 0;
   return KLF_OK;
@@ -1796,6 +1934,7 @@ extern "C" int klf_result_timing(const klf_result* r, double* ms, uint32_t cap, 
 }
 
 extern "C" int klf_result_index_mode(const klf_result* r) { return r ? r->index_mode : KLF_EINVAL; }
+extern "C" int klf_result_compaction(const klf_result* r) { return r ? r->compaction : KLF_EINVAL; }
 
 extern "C" int klf_result_totals(const klf_result* r, klf_counts* t) {
   if (!r || !t) return KLF_EINVAL;

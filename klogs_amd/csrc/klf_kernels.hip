@@ -448,16 +448,34 @@ constexpr int kScanPlain = 0, kScanLit = 1, kScanGen = 2;
 // behind the in-flight prefetch by vmcnt and stall every tile on the next tile's bytes.
 // General sets: QS sampling stride, QK bits per gram, QQ gram bytes (3 or 4), QA (stride 8
 // only) the short needles' anchor test (DevPatterns::qf_anc_*).
-template <int MODE, int QS, int QK, int QQ = 4, bool QA = false>
+__device__ __forceinline__ void copy_tile_runs(const uint8_t* s_buf, uint32_t* s_run, uint16_t* s_map, uint32_t nr,
+                                               uint32_t kept, uint64_t obase, uint8_t* out, int lane);
+
+// FUSE (plain scan only; RunArgs::fuse): the one-pass compaction of runs without patterns and
+// with --tail -1.  Each wave owns a contiguous range of fuse_range tiles (a multiple of
+// kScanGroup) and compacts their kept bytes in place: the range's output starts where its
+// input starts (output <= input), so no offset depends on another wave.  A range's output is
+// one extent per stream it touches (fuse_ext[fuse_ext0[range] + k] = {start, length});
+// the bytes before the range's first line start belong to a line that started in an earlier
+// range: the wave leaves that many bytes free in front of its output and k_fcarry fills them
+// from the state the earlier ranges left (fuse_rinfo) once every range has been scanned.
+// A dense tile or a deferred line voids the pass (counters[kCtrFuseBad]: the host reruns
+// the two-pass compaction).
+template <int MODE, int QS, int QK, int QQ = 4, bool QA = false, bool FUSE = false>
 __global__ __launch_bounds__(kThreads, MODE == kScanGen ? 3 : KLF_SCAN_OCC) void k_scan(RunArgs a, const uint32_t* __restrict__ tseg,
                                                                const SegDesc* __restrict__ segs) {
+  static_assert(!FUSE || MODE == kScanPlain, "the fused compaction runs in the plain scan");
   constexpr bool LIT = MODE == kScanLit;
   constexpr bool GEN = MODE == kScanGen;
   constexpr bool ANC = GEN && QA;
   static_assert(QQ == 3 || QQ == 4, "3- or 4-byte grams");
   constexpr int kWaves = kThreads / 64;
   constexpr int kRows = kTile / 1024;  // 1 KiB rows: 16 B per lane per row
-  __shared__ __attribute__((aligned(16))) uint8_t s_tile_all[kWaves][kTile + kHalo];
+  // (FUSE: 16 B of front pad, which copy_tile_runs' unaligned windows read)
+  constexpr int kPad = FUSE ? 16 : 0;
+  __shared__ __attribute__((aligned(16))) uint8_t s_tile_all[kWaves][kPad + kTile + kHalo];
+  __shared__ __attribute__((aligned(16))) uint32_t s_frun_all[FUSE ? kWaves : 1][FUSE ? kTcRuns : 1];
+  __shared__ __attribute__((aligned(16))) uint16_t s_fmap_all[FUSE ? kWaves : 1][FUSE ? kTcChunks : 8];
   __shared__ __attribute__((aligned(16))) uint32_t s_list_all[kWaves][kSlotStride];
   __shared__ __attribute__((aligned(16))) uint32_t s_lit[kMaxFusedLiteral / 4 + 1];  // literal, zero padded
   __shared__ uint32_t s_month[16];
@@ -468,7 +486,7 @@ __global__ __launch_bounds__(kThreads, MODE == kScanGen ? 3 : KLF_SCAN_OCC) void
   // wv is wave-uniform; readfirstlane tells the compiler so (tile indices stay in SGPRs and
   // the descriptor reads stay scalar loads)
   const int t = threadIdx.x, lane = t & 63, wv = __builtin_amdgcn_readfirstlane(t >> 6);
-  uint8_t* s_tile = s_tile_all[wv];
+  uint8_t* s_tile = s_tile_all[wv] + kPad;
   uint32_t* s_list = s_list_all[wv];
   uint32_t* err_flag = a.counters + 2;
   for (uint32_t i = t; i < kMaxFusedLiteral / 4 + 1; i += kThreads)
@@ -502,10 +520,14 @@ __global__ __launch_bounds__(kThreads, MODE == kScanGen ? 3 : KLF_SCAN_OCC) void
   uint4 pfh = make_uint4(0, 0, 0, 0);
   // A wave takes groups of kScanGroup consecutive tiles (group g, g + nwaves, ...): their
   // TileStats go out together as one whole-line store into the compact tstat array.
+  // (FUSE: the wave's own range of consecutive tiles instead)
   auto next_tile = [&](uint32_t x) -> uint32_t {
-    return (x % kScanGroup) == kScanGroup - 1 ? x + 1 + kScanGroup * (nwaves - 1) : x + 1;
+    return (FUSE || (x % kScanGroup) != kScanGroup - 1) ? x + 1 : x + 1 + kScanGroup * (nwaves - 1);
   };
-  uint32_t tile = (blockIdx.x * kWaves + wv) * kScanGroup;
+  const uint32_t gw = blockIdx.x * kWaves + wv;
+  uint32_t tile = FUSE ? gw * a.fuse_range : gw * kScanGroup;
+  const uint32_t tile_end = FUSE ? (tile + a.fuse_range < a.ntiles ? tile + a.fuse_range : a.ntiles) : a.ntiles;
+  const uint32_t range_t0 = tile;
   uint4 stv = make_uint4(0, 0, 0, 0);  // GEN: lane k holds the group's TileStat k
   // The segment of the prefetched tile travels with it (scalar registers): a stride of
   // nwaves tiles stays inside one stream for all but the last tiles of a long stream, so
@@ -530,7 +552,32 @@ __global__ __launch_bounds__(kThreads, MODE == kScanGen ? 3 : KLF_SCAN_OCC) void
     __builtin_amdgcn_raw_buffer_store_b32(0u, none, 0x7FFF0000u, 0, 0);
   }
   bool any_defer = false;
-  for (; tile < a.ntiles; tile = next_tile(tile)) {
+  // FUSE state of the wave's range (wave-uniform): whether the line open at the current tile
+  // start is decided (a line started in this range's part of the stream, or the part began
+  // at the stream's start), that line's kept bit and content start - the tile start (f_sat),
+  // the output position, the current extent
+  bool fz_known = false, fz_sel = false, fz_res_set = false;
+  int32_t fz_crel = -1;
+  uint64_t fz_obase = 0, fz_estart = 0, fz_res = 0, fz_part = 0, fz_rbase = 0;
+  uint32_t fz_ext = 0;
+  if (FUSE && tile < tile_end) {
+    fz_rbase = pf_sd.base + (uint64_t)(tile - pf_sd.tile0) * kTile;
+    fz_ext = a.fuse_ext0[gw];
+  }
+  // closes the current extent (a range part that saw no line start: all of it is left to
+  // k_fcarry, the extent empty at its end)
+  auto fz_close = [&]() __attribute__((always_inline)) {
+    if (!fz_res_set) {
+      fz_res = fz_part;
+      fz_res_set = true;
+      fz_estart = fz_obase = fz_rbase + fz_part;
+    }
+    if (lane == 0) {
+      a.fuse_ext[2 * (size_t)fz_ext] = fz_estart;
+      a.fuse_ext[2 * (size_t)fz_ext + 1] = fz_obase - fz_estart;
+    }
+  };
+  for (; tile < tile_end; tile = next_tile(tile)) {
     const uint32_t s = pf_s;
     const SegDesc sd = pf_sd;
     const int64_t rel_lo = (int64_t)(tile - sd.tile0) * kTile;
@@ -546,7 +593,7 @@ __global__ __launch_bounds__(kThreads, MODE == kScanGen ? 3 : KLF_SCAN_OCC) void
       KLF_ROWS(KLF_STORE)
       if (lane < kHalo / 16) l[kTile / 16 + lane] = pfh;
       const uint32_t nx = next_tile(tile);
-      if (nx < a.ntiles) {
+      if (nx < tile_end) {
         if (nx - sd.tile0 >= sd.ntiles) {
           pf_s = tseg[nx];
           pf_sd = segs[pf_s];
@@ -679,7 +726,16 @@ __global__ __launch_bounds__(kThreads, MODE == kScanGen ? 3 : KLF_SCAN_OCC) void
           } else if (rel_lo + (int64_t)off + 31 <= seg_len) {
             fast = parse_fast(s_tile, off, s_month, a.since_day, a.since_sod, a.since_nsec, so);
           }
-          {
+          if (FUSE && !fast) {  // the one-pass compaction decides every line here: Go time.Parse
+            TsResult tr;
+            uint32_t plen = 0;
+            const bool ok = parse_line_prefix(GlobalBytes{segp, rel_lo + (int64_t)off, seg_len}, tr, plen);
+            const bool so2 = ok && !time_before(tr.sec, tr.nsec, a.since_sec, a.since_nsec);
+            list[j] = off | ((uint32_t)make_meta(ok, so2, ok ? plen : 0u) << 16);
+            if (ok && plen >= kPlenEscape) atomicOr(&a.counters[kCtrFuseBad], 1u);  // (a prefix longer than the meta holds)
+            n_parsed += ok ? 1u : 0u;
+            n_since += so2 ? 1u : 0u;
+          } else {
             list[j] = fast ? (off | ((uint32_t)make_meta(true, so, 31) << 16)) : (off | kSlotDefer);
             n_parsed += fast ? 1u : 0u;
             n_since += (fast && so) ? 1u : 0u;
@@ -692,7 +748,80 @@ __global__ __launch_bounds__(kThreads, MODE == kScanGen ? 3 : KLF_SCAN_OCC) void
       // run, or past the record, dropped) and the plan in one more: a fixed store count per
       // tile (see the record stores below).  Tiles with more lines leave their runs to
       // k_tcopy (kRunsRecompute).
-      if constexpr (MODE == kScanPlain) {
+      if constexpr (MODE == kScanPlain && FUSE) {
+        // ---- one-pass compaction: this tile's kept runs (the carried-in line's, then the
+        // lines starting here), copied to the range's output at once (a dense tile voids
+        // the pass) ----
+        if (!dense) {
+        wave_lds_sync();
+        if (__any(n_defer != 0) && lane == 0) a.counters[kCtrFuseBad] = 1u;  // decided later: rerun
+        const uint64_t tin = sd.base + (uint64_t)rel_lo;  // the tile's input = output position
+        if (first) {  // a stream starts here: nothing carried in
+          if (tile != range_t0) {
+            fz_close();
+            ++fz_ext;
+          } else {
+            fz_res_set = true;
+          }
+          fz_known = true;
+          fz_sel = false;
+          fz_crel = -1;
+          fz_obase = fz_estart = tin;
+          fz_part = 0;
+        }
+        const uint32_t span = nlines ? (list[0] & kSlotOff) : (uint32_t)tile_len;
+        uint32_t clen = 0, csrc = 0;
+        if (fz_known) {
+          clen = f_carried(span, fz_sel, fz_crel);
+          csrc = fz_crel > 0 ? (uint32_t)fz_crel : 0u;
+        } else if (nlines) {  // the range's first line start: the bytes before it are k_fcarry's
+          fz_res = fz_part + span;
+          fz_res_set = true;
+          fz_obase = fz_estart = tin + span;
+        }
+        uint32_t* s_frun = s_frun_all[wv];
+        uint32_t nr = 0, dacc = 0, lsel = 0;
+        int32_t lcrel = -1;
+        for (uint32_t b0 = 0; b0 < nlines; b0 += 64) {
+          const uint32_t j = b0 + (uint32_t)lane;
+          uint32_t src = 0, len = 0;
+          if (j < nlines) {
+            const uint32_t v = list[j], off = v & kSlotOff, mt = v >> 16;
+            const bool sel = !(v & kSlotDefer) && (mt & Meta::kParsed) && (mt & Meta::kSince);
+            const uint32_t c = off + (mt >> 2);
+            const uint32_t e = j + 1 < nlines ? (list[j + 1] & kSlotOff) : (uint32_t)tile_len;
+            if (sel && e > c) { src = c; len = e - c; }
+            if (j + 1 == nlines) { lsel = sel ? 1u : 0u; lcrel = f_sat((int32_t)c - tile_len); }
+          }
+          const uint32_t incl = wave_incl_scan_add(len, lane);
+          const uint64_t bm = __ballot(len != 0);
+          const uint32_t idx = nr + (uint32_t)__popcll(bm & ((1ull << lane) - 1ull));
+          if (len) s_frun[1 + idx] = src | ((clen + dacc + incl - len) << 16);
+          nr += (uint32_t)__popcll(bm);
+          dacc += (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+        }
+        if (clen && lane == 0) s_frun[0] = csrc;  // (output offset 0)
+        const uint32_t kept = clen + dacc;
+        if (kept) {
+          if (fz_obase + kept + 16 > a.out_cap) {
+            if (lane == 0) a.counters[kCtrFuseBad] = 1u;
+          } else {
+            copy_tile_runs(s_tile, clen ? s_frun : s_frun + 1, s_fmap_all[wv], nr + (clen ? 1u : 0u), kept, fz_obase,
+                           a.out, lane);
+          }
+          fz_obase += kept;
+        }
+        if (nlines) {
+          const uint32_t lastl = (nlines - 1u) & 63u;
+          fz_sel = __builtin_amdgcn_readlane((int)lsel, (int)lastl) != 0;
+          fz_crel = __builtin_amdgcn_readlane(lcrel, (int)lastl);
+          fz_known = true;
+        } else if (fz_known) {
+          fz_crel = f_sat(fz_crel - tile_len);
+        }
+        fz_part += (uint64_t)tile_len;
+        }
+      } else if constexpr (MODE == kScanPlain) {
         if (a.plan_runs) {
           if (dense) __threadfence_block();
           wave_lds_sync();
@@ -830,6 +959,7 @@ __global__ __launch_bounds__(kThreads, MODE == kScanGen ? 3 : KLF_SCAN_OCC) void
     } else if (!dense) {
       work(s_list);
     } else if (pool_ok && !abl) {
+      if (FUSE && lane == 0) a.counters[kCtrFuseBad] = 1u;  // (a dense tile: the two-pass rerun)
       work(gslot);
     }
 
@@ -1099,6 +1229,16 @@ __global__ __launch_bounds__(kThreads, MODE == kScanGen ? 3 : KLF_SCAN_OCC) void
     asm volatile("" ::: "memory");  // the next stage overwrites the LDS region read above
   }
   if (any_defer && lane == 0 && !abl) a.counters[kCtrDefer] = 1u;
+  if (FUSE && range_t0 < tile_end) {  // the range's last extent and the state it leaves
+    fz_close();
+    if (lane == 0) {
+      uint64_t* ri = a.fuse_rinfo + 4 * (size_t)gw;
+      ri[0] = fz_res;
+      ri[1] = (fz_known ? 1u : 0u) | (fz_sel ? 2u : 0u);
+      ri[2] = (uint64_t)(int64_t)fz_crel;
+      ri[3] = fz_part;
+    }
+  }
   if (KLF_ABL != 0 && lane == 0) atomicAdd(&g_abl_waves, 1u);
 #undef ABL
 }
@@ -3580,6 +3720,50 @@ __global__ __launch_bounds__(64 * kTcWaves) void k_tcopy(RunArgs a, const uint4*
 #undef KLF_TC_STORE
 }
 
+// One-pass compaction, second kernel (one wave per range): the bytes in front of a range's
+// first line start belong to the line open at the range start, which started in an earlier
+// range.  Its state (kept?, content start) is the one the nearest earlier range with a line
+// start left (the ranges in between lie inside that line); the kept part of those bytes is
+// copied from the input to just in front of the range's output, whose first extent grows by
+// it.  (A carried part is at most one line: copied a byte per lane.)
+__global__ __launch_bounds__(256) void k_fcarry(RunArgs a) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t r = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= a.fuse_nranges || a.counters[kCtrFuseBad] || a.counters[2]) return;
+  const uint32_t t0 = r * a.fuse_range;
+  if (t0 >= a.ntiles) return;
+  const SegDesc sd = a.segs[a.tile_seg[t0]];
+  if (t0 == sd.tile0) return;  // a stream starts here: nothing carried in
+  const uint64_t* ri = a.fuse_rinfo;
+  const uint64_t res = ri[4 * (size_t)r];
+  if (res == 0) return;
+  int64_t back = 0;
+  bool sel = false;
+  int64_t crel = -1;
+  for (uint32_t k = r; k-- > 0;) {
+    const uint64_t fl = ri[4 * (size_t)k + 1];
+    if (fl & 1u) {
+      sel = (fl & 2u) != 0;
+      crel = (int64_t)ri[4 * (size_t)k + 2];
+      break;
+    }
+    back += (int64_t)ri[4 * (size_t)k + 3];  // (a whole range inside the line)
+  }
+  if (crel >= 0) crel -= back;  // relative to this range's start (f_sat: before it = -1)
+  const uint64_t lo = crel > 0 ? (uint64_t)crel : 0u;
+  const uint64_t clen = (sel && res > lo) ? res - lo : 0u;
+  if (clen == 0) return;
+  const uint64_t rbase = sd.base + (uint64_t)(t0 - sd.tile0) * kTile;
+  const uint8_t* src = a.bytes + rbase + lo;
+  uint8_t* dst = a.out + rbase + res - clen;
+  for (uint64_t i = (uint64_t)lane; i < clen; i += 64) dst[i] = src[i];
+  if (lane == 0) {
+    uint64_t* ex = a.fuse_ext + 2 * (size_t)a.fuse_ext0[r];
+    ex[0] -= clen;
+    ex[1] += clen;
+  }
+}
+
 // Data statistics for the prefilter's layout and window choice (one-off, first batch): the
 // 2-grams at even offsets of a sample of the batch and every byte, counted per block in LDS
 // (65,536 u16 pair counters, two per dword: a block's 1,024 dwords add at most 2,048 to one
@@ -3713,22 +3897,29 @@ static bool env_off(const char* name) {
 // the scan's timing events for the current launch_pipeline call (ev[7], ev[8]), else null
 thread_local hipEvent_t t_scan_ev[2] = {nullptr, nullptr};
 
-template <int MODE, int QS, int QK = 3, int QQ = 4, bool QA = false>
-hipError_t launch_scan(const RunArgs& a, hipStream_t st, int num_cus) {
+template <int MODE, int QS, int QK = 3, int QQ = 4, bool QA = false, bool FUSE = false>
+int scan_occupancy() {
   static int occ = 0;  // queried once per variant: the host query delays the launch
   if (occ == 0) {
-    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_scan<MODE, QS, QK, QQ, QA>, kThreads, 0);
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_scan<MODE, QS, QK, QQ, QA, FUSE>, kThreads, 0);
     occ = occ < 1 ? 1 : (occ > 8 ? 8 : occ);
     if (getenv("KLF_DIAG"))
-      fprintf(stderr, "[klf] k_scan<%d,%d,%d,%d,%d>: %d blocks per CU\n", MODE, QS, QK, QQ, (int)QA, occ);
+      fprintf(stderr, "[klf] k_scan<%d,%d,%d,%d,%d,%d>: %d blocks per CU\n", MODE, QS, QK, QQ, (int)QA, (int)FUSE, occ);
   }
+  return occ;
+}
+template <int MODE, int QS, int QK = 3, int QQ = 4, bool QA = false, bool FUSE = false>
+hipError_t launch_scan(const RunArgs& a, hipStream_t st, int num_cus) {
+  const int occ = scan_occupancy<MODE, QS, QK, QQ, QA, FUSE>();
   uint32_t grid = (uint32_t)(num_cus * occ);
   if (grid > a.ntiles) grid = a.ntiles;
+  if (FUSE) grid = (a.fuse_nranges + kThreads / 64 - 1) / (kThreads / 64);  // a wave per range
   if (t_scan_ev[0])  // the dispatch's own start / end timestamps (no event record beside it)
-    hipExtLaunchKernelGGL((k_scan<MODE, QS, QK, QQ, QA>), dim3(grid), dim3(kThreads), 0, st, t_scan_ev[0],
+    hipExtLaunchKernelGGL((k_scan<MODE, QS, QK, QQ, QA, FUSE>), dim3(grid), dim3(kThreads), 0, st, t_scan_ev[0],
                           t_scan_ev[1], 0, a, a.tile_seg, a.segs);
   else
-    hipLaunchKernelGGL((k_scan<MODE, QS, QK, QQ, QA>), dim3(grid), dim3(kThreads), 0, st, a, a.tile_seg, a.segs);
+    hipLaunchKernelGGL((k_scan<MODE, QS, QK, QQ, QA, FUSE>), dim3(grid), dim3(kThreads), 0, st, a, a.tile_seg,
+                       a.segs);
   return hipGetLastError();
 }
 template <int QS, int QQ>
@@ -3748,6 +3939,10 @@ hipError_t launch_gen(const RunArgs& a, hipStream_t st, int num_cus) {
 }
 
 static hipError_t launch_tail_stage(const RunArgs& a, hipStream_t st, hipEvent_t* ev, int num_cus, uint32_t& m);
+
+int fuse_waves(int num_cus) {
+  return num_cus * scan_occupancy<kScanPlain, 1, 3, 4, false, true>() * (kThreads / 64);
+}
 
 hipError_t launch_scatter(const RunArgs& a, hipStream_t st, int num_cus) {
 #ifndef KLF_SCATTER_GRID
@@ -3807,6 +4002,8 @@ hipError_t launch_pipeline(const RunArgs& a0, hipStream_t st, hipEvent_t* ev, in
       KLF_TRY((launch_gen<2>(a, st, num_cus)));
     else if (a.grep_mode == kGrepGeneral && a.pats.qf_on)
       KLF_TRY((launch_gen<1>(a, st, num_cus)));
+    else if (a.fuse)
+      KLF_TRY((launch_scan<kScanPlain, 1, 3, 4, false, true>(a, st, num_cus)));
     else
       KLF_TRY((launch_scan<kScanPlain, 1>(a, st, num_cus)));
     t_scan_ev[0] = t_scan_ev[1] = nullptr;  // (no event record behind it: each idles the GPU ~6 us)
@@ -3898,7 +4095,7 @@ static hipError_t launch_tail_stage(const RunArgs& a, hipStream_t st, hipEvent_t
   }
   hipLaunchKernelGGL(k_tailw, dim3(a.nsegs), dim3(256), 0, st, a);
   KLF_TRY(hipGetLastError());
-  if (a.lazy_index) KLF_TRY(launch_scatter(a, st, num_cus));  // (exits at once on the dense path)
+  if (a.lazy_index && !a.fuse) KLF_TRY(launch_scatter(a, st, num_cus));  // (exits at once on the dense path)
   if (a.win_index) {  // the tail windows' lines
     RunArgs w = a;
     w.scatter_mode = 2;
@@ -3907,6 +4104,11 @@ static hipError_t launch_tail_stage(const RunArgs& a, hipStream_t st, hipEvent_t
   if (ev && a.stage_times) {  // ~5 us of idle GPU each
     KLF_TRY(hipEventRecord(ev[4], st));
     m |= 1u << 4;
+  }
+  if (a.fuse) {  // the scan compacted every range: only the bytes carried into them are left
+    hipLaunchKernelGGL(k_fcarry, dim3((a.fuse_nranges + 3) / 4), dim3(256), 0, st, a);
+    KLF_TRY(hipGetLastError());
+    return hipSuccess;
   }
   {
     const uint32_t gt = (a.ntiles + 4 * kTkBatch - 1) / (4 * kTkBatch);

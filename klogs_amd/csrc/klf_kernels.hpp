@@ -60,6 +60,7 @@ constexpr uint32_t kCtrChunkLog2 = 16;               // counters[16]: log2 of th
 constexpr uint32_t kCtrTailDone = 18;                // counters[18]: k_tailw blocks done
 constexpr uint32_t kCtrVerified = 10;                // counters[10]: hits k_verify walked (diagnostics)
 constexpr uint32_t kCtrDense = 14;                   // counters[14]: dense compaction (k_tkeep / k_tcopy)
+constexpr uint32_t kCtrFuseBad = 24;                 // counters[24]: the one-pass compaction was voided (rerun)
 constexpr uint32_t kCtrOutShort = 22;                // counters[22]: the output did not fit out_cap
 constexpr uint32_t kCtrPairsOver = 15;               // counters[15]: failed (line, pattern) pair inserts (set full)
 constexpr uint32_t kQfRegex = 1u << 24;              // entry flags: regex factor (else literal)
@@ -316,6 +317,18 @@ struct RunArgs {
   uint32_t* pcount;
   uint64_t* pairs;
   uint32_t pairs_log2;
+  // one-pass compaction (no patterns, --tail -1; k_scan<plain, FUSE> + k_fcarry): each wave
+  // compacts its own range of fuse_range consecutive tiles in place; fuse_ext0[range] = the
+  // range's first extent, fuse_ext[2 e .. 2 e + 1] = {output start, length} of extent e (one
+  // per stream the range touches), fuse_rinfo[4 range ..] = {bytes before the range's first
+  // line start, known | sel << 1 at its end, the open line's content start - the range end,
+  // bytes of its last stream part}
+  uint32_t fuse;
+  uint32_t fuse_range;
+  uint32_t fuse_nranges;
+  const uint32_t* fuse_ext0;
+  uint64_t* fuse_ext;
+  uint64_t* fuse_rinfo;
 };
 
 // Enqueues the whole pipeline on `stream`; `ev` (6 events) brackets the stages for
@@ -350,6 +363,9 @@ hipError_t launch_assemble(const AsmPiece* pieces, uint32_t n, uint8_t* batch, h
 // Global index of the last line in [lo, hi) whose meta has no parsed bit, +1 (0 = none),
 // atomically max-ed into *res (zeroed here).  Needs the latest run's meta (a.meta).
 hipError_t launch_lastbad(const RunArgs& a, uint64_t lo, uint64_t hi, uint64_t* res, hipStream_t stream);
+// waves of a full-occupancy launch of the one-pass compaction scan (RunArgs::fuse): the host
+// cuts the batch into that many tile ranges
+int fuse_waves(int num_cus);
 // Diagnostic builds (-DKLF_TIMELINE=1): per-tile scan timeline; hipErrorNotSupported otherwise.
 hipError_t dump_timeline(void* host, size_t bytes);
 hipError_t clear_timeline();

@@ -91,6 +91,7 @@ SIGNATURES = {
     "klf_result_timing": (C.c_int, [C.c_void_p, C.POINTER(C.c_double), C.c_uint32, C.POINTER(C.c_uint32)]),
     "klf_result_totals": (C.c_int, [C.c_void_p, C.POINTER(_Counts)]),
     "klf_result_index_mode": (C.c_int, [C.c_void_p]),
+    "klf_result_compaction": (C.c_int, [C.c_void_p]),
     "klf_result_free": (None, [C.c_void_p]),
     "klf_follow_open": (C.c_int, [C.c_void_p, C.POINTER(_Filter), C.POINTER(C.c_void_p)]),
     "klf_follow_feed": (C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p, C.c_size_t]),
@@ -172,6 +173,7 @@ KLF_FILTER_STAGE_TIMES = 1
 KLF_FILTER_PATTERN_COUNTS = 2
 KLF_FILTER_FULL_INDEX = 4
 INDEX_MODES = {0: "full", 1: "windowed", 2: "on_demand"}  # klf_result_index_mode
+COMPACTIONS = {0: "gather", 1: "tiles", 2: "one_pass"}  # klf_result_compaction
 
 
 def _filter(since: Optional[Tuple[int, int]], tail: int, stage_times: bool = False,
@@ -355,6 +357,14 @@ class Result:
         if m < 0:
             _check(m)
         return INDEX_MODES[m]
+
+    def compaction(self) -> str:
+        """klf_result_compaction: "gather" (the selected lines gathered), "tiles" (tile copy
+        after the scan) or "one_pass" (compacted in the scan, range by range)."""
+        m = _lib.klf_result_compaction(self._p)
+        if m < 0:
+            _check(m)
+        return COMPACTIONS[m]
 
     def totals(self) -> dict:
         c = _Counts()

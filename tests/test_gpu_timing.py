@@ -52,12 +52,18 @@ def test_events_off_then_stage_times_same_engine(gpu, monkeypatch, grep):
             r.free()
 
 
-def test_dense_copy_kernel_timed(gpu):
-    """A run without patterns and --tail -1 takes the dense copy (k_tcopy): timing [7] is
-    its dispatch alone, inside the compaction stage [3]; on a --tail run (the sparse gather)
-    k_tcopy exits at once."""
+def test_dense_copy_kernel_timed(gpu, monkeypatch):
+    """With the one-pass compaction off, a run without patterns and --tail -1 takes the
+    dense copy (k_tcopy): timing [7] is its dispatch alone, inside the compaction stage [3];
+    on a --tail run (the sparse gather) k_tcopy exits at once.  The one-pass run has no
+    k_tcopy."""
     streams = [synth.generate(synth.TEXT, 22, i, 16_000_000) for i in range(4)]
     dev, seg_base, lens = _device_batch(streams)
+    with E.Engine(0, hip_stream=torch.cuda.current_stream().cuda_stream) as eng:
+        r = eng.run_device(dev.data_ptr(), seg_base, lens, stage_times=True)
+        assert r.compaction() == "one_pass" and r.timing()[7] == 0.0 and r.timing()[6] > 0.0, r.timing()
+        r.free()
+    monkeypatch.setenv("KLF_FUSE", "0")
     with E.Engine(0, hip_stream=torch.cuda.current_stream().cuda_stream) as eng:
         r = eng.run_device(dev.data_ptr(), seg_base, lens, stage_times=True)
         tm = r.timing()
