@@ -1036,6 +1036,7 @@ __global__ __launch_bounds__(kThreads, MODE == kScanGen ? 3 : KLF_SCAN_OCC) void
       uint32_t chit = 0;
       const uint32_t rot = ((uint32_t)lane >> 1) & 7u;
       uint32_t hq0 = 0, hq1 = 0, hq2 = 0, hq3 = 0;
+      uint32_t xh = 0xFFFFFFFFu;  // a hit at this tile offset (the compacted stage 2), beside hq
       if (TWO) {
         // stage 1: the exact set of the probed grams' low two bytes (pair words [0, 2048)):
         // sv bit i = the sample at my0 + 4i passes (each chunk's four dwords, two chunks per
@@ -1053,7 +1054,8 @@ __global__ __launch_bounds__(kThreads, MODE == kScanGen ? 3 : KLF_SCAN_OCC) void
           uint32_t w[8];
 #pragma unroll
           for (int k = 0; k < 8; ++k)
-            w[k] = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(s_qf) + (bfe_u32(g[k], 5, 11) << 2));
+            w[k] = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(s_qf) +
+                                                      ((KLF_PAIR_SWZ ? bfe_u32(g[k], 5, 11) ^ (g[k] & 31u) : bfe_u32(g[k], 5, 11)) << 2));
 #pragma unroll
           for (int k = 0; k < 8; ++k)
             sv |= __builtin_amdgcn_ubfe(w[k], g[k], 1u) << (4 * v + k);  // bit g mod 32 (v_bfe_u32 reads offset[4:0])
@@ -1061,16 +1063,41 @@ __global__ __launch_bounds__(kThreads, MODE == kScanGen ? 3 : KLF_SCAN_OCC) void
         sv = __builtin_amdgcn_alignbit(sv, sv, 32u - 4u * rot);  // rotate left by 4 rot (shift mod 32): chunk c at bits 4c..
         // samples at or past the tile's end (4i >= nvalid) do not count
         sv &= nvalid >= kLaneBytes ? ~0u : ((1u << ((uint32_t)(nvalid + 3) >> 2)) - 1u);
-        // stage 2: the survivors' 3-bit probe into the Bloom half; a hit's byte position
-        // 4i -> its 32-B group q = i / 8, bit 4i mod 32
-        for (uint32_t m = sv; m; m &= m - 1u) {
-          const uint32_t i = (uint32_t)__builtin_ctz(m);
-          if (hbits(s32[(my0 >> 2) + i]) & 1u) {
-            const uint32_t q = i >> 3, b = 1u << ((4u * i) & 31u);
-            hq0 |= q == 0 ? b : 0u;
-            hq1 |= q == 1 ? b : 0u;
-            hq2 |= q == 2 ? b : 0u;
-            hq3 |= q == 3 ? b : 0u;
+        // stage 2: the survivors' 3-bit probe into the Bloom half.  The ~1.4 % survivors
+        // (~30 per tile) are compacted over the wave first, so that one round of 64 lanes
+        // probes them all (each lane's own walk took as many dependent LDS round trips as
+        // the busiest lane had survivors); a hit's tile offset goes to xh.  Past 64
+        // survivors each lane walks its own: a hit's byte position 4i -> its 32-B group
+        // q = i / 8, bit 4i mod 32
+        if (ABL(16)) sv = 0u;  // (KLF_ABL 16: no stage 2)
+        const uint32_t scnt = (uint32_t)__popc(sv);
+        const uint32_t sincl = wave_incl_scan_add(scnt, lane);
+        const uint32_t stot = (uint32_t)__builtin_amdgcn_readlane((int)sincl, 63);
+        // (the list: the last 32 words of the wave's slot list, free unless more than
+        // kSlotStride - 32 lines start in the tile; a 512-B LDS array of its own cost a third
+        // of the workgroups: 7.7 -> 10.4 ms)
+        if (stot <= 64u && nlines <= (uint32_t)kSlotStride - 32u) {
+          if (stot) {
+            uint16_t* sl = reinterpret_cast<uint16_t*>(s_list + kSlotStride - 32);
+            uint32_t k = sincl - scnt;
+            for (uint32_t m = sv; m; m &= m - 1u) sl[k++] = (uint16_t)(((uint32_t)lane << 5) | (uint32_t)__builtin_ctz(m));
+            wave_lds_sync();
+            if ((uint32_t)lane < stot) {
+              const uint32_t e = sl[lane];  // sample e & 31 of lane e >> 5: tile offset 4 e
+              if (hbits(s32[e]) & 1u) xh = 4u * e;
+            }
+            wave_lds_sync();  // (the next tile rewrites the list)
+          }
+        } else {
+          for (uint32_t m = sv; m; m &= m - 1u) {
+            const uint32_t i = (uint32_t)__builtin_ctz(m);
+            if (hbits(s32[(my0 >> 2) + i]) & 1u) {
+              const uint32_t q = i >> 3, b = 1u << ((4u * i) & 31u);
+              hq0 |= q == 0 ? b : 0u;
+              hq1 |= q == 1 ? b : 0u;
+              hq2 |= q == 2 ? b : 0u;
+              hq3 |= q == 3 ? b : 0u;
+            }
           }
         }
       } else if (QS == 4 || QS == 6) {
@@ -1152,10 +1179,11 @@ __global__ __launch_bounds__(kThreads, MODE == kScanGen ? 3 : KLF_SCAN_OCC) void
         }
       }
       if (ABL(8)) {  // timing build: probes only
-        asm volatile("" ::"v"(hq0 | hq1 | hq2 | hq3));
+        asm volatile("" ::"v"(hq0 | hq1 | hq2 | hq3 | xh));
         hq0 = hq1 = hq2 = hq3 = 0;
+        xh = 0xFFFFFFFFu;
       }
-      const uint32_t nh = (uint32_t)(__popc(hq0) + __popc(hq1) + __popc(hq2) + __popc(hq3));
+      const uint32_t nh = (uint32_t)(__popc(hq0) + __popc(hq1) + __popc(hq2) + __popc(hq3)) + (xh != 0xFFFFFFFFu ? 1u : 0u);
       if (__any(nh != 0) && !abl) {
         // tile-owned slots (u16 tile offsets, no atomics); only a tile with more than
         // kHitSlots hits spills the rest to the global list
@@ -1168,6 +1196,16 @@ __global__ __launch_bounds__(kThreads, MODE == kScanGen ? 3 : KLF_SCAN_OCC) void
         }
         uint16_t* hs = a.hslots + (size_t)tile * kHitSlots;
         uint32_t k = ih - nh;
+        if (xh != 0xFFFFFFFFu) {
+          if (k < kHitSlots) {
+            hs[k] = (uint16_t)xh;
+          } else if ((uint64_t)ob + (k - kHitSlots) < a.qhits_cap) {
+            a.qhits[ob + (k - kHitSlots)] = sd.base + (uint64_t)rel_lo + xh;
+          } else {
+            atomicOr(&a.counters[kCtrHitsOver], 1u);
+          }
+          ++k;
+        }
         const uint32_t hq[4] = {hq0, hq1, hq2, hq3};
 #pragma unroll
         for (int q = 0; q < 4; ++q)

@@ -90,6 +90,18 @@ constexpr uint32_t kRxPreNone = 0xFFFFFFFFu;         // rx_pre: no bound (= klf_
 // 3-bit probe, into a Bloom filter of the remaining kQfPairWords words (11-bit buckets).
 constexpr uint32_t kQfTwoLevel = 5;
 constexpr uint32_t kQfPairWords = 2048;
+// The pair set's word of pair p (bit p & 31): p >> 5.  Its bank bits are the first byte's
+// top three bits and the second byte's low two: on ASCII text about a dozen of the 32 banks,
+// ~2x the LDS-active cycles in bank conflicts (C4, pmc_c4).  KLF_PAIR_SWZ=1 folds p's low
+// five bits into them (all 32 banks) for one more VALU per sample: C4 k_scan 7.60 -> 7.97 ms
+// (same box, two rounds, gpurun_out/r5k) -- the pair stage is bound by its instructions, not
+// by the conflicts.
+#ifndef KLF_PAIR_SWZ
+#define KLF_PAIR_SWZ 0
+#endif
+__host__ __device__ inline uint32_t qf_pair_word(uint32_t p) {
+  return KLF_PAIR_SWZ ? (((p >> 5) ^ (p & 31u)) & (kQfPairWords - 1u)) : ((p >> 5) & (kQfPairWords - 1u));
+}
 __host__ __device__ inline bool qf_k3(uint32_t k) { return k == 3 || k == kQfTwoLevel; }
 __host__ __device__ inline uint32_t qf_f(uint32_t g, uint32_t k) {
   const uint32_t g24 = g & 0xFFFFFFu;
@@ -125,7 +137,7 @@ __host__ __device__ inline uint32_t qf_bits(uint32_t g, uint32_t h, uint32_t k) 
 // The whole probe of a (folded, masked) gram against the bitmap (host emulation; the scan
 // computes the same from its LDS copy)
 __host__ __device__ inline bool qf_pass(const uint32_t* bm, uint32_t gq, uint32_t w24, uint32_t k) {
-  if (k == kQfTwoLevel && !((bm[(gq & 0xFFFFu) >> 5] >> (gq & 31u)) & 1u)) return false;
+  if (k == kQfTwoLevel && !((bm[qf_pair_word(gq & 0xFFFFu)] >> (gq & 31u)) & 1u)) return false;
   const uint32_t h = qf_hash(gq, w24, k), bits = qf_bits(gq, h, k);
   return (bm[qf_bloom_word(gq, w24, k)] & bits) == bits;
 }

@@ -1592,7 +1592,7 @@ void place_tables(CompiledSet& out, const DataStats* st) {
         const uint32_t g16 = g & 0xFFFFu, fv = out.qf_fold & 0xFFFFu & g16;
         for (uint32_t x = fv;; x = (x - 1u) & fv) {  // subsets of the folded bits
           const uint32_t pr = g16 & ~x;
-          out.qf_bitmap[pr >> 5] |= 1u << (pr & 31u);
+          out.qf_bitmap[qf_pair_word(pr)] |= 1u << (pr & 31u);
           if (!x) break;
         }
       }
@@ -1684,7 +1684,7 @@ PrefilterHits prefilter_hits(const CompiledSet& cs, const uint8_t* s, size_t n) 
       const uint32_t gq = (g | cs.qf_fold) & cs.qf_mask;
       hit = qf_pass(cs.qf_bitmap.data(), gq, w24, cs.qf_k);
       r.bitmap_hits += hit;
-      if (cs.qf_k == kQfTwoLevel) r.pair_pass += (cs.qf_bitmap[(gq & 0xFFFFu) >> 5] >> (gq & 31u)) & 1u;
+      if (cs.qf_k == kQfTwoLevel) r.pair_pass += (cs.qf_bitmap[qf_pair_word(gq & 0xFFFFu)] >> (gq & 31u)) & 1u;
     }
     if (!hit && cs.qf_anc_on && ((uint32_t)s[p] | (cs.qf_anc_fold & 0xFFu)) == cs.qf_anc_byte) {
       for (size_t j = 0; j + 1 < cs.qf_anc_pre.size() && !hit; j += 2)
