@@ -67,7 +67,11 @@ struct DevBuf {
 // An engine's first run maps its workspace buffers as one allocation (each hipMalloc costs
 // tens of us of host time, ~20 of them add up in a one-shot run): buffers not yet mapped
 // get 256-B aligned pieces of one block; later growth maps a buffer of its own.
-static hipError_t ensure_all(DevBuf& block, const std::vector<std::pair<DevBuf*, size_t>>& req) {
+// Maps the missing buffers of `req` into one block (an engine's first run: one allocation);
+// a buffer that later outgrows its slice gets its own allocation, and the block is freed
+// once no buffer borrows from it any more (`users`: the buffers mapped into it).
+static hipError_t ensure_all(DevBuf& block, std::vector<DevBuf*>& users,
+                             const std::vector<std::pair<DevBuf*, size_t>>& req) {
   size_t total = 0;
   for (auto& r : req)
     if (!r.first->p) total += (std::max<size_t>(r.second, 256) + 255) & ~(size_t)255;
@@ -81,11 +85,22 @@ static hipError_t ensure_all(DevBuf& block, const std::vector<std::pair<DevBuf*,
       r.first->p = static_cast<uint8_t*>(block.p) + off;
       r.first->cap = n;
       r.first->borrowed = true;
+      users.push_back(r.first);
       off += n;
     }
   }
   for (auto& r : req)
     if (hipError_t h = r.first->ensure(r.second); h != hipSuccess) return h;
+  if (block.p) {
+    const uint8_t* lo = static_cast<const uint8_t*>(block.p);
+    users.erase(std::remove_if(users.begin(), users.end(),
+                               [&](DevBuf* b) {
+                                 const uint8_t* q = static_cast<const uint8_t*>(b->p);
+                                 return !(b->borrowed && q >= lo && q < lo + block.cap);
+                               }),
+                users.end());
+    if (users.empty()) block.release();  // (every buffer outgrew its slice)
+  }
   return hipSuccess;
 }
 
@@ -181,6 +196,7 @@ struct klf_engine {
   DevBuf d_tile_seg;
   DevBuf d_cmap, d_cseg;
   DevBuf d_block;  // the first run's workspace buffers (ensure_all), freed last
+  std::vector<DevBuf*> block_users;  // the buffers still mapped into d_block
   DevBuf d_batch, d_segs, d_tstat, d_slots, d_pool, d_tile_base, d_bsum, d_cstatus, d_counters, d_line_off,
       d_meta, d_bits, d_segout, d_wpre, d_out, d_mpart, d_trec, d_truns, d_kbase;
   // one-pass compaction (RunArgs::fuse): range table, extents, range states; d_out2 the
@@ -195,11 +211,14 @@ struct klf_engine {
   bool dense_tail_seen = false;  // a --tail run took the dense compaction (keep its run table)
   HostBuf h_rb;  // run readback: counters (64 B), then the SegOut table
   HostBuf h_stage;  // pinned staging of the prefilter tables (upload_prefilter)
+  HostBuf h_acblk;  // the automaton thread's tables (pinned), uploaded on the launch stream at the join
+  size_t ac_total = 0, ac_off[5] = {0, 0, 0, 0, 0}, ac_cap[5] = {0, 0, 0, 0, 0};
   // The literals' Aho-Corasick automaton (deferred lines, the fallback matcher): klf_open
   // starts a host thread that builds it and uploads it as one block (d_acblk, one
   // synchronous copy); ensure_ac joins it before the first launch that may read it, so the
   // build overlaps the first run's sampling and needle placement
   std::thread ac_thread;
+  bool ac_pending = false;  // the automaton is built (or being built) but not yet uploaded
   std::vector<std::vector<uint8_t>> ac_lits;
   klf::AcTables ac_tabs;
   hipError_t ac_err = hipSuccess;
@@ -461,6 +480,11 @@ static hipError_t upload_pattern_tables(klf_engine* e, bool tune_later) {
 }
 
 // the automaton thread: build, then one block on the device and one copy
+// The literal automaton's thread: builds the tables, lays them out as one pinned block and
+// maps the device block.  The upload itself is left to the join (ensure_ac), on the launch
+// stream: a copy from this thread would go to HIP's null stream, where it queues behind a
+// scan already running on that stream (an engine opened without a stream) and the join
+// then waits for the scan (advisor r04).
 static void ac_build_upload(klf_engine* e) {
   klf::build_ac(e->ac_lits, e->ac_tabs);
   const klf::AcTables& t = e->ac_tabs;
@@ -468,31 +492,39 @@ static void ac_build_upload(klf_engine* e) {
   const std::pair<const void*, size_t> parts[5] = {
       {t.cls.data(), t.cls.size()}, {t.next.data(), t.next.size() * 4}, {t.accept.data(), t.accept.size()},
       {t.out.data(), t.out.size() * 4}, {t.dict.data(), t.dict.size() * 4}};
-  DevBuf* dst[5] = {&e->d_ac_class, &e->d_ac_next, &e->d_ac_accept, &e->d_ac_out, &e->d_ac_dict};
-  size_t off[5], total = 0;
+  size_t total = 0;
   for (int k = 0; k < 5; ++k) {
-    off[k] = total;
-    total += (std::max<size_t>(parts[k].second, 256) + 255) & ~(size_t)255;
+    e->ac_off[k] = total;
+    e->ac_cap[k] = (std::max<size_t>(parts[k].second, 256) + 255) & ~(size_t)255;
+    total += e->ac_cap[k];
   }
-  std::vector<uint8_t> host(total, 0);
-  for (int k = 0; k < 5; ++k) memcpy(host.data() + off[k], parts[k].first, parts[k].second);
+  e->ac_total = total;
+  if (h == hipSuccess) h = e->h_acblk.ensure(total);
+  if (h == hipSuccess) {
+    memset(e->h_acblk.p, 0, total);
+    for (int k = 0; k < 5; ++k) memcpy(e->h_acblk.as<uint8_t>() + e->ac_off[k], parts[k].first, parts[k].second);
+  }
   if (h == hipSuccess) h = e->d_acblk.ensure(total);
-  if (h == hipSuccess) h = hipMemcpy(e->d_acblk.p, host.data(), total, hipMemcpyHostToDevice);
-  if (h == hipSuccess)
-    for (int k = 0; k < 5; ++k) {
-      dst[k]->release();
-      dst[k]->p = e->d_acblk.as<uint8_t>() + off[k];
-      dst[k]->cap = (std::max<size_t>(parts[k].second, 256) + 255) & ~(size_t)255;
-      dst[k]->borrowed = true;
-    }
   e->ac_err = h;
 }
 
 // Joins the automaton thread (if any) and points the device patterns at its tables.
 static int ensure_ac(klf_engine* e) {
-  if (!e->ac_thread.joinable()) return KLF_OK;
-  e->ac_thread.join();
+  if (e->ac_thread.joinable()) e->ac_thread.join();
+  if (!e->ac_pending) return KLF_OK;
+  e->ac_pending = false;
   if (e->ac_err != hipSuccess) return hip_err(e, e->ac_err, "Aho-Corasick tables");
+  // the upload, ordered on the launch stream before the first kernel that reads it (the
+  // pinned block stays until klf_close)
+  HIPCHK(e, hipMemcpyAsync(e->d_acblk.p, e->h_acblk.p, e->ac_total, hipMemcpyHostToDevice, e->stream),
+         "upload Aho-Corasick tables");
+  DevBuf* dst[5] = {&e->d_ac_class, &e->d_ac_next, &e->d_ac_accept, &e->d_ac_out, &e->d_ac_dict};
+  for (int k = 0; k < 5; ++k) {
+    dst[k]->release();
+    dst[k]->p = e->d_acblk.as<uint8_t>() + e->ac_off[k];
+    dst[k]->cap = e->ac_cap[k];
+    dst[k]->borrowed = true;
+  }
   klf::CompiledSet& cs = e->cs;
   klf::AcTables& t = e->ac_tabs;
   cs.ac_states = t.states;
@@ -599,6 +631,7 @@ extern "C" int klf_open(const klf_config* cfg, klf_engine** out) {
   if (const char* hc = getenv("KLF_HITS_CAP"))  // tests: force the hit-list overflow fallback
     e->hits_cap_max = (uint64_t)std::max(1L, std::min(atol(hc), 1L << 28));
   if (!e->ac_lits.empty()) {
+    e->ac_pending = true;
     try {
       e->ac_thread = std::thread(ac_build_upload, e);
     } catch (...) {  // no thread: build it here
@@ -630,6 +663,7 @@ extern "C" void klf_close(klf_engine* e) {
   e->d_asm.release();
   e->d_scratch.release();
   e->h_rb.release();
+  e->h_acblk.release();
   e->h_hist.release();
   e->h_stage.release();
   for (DevBuf* b : {&e->d_ac_out, &e->d_ac_dict, &e->d_pcount, &e->d_pairs}) b->release();
@@ -1140,7 +1174,7 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
     ws.push_back({&e->d_hslots, (size_t)ntiles * klf::kHitSlots * 2});
     ws.push_back({&e->d_hflat, (size_t)hflat_cap * 4});
   }
-  HIPCHK(e, ensure_all(e->d_block, ws), "alloc workspace");
+  HIPCHK(e, ensure_all(e->d_block, e->block_users, ws), "alloc workspace");
 
   const bool count = (f->flags & KLF_FILTER_PATTERN_COUNTS) && mode == klf::CompiledSet::kGeneral && e->cs.n_cids;
   r->counted = (f->flags & KLF_FILTER_PATTERN_COUNTS) != 0;
@@ -1318,7 +1352,7 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
         HIPCHK(e, hipMemsetAsync(a.bits, 0, (cap / 32 + 1) * 4, st), "zero bits");
       HIPCHK(e, klf::launch_pipeline(a, st, e->ev, e->num_cus, 2, &ev_mask), "launch");
       mark("phase 2 launched");
-    } else if (e->ac_thread.joinable()) {  // joined while the scan runs
+    } else if (e->ac_pending) {  // joined while the scan runs
       HIPCHK(e, alloc_lines(a, cap), "alloc line arrays");
       HIPCHK(e, klf::launch_pipeline(a, st, e->ev, e->num_cus, 3, &ev_mask), "launch");
       if (const int rc = join_ac(); rc != KLF_OK) return rc;
