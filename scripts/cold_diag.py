@@ -26,6 +26,21 @@ def main():
             w.run_device(dev.data_ptr(), seg_base, lens, since=since, tail=tail).free()
     torch.cuda.synchronize()
     time.sleep(0.2)
+    # the same warm engine after an idle gap: what a one-shot run pays for the board's state
+    with E.Engine(0, hip_stream=st, **pats) as w:
+        for _ in range(3):
+            w.run_device(dev.data_ptr(), seg_base, lens, since=since, tail=tail).free()
+        torch.cuda.synchronize()
+        res = {}
+        for gap_ms in (0, 1, 3, 10, 30):
+            ts = []
+            for _ in range(3):
+                time.sleep(gap_ms / 1e3)
+                t0 = time.perf_counter()
+                w.run_device(dev.data_ptr(), seg_base, lens, since=since, tail=tail).free()
+                ts.append((time.perf_counter() - t0) * 1e3)
+            res[gap_ms] = round(min(ts), 3), round(sum(ts) / len(ts), 3)
+        print({"warm_run_after_idle_gap_ms": res}, flush=True)
     print("== cold engine", file=sys.stderr, flush=True)
     print(bench.cold_run(0, pats, dev.data_ptr(), seg_base, lens, since, tail), flush=True)
     print(bench.cold_run(0, pats, dev.data_ptr(), seg_base, lens, since, tail), flush=True)
