@@ -400,10 +400,21 @@ def cold_run(local: int, pats: dict, ptr: int, seg_base, lens, since, tail: int)
     r = eng.run_device(ptr, seg_base, lens, since=since, tail=tail)
     t4 = time.perf_counter()
     r.free()
+    # the same warm engine after 3 ms with the GPU idle (about the host work in front of a
+    # cold run's kernels): a long VALU-bound scan runs slower after an idle gap (C5 6.67 ms
+    # back to back, 7.25 ms after 3 ms, 7.87 ms after 30 ms: gpurun_out/r5o), which the
+    # cold run pays too
+    time.sleep(0.003)
+    t5 = time.perf_counter()
+    r = eng.run_device(ptr, seg_base, lens, since=since, tail=tail)
+    t6 = time.perf_counter()
+    r.free()
     eng.close()
     return {"open_ms": round((t1 - t0) * 1e3, 3), "first_run_ms": round((t2 - t1) * 1e3, 3),
             "cold_ms": round((t2 - t0) * 1e3, 3), "second_run_ms": round((t4 - t3) * 1e3, 3),
-            "ratio": round((t2 - t0) / max(t4 - t3, 1e-9), 3)}
+            "ratio": round((t2 - t0) / max(t4 - t3, 1e-9), 3),
+            "warm_run_after_3ms_idle_ms": round((t6 - t5) * 1e3, 3),
+            "ratio_vs_warm_after_idle": round((t2 - t0) / max(t6 - t5, 1e-9), 3)}
 
 
 # ---------------------------------------------------------------- CPU baseline ------
