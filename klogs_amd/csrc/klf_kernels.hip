@@ -409,6 +409,9 @@ __device__ __forceinline__ bool parse_fast(const uint8_t* lds, uint32_t o, const
 // each, gpurun_out/r5d, r5e)
 #define KLF_SCAN_NT 1
 #endif
+#ifndef KLF_SCAN_PRIO
+#define KLF_SCAN_PRIO 0  // s_setprio level while a wave stages its tile and issues the next one
+#endif
 #ifndef KLF_SCAN_SUMSKIP
 // no count reductions on tiles where no line starts (C5: ~half its tiles): 6.33 -> 6.29 ms
 #define KLF_SCAN_SUMSKIP 1
@@ -588,6 +591,7 @@ __global__ __launch_bounds__(kThreads, MODE == kScanGen ? 3 : KLF_SCAN_OCC) void
     const uint8_t* segp = a.bytes + sd.base;
 
     // ---- stage this tile in the wave's LDS region, then start loading the next one ----
+    if (KLF_SCAN_PRIO) __builtin_amdgcn_s_setprio(KLF_SCAN_PRIO);  // A/B: the prefetch issue first
     {
       uint4* l = reinterpret_cast<uint4*>(s_tile);
       KLF_ROWS(KLF_STORE)
@@ -603,6 +607,7 @@ __global__ __launch_bounds__(kThreads, MODE == kScanGen ? 3 : KLF_SCAN_OCC) void
         if (lane < kHalo / 16) pfh = (KLF_SCAN_NT && MODE != kScanPlain) ? ld_nt(&gp[kTile / 16 + lane]) : gp[kTile / 16 + lane];
       }
     }
+    if (KLF_SCAN_PRIO) __builtin_amdgcn_s_setprio(0);
     wave_lds_sync();
 
     // ---- any-tests over my 128 bytes: 8 chunks of 16 B, read rotated (chunk (v + lane/2)
