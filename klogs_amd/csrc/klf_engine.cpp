@@ -268,6 +268,42 @@ static int set_err(klf_engine* e, int code, const std::string& m) {
   if (e) e->err = m;
   return code;
 }
+
+// The since cutoff as the scan compares it (RunArgs::since_dig): the 23 digits of its
+// canonical UTC prefix, packed like parse_fast's p0..p5.  The fast path only accepts years
+// 1970..2099, so an earlier cutoff passes every such line (1970-01-01T00:00:00Z) and a
+// later one none (all '9').
+static void since_digits(int64_t sec, int64_t nsec, uint32_t out[6]) {
+  sec += nsec / 1000000000;  // (nsec normalised into [0, 1e9))
+  nsec %= 1000000000;
+  if (nsec < 0) {
+    nsec += 1000000000;
+    --sec;
+  }
+  char d[48];
+  if (sec < 0) {
+    memcpy(d, "19700101000000000000000", 23);
+  } else if (sec >= 4102444800LL) {  // 2100-01-01T00:00:00Z
+    memset(d, '9', 23);
+  } else {
+    const int64_t z = sec / 86400 + 719468, era = z / 146097;  // civil from days (proleptic Gregorian)
+    const int64_t doe = z - era * 146097, yoe = (doe - doe / 1460 + doe / 36524 - doe / 146096) / 365;
+    const int64_t doy = doe - (365 * yoe + yoe / 4 - yoe / 100), mp = (5 * doy + 2) / 153;
+    const int64_t day = doy - (153 * mp + 2) / 5 + 1, month = mp < 10 ? mp + 3 : mp - 9;
+    const int64_t year = yoe + era * 400 + (month <= 2 ? 1 : 0), sod = sec % 86400;
+    snprintf(d, sizeof d, "%04d%02d%02d%02d%02d%02d%09d", (int)year, (int)month, (int)day, (int)(sod / 3600),
+             (int)(sod / 60 % 60), (int)(sod % 60), (int)nsec);
+  }
+  auto be = [&](char a, char b, char c, char e) {
+    return (uint32_t)(uint8_t)a << 24 | (uint32_t)(uint8_t)b << 16 | (uint32_t)(uint8_t)c << 8 | (uint8_t)e;
+  };
+  out[0] = be(d[0], d[1], d[2], d[3]);      // YYYY
+  out[1] = be(d[4], d[5], d[6], d[7]);      // MMDD
+  out[2] = be(d[8], d[9], d[10], d[11]);    // hhmm
+  out[3] = be(d[12], d[13], d[14], d[15]);  // ss n0 n1
+  out[4] = be(d[16], d[17], d[18], d[19]);  // n2..n5
+  out[5] = be(d[20], d[21], '0', d[22]);    // n6 n7 pad n8
+}
 static int hip_err(klf_engine* e, hipError_t h, const char* where) {
   return set_err(e, KLF_EHIP, std::string(where) + ": " + hipGetErrorString(h));
 }
@@ -1201,14 +1237,7 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
     a.tindex_wide = (ntiles > klf::kScanSmallTiles || getenv("KLF_DEBUG_TINDEX_WIDE")) ? 1u : 0u;
     a.since_sec = f->since.sec;
     a.since_nsec = f->since.nsec;
-    {
-      const int64_t sec = f->since.sec;
-      const int64_t day = sec >= 0 ? sec / 86400 : -((-sec + 86399) / 86400);
-      a.since_day = (int32_t)std::max<int64_t>(std::min<int64_t>(day, INT32_MAX), INT32_MIN);
-      a.since_sod = (uint32_t)(sec - day * 86400);
-      if (day > INT32_MAX) a.since_sod = 86400;  // later than any fast-path instant
-      if (day < INT32_MIN) a.since_sod = 0;
-    }
+    since_digits(f->since.sec, f->since.nsec, a.since_dig);
     a.tail = f->tail;
     a.grep_mode = (uint32_t)mode;
     a.match_all = e->cs.also_all ? 1u : 0u;

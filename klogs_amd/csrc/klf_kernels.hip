@@ -293,13 +293,6 @@ __global__ __launch_bounds__(256) void k_tiles(const SegDesc* segs, uint32_t nse
     tile_seg[tile] = find_seg_by_tile(segs, nsegs, tile);
 }
 
-// Cumulative days before month m (non-leap, low 16 bits) and the month's length (high).
-__constant__ uint32_t c_month[16] = {0,
-                                     0 | (31u << 16),   31 | (28u << 16),  59 | (31u << 16),  90 | (30u << 16),
-                                     120 | (31u << 16), 151 | (30u << 16), 181 | (31u << 16), 212 | (31u << 16),
-                                     243 | (30u << 16), 273 | (31u << 16), 304 | (30u << 16), 334 | (31u << 16),
-                                     0, 0, 0};
-
 // v_mul_hi_u32_u24: bits 32..47 of the product of the low 24 bits of a and b (no intrinsic;
 // the 64-bit C++ form only lowers to it when a is known to fit in 24 bits)
 __device__ __forceinline__ uint32_t mul_hi_u24(uint32_t a, uint32_t b) {
@@ -332,23 +325,15 @@ __device__ __forceinline__ uint32_t shr_byte1(uint32_t w, uint32_t h) {
       : "=v"(r) : "v"(h), "v"(w));
   return r;
 }
-// v_mad_u32_u24: a * b + c for a, b < 2^24 (low 32 bits of the product)
-__device__ __forceinline__ uint32_t mad24(uint32_t a, uint32_t b, uint32_t c) { return __umul24(a, b) + c; }
-
-// Two decimal digits per 16-bit half of a dword holding 4 digit values (bytes 0..9):
-// low half = b0 * 10 + b1, high half = b2 * 10 + b3.
-__device__ __forceinline__ uint32_t digit_pairs(uint32_t t) {
-  const uint32_t ev = t & 0x00FF00FFu;                                // b0, b2
-  const uint32_t od = __builtin_amdgcn_perm(0u, t, 0x0C030C01u);      // b1, b3
-  return mad24(ev, 10u, od);
-}
-
 // Canonical kubelet prefix at LDS byte offset o (bytes o .. o + 30 valid): true with
 // since_ok set when the line starts "YYYY-MM-DDTHH:MM:SS.nnnnnnnnnZ " with a valid date,
-// year 1970..2099 (where the Gregorian leap rule is y % 4 == 0).  The value equals Go
-// time.Parse's for exactly these inputs; false sends the line to the general parser.
-__device__ __forceinline__ bool parse_fast(const uint8_t* lds, uint32_t o, const uint32_t* s_month, int32_t sday,
-                                           uint32_t ssod, int32_t snsec, bool& since_ok) {
+// year 1970..2099 (where the Gregorian leap rule is y % 4 == 0).  The 23 digits are packed
+// big-endian (p0..p5: first digit in the top byte), so for valid dates the digit strings
+// order like the instants and since is one lexicographic compare against the cutoff's
+// digits (RunArgs::since_dig): no day / second arithmetic.  Only days 29..31 (and 00)
+// need the month's length.  The value equals Go time.Parse's for exactly these inputs;
+// false sends the line to the general parser.
+__device__ __forceinline__ bool parse_fast(const uint8_t* lds, uint32_t o, const uint32_t (&cut)[6], bool& since_ok) {
   const uint32_t* s32 = reinterpret_cast<const uint32_t*>(lds);
   const uint32_t base = o >> 2, sh = o & 3u;
   uint32_t w[8];
@@ -363,40 +348,36 @@ __device__ __forceinline__ bool parse_fast(const uint8_t* lds, uint32_t o, const
   const uint32_t sep = ((w[1] ^ 0x2D00002Du) & 0xFF0000FFu) | ((w[2] ^ 0x00540000u) & 0x00FF0000u) |
                        ((w[3] ^ 0x00003A00u) & 0x0000FF00u) | ((w[4] ^ 0x2E00003Au) & 0xFF0000FFu) |
                        ((w[7] ^ 0x00205A00u) & 0x00FFFF00u);
-  // the 23 digits packed into 6 dwords (one pad '0')
-  const uint32_t p0 = w[0];                                                  // Y Y Y Y
-  const uint32_t p1 = __builtin_amdgcn_perm(w[2], w[1], 0x05040201u);        // M M D D
-  const uint32_t p2 = __builtin_amdgcn_perm(w[3], w[2], 0x07060403u);        // h h m m
-  const uint32_t p3 = __builtin_amdgcn_perm(w[5], w[4], 0x05040201u);        // s s n0 n1
-  const uint32_t p4 = __builtin_amdgcn_perm(w[6], w[5], 0x05040302u);        // n2 n3 n4 n5
-  const uint32_t p5 = __builtin_amdgcn_perm(w[7], w[6], 0x040C0302u) | 0x00300000u;  // n6 n7 0 n8
+  // the 23 digits in 6 dwords, big-endian (one pad '0' before the last digit)
+  const uint32_t p0 = __builtin_amdgcn_perm(0u, w[0], 0x00010203u);                   // Y Y Y Y
+  const uint32_t p1 = __builtin_amdgcn_perm(w[2], w[1], 0x01020405u);                 // M M D D
+  const uint32_t p2 = __builtin_amdgcn_perm(w[3], w[2], 0x03040607u);                 // h h m m
+  const uint32_t p3 = __builtin_amdgcn_perm(w[5], w[4], 0x01020405u);                 // s s n0 n1
+  const uint32_t p4 = __builtin_amdgcn_perm(w[6], w[5], 0x02030405u);                 // n2 n3 n4 n5
+  const uint32_t p5 = __builtin_amdgcn_perm(w[7], w[6], 0x02030C04u) | 0x00003000u;  // n6 n7 0 n8
   // digit check: high nibble 3 everywhere, low nibble <= 9 (no cross-byte carry once the
   // high nibbles are 3)
-  const uint32_t t0 = p0 ^ 0x30303030u, t1 = p1 ^ 0x30303030u, t2 = p2 ^ 0x30303030u, t3 = p3 ^ 0x30303030u,
-                 t4 = p4 ^ 0x30303030u, t5 = p5 ^ 0x30303030u;
-  const uint32_t hi = (t0 | t1 | t2 | t3 | t4 | t5) & 0xF0F0F0F0u;
+  const uint32_t hi = ((p0 ^ 0x30303030u) | (p1 ^ 0x30303030u) | (p2 ^ 0x30303030u) | (p3 ^ 0x30303030u) |
+                       (p4 ^ 0x30303030u) | (p5 ^ 0x30303030u)) & 0xF0F0F0F0u;
   const uint32_t lo = ((p0 + 0x06060606u) | (p1 + 0x06060606u) | (p2 + 0x06060606u) | (p3 + 0x06060606u) |
                        (p4 + 0x06060606u) | (p5 + 0x06060606u)) & 0x40404040u;
   if ((sep | hi | lo) != 0u) return false;
-  const uint32_t v0 = digit_pairs(t0), v1 = digit_pairs(t1), v2 = digit_pairs(t2), v3 = digit_pairs(t3),
-                 v4 = digit_pairs(t4), v5 = digit_pairs(t5);
-  const uint32_t year = mad24(v0 & 0xFFFFu, 100u, v0 >> 16);
-  const uint32_t month = v1 & 0xFFFFu, day = v1 >> 16, hour = v2 & 0xFFFFu, minute = v2 >> 16;
-  const uint32_t second = v3 & 0xFFFFu;
-  uint32_t ns = mad24(v3 >> 16, 10000000u, 0u);
-  ns = mad24(v4 & 0xFFFFu, 100000u, ns);
-  ns = mad24(v4 >> 16, 1000u, ns);
-  ns = mad24(v5 & 0xFFFFu, 10u, ns) + (v5 >> 16);
-  if (year - 1970u >= 130u || month - 1u >= 12u || hour >= 24u || minute >= 60u || second >= 60u) return false;
-  const uint32_t mt = s_month[month];
-  const uint32_t leap = (year & 3u) == 0u ? 1u : 0u;
-  const uint32_t dim = (mt >> 16) + (month == 2u ? leap : 0u);
-  if (day - 1u >= dim) return false;
-  const int32_t days = (int32_t)(mad24(year - 1970u, 365u, (year - 1969u) >> 2) + (mt & 0xFFFFu) +
-                                 (month > 2u ? leap : 0u) + day - 1u);
-  const uint32_t sod = mad24(hour, 3600u, mad24(minute, 60u, second));
-  const bool before = days < sday || (days == sday && (sod < ssod || (sod == ssod && (int32_t)ns < snsec)));
-  since_ok = !before;
+  // field ranges on the big-endian digit pairs (all bytes are digits here)
+  if (p0 - 0x31393730u > 0x32303939u - 0x31393730u) return false;        // year 1970..2099
+  if ((p1 >> 16) - 0x3031u > 0x3132u - 0x3031u) return false;            // month 01..12
+  if ((p2 >> 16) > 0x3233u || (p2 & 0xFFFFu) > 0x3539u || (p3 >> 16) > 0x3539u) return false;  // hh mm ss
+  if ((p1 & 0xFFFFu) - 0x3031u > 0x3238u - 0x3031u) {  // day outside 01..28: the month's length
+    const uint32_t day = ((p1 >> 8) & 15u) * 10u + (p1 & 15u);
+    const uint32_t month = ((p1 >> 24) & 15u) * 10u + ((p1 >> 16) & 15u);
+    const uint32_t yy = ((p0 >> 8) & 15u) * 10u + (p0 & 15u);  // year mod 100 (100 = 0 mod 4)
+    const uint32_t dim = month == 2u ? 28u + ((yy & 3u) == 0u ? 1u : 0u) : 30u + ((month + (month >> 3)) & 1u);
+    if (day - 1u >= dim) return false;
+  }
+  // lexicographic: the line's digits >= the cutoff's (not Before(since))
+  const uint64_t a0 = (uint64_t)p0 << 32 | p1, a1 = (uint64_t)p2 << 32 | p3, a2 = (uint64_t)p4 << 32 | p5;
+  const uint64_t c0 = (uint64_t)cut[0] << 32 | cut[1], c1 = (uint64_t)cut[2] << 32 | cut[3],
+                 c2 = (uint64_t)cut[4] << 32 | cut[5];
+  since_ok = a0 > c0 || (a0 == c0 && (a1 > c1 || (a1 == c1 && a2 >= c2)));
   return true;
 }
 
@@ -481,7 +462,6 @@ __global__ __launch_bounds__(kThreads, MODE == kScanGen ? 3 : KLF_SCAN_OCC) void
   __shared__ __attribute__((aligned(16))) uint16_t s_fmap_all[FUSE ? kWaves : 1][FUSE ? kTcChunks : 8];
   __shared__ __attribute__((aligned(16))) uint32_t s_list_all[kWaves][kSlotStride];
   __shared__ __attribute__((aligned(16))) uint32_t s_lit[kMaxFusedLiteral / 4 + 1];  // literal, zero padded
-  __shared__ uint32_t s_month[16];
   // the TileStats of the wave's current tile group: LDS for the plain / literal scans (a
   // register quad there spills), a register quad for GEN (LDS is what bounds its occupancy)
   __shared__ uint4 s_gstat[GEN ? 1 : kWaves][kScanGroup];
@@ -494,7 +474,6 @@ __global__ __launch_bounds__(kThreads, MODE == kScanGen ? 3 : KLF_SCAN_OCC) void
   uint32_t* err_flag = a.counters + 2;
   for (uint32_t i = t; i < kMaxFusedLiteral / 4 + 1; i += kThreads)
     s_lit[i] = (LIT && i < (a.lit_len + 3) / 4) ? a.lit_words[i] : 0u;
-  if (t < 16) s_month[t] = c_month[t];
   if (GEN)
     for (uint32_t i = t; i < kQfWords; i += kThreads) s_qf[i] = a.pats.qf_bitmap[i];
   __syncthreads();  // the kernel's only block barrier
@@ -729,7 +708,7 @@ __global__ __launch_bounds__(kThreads, MODE == kScanGen ? 3 : KLF_SCAN_OCC) void
           if (ABL(1)) {
             fast = so = true;
           } else if (rel_lo + (int64_t)off + 31 <= seg_len) {
-            fast = parse_fast(s_tile, off, s_month, a.since_day, a.since_sod, a.since_nsec, so);
+            fast = parse_fast(s_tile, off, a.since_dig, so);
           }
           if (FUSE && !fast) {  // the one-pass compaction decides every line here: Go time.Parse
             TsResult tr;

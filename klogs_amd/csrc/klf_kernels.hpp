@@ -258,8 +258,10 @@ struct RunArgs {
   // filter
   int64_t since_sec;
   int32_t since_nsec;
-  int32_t since_day;    // floor(since_sec / 86400)
-  uint32_t since_sod;   // since_sec - since_day * 86400
+  // the cutoff as the canonical prefix's 23 digits (YYYYMMDDhhmmss + 9 fraction digits),
+  // packed like parse_fast's p0..p5 (big-endian digit order, a '0' pad before the last
+  // digit); before 1970: 1970-01-01T00:00:00Z, from 2100 on: all '9'
+  uint32_t since_dig[6];
   int64_t tail;
   uint32_t grep_mode;
   uint32_t match_all;  // kGrepGeneral: the set also matches every content (k_match marks every parsed line)
