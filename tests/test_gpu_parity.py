@@ -94,6 +94,37 @@ def test_dense_tiles(gpu):
         check_against_c([d, synth.generate(synth.TEXT, 1, 0, 100_000), d[:70001]], since, tail, grep)
 
 
+def _date_edge_lines(n, seed):
+    """Canonical prefixes around every rule of the scan's fast path (digits compared against
+    the cutoff's digits; the month's length only for days 29..31): years 1969/1970/2099/2100,
+    Feb 29 in leap / non-leap years (2000, 2024, 2023, 2100), day 00 / 31 of 30-day months,
+    hour 24, minute / second 60, fraction digits at both ends, and a corrupted byte."""
+    rnd = random.Random(seed)
+    out = []
+    for i in range(n):
+        y = rnd.choice([1969, 1970, 1971, 2000, 2023, 2024, 2099, 2100, rnd.randint(1965, 2105)])
+        mo = rnd.choice([0, 1, 2, 2, 2, 4, 6, 9, 11, 12, 13, rnd.randint(1, 12)])
+        d = rnd.choice([0, 1, 28, 29, 29, 30, 31, 32, rnd.randint(1, 31)])
+        h, mi, s = rnd.choice([0, 23, 24, 12]), rnd.choice([0, 59, 60, 30]), rnd.choice([0, 59, 60, 30])
+        ns = rnd.choice([0, 999_999_999, rnd.randint(0, 999_999_999)])
+        t = b"%04d-%02d-%02dT%02d:%02d:%02d.%09dZ " % (y, mo, d, h, mi, s, ns)
+        if rnd.random() < 0.05:
+            k = rnd.randrange(31)
+            t = t[:k] + bytes([rnd.choice(b"0123456789:-TZ. /a")]) + t[k + 1:]
+        out.append(t + b"line %d ERR_CONN_RESET\n" % i if i % 3 == 0 else t + b"line %d\n" % i)
+    return b"".join(out)
+
+
+@pytest.mark.parametrize("grep", [[], [synth.NEEDLE], [b"ERR_CONN"] + [b"lit%03d" % i for i in range(20)]])
+def test_fast_timestamp_date_edges(gpu, grep):
+    d = _date_edge_lines(40_000, 17)
+    cuts = [None, (951_782_400, 0), (951_868_799, 999_999_999), (1_709_164_800, 1),  # 2000-02-29, 2024-02-29
+            (-1, 999_999_999), (0, 0), (4_102_444_799, 999_999_999), (4_102_444_800, 0), (1_729_555_200 + 7, 5)]
+    for since in cuts:
+        for tail in ([-1, 100] if not grep else [-1]):
+            check_against_c([d, d[:100_001]], since, tail, grep)
+
+
 def _golden():
     import json
     from pathlib import Path
