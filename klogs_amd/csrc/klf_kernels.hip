@@ -325,6 +325,9 @@ __device__ __forceinline__ uint32_t shr_byte1(uint32_t w, uint32_t h) {
       : "=v"(r) : "v"(h), "v"(w));
   return r;
 }
+#ifndef KLF_PARSE_UNALIGNED
+#define KLF_PARSE_UNALIGNED 1  // the timestamp prefix read with unaligned 16-B LDS loads
+#endif
 // Canonical kubelet prefix at LDS byte offset o (bytes o .. o + 30 valid): true with
 // since_ok set when the line starts "YYYY-MM-DDTHH:MM:SS.nnnnnnnnnZ " with a valid date,
 // year 1970..2099 (where the Gregorian leap rule is y % 4 == 0).  The 23 digits are packed
@@ -334,15 +337,26 @@ __device__ __forceinline__ uint32_t shr_byte1(uint32_t w, uint32_t h) {
 // need the month's length.  The value equals Go time.Parse's for exactly these inputs;
 // false sends the line to the general parser.
 __device__ __forceinline__ bool parse_fast(const uint8_t* lds, uint32_t o, const uint32_t (&cut)[6], bool& since_ok) {
-  const uint32_t* s32 = reinterpret_cast<const uint32_t*>(lds);
-  const uint32_t base = o >> 2, sh = o & 3u;
   uint32_t w[8];
-  uint32_t prev = s32[base];
+  if (KLF_PARSE_UNALIGNED) {
+    // two 16-B reads at the line start itself: gfx950 LDS serves unaligned ds_read_b128
+    // (the HSA default unaligned access mode), so no byte alignment in VALU
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    u32x4 x0, x1;
+    __builtin_memcpy(&x0, lds + o, 16);
+    __builtin_memcpy(&x1, lds + o + 16, 16);
+    w[0] = x0.x; w[1] = x0.y; w[2] = x0.z; w[3] = x0.w;
+    w[4] = x1.x; w[5] = x1.y; w[6] = x1.z; w[7] = x1.w;
+  } else {
+    const uint32_t* s32 = reinterpret_cast<const uint32_t*>(lds);
+    const uint32_t base = o >> 2, sh = o & 3u;
+    uint32_t prev = s32[base];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const uint32_t nx = s32[base + j + 1];
-    w[j] = __builtin_amdgcn_alignbyte(nx, prev, sh);
-    prev = nx;
+    for (int j = 0; j < 8; ++j) {
+      const uint32_t nx = s32[base + j + 1];
+      w[j] = __builtin_amdgcn_alignbyte(nx, prev, sh);
+      prev = nx;
+    }
   }
   // separators: '-' 4, '-' 7, 'T' 10, ':' 13, ':' 16, '.' 19, 'Z' 29, ' ' 30
   const uint32_t sep = ((w[1] ^ 0x2D00002Du) & 0xFF0000FFu) | ((w[2] ^ 0x00540000u) & 0x00FF0000u) |
