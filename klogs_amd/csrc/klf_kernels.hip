@@ -4065,7 +4065,10 @@ hipError_t launch_pipeline(const RunArgs& a0, hipStream_t st, hipEvent_t* ev, in
   // Regex sets: k_scatter and k_verify as one launch (k_scatter_verify; measured with two
   // streams: C5 -0.10 ms per step); a literal set's heavier verification (C4: 1,024 literals)
   // contends with the scatter instead (+0.08 ms), so literal-only sets keep the serial order.
-  const bool fused_sv = a.grep_mode == kGrepGeneral && a.pats.qf_on && a.pats.rx_count;
+#ifndef KLF_SV_FUSED
+#define KLF_SV_FUSED 1  // regex sets: k_scatter and k_verify as one launch (0: two, for traces)
+#endif
+  const bool fused_sv = KLF_SV_FUSED && a.grep_mode == kGrepGeneral && a.pats.qf_on && a.pats.rx_count;
   if (fused_sv) {
     uint32_t nsb = ((a.ntiles + kScatterGroup - 1) / kScatterGroup + 3) / 4;
     if (nsb > (uint32_t)num_cus * 4) nsb = num_cus * 4;
