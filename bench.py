@@ -149,6 +149,38 @@ def gpu_state(local: int) -> dict:
         return {"error": f"{type(ex).__name__}: {ex}"[:200]}
 
 
+def box_probe(local: int) -> dict:
+    """This box's own HBM rates, so that a box-to-box spread of the scan can be attributed:
+    the runtime's device-to-device copy (2 GiB read + 2 GiB written) and a read-only
+    reduction (torch sum over 4 GiB), best of 5 each, timed with events on cuda:local."""
+    try:
+        n = 2 << 30
+        src = torch.empty(n, dtype=torch.uint8, device=f"cuda:{local}").fill_(1)
+        dst = torch.empty_like(src)
+        rd = torch.empty(2 * n // 8, dtype=torch.int64, device=f"cuda:{local}").fill_(1)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+
+        def best(f):
+            f()
+            ts = []
+            for _ in range(5):
+                e0.record()
+                f()
+                e1.record()
+                e1.synchronize()
+                ts.append(e0.elapsed_time(e1))
+            return min(ts)
+        tc = best(lambda: dst.copy_(src))
+        tr = best(lambda: rd.sum())
+        out = {"d2d_copy_GBps": round(2 * n / tc / 1e6, 1), "read_sum_GBps": round(2 * n / tr / 1e6, 1),
+               "how": "torch copy_ (2 GiB in + 2 GiB out) and int64 sum over 4 GiB, best of 5"}
+        del src, dst, rd
+        torch.cuda.empty_cache()
+        return out
+    except Exception as ex:  # noqa: BLE001 (diagnostic only)
+        return {"error": f"{type(ex).__name__}: {ex}"[:200]}
+
+
 # ---------------------------------------------------------------- bytes -------------
 def step_bytes(n_in: int, tot: dict, n_streams: int, has_patterns: bool, index_full: bool) -> int:
     """SURVEY.md §8d B_alg = B_in + B_out + 8 (L + S) + ceil(L / 8), with the u64 line index
@@ -678,6 +710,7 @@ def main():
         extras = "c2,c1,c3,c4" if world == 1 else "c2,c3"
     extras = [x for x in extras.split(",") if x and x != HEADLINE]
 
+    probe = box_probe(local)
     if world == 1:
         head = run_config(HEADLINE, args, local, now, headline=True)
         value, ms = head["value_GBps"], head["ms_per_step"]
@@ -717,7 +750,7 @@ def main():
                    "parallelism": f"stream table LPT-sharded over {world} GPU(s), one process per GPU"},
         "roofline": roof,
         "cpu_baseline": cpu,
-        "extra": {"headline": head, "configs": {}},
+        "extra": {"headline": head, "configs": {}, "box_probe": probe},
     }
     for name in extras:
         try:

@@ -21,11 +21,15 @@ def main():
     ap.add_argument("config")
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--probe", action="store_true", help="add bench.box_probe (the box's copy / read rates)")
     a = ap.parse_args()
     ns = argparse.Namespace(steps=a.steps, warmup=a.warmup, no_verify=True, no_write=True, no_capture=True,
                             no_cpu_baseline=True, capture_piece=4 << 20)
     now = bench.synth.T0 + bench.synth.SPAN + 1
+    probe = bench.box_probe(0) if a.probe else None
     out = bench.run_config(a.config, ns, 0, now)
+    if probe:
+        out["box_probe"] = probe
     print(json.dumps(out))
 
 
