@@ -727,6 +727,8 @@ def main():
                 "frac_min_over_ranks": head["scan_frac_min_over_ranks"],
                 "frac_source": "rank 0's k_scan dispatch events (hipExtLaunchKernel), this run"}
         cpu = None  # (rank 0 at N = 1 only)
+    if "read_sum_GBps" in probe:  # the scan against what this box reads at all
+        roof["frac_of_box_read_rate"] = round(roof["achieved"] / probe["read_sum_GBps"], 4)
     traffic, src_t, frac_rp, src_f = committed(HEADLINE)
     roof["traffic"] = traffic
     roof["traffic_source"] = src_t
