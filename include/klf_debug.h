@@ -42,6 +42,12 @@ int klf_debug_prefilter_hits(const klf_pattern* pats, uint32_t n, const uint8_t*
 int klf_debug_factors(const uint8_t* pat, size_t len, uint32_t want, char* buf, size_t cap, uint32_t* n,
                       uint32_t* pre, uint32_t* loose);
 
+/* The since cutoff as the scan's fast timestamp path compares it: out[6] = the 23 digits
+ * of its canonical UTC prefix (YYYYMMDDhhmmss + 9 fraction digits) packed big-endian, a
+ * '0' pad before the last digit; before 1970 the digits of 1970-01-01T00:00:00Z, from 2100
+ * on all '9'. */
+int klf_debug_since_digits(int64_t sec, int32_t nsec, uint32_t* out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -2161,6 +2161,12 @@ extern "C" int klf_debug_match(const klf_pattern* pats, uint32_t n, const uint8_
   return KLF_OK;
 }
 
+extern "C" int klf_debug_since_digits(int64_t sec, int32_t nsec, uint32_t* out) {
+  if (!out) return KLF_EINVAL;
+  since_digits(sec, nsec, out);
+  return KLF_OK;
+}
+
 extern "C" int klf_debug_prefilter(const klf_pattern* pats, uint32_t n, const uint8_t* content, size_t len,
                                    uint32_t phase, int* match, uint32_t* info) {
   if ((n && !pats) || (len && !content) || !match) return KLF_EINVAL;

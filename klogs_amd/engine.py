@@ -103,6 +103,7 @@ SIGNATURES = {
                                     C.c_size_t]),
     "klf_debug_match": (C.c_int, [C.POINTER(_Pattern), C.c_uint32, C.c_void_p, C.c_size_t,
                                   C.POINTER(C.c_int)]),
+    "klf_debug_since_digits": (C.c_int, [C.c_int64, C.c_int32, C.c_void_p]),
     "klf_debug_factors": (C.c_int, [C.c_void_p, C.c_size_t, C.c_uint32, C.c_char_p, C.c_size_t,
                                     C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]),
     "klf_debug_prefilter": (C.c_int, [C.POINTER(_Pattern), C.c_uint32, C.c_void_p, C.c_size_t, C.c_uint32,
@@ -256,6 +257,14 @@ def debug_factors(pattern: bytes, want: int = 0):
     _check(rc)
     alts = buf.raw.split(b"\0")[: n.value]
     return alts, (None if pre.value == 0xFFFFFFFF else pre.value), bool(loose.value)
+
+
+def debug_since_digits(sec: int, nsec: int = 0):
+    """The since cutoff's packed digits as the scan's fast timestamp path compares them
+    (six u32, klf_debug_since_digits)."""
+    out = (C.c_uint32 * 6)()
+    _check(_lib.klf_debug_since_digits(sec, nsec, out))
+    return list(out)
 
 
 @dataclass
