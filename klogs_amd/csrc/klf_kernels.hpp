@@ -55,7 +55,10 @@ constexpr uint64_t kCopyChunk = KLF_COPY_CHUNK_KB * 1024;  // output bytes per k
 // up to kCopyChunk: a small output (tail-limited runs: C2, C5) is then spread over the
 // whole chip instead of a few workgroups walking 128 KiB each.
 constexpr uint32_t kCopyChunkMinLog2 = 12;
-constexpr uint32_t kCopyChunksTarget = 1024;  // one resident generation of k_cmove workgroups (4 per CU)
+#ifndef KLF_COPY_CHUNKS_TARGET
+#define KLF_COPY_CHUNKS_TARGET 1024
+#endif
+constexpr uint32_t kCopyChunksTarget = KLF_COPY_CHUNKS_TARGET;  // one resident generation of k_cmove workgroups (4 per CU)
 constexpr uint32_t kCtrChunkLog2 = 16;               // counters[16]: log2 of this run's copy chunk
 constexpr uint32_t kCtrTailDone = 18;                // counters[18]: k_tailw blocks done
 constexpr uint32_t kCtrVerified = 10;                // counters[10]: hits k_verify walked (diagnostics)
