@@ -407,6 +407,9 @@ __device__ __forceinline__ bool parse_fast(const uint8_t* lds, uint32_t o, const
 #ifndef KLF_SCAN_PRIO
 #define KLF_SCAN_PRIO 0  // s_setprio level while a wave stages its tile and issues the next one
 #endif
+#ifndef KLF_SCAN_PACKSUM
+#define KLF_SCAN_PACKSUM 1  // the tile's parsed / since_ok counts in one wave reduction
+#endif
 #ifndef KLF_SCAN_SUMSKIP
 // no count reductions on tiles where no line starts (C5: ~half its tiles): 6.33 -> 6.29 ms
 #define KLF_SCAN_SUMSKIP 1
@@ -1223,7 +1226,13 @@ __global__ __launch_bounds__(kThreads, MODE == kScanGen ? 3 : KLF_SCAN_OCC) void
 
     // ---- per-tile record: the first 64 slots and the TileStat, two store instructions
     // on every path (see the loop entry) ----
-#if KLF_SCAN_SUMSKIP  // A/B: no reductions on tiles where no line starts (wave-uniform)
+#if KLF_SCAN_PACKSUM
+    // one reduction for both counts (each <= 8,193 per tile: 16 bits apiece, no carry from
+    // the low half) and a ballot for the deferred lines, whose count nothing reads
+    const uint32_t pq = wave_sum(n_parsed | (n_since << 16));
+    const uint32_t pp = pq & 0xFFFFu, qq = pq >> 16;
+    const uint32_t dd = __any(n_defer != 0) ? 1u : 0u;
+#elif KLF_SCAN_SUMSKIP  // A/B: no reductions on tiles where no line starts (wave-uniform)
     uint32_t pp = 0, qq = 0, dd = 0;
     if (nlines) { pp = wave_sum(n_parsed); qq = wave_sum(n_since); dd = wave_sum(n_defer); }
 #else
