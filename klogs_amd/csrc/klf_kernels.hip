@@ -407,6 +407,9 @@ __device__ __forceinline__ bool parse_fast(const uint8_t* lds, uint32_t o, const
 #ifndef KLF_SCAN_PRIO
 #define KLF_SCAN_PRIO 0  // s_setprio level while a wave stages its tile and issues the next one
 #endif
+#ifndef KLF_SCAN_BALLOT
+#define KLF_SCAN_BALLOT 1  // per-lane 0/1 counts (sparse lines) summed / ranked by ballots
+#endif
 #ifndef KLF_SCAN_PACKSUM
 #define KLF_SCAN_PACKSUM 1  // the tile's parsed / since_ok counts in one wave reduction
 #endif
@@ -676,7 +679,11 @@ __global__ __launch_bounds__(kThreads, MODE == kScanGen ? 3 : KLF_SCAN_OCC) void
       if (!abl) a.segout[s].frag = nl_at_end ? 0 : 1;
     }
     const uint32_t cnt = (uint32_t)(__popc(em[0]) + __popc(em[1]) + __popc(em[2]) + __popc(em[3]));
-    const uint32_t incl = wave_incl_scan_add(cnt, lane);
+    // (at most one event per lane -- lines of 128 B and more: a ballot's rank is the scan)
+    const uint32_t incl = (KLF_SCAN_BALLOT && !__any(cnt > 1u))
+                              ? cnt + __builtin_amdgcn_mbcnt_hi((uint32_t)(__ballot(cnt != 0u) >> 32),
+                                                                __builtin_amdgcn_mbcnt_lo((uint32_t)__ballot(cnt != 0u), 0u))
+                              : wave_incl_scan_add(cnt, lane);
     const uint32_t agg = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
     // Local line k = the line after the tile's k-th event (k = 0: the line open at the
     // tile start).  Lines starting here: k in [k0, k1), slot j = k - k0.
@@ -1229,7 +1236,10 @@ __global__ __launch_bounds__(kThreads, MODE == kScanGen ? 3 : KLF_SCAN_OCC) void
 #if KLF_SCAN_PACKSUM
     // one reduction for both counts (each <= 8,193 per tile: 16 bits apiece, no carry from
     // the low half) and a ballot for the deferred lines, whose count nothing reads
-    const uint32_t pq = wave_sum(n_parsed | (n_since << 16));
+    // (at most one line per lane -- 64 lines or fewer: two ballots' popcounts)
+    const uint32_t pq = (KLF_SCAN_BALLOT && nlines <= 64u)
+                            ? (uint32_t)__popcll(__ballot(n_parsed != 0u)) | ((uint32_t)__popcll(__ballot(n_since != 0u)) << 16)
+                            : wave_sum(n_parsed | (n_since << 16));
     const uint32_t pp = pq & 0xFFFFu, qq = pq >> 16;
     const uint32_t dd = __any(n_defer != 0) ? 1u : 0u;
 #elif KLF_SCAN_SUMSKIP  // A/B: no reductions on tiles where no line starts (wave-uniform)
