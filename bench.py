@@ -174,6 +174,10 @@ def box_probe(local: int) -> dict:
         tr = best(lambda: rd.sum())
         out = {"d2d_copy_GBps": round(2 * n / tc / 1e6, 1), "read_sum_GBps": round(2 * n / tr / 1e6, 1),
                "how": "torch copy_ (2 GiB in + 2 GiB out) and int64 sum over 4 GiB, best of 5"}
+        try:  # the clock a VALU loop holds (s_memtime / s_memrealtime over every CU)
+            out["valu_loop_clock"] = E.debug_clock(local)
+        except Exception as ex:  # noqa: BLE001 (diagnostic only)
+            out["valu_loop_clock"] = {"error": f"{type(ex).__name__}: {ex}"[:120]}
         del src, dst, rd
         torch.cuda.empty_cache()
         return out

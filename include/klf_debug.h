@@ -48,6 +48,12 @@ int klf_debug_factors(const uint8_t* pat, size_t len, uint32_t want, char* buf, 
  * on all '9'. */
 int klf_debug_since_digits(int64_t sec, int32_t nsec, uint32_t* out);
 
+/* The clock a VALU-bound loop holds on `device` (needs a GPU): `reps` back-to-back
+ * launches of a multiply-add loop over every CU, `iters` iterations each; per workgroup of
+ * the last launch the shader-clock delta over the 100 MHz real-time delta.  mhz[3] =
+ * {median, min, max} over the workgroups.  A yardstick of the board, not of a kernel. */
+int klf_debug_clock(int device, uint32_t iters, uint32_t reps, double* mhz);
+
 #ifdef __cplusplus
 }
 #endif

@@ -2161,6 +2161,35 @@ extern "C" int klf_debug_match(const klf_pattern* pats, uint32_t n, const uint8_
   return KLF_OK;
 }
 
+extern "C" int klf_debug_clock(int device, uint32_t iters, uint32_t reps, double* mhz) {
+  if (!mhz || !iters || !reps) return KLF_EINVAL;
+  if (hipSetDevice(device) != hipSuccess) return KLF_EHIP;
+  int ncu = 0;
+  if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || ncu <= 0)
+    return KLF_EHIP;
+  const size_t nb = (size_t)ncu * 4;
+  uint64_t* d = nullptr;
+  if (hipMalloc(&d, (2 * nb + 1) * 8) != hipSuccess) return KLF_ENOMEM;
+  hipStream_t st = nullptr;
+  hipError_t h = hipStreamCreateWithFlags(&st, hipStreamNonBlocking);
+  if (h == hipSuccess) h = klf::clock_probe(ncu, iters, reps, d, st);
+  std::vector<uint64_t> v(2 * nb + 1, 0);
+  if (h == hipSuccess) h = hipMemcpyAsync(v.data(), d, v.size() * 8, hipMemcpyDeviceToHost, st);
+  if (h == hipSuccess) h = hipStreamSynchronize(st);
+  if (st) (void)hipStreamDestroy(st);
+  (void)hipFree(d);
+  if (h != hipSuccess) return KLF_EHIP;
+  std::vector<double> f;
+  for (size_t b = 0; b < nb; ++b)
+    if (v[2 * b + 1]) f.push_back(100.0 * (double)v[2 * b] / (double)v[2 * b + 1]);  // 100 MHz real time
+  if (f.empty()) return KLF_EHIP;
+  std::sort(f.begin(), f.end());
+  mhz[0] = f[f.size() / 2];
+  mhz[1] = f.front();
+  mhz[2] = f.back();
+  return KLF_OK;
+}
+
 extern "C" int klf_debug_since_digits(int64_t sec, int32_t nsec, uint32_t* out) {
   if (!out) return KLF_EINVAL;
   since_digits(sec, nsec, out);

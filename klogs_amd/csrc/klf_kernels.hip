@@ -3928,6 +3928,34 @@ hipError_t clear_timeline() {
 #endif
 }
 
+// Diagnostic (klf_debug_clock): the clock a VALU-bound loop holds on this board.  Per
+// workgroup the shader-clock and 100 MHz real-time deltas around the loop (s_memtime /
+// s_memrealtime reads) go to out[2 b], out[2 b + 1]; out[2 nblocks] only keeps the loop
+// alive.  Nothing else reads the buffer.
+__global__ __launch_bounds__(256) void k_clock(uint64_t* out, uint32_t iters) {
+  uint32_t x = threadIdx.x * 2654435761u + blockIdx.x, y = x ^ 0x9E3779B9u;
+  const uint64_t t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
+  for (uint32_t i = 0; i < iters; ++i) {
+    x = x * 1664525u + 1013904223u;
+    y = (y ^ (x >> 7)) + (x << 3);
+  }
+  const uint64_t t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+  if (threadIdx.x == 0) {
+    out[2 * blockIdx.x] = t1 - t0;
+    out[2 * blockIdx.x + 1] = r1 - r0;
+  }
+  if ((x ^ y) == 0x7E57C10Cu) out[2 * gridDim.x] = y;
+}
+hipError_t clock_probe(int num_cus, uint32_t iters, uint32_t reps, uint64_t* out, hipStream_t st) {
+  const uint32_t nb = (uint32_t)num_cus * 4;
+  for (uint32_t r = 0; r < reps; ++r) {  // back to back: the last one is read
+    hipLaunchKernelGGL(k_clock, dim3(nb), dim3(256), 0, st, out, iters);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
 hipError_t launch_gramhist(const uint8_t* bytes, const SegDesc* segs, uint32_t nsegs, uint64_t sample, uint32_t fold,
                            uint32_t* hist, hipStream_t st) {
   hipError_t e = hipMemsetAsync(hist, 0, kGramHistWords * 4, st);

@@ -368,6 +368,9 @@ hipError_t launch_retail(const RunArgs& a, hipStream_t stream, hipEvent_t* ev, i
 // Data statistics (kGramHistWords u32, zeroed here) of the first `sample` bytes of each of
 // up to 16 segments: byte counts, and the 2-grams at even offsets (folded like the
 // prefilter's grams).
+// Diagnostic: reps back-to-back launches of a VALU loop (num_cus x 4 workgroups); out
+// (2 num_cus x 4 + 1 u64) gets the last launch's per-workgroup shader / real-time deltas.
+hipError_t clock_probe(int num_cus, uint32_t iters, uint32_t reps, uint64_t* out, hipStream_t stream);
 hipError_t launch_gramhist(const uint8_t* bytes, const SegDesc* segs, uint32_t nsegs, uint64_t sample, uint32_t fold,
                            uint32_t* hist, hipStream_t stream);
 // Staged capture (klf_run): device chunks of the early H2D -> their places in the batch.

@@ -104,6 +104,7 @@ SIGNATURES = {
     "klf_debug_match": (C.c_int, [C.POINTER(_Pattern), C.c_uint32, C.c_void_p, C.c_size_t,
                                   C.POINTER(C.c_int)]),
     "klf_debug_since_digits": (C.c_int, [C.c_int64, C.c_int32, C.c_void_p]),
+    "klf_debug_clock": (C.c_int, [C.c_int, C.c_uint32, C.c_uint32, C.c_void_p]),
     "klf_debug_factors": (C.c_int, [C.c_void_p, C.c_size_t, C.c_uint32, C.c_char_p, C.c_size_t,
                                     C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]),
     "klf_debug_prefilter": (C.c_int, [C.POINTER(_Pattern), C.c_uint32, C.c_void_p, C.c_size_t, C.c_uint32,
@@ -265,6 +266,13 @@ def debug_since_digits(sec: int, nsec: int = 0):
     out = (C.c_uint32 * 6)()
     _check(_lib.klf_debug_since_digits(sec, nsec, out))
     return list(out)
+
+
+def debug_clock(device: int = 0, iters: int = 200_000, reps: int = 20):
+    """{median, min, max} MHz that a VALU loop holds on the device (needs a GPU)."""
+    out = (C.c_double * 3)()
+    _check(_lib.klf_debug_clock(device, iters, reps, out))
+    return {"median_mhz": round(out[0], 1), "min_mhz": round(out[1], 1), "max_mhz": round(out[2], 1)}
 
 
 @dataclass
