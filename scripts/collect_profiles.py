@@ -130,8 +130,10 @@ def main():
     for c, v in out.items():
         lines.append(f"* {c.upper()}: " + ", ".join(f"`{k}` {t}" for k, t in v["kernels"].items()))
     # counters of the roofline kernels: VALU per 8 KiB tile, LDS bank conflicts / LDS-active
-    lines += ["", "Counters of the scans (per launch):", "",
-              "| config | kernel | SQ_INSTS_VALU / 8 KiB tile | SQ_LDS_BANK_CONFLICT / SQ_ACTIVE_INST_LDS |", "|---|---|---|---|"]
+    lines += ["", "Counters of the scans (per launch; effective clock = GRBM_GUI_ACTIVE / 8 XCDs / the steady",
+              "launch time, the DVFS clock the chip holds under the kernel, MI355X_MICROARCH.md):", "",
+              "| config | kernel | SQ_INSTS_VALU / 8 KiB tile | SQ_LDS_BANK_CONFLICT / SQ_ACTIVE_INST_LDS | effective clock (GHz) |",
+              "|---|---|---|---|---|"]
     for c in CONFIGS:
         if c not in pmc or c not in out:
             continue
@@ -143,7 +145,12 @@ def main():
             v = p["SQ_INSTS_VALU"] / tiles if tiles else None  # (summed over the dispatch's rows)
             bc = p.get("SQ_LDS_BANK_CONFLICT"), p.get("SQ_ACTIVE_INST_LDS")
             r = bc[0] / bc[1] if bc[0] is not None and bc[1] else None
-            lines.append(f"| {c.upper()} | `{k}` | {'%.0f' % v if v else '—'} | {'%.2f' % r if r else '—'} |")
+            st = out[c].get("steady_us") if out[c]["kernel"] == k else None
+            clk = p["GRBM_GUI_ACTIVE"] / 8 / (st * 1e-6) / 1e9 if st and p.get("GRBM_GUI_ACTIVE") else None
+            if clk:
+                out[c]["effective_clock_ghz"] = round(clk, 3)
+            lines.append(f"| {c.upper()} | `{k}` | {'%.0f' % v if v else '—'} | {'%.2f' % r if r else '—'} | "
+                         f"{'%.2f' % clk if clk else '—'} |")
     (dst / "summary.md").write_text("\n".join(lines) + "\n")
     json.dump(out, open(dst / "summary.json", "w"), indent=1)
     print("\n".join(lines))
