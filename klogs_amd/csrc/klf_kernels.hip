@@ -1191,8 +1191,9 @@ __global__ __launch_bounds__(kThreads, MODE == kScanGen ? 3 : KLF_SCAN_OCC) void
         hq0 = hq1 = hq2 = hq3 = 0;
         xh = 0xFFFFFFFFu;
       }
-      const uint32_t nh = (uint32_t)(__popc(hq0) + __popc(hq1) + __popc(hq2) + __popc(hq3)) + (xh != 0xFFFFFFFFu ? 1u : 0u);
-      if (__any(nh != 0) && !abl) {
+      // (the count only where some lane has a hit: ~1.5 % of C5's tiles)
+      if (__any((hq0 | hq1 | hq2 | hq3) != 0u || xh != 0xFFFFFFFFu) && !abl) {
+        const uint32_t nh = (uint32_t)(__popc(hq0) + __popc(hq1) + __popc(hq2) + __popc(hq3)) + (xh != 0xFFFFFFFFu ? 1u : 0u);
         // tile-owned slots (u16 tile offsets, no atomics); only a tile with more than
         // kHitSlots hits spills the rest to the global list
         const uint32_t ih = wave_incl_scan_add(nh, lane);
