@@ -272,6 +272,23 @@ __device__ __forceinline__ uint32_t eq_mask16(const uint4& v, uint32_t c4) {
   return z(v.x) | (z(v.y) << 4) | (z(v.z) << 8) | (z(v.w) << 12);
 }
 
+// eq_mask16 for '\n' (any byte with bit 7 clear): bit 7 of x ^ c is bit 7 of x, so an
+// equal byte is ~((((x & 0x7F..) ^ c) + 0x7F..) | x) & 0x80..: and, xad, one 3-input op
+// per dword instead of six
+__device__ __forceinline__ uint32_t nor_and(uint32_t a, uint32_t b, uint32_t c) {  // ~(a | b) & c
+  uint32_t r;  // (v_bitop3 table: bit a*4 + b*2 + c; the compiler emits or, not, and)
+  asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x02" : "=v"(r) : "v"(a), "v"(b), "s"(c));
+  return r;
+}
+__device__ __forceinline__ uint32_t eq_mask16_nl(const uint4& v) {
+  auto z = [](uint32_t x) {
+    const uint32_t t = xad(x & 0x7F7F7F7Fu, 0x0A0A0A0Au, 0x7F7F7F7Fu);
+    const uint32_t f = nor_and(t, x, 0x80808080u);  // 0x80 per '\n'
+    return (f * 0x00204081u) >> 28;  // flags 7,15,23,31 -> bits 0..3 (no carries)
+  };
+  return z(v.x) | (z(v.y) << 4) | (z(v.z) << 8) | (z(v.w) << 12);
+}
+
 template <class T>
 __device__ __forceinline__ T wave_max(T x) {
 #pragma unroll
@@ -406,6 +423,9 @@ __device__ __forceinline__ bool parse_fast(const uint8_t* lds, uint32_t o, const
 #endif
 #ifndef KLF_SCAN_PRIO
 #define KLF_SCAN_PRIO 0  // s_setprio level while a wave stages its tile and issues the next one
+#endif
+#ifndef KLF_NL_MASK
+#define KLF_NL_MASK 1  // the exact newline positions with the three-op test (eq_mask16_nl)
 #endif
 #ifndef KLF_SCAN_BALLOT
 #define KLF_SCAN_BALLOT 1  // per-lane 0/1 counts (sparse lines) summed / ranked by ballots
@@ -657,7 +677,7 @@ __global__ __launch_bounds__(kThreads, MODE == kScanGen ? 3 : KLF_SCAN_OCC) void
     for (uint32_t m = nlc; m; m &= m - 1u) {
       const uint32_t c = (uint32_t)__builtin_ctz(m);
       const uint4 x = *reinterpret_cast<const uint4*>(s_tile + my0 + 16u * c);
-      const uint32_t e = clip(eq_mask16(x, 0x0A0A0A0Au), c) << ((c & 1u) * 16u);
+      const uint32_t e = clip(KLF_NL_MASK ? eq_mask16_nl(x) : eq_mask16(x, 0x0A0A0A0Au), c) << ((c & 1u) * 16u);
       const uint32_t q = c >> 1;
       em[0] |= q == 0 ? e : 0u;
       em[1] |= q == 1 ? e : 0u;
