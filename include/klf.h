@@ -184,7 +184,10 @@ int klf_result_pattern_counts(klf_result* r, uint32_t stream_id, uint64_t* count
  * fragment when the --tail window holds an unparseable line (SPEC.md S4), and that line
  * may sit in an earlier shard.  Reads the latest run's line meta (KLF_ESTATE otherwise). */
 int klf_result_last_unparsed(klf_result* r, uint32_t stream_id, uint64_t* rank);
-/* Device views (no copy): the concatenated output and the stream's [off, len) in it. */
+/* Device views: the concatenated output and the stream's [off, len) in it.  No copy, except
+ * for a one-pass result (KLF_COMPACT_ONEPASS), whose per-range extents the first call joins
+ * into a second engine-owned device buffer the size of the output; that buffer is freed when
+ * the engine's next run starts (the view is stale by then anyway) or at klf_close. */
 int klf_result_device_out(klf_result* r, uint32_t stream_id, const uint8_t** d_out,
                           uint64_t* off, uint64_t* len);
 /* Output write path: appends every stream's selected bytes to its open

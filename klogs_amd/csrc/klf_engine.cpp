@@ -204,6 +204,9 @@ struct klf_engine {
   DevBuf d_fext0, d_fext, d_frinfo, d_out2;
   uint32_t fuse_range = 0, fuse_nranges = 0, fuse_next = 0;  // the layout d_fext0 was made for
   std::vector<uint32_t> fuse_ext0;
+  // the segment table the extent table was built for: its own cache key (last_segs follows
+  // every run, fused or not, and a failed run may leave it behind d_fext0)
+  std::vector<SegDesc> fuse_segs;
   uint64_t pool_cap = 1 << 20;
   // lines per input byte of the last run (0: no run yet): sizes the line arrays of the next
   // runs (the first run sizes them from its own tile index, between two launch phases)
@@ -999,6 +1002,9 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
   if (!r) return KLF_ENOMEM;
   r->e = e;
   r->gen = ++e->gen;
+  // the contiguous copy of an earlier one-pass result (klf_result_device_out): that result
+  // is stale from here on (KLF_ESTATE), so is the copy
+  if (e->d_out2.p) e->d_out2.release();
   r->n_streams = n_streams;
   r->seg_of.assign(n_streams, -1);
   if (e->cs.also_all_pending && (f->flags & KLF_FILTER_PATTERN_COUNTS)) {
@@ -1161,7 +1167,10 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
     if (const char* v = getenv("KLF_DEBUG_FUSE_RANGE"))  // tests: short ranges (many range seams)
       R = std::max<uint64_t>(klf::kScanGroup, (uint64_t)atol(v) / klf::kScanGroup * klf::kScanGroup);
     const uint32_t nr = (uint32_t)((ntiles + R - 1) / R);
-    if (!same_layout || e->fuse_range != (uint32_t)R || e->fuse_nranges != nr) {
+    const bool same_fuse_layout = segs.size() == e->fuse_segs.size() &&
+                                  memcmp(segs.data(), e->fuse_segs.data(), segs.size() * sizeof(SegDesc)) == 0;
+    if (!same_fuse_layout || e->fuse_range != (uint32_t)R || e->fuse_nranges != nr) {
+      e->fuse_segs.clear();  // (invalid until the table below is on its way)
       e->fuse_ext0.assign(nr + 1, 0);
       for (uint32_t q = 0; q < nr; ++q) {
         const uint64_t t0 = (uint64_t)q * R, t1 = std::min<uint64_t>(t0 + R, ntiles) - 1;
@@ -1173,6 +1182,7 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
       e->fuse_range = (uint32_t)R;
       e->fuse_nranges = nr;
       e->fuse_next = e->fuse_ext0[nr];
+      e->fuse_segs = segs;
     }
     HIPCHK(e, e->d_fext.ensure((size_t)e->fuse_next * 16), "alloc fuse extents");
     HIPCHK(e, e->d_frinfo.ensure((size_t)e->fuse_nranges * 32), "alloc fuse range states");
@@ -1338,7 +1348,9 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
     ev_mask = 0;  // the events this attempt records (the timing queries read only those)
     r->so.resize(nsegs);
     uint32_t counters[32];
-    HIPCHK(e, e->h_rb.ensure(sizeof(counters) + nsegs * sizeof(SegOut)), "alloc readback");
+    // (+ a one-pass run's extents, read back with the counters: one sync on e->stream)
+    const size_t rb_ext = fuse_ok ? (size_t)e->fuse_next * 16 : 0;
+    HIPCHK(e, e->h_rb.ensure(sizeof(counters) + nsegs * sizeof(SegOut) + rb_ext), "alloc readback");
     // the literal automaton (klf_open's thread) is read from k_tindex on (deferred lines)
     auto join_ac = [&]() -> int {
       if (const int rc = ensure_ac(e); rc != KLF_OK) return rc;
@@ -1394,6 +1406,9 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
     HIPCHK(e, hipMemcpyAsync(rb, e->d_counters.p, sizeof(counters), hipMemcpyDeviceToHost, st), "D2H counters");
     HIPCHK(e, hipMemcpyAsync(rb + sizeof(counters), e->d_segout.p, nsegs * sizeof(SegOut), hipMemcpyDeviceToHost, st),
            "D2H segout");
+    if (a.fuse)
+      HIPCHK(e, hipMemcpyAsync(rb + sizeof(counters) + nsegs * sizeof(SegOut), e->d_fext.p, rb_ext,
+                               hipMemcpyDeviceToHost, st), "D2H extents");
     HIPCHK(e, wait_stream(st, 1000 + total_bytes / 2000000), "sync");
     mark("pipeline done");
     memcpy(counters, rb, sizeof(counters));
@@ -1435,7 +1450,7 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
     if (a.fuse) {  // the extents, in stream order (ranges ascend, and so do a range's streams)
       r->fused = true;
       r->fx.resize((size_t)e->fuse_next * 2);
-      HIPCHK(e, hipMemcpy(r->fx.data(), e->d_fext.p, (size_t)e->fuse_next * 16, hipMemcpyDeviceToHost), "D2H extents");
+      memcpy(r->fx.data(), rb + sizeof(counters) + nsegs * sizeof(SegOut), (size_t)e->fuse_next * 16);
       r->fx_first.assign(nsegs + 1, e->fuse_next);
       for (uint32_t q = e->fuse_nranges; q-- > 0;) {
         const uint32_t s0 = seg_of_tile((uint64_t)q * e->fuse_range);
@@ -1490,24 +1505,25 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
     }
   }
   // only the event pairs this run recorded (ev_mask): a pair it did not record would fail
-  // the query (or time an earlier run); a recorded pair that fails to read is an error
-  static const int kPairs[6][3] = {{1, 2, 0}, {2, 3, 1}, {3, 4, 2}, {4, 5, 3}, {0, 5, 4}, {0, 1, 5}};
-  for (const auto& q : kPairs)
-    if ((ev_mask >> q[0] & 1u) && (ev_mask >> q[1] & 1u)) {
-      float ms = 0.f;
-      HIPCHK(e, hipEventElapsedTime(&ms, e->ev[q[0]], e->ev[q[1]]), "timing events");
-      r->ms[q[2]] = ms;
+  // the query (or time an earlier run).  Timing is diagnostic: a recorded pair that fails to
+  // read leaves -1 in its slot (KLF_DIAG says so) and the filter result stands.
+  auto elapsed = [&](int k0, int k1, int slot) {
+    if (!((ev_mask >> k0 & 1u) && (ev_mask >> k1 & 1u))) return;
+    float ms = 0.f;
+    const hipError_t h = hipEventElapsedTime(&ms, e->ev[k0], e->ev[k1]);
+    if (h == hipSuccess) {
+      r->ms[slot] = ms;
+      return;
     }
-  if ((ev_mask >> 7 & 1u) && (ev_mask >> 8 & 1u)) {  // k_scan's dispatch alone
-    float ms = 0.f;
-    HIPCHK(e, hipEventElapsedTime(&ms, e->ev[7], e->ev[8]), "scan timing events");
-    r->ms[6] = ms;
-  }
-  if ((ev_mask >> 9 & 1u) && (ev_mask >> 10 & 1u)) {  // k_tcopy's dispatch alone (dense copy)
-    float ms = 0.f;
-    HIPCHK(e, hipEventElapsedTime(&ms, e->ev[9], e->ev[10]), "copy timing events");
-    r->ms[7] = ms;
-  }
+    (void)hipGetLastError();  // (the failed query's error is not the next call's)
+    r->ms[slot] = -1.0;
+    if (getenv("KLF_DIAG"))
+      fprintf(stderr, "[klf] timing events %d/%d unreadable: %s\n", k0, k1, hipGetErrorString(h));
+  };
+  static const int kPairs[6][3] = {{1, 2, 0}, {2, 3, 1}, {3, 4, 2}, {4, 5, 3}, {0, 5, 4}, {0, 1, 5}};
+  for (const auto& q : kPairs) elapsed(q[0], q[1], q[2]);
+  elapsed(7, 8, 6);   // k_scan's dispatch alone
+  elapsed(9, 10, 7);  // k_tcopy's dispatch alone (dense copy)
   r->ev_mask = ev_mask;
   r->total_lines = r->so[nsegs - 1].line_hi;
   for (auto& s : r->so) r->total_out = std::max(r->total_out, s.out_hi);

@@ -3832,7 +3832,26 @@ __global__ __launch_bounds__(256) void k_fcarry(RunArgs a) {
   const uint64_t rbase = sd.base + (uint64_t)(t0 - sd.tile0) * kTile;
   const uint8_t* src = a.bytes + rbase + lo;
   uint8_t* dst = a.out + rbase + res - clen;
-  for (uint64_t i = (uint64_t)lane; i < clen; i += 64) dst[i] = src[i];
+  // A range inside one long line carries up to the whole range (fuse_range tiles): the
+  // middle goes as aligned 16-B stores, each built from two aligned 16-B loads of the
+  // source (which may read up to 16 B past the carried bytes: inside the batch, whose
+  // allocation has kAllocSlack bytes past its last stream); bytewise only up to the first
+  // aligned destination chunk and after the last.
+  uint64_t head = (16u - (reinterpret_cast<uintptr_t>(dst) & 15u)) & 15u;
+  head = head < clen ? head : clen;
+  const uint64_t nmid = (clen - head) >> 4;
+  for (uint64_t i = (uint64_t)lane; i < head; i += 64) dst[i] = src[i];
+  {
+    const uintptr_t sa = reinterpret_cast<uintptr_t>(src + head);
+    const uint4* sb = reinterpret_cast<const uint4*>(sa & ~(uintptr_t)15);
+    const uint32_t so = (uint32_t)(sa & 15u);
+    uint4* db = reinterpret_cast<uint4*>(dst + head);
+    for (uint64_t k = (uint64_t)lane; k < nmid; k += 64) {
+      const uint4 x0 = sb[k];
+      db[k] = so ? extract16(x0, sb[k + 1], so) : x0;
+    }
+  }
+  for (uint64_t i = head + (nmid << 4) + (uint64_t)lane; i < clen; i += 64) dst[i] = src[i];
   if (lane == 0) {
     uint64_t* ex = a.fuse_ext + 2 * (size_t)a.fuse_ext0[r];
     ex[0] -= clen;

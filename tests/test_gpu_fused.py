@@ -151,6 +151,34 @@ def test_dense_tiles_rerun_two_pass(gpu):
     check([synth.generate(synth.TEXT, 34, 1, 200_000)])
 
 
+def test_extent_table_follows_the_layout(gpu, monkeypatch):
+    """One engine: a one-pass run on layout A, a --tail run on layout B (the same tile count,
+    other stream boundaries: more streams per range), then a one-pass run on B.  The third
+    run must rebuild the per-range extent table for B (the advisor's round-5 finding: it was
+    keyed on the last run's layout, which the --tail run had moved to B, so A's extent counts
+    were reused: writes past a range's extents and streams' bytes swapped)."""
+    monkeypatch.setenv("KLF_DEBUG_FUSE_RANGE", "8")
+    b = [synth.generate(synth.TEXT, 36, 1 + i, n) for i, n in enumerate((300_000, 300_000, 400_000))]
+    ntiles = lambda ss: sum((len(s) + 8191) // 8192 for s in ss)  # noqa: E731
+    nt = ntiles(b)
+    big = synth.generate(synth.TEXT, 36, 0, nt * 8192 + 100_000)
+    a = [big[:big.rindex(b"\n", 0, nt * 8192) + 1]]  # whole lines, the same tile count as b
+    assert ntiles(a) == nt
+    with E.Engine(0) as eng:
+        for streams, tail in ((a, -1), (b, 5), (b, -1), (a, -1)):
+            eng.reset()
+            eng.set_streams(len(streams))
+            for i, s in enumerate(streams):
+                eng.stage(i, s)
+            r = eng.run(tail=tail, n_streams=len(streams))
+            if tail < 0:
+                assert r.compaction() == "one_pass"
+            for i, s in enumerate(streams):
+                want = co.filter_stream(s, co.GO_ZERO_TIME, tail, [], want_lines=False, want_bits=False)[0]
+                assert r.stream(i).out == want, (tail, i)
+            r.free()
+
+
 def test_disabled_by_env(gpu, monkeypatch):
     monkeypatch.setenv("KLF_FUSE", "0")
     check([synth.generate(synth.TEXT, 35, 0, 500_000)], want_mode="tiles|gather")
