@@ -1284,11 +1284,18 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
     a.lazy_index = lazy_index ? 1u : 0u;
     a.plan_runs = (lazy_index && want_truns && compact_mode != 1 &&
                    !(getenv("KLF_PLAN_RUNS") && !strcmp(getenv("KLF_PLAN_RUNS"), "0"))) ? 1u : 0u;
+    // windowed line index: literal patterns, and (round 6) prefiltered regex sets, whose
+    // candidate lines get their bounds from k_verify; per-pattern counts too (k_fixcount's
+    // deferred lines, like k_match's fallback, ask for a rerun with the whole index)
+    const bool win_rx = !(getenv("KLF_WIN_INDEX_RX") && !strcmp(getenv("KLF_WIN_INDEX_RX"), "0"));
     a.win_index = (win_ok &&
                    (mode == klf::CompiledSet::kLiteral1 ||
-                    (mode == klf::CompiledSet::kGeneral && e->cs.qf_on && e->cs.rx_count == 0 && !count && !e->cs.also_all)) &&
+                    (mode == klf::CompiledSet::kGeneral && e->cs.qf_on && !e->cs.also_all &&
+                     ((e->cs.rx_count == 0 && !count) || win_rx))) &&
                    !(getenv("KLF_WIN_INDEX") && !strcmp(getenv("KLF_WIN_INDEX"), "0"))) ? 1u : 0u;
     a.scatter_mode = 0;
+    // waves per scatter group (0: k_scatter picks it from its grid; tests force a split)
+    a.scatter_split = getenv("KLF_SCATTER_SPLIT") ? (uint32_t)std::max(0L, atol(getenv("KLF_SCATTER_SPLIT"))) : 0u;
     a.count_pats = count ? 1u : 0u;
     a.pcount = count ? e->d_pcount.as<uint32_t>() : nullptr;
     a.pairs = count ? e->d_pairs.as<uint64_t>() : nullptr;

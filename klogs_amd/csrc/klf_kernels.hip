@@ -1278,7 +1278,10 @@ __global__ __launch_bounds__(kThreads, MODE == kScanGen ? 3 : KLF_SCAN_OCC) void
       const bool hh = LIT && __any(n_hit != 0);  // some line starting here holds the literal
       const uint32_t w3 = ((dense ? 1u : 0u) | (carry ? 2u : 0u) | (dd ? 4u : 0u) | (hh ? 8u : 0u)) |
                           ((uint32_t)(uint16_t)(GEN ? tile_hits : carry) << 16);  // GEN: hit slots used
-      const uint32_t nunits = abl ? 0u : (dense ? 8u : ((kRecHead + nlines + 31u) & ~31u) / 4u);
+      // (every reader takes the TileStat from the compact tstat array and a tile's slots only
+      // below its line count: a tile where no line starts writes nothing here -- C5: ~40 % of
+      // its tiles, 128 B each)
+      const uint32_t nunits = (abl || (nlines == 0u && !dense)) ? 0u : (dense ? 8u : ((kRecHead + nlines + 31u) & ~31u) / 4u);
       const __amdgpu_buffer_rsrc_t rrs = __builtin_amdgcn_make_buffer_rsrc(trec, 0, (int)(nunits * 16u), 0x00020000);
       typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
       for (uint32_t u = (uint32_t)lane; u < (nunits > 64u ? 128u : 64u); u += 64) {  // one or two stores
@@ -1653,6 +1656,9 @@ __device__ __forceinline__ void scatter_body(RunArgs& a, uint32_t bid, uint32_t 
   // needs the index; the dense path lists lines from the slots (the host builds the index
   // on demand: klf_result_lines, klf_retail, klf_result_last_unparsed)
   if (a.lazy_index && a.counters[kCtrDense]) return;
+  // the windowed index's pre-count pass of a general set: only deferred lines (fix_tile's
+  // matches) carry slot hit bits there, and without a deferred line there is nothing to do
+  if (a.scatter_mode == 1 && a.grep_mode == kGrepGeneral && !a.counters[kCtrDefer]) return;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   uint32_t* err_flag = a.counters + 2;
   const uint32_t ngroups = (a.ntiles + kScatterGroup - 1) / kScatterGroup;
@@ -1660,7 +1666,17 @@ __device__ __forceinline__ void scatter_body(RunArgs& a, uint32_t bid, uint32_t 
   // their concatenation: the stream by a search of the prefix)
   const bool wpass = a.scatter_mode == 2;
   const uint64_t F = wpass ? (a.counters[2] ? 0 : a.wgrp[2 * a.nsegs]) : ngroups;  // (overflow: no list)
-  for (uint64_t f = bid * 4 + wv; f < F; f += nb * 4) {
+  // small batches: P waves per group, each writing a P-th of the group's lines (C1: 128
+  // groups of ~5,400 lines were 128 waves walking their lines 64 at a time)
+  // (P from the grid: up to 8; RunArgs::scatter_split overrides it, tests)
+  uint32_t P = a.scatter_split;
+  if (P == 0) {
+    const uint64_t w = (uint64_t)nb * 4 / (F ? F : 1);
+    P = w < 1 ? 1u : (w > 8 ? 8u : (uint32_t)w);
+  }
+  for (uint64_t fp = bid * 4 + wv; fp < F * P; fp += nb * 4) {
+    const uint64_t f = fp / P;
+    const uint32_t part = (uint32_t)(fp - f * P);
     uint32_t g = (uint32_t)f;
     if (wpass) {
       uint32_t lo = 0, hi = a.nsegs;  // the last stream whose prefix is <= f
@@ -1695,7 +1711,7 @@ __device__ __forceinline__ void scatter_body(RunArgs& a, uint32_t bid, uint32_t 
       e.seg = s;
       e.pad[0] = e.pad[1] = 0;
       s_ent[wv][lane] = e;
-      if ((ts.flags & 2u) && base < a.cap_lines && a.scatter_mode != 2) {
+      if ((ts.flags & 2u) && base < a.cap_lines && a.scatter_mode != 2 && part == 0) {
         // literal hit inside the line carried in from an earlier tile: that line's start
         // is the last staged start of the nearest earlier tile of the stream that has one
         // (the window pass skips it: the pre-count pass set those bits already)
@@ -1717,7 +1733,7 @@ __device__ __forceinline__ void scatter_body(RunArgs& a, uint32_t bid, uint32_t 
         if (cs >= 0 && rel_lo + (int64_t)ts.carry_off - 1 - (int64_t)kCarryBias >= cs)
           atomicOr(&a.bits[base >> 5], 1u << (base & 31));
       }
-      if (last) {
+      if (last && part == 0) {
         const uint64_t lend = base + ts.events;
         if (lend <= a.cap_lines) a.line_off[lend + s] = sd.len;
         else atomicOr(err_flag, 1u);
@@ -1725,9 +1741,11 @@ __device__ __forceinline__ void scatter_body(RunArgs& a, uint32_t bid, uint32_t 
     }
     const uint32_t incl = wave_incl_scan_add(n, lane);
     s_pre[wv][lane] = incl;
-    const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+    const uint32_t gtotal = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+    // this wave's part of the group's lines: [lb, total)
+    const uint32_t lb = (uint32_t)((uint64_t)gtotal * part / P), total = (uint32_t)((uint64_t)gtotal * (part + 1) / P);
     wave_lds_sync();
-    for (uint32_t l0 = 0; l0 < total; l0 += 64 * kScatterBatch) {
+    for (uint32_t l0 = lb; l0 < total; l0 += 64 * kScatterBatch) {
       uint32_t sl[kScatterBatch], kk[kScatterBatch], jj[kScatterBatch];
 #pragma unroll
       for (int u = 0; u < kScatterBatch; ++u) {
@@ -1933,7 +1951,31 @@ __device__ void verify_hit_from(const RunArgs& a, uint32_t tile, uint32_t s, con
       continue;
     }
     if (!a.count_pats && ((a.bits[l >> 5] >> (l & 31)) & 1u)) continue;  // counting: every regex decides
-    push_candidate(a, vq, l | ((uint64_t)E.z << 40), (uint64_t)(rel_lo + x));  // (the occurrence: stream offset)
+    if (a.win_index) {
+      // windowed line index (no full k_scatter): the candidate line's start, end and meta for
+      // k_nfa_win / k_nfa.  Its end is the next line start: this tile's next slot, else the
+      // first start a later tile of the stream lists, else the stream end (every writer of
+      // these entries writes the same values)
+      uint64_t le = sd.len;
+      if ((uint32_t)lo < nl) {
+        le = (uint64_t)rel_lo + (list[lo] & kSlotOff);
+      } else {
+        for (uint32_t pt = tile + 1; pt < sd.tile0 + sd.ntiles; ++pt) {
+          const TileStat pst = a.tstat[pt];
+          const int64_t prel = (int64_t)(pt - sd.tile0) * kTile;
+          const uint32_t pk1 = prel + kTile >= (int64_t)sd.len ? pst.events : pst.events + 1;
+          if (pk1 <= 1u) continue;  // (k0 = 1: no line starts in tile pt)
+          const uint32_t* psrc = (pst.flags & 1u) ? a.pool + pst.pool_base : a.slots + (size_t)pt * kRecStride + kRecHead;
+          le = (uint64_t)prel + (psrc[0] & kSlotOff);
+          break;
+        }
+      }
+      a.line_off[l + s] = ls;
+      a.line_off[l + s + 1] = le;
+      a.meta[l] = mt;
+    }
+    // {line | regex << 40, the occurrence (stream offset) | stream << 40}
+    push_candidate(a, vq, l | ((uint64_t)E.z << 40), (uint64_t)(rel_lo + x) | ((uint64_t)s << 40));
   }
 }
 
@@ -2169,7 +2211,7 @@ __global__ __launch_bounds__(256) void k_nfa(RunArgs a) {
     const uint64_t l = e & ((1ull << 40) - 1);
     const uint32_t r = (uint32_t)(e >> 40);
     if (P.rx_pre[r] != kRxPreNone) continue;  // bounded window: k_nfa_win
-    const uint32_t s = find_seg_by_line(a.segout, a.nsegs, l);
+    const uint32_t s = (uint32_t)(a.cand[2 * (size_t)i + 1] >> 40);  // (k_verify: the stream)
     if (!a.count_pats && ((a.bits[l >> 5] >> (l & 31)) & 1u)) continue;
     const uint16_t m = a.meta[l];
     if (!(m & Meta::kParsed)) continue;
@@ -2192,6 +2234,10 @@ __global__ __launch_bounds__(256) void k_nfa(RunArgs a) {
 // lines runs here, one wave per tile that deferred a line, once the line index is built.
 __global__ __launch_bounds__(256) void k_fixcount(RunArgs a) {
   if (!a.counters[kCtrDefer] || a.counters[2]) return;
+  if (a.win_index) {  // the deferred lines' bounds need the whole index: the host reruns with it
+    if (blockIdx.x == 0 && threadIdx.x == 0) a.counters[kCtrRedo] = 1u;
+    return;
+  }
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   for (uint32_t tile = blockIdx.x * 4 + wv; tile < a.ntiles; tile += gridDim.x * 4) {
     const TileStat ts = a.tstat[tile];
@@ -2263,13 +2309,14 @@ __global__ __launch_bounds__(256) void k_nfa_win(RunArgs a) {
     if (!a.count_pats && ((a.bits[l >> 5] >> (l & 31)) & 1u)) continue;
     const uint16_t m = a.meta[l];
     if (!(m & Meta::kParsed)) continue;
-    const uint32_t s = find_seg_by_line(a.segout, a.nsegs, l);
+    const uint64_t xs = a.cand[2 * (size_t)i + 1];
+    const uint32_t s = (uint32_t)(xs >> 40);  // (k_verify: the stream, no search of the segments)
+    const uint64_t x = xs & ((1ull << 40) - 1);
     const uint8_t* segp = a.bytes + a.segs[s].base;
     const uint64_t ls = a.line_off[l + s], le = a.line_off[l + s + 1];
     const uint64_t cs = ls + line_plen(a, m, segp, ls, le);
     uint64_t ce = le;
     if (ce > cs && segp[ce - 1] == '\n') --ce;
-    const uint64_t x = a.cand[2 * (size_t)i + 1];
     if (x < cs || x >= ce) continue;  // an occurrence in the timestamp prefix: no match holds it
     bool hit = (P.rx_flags[r] & 1u) != 0;
     if (!hit) {
@@ -2279,13 +2326,22 @@ __global__ __launch_bounds__(256) void k_nfa_win(RunArgs a) {
       const uint64_t* F = T.fol + (size_t)r * T.fstride;
       const uint64_t ws = x - cs > pre ? x - pre : cs;
       uint64_t d = ws == cs ? V[2] : first;
-      uint64_t p = ws;
-      for (; p < ce && d; ++p) {
-        const uint64_t c = d & B[T.cls[segp[p]]];
-        if (c & lastm) { hit = true; break; }
-        uint64_t nd = p + 1 <= x ? first : 0ull;
-        for (uint64_t mm = c; mm; mm &= mm - 1) nd |= F[__ffsll((unsigned long long)mm) - 1];
-        d = nd;
+      uint64_t p = ws;  // the next byte to run
+      // the window's bytes 16 at a time (aligned loads; segments are 256-B aligned and the
+      // batch has read slack past its end): one load round trip per 16 bytes, not per byte
+      for (uint64_t q = ws & ~15ull; q < ce && d && !hit; q += 16) {
+        const uint4 v = *reinterpret_cast<const uint4*>(segp + q);
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+          if (q + j != p || p >= ce || !d || hit) continue;
+          const uint64_t c = d & B[T.cls[(w[j >> 2] >> (8 * (j & 3))) & 0xFFu]];
+          if (c & lastm) { hit = true; continue; }
+          uint64_t nd = p + 1 <= x ? first : 0ull;
+          for (uint64_t mm = c; mm; mm &= mm - 1) nd |= F[__ffsll((unsigned long long)mm) - 1];
+          d = nd;
+          ++p;
+        }
       }
       if (!hit && p == ce) hit = (d & V[3]) != 0;
     }
@@ -4071,7 +4127,8 @@ hipError_t launch_scatter(const RunArgs& a, hipStream_t st, int num_cus) {
 #ifndef KLF_SCATTER_GRID
 #define KLF_SCATTER_GRID 8  // k_scatter workgroups per CU at most
 #endif
-  uint32_t sg = ((a.ntiles + kScatterGroup - 1) / kScatterGroup + 3) / 4;
+  // up to 8 waves per 64-tile group (scatter_body splits a group's lines over them)
+  uint32_t sg = ((a.ntiles + kScatterGroup - 1) / kScatterGroup * 8 + 3) / 4;
   if (sg > (uint32_t)num_cus * KLF_SCATTER_GRID) sg = num_cus * KLF_SCATTER_GRID;
   if (sg == 0) return hipSuccess;
   hipLaunchKernelGGL(k_scatter, dim3(sg), dim3(256), 0, st, a);
@@ -4160,7 +4217,9 @@ hipError_t launch_pipeline(const RunArgs& a0, hipStream_t st, hipEvent_t* ev, in
     uint32_t nsb = ((a.ntiles + kScatterGroup - 1) / kScatterGroup + 3) / 4;
     if (nsb > (uint32_t)num_cus * 4) nsb = num_cus * 4;
     if (nsb == 0) nsb = 1;
-    hipLaunchKernelGGL(k_scatter_verify, dim3(nsb + num_cus * 8), dim3(256), 0, st, a, nsb);
+    RunArgs w = a;  // windowed index: the scatter part is the pre-count pass (deferred lines only)
+    if (a.win_index) w.scatter_mode = 1;
+    hipLaunchKernelGGL(k_scatter_verify, dim3(nsb + num_cus * 8), dim3(256), 0, st, w, nsb);
     KLF_TRY(hipGetLastError());
   } else if (a.win_index) {  // tiles with deferred lines now: their match bits come from the slots
     RunArgs w = a;

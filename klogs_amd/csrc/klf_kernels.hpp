@@ -303,7 +303,7 @@ struct RunArgs {
   uint32_t max_cblocks; // compaction block capacity
   uint32_t stage_times; // record the inner stage events (ev[2..4])
   uint64_t* cand;       // [2 * cand_cap] NFA candidates: {global line index | regex << 40,
-                        //  stream offset of the factor occurrence}
+                        //  stream offset of the factor occurrence | stream << 40}
   uint32_t cand_cap;
   uint16_t* hslots;     // [ntiles * kHitSlots] prefilter hits (tile offsets of the samples)
   uint32_t* hflat;      // [hflat_cap] hit slot ids (tile * kHitSlots + j), flattened by k_tbase
@@ -322,12 +322,13 @@ struct RunArgs {
   // the scan plans the dense compaction (kept runs per tile + tile aggregates; needs truns):
   // k_tkeep's listing pass is skipped unless a line was deferred
   uint32_t plan_runs;
-  // literal patterns only (one literal, or a set without regexes and per-pattern counts):
-  // the global line index is built after k_tailw for the lines of the tail windows only
-  // (k_scatter mode 2); tiles with deferred lines or single-literal hits before k_mcount
-  // (mode 1: their match bits come from the slots)
+  // literal patterns and prefiltered regex sets (round 6): the global line index is built
+  // after k_tailw for the lines of the tail windows only (k_scatter mode 2); tiles with
+  // deferred lines or single-literal hits before k_mcount (mode 1: their match bits come
+  // from the slots); k_verify writes the NFA candidate lines' bounds and meta
   uint32_t win_index;
   uint32_t scatter_mode;  // k_scatter: 0 every tile, 1 tiles with deferred lines, 2 tiles meeting a window
+  uint32_t scatter_split; // k_scatter: waves per 64-tile group (small batches: a group's lines split over them; 0 = 1)
   // per-pattern counts (KLF_FILTER_PATTERN_COUNTS): pcount[segment * n_cids + cid] lines,
   // each (line, cid) counted once through the `pairs` hash set (open addressing, u64 keys)
   uint32_t count_pats;

@@ -455,6 +455,60 @@ def test_windowed_line_index(gpu, monkeypatch, win):
     check_against_c(streams, None, 50, lits)
 
 
+@pytest.mark.parametrize("win", ["1", "0"])
+def test_windowed_index_regex_sets(gpu, monkeypatch, win):
+    """Regex sets index only their tail windows too (round 6): k_verify writes each NFA
+    candidate line's start, end and meta -- the end from this tile's next slot or the first
+    later tile that lists a line start (1-32 KiB lines span several tiles) -- for k_nfa_win /
+    k_nfa, and the whole index is built on demand (r.lines).  Against the Python oracle with
+    KLF_WIN_INDEX_RX on and off: tails from none to all lines, since, deferred lines
+    (adversarial prefixes), unbounded regexes (k_nfa), mixed literal + regex sets, klf_retail
+    to other tails, and the candidate-queue overflow (k_match needs every line: the run is
+    redone with the whole index)."""
+    monkeypatch.setenv("KLF_WIN_INDEX_RX", win)
+    rx = synth.c5_regexes()
+    streams = [synth.generate(synth.LONGJSON, 41, 0, 1_200_000, permille=30),
+               synth.generate(synth.ADVERSARIAL, 42, 1, 3000, drop_final_nl=True, permille=40), b"",
+               synth.generate(synth.LONGJSON, 43, 3, 700_000, drop_final_nl=True, permille=30)]
+    for tail in (-1, 0, 1, 7, 10**9):
+        check_against_py(streams, None, tail, match=rx)
+    check_against_py(streams, (synth.T0 + 1800, 0), 25, match=rx)
+    for grep, match in (GEN_SETS[0], GEN_SETS[2], GEN_SETS[4]):
+        check_against_py(streams, None, 9, grep, match)
+    # klf_retail on the windowed run: the tail stage again over the index and bitmap in HBM
+    pats = po.compile_patterns([], rx)
+    with E.Engine(0, match=rx) as eng:
+        eng.set_streams(len(streams))
+        for i, s in enumerate(streams):
+            if s:
+                eng.stage(i, s)
+        r = eng.run(tail=3, n_streams=len(streams))
+        for t2 in (50, 1, -1):
+            r2 = r.retail(t2)
+            for i, s in enumerate(streams):
+                assert r2.stream(i).out == po.filter_stream(s, GZ, t2, pats).out, (t2, i)
+            r = r2
+        r.free()
+    monkeypatch.setenv("KLF_CAND_CAP", "16")
+    check_against_py(streams[:1], None, 5, match=rx)
+
+
+@pytest.mark.parametrize("split", ["3", "8"])
+def test_scatter_split(gpu, monkeypatch, split):
+    """k_scatter with each 64-tile group's lines split over several waves (small batches
+    such as C1 pick the split from the grid; forced here on every shape): the whole index,
+    the window pass, the pre-count pass, on-demand indexes."""
+    monkeypatch.setenv("KLF_SCATTER_SPLIT", split)
+    streams = [synth.generate(synth.TEXT, 71, 0, 3_000_000),
+               synth.generate(synth.ADVERSARIAL, 72, 1, 3000, drop_final_nl=True, permille=40), b"",
+               synth.generate(synth.JSON, 73, 2, 900_000, permille=20)]
+    for tail in (-1, 100):
+        check_against_c(streams, None, tail, [])
+    check_against_c(streams, (synth.T0 + 1800, 0), 40, [synth.NEEDLE])
+    check_against_c(streams, None, 30, synth.c4_literals(1024)[:200])
+    check_against_py(streams[:2], None, 12, match=synth.c5_regexes())
+
+
 def _long_window_stream(pre_bytes, long_len, after, lit=b"ms"):
     """Short lines up to `pre_bytes`, then one line of `long_len` content bytes holding `lit`,
     then `after` short lines holding it: a --tail after+1 window starts at the long line."""
