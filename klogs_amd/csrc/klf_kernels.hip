@@ -166,6 +166,7 @@ __device__ __forceinline__ uint16_t make_meta(bool ok, bool since_ok, uint32_t p
 
 constexpr uint32_t kSlotOff = 0x3FFFu, kSlotDefer = 0x4000u, kSlotHit = 0x8000u;
 constexpr uint32_t kCtrDefer = 5;  // counters[5]: some line of this run was deferred
+constexpr uint32_t kTsInline = 16u;  // TileStat.flags: the tile's single line slot is its pool_base word
 // Kept runs of one tile (a selected line carries a >= 20-B prefix, so at most kTile / 20
 // + 2 runs: the carried-in line's and those of the lines starting in the tile) and its
 // 16-B output chunks (513 at most, in groups of 8: 16-B LDS accesses).
@@ -432,6 +433,9 @@ __device__ __forceinline__ bool parse_fast(const uint8_t* lds, uint32_t o, const
 #endif
 #ifndef KLF_SCAN_PACKSUM
 #define KLF_SCAN_PACKSUM 1  // the tile's parsed / since_ok counts in one wave reduction
+#endif
+#ifndef KLF_TS_INLINE
+#define KLF_TS_INLINE 1  // a tile where one line starts keeps its slot in the TileStat (no record store)
 #endif
 #ifndef KLF_SCAN_SUMSKIP
 // no count reductions on tiles where no line starts (C5: ~half its tiles): 6.33 -> 6.29 ms
@@ -1273,15 +1277,17 @@ __global__ __launch_bounds__(kThreads, MODE == kScanGen ? 3 : KLF_SCAN_OCC) void
     {  // the record region in 16-B units, whole 128-B lines: unit 0 the TileStat, unit u
        // slots 4u - 4 .. 4u - 1 (garbage past the last slot; a dense tile's slots are in
        // the pool).  16 B per lane: narrower per-lane stores cost several times more per byte.
-      const uint32_t w0 = agg, w1 = dense ? pool_base : 0u;
+      // (a tile where exactly one line starts keeps that slot in its TileStat: kTsInline)
+      const bool inl = KLF_TS_INLINE && !dense && nlines == 1u;
+      const uint32_t w0 = agg, w1 = dense ? pool_base : (inl ? s_list[0] : 0u);
       const uint32_t w2 = (pp & 0xFFFFu) | (qq << 16);
       const bool hh = LIT && __any(n_hit != 0);  // some line starting here holds the literal
-      const uint32_t w3 = ((dense ? 1u : 0u) | (carry ? 2u : 0u) | (dd ? 4u : 0u) | (hh ? 8u : 0u)) |
+      const uint32_t w3 = ((dense ? 1u : 0u) | (carry ? 2u : 0u) | (dd ? 4u : 0u) | (hh ? 8u : 0u) | (inl ? kTsInline : 0u)) |
                           ((uint32_t)(uint16_t)(GEN ? tile_hits : carry) << 16);  // GEN: hit slots used
       // (every reader takes the TileStat from the compact tstat array and a tile's slots only
       // below its line count: a tile where no line starts writes nothing here -- C5: ~40 % of
       // its tiles, 128 B each)
-      const uint32_t nunits = (abl || (nlines == 0u && !dense)) ? 0u : (dense ? 8u : ((kRecHead + nlines + 31u) & ~31u) / 4u);
+      const uint32_t nunits = (abl || (nlines == 0u && !dense) || inl) ? 0u : (dense ? 8u : ((kRecHead + nlines + 31u) & ~31u) / 4u);
       const __amdgpu_buffer_rsrc_t rrs = __builtin_amdgcn_make_buffer_rsrc(trec, 0, (int)(nunits * 16u), 0x00020000);
       typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
       for (uint32_t u = (uint32_t)lane; u < (nunits > 64u ? 128u : 64u); u += 64) {  // one or two stores
@@ -1393,6 +1399,15 @@ __device__ bool general_count(const RunArgs& a, const uint8_t* p, int64_t n, uin
   return any;
 }
 
+// A tile's line slots: dense tiles in the pool, a tile where exactly one line starts in its
+// TileStat's pool_base word (kTsInline, round 6: no 128-B record store for it; C5's most
+// common tile), every other tile in its record region.
+__device__ __forceinline__ uint32_t* slot_list(const RunArgs& a, const TileStat& ts, uint32_t tile) {
+  return (ts.flags & 1u) ? a.pool + ts.pool_base
+         : (ts.flags & kTsInline) ? reinterpret_cast<uint32_t*>(a.tstat + tile) + 1
+                                  : a.slots + (size_t)tile * kRecStride + kRecHead;
+}
+
 // One wave: the deferred lines of `tile` (TileStat ts) through the general parse; their
 // slots are rewritten in place and the parsed / since_ok counts the tile gains are
 // returned (wave-uniform).
@@ -1405,7 +1420,7 @@ __device__ void fix_tile(const RunArgs& a, uint32_t tile, const TileStat& ts, in
   const bool first = rel_lo == 0, last = rel_lo + kTile >= seg_len;
   const uint32_t k0 = first ? 0 : 1, k1 = last ? ts.events : ts.events + 1;
   const uint32_t nlines = k1 > k0 ? k1 - k0 : 0;
-  uint32_t* list = (ts.flags & 1u) ? a.pool + ts.pool_base : a.slots + (size_t)tile * kRecStride + kRecHead;
+  uint32_t* list = slot_list(a, ts, tile);
   const uint8_t* segp = a.bytes + sd.base;
   uint32_t dp = 0, dq = 0;
   for (uint32_t j = lane; j < nlines; j += 64) {
@@ -1526,7 +1541,9 @@ __global__ __launch_bounds__(256) void k_tindex(RunArgs a) {
         if ((uint32_t)r == rr) {
           ts[r].parsed = (uint16_t)(ts[r].parsed + s_fix[slot][0]);
           ts[r].since_ok = (uint16_t)(ts[r].since_ok + s_fix[slot][1]);
-          a.tstat[tb + r] = ts[r];  // the corrected counts for every later kernel
+          // the corrected counts for every later kernel (only their word: fix_tile rewrote an
+          // inline slot in pool_base, which ts[r] holds from before)
+          reinterpret_cast<uint32_t*>(a.tstat + tb + r)[2] = (uint32_t)ts[r].parsed | ((uint32_t)ts[r].since_ok << 16);
         }
       dmask &= dmask - 1u;
     }
@@ -1707,7 +1724,8 @@ __device__ __forceinline__ void scatter_body(RunArgs& a, uint32_t bid, uint32_t 
       ScatterEnt e;
       e.base = base + k0;
       e.rel_lo = (uint64_t)rel_lo;
-      e.src = (ts.flags & 1u) ? (ts.pool_base | 0x80000000u) : 0u;
+      // slot 0's source: the pool (bit 31), the TileStat itself (bit 30: kTsInline), the record
+      e.src = (ts.flags & 1u) ? (ts.pool_base | 0x80000000u) : (ts.flags & kTsInline) ? 0x40000000u : 0u;
       e.seg = s;
       e.pad[0] = e.pad[1] = 0;
       s_ent[wv][lane] = e;
@@ -1723,7 +1741,7 @@ __device__ __forceinline__ void scatter_body(RunArgs& a, uint32_t bid, uint32_t 
           const uint32_t pk0 = prel == 0 ? 0 : 1;
           const uint32_t pn = pst.events + 1 > pk0 ? pst.events + 1 - pk0 : 0;  // never the stream's last tile
           if (pn == 0) continue;
-          const uint32_t* psrc = (pst.flags & 1u) ? a.pool + pst.pool_base : a.slots + (size_t)pt * kRecStride + kRecHead;
+          const uint32_t* psrc = slot_list(a, pst, pt);
           const uint32_t v = psrc[pn - 1];
           const uint32_t mt = v >> 16;
           // a deferred line had its whole content searched by k_fixup
@@ -1762,7 +1780,8 @@ __device__ __forceinline__ void scatter_body(RunArgs& a, uint32_t bid, uint32_t 
           const uint32_t j = l - (lo ? s_pre[wv][lo - 1] : 0u);
           const uint32_t src = s_ent[wv][lo].src;
           const uint32_t* sp = (src & 0x80000000u) ? a.pool + (src & 0x7FFFFFFFu)
-                                                   : a.slots + (size_t)(g * kScatterGroup + lo) * kRecStride + kRecHead;
+                               : (src & 0x40000000u) ? reinterpret_cast<const uint32_t*>(a.tstat + g * kScatterGroup + lo) + 1
+                                                     : a.slots + (size_t)(g * kScatterGroup + lo) * kRecStride + kRecHead;
           sl[u] = sp[j];
           kk[u] = lo;
           jj[u] = j;
@@ -1889,12 +1908,27 @@ __device__ void verify_hit_from(const RunArgs& a, uint32_t tile, uint32_t s, con
     const int32_t x = p - (int32_t)((E.y >> 16) & 0xFFu);
     if (rel_lo + x < 0 || rel_lo + x + (int64_t)m > (int64_t)sd.len) continue;
     const uint32_t lm = (E.y & kQfLoose) ? 0x20202020u : 0u;
-    bool eq = true;
-    for (uint32_t k = 0; k < m && eq; k += 4) {
-      const uint32_t nb = m - k < 4 ? m - k : 4;
-      const uint32_t msk = nb == 4 ? 0xFFFFFFFFu : ((1u << (8 * nb)) - 1);
-      const uint32_t want = k == 0 ? E.w : P.qf_nbytes[E.x + (k >> 2)];
-      eq = (((gword(segp + rel_lo + x + k) | lm) ^ want) & msk) == 0;
+    auto msk_of = [&](uint32_t k) { return m - k >= 4 ? 0xFFFFFFFFu : ((1u << (8 * (m - k))) - 1u); };
+    // the first dword (from the entry: most prefilter false hits end here), then dwords 1..7
+    // with every load in flight at once (one memory round trip, not one per dword), then
+    // the rest of a needle longer than 32 bytes dword by dword
+    const uint8_t* q = segp + rel_lo + x;
+    bool eq = (((gword(q) | lm) ^ E.w) & msk_of(0)) == 0;
+    if (eq && m > 4) {
+      const uintptr_t qa = reinterpret_cast<uintptr_t>(q);
+      const uint32_t* qw = reinterpret_cast<const uint32_t*>(qa & ~(uintptr_t)3);
+      const uint32_t sh = (uint32_t)(qa & 3);
+      uint32_t d[9], want[8];
+#pragma unroll
+      for (int k = 1; k < 9; ++k) d[k] = (4u * (uint32_t)k < m + 4u) ? qw[k] : 0u;  // (read slack past the batch)
+#pragma unroll
+      for (int k = 1; k < 8; ++k) want[k] = 4u * (uint32_t)k < m ? P.qf_nbytes[E.x + (uint32_t)k] : 0u;
+#pragma unroll
+      for (int k = 1; k < 8; ++k)
+        if (4u * (uint32_t)k < m)
+          eq = eq && ((((__builtin_amdgcn_alignbyte(d[k + 1], d[k], sh)) | lm) ^ want[k]) & msk_of(4u * (uint32_t)k)) == 0;
+      for (uint32_t k = 32; k < m && eq; k += 4)
+        eq = (((gword(q + k) | lm) ^ P.qf_nbytes[E.x + (k >> 2)]) & msk_of(k)) == 0;
     }
     if (!eq) continue;
 #if KLF_ABL & 32
@@ -1906,7 +1940,7 @@ __device__ void verify_hit_from(const RunArgs& a, uint32_t tile, uint32_t s, con
     const bool first = rel_lo == 0, last = rel_lo + kTile >= (int64_t)sd.len;
     const uint32_t k0 = first ? 0 : 1, k1 = last ? ts.events : ts.events + 1;
     const uint32_t nl = k1 > k0 ? k1 - k0 : 0;
-    const uint32_t* list = (ts.flags & 1u) ? a.pool + ts.pool_base : a.slots + (size_t)tile * kRecStride + kRecHead;
+    const uint32_t* list = slot_list(a, ts, tile);
     int lo = 0, hi = x < 0 ? 0 : (int)nl;  // starts <= x
     while (lo < hi) {
       const int mid = (lo + hi) >> 1;
@@ -1932,7 +1966,7 @@ __device__ void verify_hit_from(const RunArgs& a, uint32_t tile, uint32_t s, con
         const uint32_t pk0 = prel == 0 ? 0u : 1u;
         const uint32_t pn = pst.events + 1 - pk0;  // an earlier tile is never the stream's last
         if (pn == 0) continue;
-        const uint32_t* psrc = (pst.flags & 1u) ? a.pool + pst.pool_base : a.slots + (size_t)pt * kRecStride + kRecHead;
+        const uint32_t* psrc = slot_list(a, pst, pt);
         v = psrc[pn - 1];
         vrel = prel;
         break;
@@ -1965,7 +1999,7 @@ __device__ void verify_hit_from(const RunArgs& a, uint32_t tile, uint32_t s, con
           const int64_t prel = (int64_t)(pt - sd.tile0) * kTile;
           const uint32_t pk1 = prel + kTile >= (int64_t)sd.len ? pst.events : pst.events + 1;
           if (pk1 <= 1u) continue;  // (k0 = 1: no line starts in tile pt)
-          const uint32_t* psrc = (pst.flags & 1u) ? a.pool + pst.pool_base : a.slots + (size_t)pt * kRecStride + kRecHead;
+          const uint32_t* psrc = slot_list(a, pst, pt);
           le = (uint64_t)prel + (psrc[0] & kSlotOff);
           break;
         }
@@ -2248,7 +2282,7 @@ __global__ __launch_bounds__(256) void k_fixcount(RunArgs a) {
     const bool first = rel_lo == 0, last = rel_lo + kTile >= (int64_t)sd.len;
     const uint32_t k0 = first ? 0 : 1, k1 = last ? ts.events : ts.events + 1;
     const uint32_t nlines = k1 > k0 ? k1 - k0 : 0;
-    const uint32_t* list = (ts.flags & 1u) ? a.pool + ts.pool_base : a.slots + (size_t)tile * kRecStride + kRecHead;
+    const uint32_t* list = slot_list(a, ts, tile);
     const uint8_t* segp = a.bytes + sd.base;
     for (uint32_t j = lane; j < nlines; j += 64) {
       const uint32_t sl = list[j];
@@ -2319,7 +2353,7 @@ __global__ __launch_bounds__(256) void k_nfa_win(RunArgs a) {
     if (ce > cs && segp[ce - 1] == '\n') --ce;
     if (x < cs || x >= ce) continue;  // an occurrence in the timestamp prefix: no match holds it
     bool hit = (P.rx_flags[r] & 1u) != 0;
-    if (!hit) {
+    if (!hit && !(KLF_ABL & 32768)) {  // (timing build 32768: no window runs)
       const uint64_t* V = T.vec + 4 * (size_t)r;
       const uint64_t first = V[0], lastm = V[1];
       const uint64_t* B = T.b + (size_t)r * T.classes;
@@ -2938,18 +2972,25 @@ __device__ __forceinline__ void cgather_body(RunArgs& a) {
     if (lane == 63) { s_wb[wv] = ib; s_wc[wv] = ic; }
     __syncthreads();
     uint64_t ob = a.csum[3 * blk] + ib - r.bytes, oc = a.csum[3 * blk + 1] + ic - r.nsel;
-    for (int k = 0; k < wv; ++k) { ob += s_wb[k]; oc += s_wc[k]; }
+    // the block's selected lines only, compacted (k: selected lines of the block before
+    // this one): a window block holds mostly unselected lines when a pattern is given (C2:
+    // ~1 in 100), whose zero-length entries the chunk walks below stepped over one by one
+    uint32_t k = (uint32_t)(ic - r.nsel);
+    for (int w = 0; w < wv; ++w) { ob += s_wb[w]; oc += s_wc[w]; k += (uint32_t)s_wc[w]; }
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const int i = t * 4 + j;
       if (sub == 0 && r.first[j]) { a.segout[r.seg[j]].out_lo = ob; a.segout[r.seg[j]].sel_lo = oc; }
-      s_src[i] = r.src[j];
-      s_dst[i] = ob;
-      s_len[i] = r.len[j];
+      if (r.sel[j]) {
+        s_src[k] = r.src[j];
+        s_dst[k] = ob;
+        s_len[k] = r.len[j];
+        ++k;
+      }
       ob += r.len[j];
       oc += r.sel[j] ? 1 : 0;  // = k_csum's count (an empty fragment is still a line out)
       if (sub == 0 && r.last[j]) { a.segout[r.seg[j]].out_hi = ob; a.segout[r.seg[j]].sel_hi = oc; }
     }
+    const uint32_t nsel_blk = (uint32_t)(s_wc[0] + s_wc[1] + s_wc[2] + s_wc[3]);
     const uint64_t ob0 = a.csum[3 * blk];
     const uint64_t ob1 = ob0 + s_wb[0] + s_wb[1] + s_wb[2] + s_wb[3];
     const uint64_t c0 = ob0 + (uint64_t)sub * cs;
@@ -2964,9 +3005,7 @@ __device__ __forceinline__ void cgather_body(RunArgs& a) {
       const uint32_t nmap = c1 > c0 ? (uint32_t)(((c1 + 15) >> 4) - cb0) : 0u;
       for (uint32_t k = (uint32_t)t; k < nmap; k += kThreads) s_map[k] = 0;
       __syncthreads();
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int i = t * 4 + j;
+      for (uint32_t i = (uint32_t)t; i < nsel_blk; i += kThreads) {
         const uint64_t d = s_dst[i], e = d + s_len[i];
         const uint64_t lo = d > c0 ? d : c0, hi = e < c1 ? e : c1;
         if (lo >= hi) continue;
@@ -3038,7 +3077,7 @@ struct TileLines {
   int64_t cstart;
 };
 __device__ __forceinline__ const uint32_t* tile_slot_list(const RunArgs& a, const TileStat& ts, uint32_t tile) {
-  return (ts.flags & 1u) ? a.pool + ts.pool_base : a.slots + (size_t)tile * kRecStride + kRecHead;
+  return slot_list(a, ts, tile);
 }
 // (wave-uniform) the slot fields of g, grep-none runs only.  The stream's first tile lists
 // its line 0 at offset 0, so the walk back always ends at a tile with a slot.
@@ -3573,6 +3612,9 @@ __global__ __launch_bounds__(256) void k_cmove(RunArgs a) {
 #ifndef KLF_TC_ABL
 #define KLF_TC_ABL 0  // timing builds: 1 no copy loop, 2 no map and no copy, 4 no tile loads
 #endif
+#ifndef KLF_COPY_UNALIGNED
+#define KLF_COPY_UNALIGNED 1  // copy_tile_runs' 16-B windows as one unaligned LDS read (0: five dwords + v_alignbyte)
+#endif
 // The compaction copy of one tile, one wave: the tile's bytes in LDS (s_buf; 16 B readable
 // before it and 32 B after it), its kept runs s_run[0, nr) (u32: tile offset of the run's
 // first byte | its offset in the tile's output << 16, ascending), `kept` output bytes at
@@ -3641,6 +3683,16 @@ __device__ __forceinline__ void copy_tile_runs(const uint8_t* s_buf, uint32_t* s
     // LDS window at any alignment (five dword reads + v_alignbyte; +16: the front pad)
     auto window = [&](uint32_t r, uint32_t x0, uint32_t (&y)[4]) __attribute__((always_inline)) {
       const int32_t va = (int32_t)(r & 0xFFFFu) + (int32_t)x0 - (int32_t)(r >> 16) + 16;
+      if (KLF_COPY_UNALIGNED) {
+        // one unaligned 16-B LDS read (gfx950, HSA default unaligned mode; parse_fast reads
+        // the same way): consecutive lanes read consecutive 16 B, where five dword reads at a
+        // 4-dword lane stride hit every bank four times (C3: 2.04x conflict cycles)
+        typedef uint32_t u32x4w __attribute__((ext_vector_type(4)));
+        u32x4w v;
+        __builtin_memcpy(&v, reinterpret_cast<const uint8_t*>(s32) + va, 16);
+        y[0] = v.x; y[1] = v.y; y[2] = v.z; y[3] = v.w;
+        return;
+      }
       const int32_t wa = va >> 2;
       const uint32_t w0 = s32[wa], w1 = s32[wa + 1], w2 = s32[wa + 2], w3 = s32[wa + 3], w4 = s32[wa + 4];
       y[0] = __builtin_amdgcn_alignbyte(w1, w0, (uint32_t)va);
@@ -4060,6 +4112,42 @@ hipError_t launch_gramhist(const uint8_t* bytes, const SegDesc* segs, uint32_t n
   const uint64_t dwords = nseg * (sample / 4);
   const uint32_t grid = (uint32_t)((dwords + kGhDwords - 1) / kGhDwords);
   hipLaunchKernelGGL(k_gramhist, dim3(grid ? grid : 1), dim3(256), 0, st, bytes, segs, nsegs, sample, fold, hist);
+  return hipGetLastError();
+}
+
+// A first run's line density without a mid-run readback (literal and pattern-less runs; the
+// prefiltered sets take it from k_gramhist's sample): block b counts the newlines of one
+// 8 KiB tile spread evenly over the batch and writes {newlines, bytes} to out[2 b].
+__global__ __launch_bounds__(256) void k_nlsample(const uint8_t* __restrict__ bytes, const SegDesc* __restrict__ segs,
+                                                  uint32_t nsegs, uint32_t ntiles, uint32_t* __restrict__ out) {
+  __shared__ uint32_t s_w[4];
+  const uint32_t tile = (uint32_t)((uint64_t)blockIdx.x * ntiles / gridDim.x);
+  const uint32_t s = find_seg_by_tile(segs, nsegs, tile);
+  const SegDesc sd = segs[s];
+  const uint64_t rel = (uint64_t)(tile - sd.tile0) * kTile;
+  const uint32_t valid = (uint32_t)(sd.len - rel < (uint64_t)kTile ? sd.len - rel : (uint64_t)kTile);
+  const uint32_t o = threadIdx.x * 32u;
+  uint32_t nl = 0;
+  if (o < valid) {
+    const uint4* p = reinterpret_cast<const uint4*>(bytes + sd.base + rel + o);
+    const uint4 x0 = p[0], x1 = p[1];  // (past the stream end: masked below; the batch has read slack)
+    const uint32_t m = eq_mask16_nl(x0) | (eq_mask16_nl(x1) << 16);
+    const uint32_t n = valid - o;
+    nl = (uint32_t)__popc(n >= 32u ? m : (m & ((1u << n) - 1u)));
+  }
+  nl = wave_sum(nl);
+  if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = nl;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    out[2 * blockIdx.x] = s_w[0] + s_w[1] + s_w[2] + s_w[3];
+    out[2 * blockIdx.x + 1] = valid;
+  }
+}
+
+hipError_t launch_nlsample(const uint8_t* bytes, const SegDesc* segs, uint32_t nsegs, uint32_t ntiles, uint32_t blocks,
+                           uint32_t* out, hipStream_t st) {
+  if (ntiles == 0 || blocks == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_nlsample, dim3(blocks), dim3(256), 0, st, bytes, segs, nsegs, ntiles, out);
   return hipGetLastError();
 }
 

@@ -180,10 +180,11 @@ static_assert(sizeof(TRec) == 16, "TRec is one 16-B record");
 // Per-tile record of the scan (K1a), 16 B.
 struct TileStat {
   uint32_t events;     // line-end events in the tile
-  uint32_t pool_base;  // dense tiles: first pool slot
+  uint32_t pool_base;  // dense tiles: first pool slot; a tile where one line starts (bit4): that slot
   uint16_t parsed, since_ok;
   uint16_t flags;      // bit0 dense (slots in the pool), bit1 literal hit in the carried-in line,
-                       // bit2 some line deferred to k_fixup, bit3 literal hit in a line starting here
+                       // bit2 some line deferred to k_fixup, bit3 literal hit in a line starting here,
+                       // bit4 the tile's single slot is pool_base (no record region written)
   uint16_t carry_off;  // literal: 1 + kCarryBias + tile offset of the furthest hit in the
                        // carried-in line (0 = none); general sets: hit slots used
 };
@@ -372,6 +373,8 @@ hipError_t launch_retail(const RunArgs& a, hipStream_t stream, hipEvent_t* ev, i
 // Diagnostic: reps back-to-back launches of a VALU loop (num_cus x 4 workgroups); out
 // (2 num_cus x 4 + 1 u64) gets the last launch's per-workgroup shader / real-time deltas.
 hipError_t clock_probe(int num_cus, uint32_t iters, uint32_t reps, uint64_t* out, hipStream_t stream);
+hipError_t launch_nlsample(const uint8_t* bytes, const SegDesc* segs, uint32_t nsegs, uint32_t ntiles, uint32_t blocks,
+                           uint32_t* out, hipStream_t st);
 hipError_t launch_gramhist(const uint8_t* bytes, const SegDesc* segs, uint32_t nsegs, uint64_t sample, uint32_t fold,
                            uint32_t* hist, hipStream_t stream);
 // Staged capture (klf_run): device chunks of the early H2D -> their places in the batch.

@@ -493,6 +493,27 @@ def test_windowed_index_regex_sets(gpu, monkeypatch, win):
     check_against_py(streams[:1], None, 5, match=rx)
 
 
+@pytest.mark.parametrize("mode", ["sample", "underestimate", "two_phase"])
+def test_first_run_line_sample(gpu, monkeypatch, mode):
+    """A fresh engine's first run (literal or no patterns) sizes its line arrays from a
+    newline count over 64 tiles spread over the batch (k_nlsample, read back before the
+    scan) instead of reading the line count back between the scan and the rest.  An
+    estimate far too low (KLF_DEBUG_NL_SCALE) overflows and reruns with the exact count;
+    KLF_TWO_PHASE keeps the two-phase first run.  Dense and sparse parts in one batch,
+    against the C oracle (run_engine opens a fresh engine per call)."""
+    if mode == "underestimate":
+        monkeypatch.setenv("KLF_DEBUG_NL_SCALE", "0.0001")
+    if mode == "two_phase":
+        monkeypatch.setenv("KLF_TWO_PHASE", "1")
+    long = synth.generate(synth.LONGJSON, 81, 0, 3_000_000)
+    dense = b"".join(b"2024-10-22T00:00:%02d.000000000Z x\n" % (i % 60) for i in range(60_000)) + b"\n" * 40_000
+    streams = [long, dense, b"", synth.generate(synth.TEXT, 82, 3, 500_000)]
+    for tail in (-1, 50):
+        check_against_c(streams, None, tail, [])
+    check_against_c(streams, (synth.T0 + 1800, 0), 30, [b"x"])
+    check_against_c(streams, None, 20, synth.c4_literals(1024)[:100] + [b" x"])
+
+
 @pytest.mark.parametrize("split", ["3", "8"])
 def test_scatter_split(gpu, monkeypatch, split):
     """k_scatter with each 64-tile group's lines split over several waves (small batches
