@@ -961,6 +961,7 @@ static hipError_t wait_stream(hipStream_t st, uint64_t spin_us) {
 // still in HBM (k_mcount .. k_tcopy, tens of us), then read the stream records back.
 static hipError_t grow_out_retail(klf_engine* e, klf::RunArgs& a, std::vector<SegOut>& so) {
   a.plan_runs = 0;  // the tile plans were consumed (k_cmove rewrote them): list the runs again
+  a.skip_tcopy = 0;
   for (int k = 0; k < 2; ++k) {
     uint64_t need = 0;
     for (auto& s : so) need = std::max(need, s.out_hi);
@@ -1149,7 +1150,7 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
     return KLF_OK;
   };
   std::vector<std::pair<DevBuf*, size_t>> ws = {
-      {&e->d_tstat, ntiles * sizeof(klf::TileStat)}, {&e->d_slots, ntiles * klf::kRecStride * 4},
+      {&e->d_tstat, ntiles * sizeof(klf::TileStat)},
       {&e->d_tile_base, ntiles * 8}, {&e->d_bsum, (ntiles / 1024 + 2) * 4 * 8},
       {&e->d_counters, klf::kNumCounters * 4}, {&e->d_segout, nsegs * sizeof(SegOut)},
       {&e->d_wpre, (3 * (size_t)nsegs + 2) * 8} /* + wgrp */, {&e->d_trec, ntiles * sizeof(klf::TRec)}, {&e->d_kbase, ntiles * 16}};
@@ -1234,7 +1235,7 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
   if (need_hits) {
     ws.push_back({&e->d_qhits, (size_t)qhits_cap * 8});
     ws.push_back({&e->d_hslots, (size_t)ntiles * klf::kHitSlots * 2});
-    ws.push_back({&e->d_hflat, (size_t)hflat_cap * 4});
+    ws.push_back({&e->d_hflat, (size_t)hflat_cap * 8});
   }
   HIPCHK(e, ensure_all(e->d_block, e->block_users, ws), "alloc workspace");
 
@@ -1257,8 +1258,19 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
   // a first run with the sample's line density: the line arrays from it (x2 + a margin:
   // an overflow reruns with exact sizes), in one launch phase
   const bool density_cap = e->line_density == 0.0 && est_density > 0.0 && !getenv("KLF_TWO_PHASE");
+  // Where the scan keeps the slots of tiles with two or more line starts (round 6): long lines
+  // (under one per KiB: C5) -> per-wave chunks of the pool, no record regions allocated at all
+  // (C5 k_scan -1.4 %, cold 8.6 -> 8.3 ms); shorter lines -> the per-tile record regions,
+  // 1,152 B per tile, written as whole lines (C2 / C3 / C4 ran 0.7-1.5 % faster on them,
+  // r6g).  KLF_WAVE_POOL=1 / 0 forces either.
+  const double dens = e->line_density > 0.0 ? e->line_density : est_density;
+  const char* wpv = getenv("KLF_WAVE_POOL");
+  const bool wave_pool = wpv ? strcmp(wpv, "0") != 0 : (dens > 0.0 && dens * 1024.0 < 1.0);
+  if (!wave_pool) HIPCHK(e, e->d_slots.ensure(ntiles * klf::kRecStride * 4), "alloc line records");
   if (density_cap)
     cap = std::min<uint64_t>(cap, (uint64_t)(est_density * (double)total_bytes * 2.0) + 2ull * nsegs + 65536);
+  uint32_t pool_chunk = 256;  // (per attempt, below: the wave pool's chunk size)
+  bool force_match = false;   // an overflowed hit list / NFA queue: redo the run with k_match
   // every RunArgs field but the line arrays (alloc_lines) of a run over the whole batch
   auto fill_args = [&](klf::RunArgs& a, int attempt) {
     memset(static_cast<void*>(&a), 0, sizeof(a));
@@ -1283,9 +1295,11 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
     a.lit_words = e->d_lit.as<uint32_t>();
     memcpy(static_cast<void*>(&a.pats), &e->dpats, sizeof(a.pats));
     a.tstat = e->d_tstat.as<klf::TileStat>();
-    a.slots = e->d_slots.as<uint32_t>();
+    a.slots = wave_pool ? nullptr : e->d_slots.as<uint32_t>();
     a.pool = e->d_pool.as<uint32_t>();
     a.pool_cap = e->pool_cap;
+    a.wave_pool = wave_pool ? 1u : 0u;
+    a.pool_chunk = pool_chunk;
     a.tile_base = e->d_tile_base.as<uint64_t>();
     a.bsum = e->d_bsum.as<uint64_t>();
     a.counters = e->d_counters.as<uint32_t>();
@@ -1299,7 +1313,7 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
     a.cand_cap = need_cand ? e->cand_cap : 0;
     a.qhits = need_hits ? e->d_qhits.as<uint64_t>() : nullptr;
     a.hslots = need_hits ? e->d_hslots.as<uint16_t>() : nullptr;
-    a.hflat = need_hits ? e->d_hflat.as<uint32_t>() : nullptr;
+    a.hflat = need_hits ? e->d_hflat.as<uint64_t>() : nullptr;
     a.hflat_cap = need_hits ? hflat_cap : 0;
     a.qhits_cap = need_hits ? qhits_cap : 0;
     a.trec = e->d_trec.as<klf::TRec>();
@@ -1319,6 +1333,12 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
                      ((e->cs.rx_count == 0 && !count) || win_rx))) &&
                    !(getenv("KLF_WIN_INDEX") && !strcmp(getenv("KLF_WIN_INDEX"), "0"))) ? 1u : 0u;
     a.scatter_mode = 0;
+    // no launch of kernels that would exit at once (each costs ~4 us plus its boundary):
+    // k_match beside a working prefilter, k_tcopy in a --tail run before any went dense
+    a.skip_match = (mode == klf::CompiledSet::kGeneral && e->cs.qf_on && !e->cs.also_all && !force_match &&
+                    !(getenv("KLF_SKIP_IDLE") && !strcmp(getenv("KLF_SKIP_IDLE"), "0"))) ? 1u : 0u;
+    a.skip_tcopy = (f->tail >= 0 && !e->dense_tail_seen && compact_mode == 0 &&
+                    !(getenv("KLF_SKIP_IDLE") && !strcmp(getenv("KLF_SKIP_IDLE"), "0"))) ? 1u : 0u;
     // waves per scatter group (0: k_scatter picks it from its grid; tests force a split)
     a.scatter_split = getenv("KLF_SCATTER_SPLIT") ? (uint32_t)std::max(0L, atol(getenv("KLF_SCATTER_SPLIT"))) : 0u;
     a.count_pats = count ? 1u : 0u;
@@ -1374,9 +1394,22 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
       x.max_cblocks = (uint32_t)mcb;
       return hipSuccess;
     };
+    // the pool: every tile where two or more lines start (16-B aligned: <= 3 spare slots each),
+    // dense tiles, and the waves' partly used last chunks (wave_pool); an overflow reruns
+    // with the count the scan reserved
+    pool_chunk = 256;
+    if (wave_pool) {
+      const uint64_t nwaves = (uint64_t)e->num_cus * 16;
+      const uint64_t per_wave = (cap + 2 * ntiles) / nwaves;
+      while (pool_chunk < 4096 && pool_chunk * 4 < per_wave) pool_chunk *= 2;
+      e->pool_cap = std::max<uint64_t>(e->pool_cap, cap + 3 * ntiles + nwaves * pool_chunk + 1024);
+      if (e->pool_cap >= (1ull << 31)) return set_err(e, KLF_EINVAL, "batch too large (line slot pool)");
+    }
     HIPCHK(e, e->d_pool.ensure(e->pool_cap * 4), "alloc pool");
     klf::RunArgs a;
     fill_args(a, attempt);
+    if (attempt == 0 && getenv("KLF_DEBUG_POOL_CAP"))  // tests: a first attempt whose pool overflows
+      a.pool_cap = std::min<uint64_t>(a.pool_cap, (uint64_t)std::max(1L, atol(getenv("KLF_DEBUG_POOL_CAP"))));
     ev_mask = 0;  // the events this attempt records (the timing queries read only those)
     r->so.resize(nsegs);
     uint32_t counters[32];
@@ -1403,7 +1436,7 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
       memcpy(counters, rb1, sizeof(counters));
       memcpy(r->so.data(), rb1 + sizeof(counters), nsegs * sizeof(SegOut));
       if (counters[2]) {  // the dense-tile pool overflowed: a whole rerun (as below)
-        e->pool_cap = std::max<uint64_t>(e->pool_cap, (uint64_t)counters[klf::kCtrPool] + 1024);
+        e->pool_cap = std::max<uint64_t>(e->pool_cap, (uint64_t)counters[klf::kCtrPool] + (uint64_t)e->num_cus * 16 * 4096);
         e->line_density = (double)(r->so[nsegs - 1].line_hi + 1) / (double)total_bytes;
         cap = std::min<uint64_t>(cap, r->so[nsegs - 1].line_hi + 2);
         continue;
@@ -1454,8 +1487,20 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
     if (overflow) {  // more lines (or dense-tile slots) than estimated: rerun with exact sizes
       if (line_reruns++) break;
       cap = std::min(std::max<uint64_t>(cap, r->so[nsegs - 1].line_hi + 2), cap_clamp);
-      e->pool_cap = std::max<uint64_t>(e->pool_cap, (uint64_t)counters[klf::kCtrPool] + 1024);
+      e->pool_cap = std::max<uint64_t>(e->pool_cap, (uint64_t)counters[klf::kCtrPool] + (uint64_t)e->num_cus * 16 * 4096);
       continue;
+    }
+    if (a.skip_match && (counters[klf::kCtrQOver] || counters[klf::kCtrHitsOver])) {  // k_match decides: redo with it
+      force_match = true;
+      continue;
+    }
+    if (a.skip_tcopy && counters[klf::kCtrDense]) {  // the dense path without its copy: launch it now
+      uint32_t* rb1 = e->h_rb.as<uint32_t>();
+      HIPCHK(e, klf::launch_tcopy(a, st, nullptr, e->num_cus, nullptr), "launch tile copy");
+      HIPCHK(e, hipMemcpyAsync(rb1, e->d_counters.p, sizeof(counters), hipMemcpyDeviceToHost, st), "D2H counters");
+      HIPCHK(e, hipStreamSynchronize(st), "sync tile copy");
+      counters[klf::kCtrOutShort] = rb1[klf::kCtrOutShort];
+      a.skip_tcopy = 0;  // (klf_retail from this run launches it)
     }
     if (a.fuse && counters[klf::kCtrFuseBad]) {  // a deferred line or a dense tile: the two-pass rerun
       fuse_ok = false;
@@ -1595,6 +1640,7 @@ extern "C" int klf_retail(klf_engine* e, klf_result* prev, int64_t tail, klf_res
     a.stage_times = 0;
     a.fuse = 0;  // (the two-pass compaction, over the line index)
     a.plan_runs = 0;  // (plans assume --tail -1 and are consumed by the run)
+    a.skip_tcopy = 0;  // (another window may take the dense path)
     hipStream_t st = e->stream;
     uint32_t rmask = 0;
     hipError_t h = klf::launch_retail(a, st, e->ev, e->num_cus, &rmask);

@@ -167,6 +167,7 @@ __device__ __forceinline__ uint16_t make_meta(bool ok, bool since_ok, uint32_t p
 constexpr uint32_t kSlotOff = 0x3FFFu, kSlotDefer = 0x4000u, kSlotHit = 0x8000u;
 constexpr uint32_t kCtrDefer = 5;  // counters[5]: some line of this run was deferred
 constexpr uint32_t kTsInline = 16u;  // TileStat.flags: the tile's single line slot is its pool_base word
+constexpr uint32_t kTsHitInline = 32u;  // TileStat.flags (general sets): its 1-2 prefilter hits are pool_base's halves
 // Kept runs of one tile (a selected line carries a >= 20-B prefix, so at most kTile / 20
 // + 2 runs: the carried-in line's and those of the lines starting in the tile) and its
 // 16-B output chunks (513 at most, in groups of 8: 16-B LDS accesses).
@@ -434,6 +435,12 @@ __device__ __forceinline__ bool parse_fast(const uint8_t* lds, uint32_t o, const
 #ifndef KLF_SCAN_PACKSUM
 #define KLF_SCAN_PACKSUM 1  // the tile's parsed / since_ok counts in one wave reduction
 #endif
+#ifndef KLF_VERIFY_PAR
+#define KLF_VERIFY_PAR 0  // k_verify: 1 loads a needle's dwords 1..7 at once (C4: 468 vs 452 us, more VGPRs, r6e)
+#endif
+#ifndef KLF_HIT_INLINE
+#define KLF_HIT_INLINE 0  // 1: a tile's 1-2 prefilter hits in its TileStat (C4 k_scan +2.8 %, r6e)
+#endif
 #ifndef KLF_TS_INLINE
 #define KLF_TS_INLINE 1  // a tile where one line starts keeps its slot in the TileStat (no record store)
 #endif
@@ -510,6 +517,7 @@ __global__ __launch_bounds__(kThreads, MODE == kScanGen ? 3 : KLF_SCAN_OCC) void
   // register quad there spills), a register quad for GEN (LDS is what bounds its occupancy)
   __shared__ uint4 s_gstat[GEN ? 1 : kWaves][kScanGroup];
   __shared__ uint32_t s_qf[GEN ? kQfWords : 1];  // q-gram bitmap of the needles
+  __shared__ uint32_t s_h2[GEN ? kWaves : 1][1];  // a tile's inline hits (kTsHitInline): two u16
   // wv is wave-uniform; readfirstlane tells the compiler so (tile indices stay in SGPRs and
   // the descriptor reads stay scalar loads)
   const int t = threadIdx.x, lane = t & 63, wv = __builtin_amdgcn_readfirstlane(t >> 6);
@@ -578,6 +586,7 @@ __global__ __launch_bounds__(kThreads, MODE == kScanGen ? 3 : KLF_SCAN_OCC) void
     __builtin_amdgcn_raw_buffer_store_b32(0u, none, 0x7FFF0000u, 0, 0);
   }
   bool any_defer = false;
+  uint32_t wp_cur = 0, wp_end = 0;  // the wave's pool chunk (wave_pool): next free slot, end
   // FUSE state of the wave's range (wave-uniform): whether the line open at the current tile
   // start is decided (a line started in this range's part of the stream, or the part began
   // at the stream's start), that line's kept bit and content start - the tile start (f_sat),
@@ -719,7 +728,7 @@ __global__ __launch_bounds__(kThreads, MODE == kScanGen ? 3 : KLF_SCAN_OCC) void
     if (dense) {
       uint32_t pb = 0;
       if (lane == 0 && !abl) {
-        pb = atomicAdd(&a.counters[kCtrPool], nlines);
+        pb = atomicAdd(&a.counters[kCtrPool], (nlines + 31u) & ~31u);  // (whole 128-B lines: the waves' chunks stay aligned)
         if ((uint64_t)pb + nlines > a.pool_cap) atomicOr(err_flag, 1u);
       }
       pool_base = (uint32_t)__builtin_amdgcn_readlane((int)pb, 0);
@@ -996,6 +1005,8 @@ __global__ __launch_bounds__(kThreads, MODE == kScanGen ? 3 : KLF_SCAN_OCC) void
     }
 
     uint32_t tile_hits = 0;
+    bool hinl = false;  // GEN: the tile's hits inline (kTsHitInline)
+    uint32_t hit2 = 0;
     // ---- general sets: fused q-gram prefilter ----
     // Samples p = 0 mod QS of the tile (each needle's chosen window is q + QS - 1 long, so
     // every occurrence spans exactly one sample whose gram lies in the window) probe the
@@ -1216,7 +1227,7 @@ __global__ __launch_bounds__(kThreads, MODE == kScanGen ? 3 : KLF_SCAN_OCC) void
         xh = 0xFFFFFFFFu;
       }
       // (the count only where some lane has a hit: ~1.5 % of C5's tiles)
-      if (__any((hq0 | hq1 | hq2 | hq3) != 0u || xh != 0xFFFFFFFFu) && !abl) {
+      if (__any((hq0 | hq1 | hq2 | hq3) != 0u || xh != 0xFFFFFFFFu) && (!abl || (KLF_ABL & (65536 | 131072)))) {
         const uint32_t nh = (uint32_t)(__popc(hq0) + __popc(hq1) + __popc(hq2) + __popc(hq3)) + (xh != 0xFFFFFFFFu ? 1u : 0u);
         // tile-owned slots (u16 tile offsets, no atomics); only a tile with more than
         // kHitSlots hits spills the rest to the global list
@@ -1228,10 +1239,15 @@ __global__ __launch_bounds__(kThreads, MODE == kScanGen ? 3 : KLF_SCAN_OCC) void
           ob = (uint32_t)__builtin_amdgcn_readlane((int)ob, 63);
         }
         uint16_t* hs = a.hslots + (size_t)tile * kHitSlots;
+        // one or two hits of a tile that keeps no line slot in its TileStat go to its
+        // pool_base halves (KLF_HIT_INLINE): no 2-B stores into a half-written 64-B slot line
+        // (C4: ~1.4 M tiles with hits per step)
+        hinl = KLF_HIT_INLINE && tot <= 2u && !dense && nlines != 1u;
+        uint16_t* hd = hinl ? reinterpret_cast<uint16_t*>(s_h2[GEN ? wv : 0]) : hs;
         uint32_t k = ih - nh;
         if (xh != 0xFFFFFFFFu) {
           if (k < kHitSlots) {
-            hs[k] = (uint16_t)xh;
+            hd[k] = (uint16_t)xh;
           } else if ((uint64_t)ob + (k - kHitSlots) < a.qhits_cap) {
             a.qhits[ob + (k - kHitSlots)] = sd.base + (uint64_t)rel_lo + xh;
           } else {
@@ -1245,7 +1261,7 @@ __global__ __launch_bounds__(kThreads, MODE == kScanGen ? 3 : KLF_SCAN_OCC) void
           for (uint32_t m = hq[q]; m; m &= m - 1u, ++k) {
             const uint32_t off = my0 + 32u * q + (uint32_t)__builtin_ctz(m);
             if (k < kHitSlots) {
-              hs[k] = (uint16_t)off;
+              hd[k] = (uint16_t)off;
             } else if ((uint64_t)ob + (k - kHitSlots) < a.qhits_cap) {
               a.qhits[ob + (k - kHitSlots)] = sd.base + (uint64_t)rel_lo + off;
             } else {
@@ -1253,6 +1269,11 @@ __global__ __launch_bounds__(kThreads, MODE == kScanGen ? 3 : KLF_SCAN_OCC) void
             }
           }
         tile_hits = tot < kHitSlots ? tot : kHitSlots;
+        if (hinl) {
+          wave_lds_sync();
+          const uint32_t h2 = s_h2[GEN ? wv : 0][0];  // (hit 0 in the low half, hit 1 in the high)
+          hit2 = tot > 1u ? h2 : (h2 & 0xFFFFu);
+        }
       }
     }
 
@@ -1274,26 +1295,57 @@ __global__ __launch_bounds__(kThreads, MODE == kScanGen ? 3 : KLF_SCAN_OCC) void
     const uint32_t pp = wave_sum(n_parsed), qq = wave_sum(n_since), dd = wave_sum(n_defer);
 #endif
     any_defer |= dd != 0;
-    {  // the record region in 16-B units, whole 128-B lines: unit 0 the TileStat, unit u
-       // slots 4u - 4 .. 4u - 1 (garbage past the last slot; a dense tile's slots are in
-       // the pool).  16 B per lane: narrower per-lane stores cost several times more per byte.
-      // (a tile where exactly one line starts keeps that slot in its TileStat: kTsInline)
+    {
+      // A tile's line slots: one line start -> the slot in its TileStat (kTsInline); two or
+      // more -> appended to the wave's own chunk of the pool (RunArgs::wave_pool, round 6: a
+      // sequential stream of whole lines per wave, where the 1,152-B-stride record regions
+      // took a 128-B store per tile however few its slots), 16-B aligned, TileStat bit 0 and
+      // pool_base as for a dense tile (whose slots the line list wrote to the pool itself).
+      // 16 B per lane: narrower per-lane stores cost several times more per byte.
       const bool inl = KLF_TS_INLINE && !dense && nlines == 1u;
-      const uint32_t w0 = agg, w1 = dense ? pool_base : (inl ? s_list[0] : 0u);
+      const bool pooled = a.wave_pool && !dense && nlines >= 2u;
+      // (timing builds: KLF_ABL 65536 drops only the slot stores, 131072 only the TileStat stores)
+      const bool no_slots = (abl && !(KLF_ABL & (65536 | 131072))) || ABL(65536);
+      uint32_t pb = dense ? pool_base : 0u, nunits = 0;
+      uint32_t* sdst = trec;  // the record region (a.wave_pool == 0: unit 0 the TileStat copy)
+      if (pooled && !no_slots) {
+        // 16-B granules; a run of 16 slots or more starts on a 128-B line and fills whole
+        // lines (a run straddling lines left partly written lines behind: C3 +1.6 %, r6f)
+        const bool whole = nlines > 12u;
+        const uint32_t need = whole ? (nlines + 31u) & ~31u : (nlines + 3u) & ~3u;
+        if (whole) wp_cur = (wp_cur + 31u) & ~31u;  // (chunks start 128-B aligned: see below)
+        if (wp_cur + need > wp_end) {  // (wave-uniform) a new chunk
+          const uint32_t ch = need > a.pool_chunk ? need : a.pool_chunk;
+          uint32_t b = 0;
+          if (lane == 0) b = atomicAdd(&a.counters[kCtrPool], ch);
+          b = (uint32_t)__builtin_amdgcn_readfirstlane((int)b);
+          wp_cur = b;
+          wp_end = (uint64_t)b + ch <= a.pool_cap ? b + ch : b;  // (past the pool: no room, the run is redone)
+          if (wp_end == b && lane == 0) atomicOr(err_flag, 1u);
+        }
+        if (wp_cur + need <= wp_end) {
+          pb = wp_cur;
+          wp_cur += need;
+          nunits = need / 4u;
+          sdst = a.pool + pb;
+        }
+      } else if (!a.wave_pool && !no_slots && !dense && nlines > 1u - (KLF_TS_INLINE ? 0u : 1u)) {
+        nunits = ((kRecHead + nlines + 31u) & ~31u) / 4u;  // the record region (whole 128-B lines)
+      }
+      const uint32_t w0 = agg, w1 = (dense || pooled) ? pb : (inl ? s_list[0] : (hinl ? hit2 : 0u));
       const uint32_t w2 = (pp & 0xFFFFu) | (qq << 16);
       const bool hh = LIT && __any(n_hit != 0);  // some line starting here holds the literal
-      const uint32_t w3 = ((dense ? 1u : 0u) | (carry ? 2u : 0u) | (dd ? 4u : 0u) | (hh ? 8u : 0u) | (inl ? kTsInline : 0u)) |
+      const uint32_t w3 = (((dense || (pooled && nunits)) ? 1u : 0u) | (carry ? 2u : 0u) | (dd ? 4u : 0u) | (hh ? 8u : 0u) |
+                           (inl ? kTsInline : 0u) | (hinl ? kTsHitInline : 0u)) |
                           ((uint32_t)(uint16_t)(GEN ? tile_hits : carry) << 16);  // GEN: hit slots used
-      // (every reader takes the TileStat from the compact tstat array and a tile's slots only
-      // below its line count: a tile where no line starts writes nothing here -- C5: ~40 % of
-      // its tiles, 128 B each)
-      const uint32_t nunits = (abl || (nlines == 0u && !dense) || inl) ? 0u : (dense ? 8u : ((kRecHead + nlines + 31u) & ~31u) / 4u);
-      const __amdgpu_buffer_rsrc_t rrs = __builtin_amdgcn_make_buffer_rsrc(trec, 0, (int)(nunits * 16u), 0x00020000);
+      const __amdgpu_buffer_rsrc_t rrs = __builtin_amdgcn_make_buffer_rsrc(sdst, 0, (int)(nunits * 16u), 0x00020000);
       typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
+      const uint32_t ushift = a.wave_pool ? 0u : 1u;  // (the record region: unit 0 the TileStat)
       for (uint32_t u = (uint32_t)lane; u < (nunits > 64u ? 128u : 64u); u += 64) {  // one or two stores
-        const uint32_t li = u ? (4u * u - 4u < (uint32_t)kSlotStride - 4u ? 4u * u - 4u : (uint32_t)kSlotStride - 4u) : 0u;
+        const uint32_t us = u - ushift;  // (u = 0 of a record: -1)
+        const uint32_t li = u < ushift ? 0u : (4u * us < (uint32_t)kSlotStride - 4u ? 4u * us : (uint32_t)kSlotStride - 4u);
         const uint4 sl = *reinterpret_cast<const uint4*>(s_list + li);
-        const u32x4v v = u ? u32x4v{sl.x, sl.y, sl.z, sl.w} : u32x4v{w0, w1, w2, w3};
+        const u32x4v v = u >= ushift ? u32x4v{sl.x, sl.y, sl.z, sl.w} : u32x4v{w0, w1, w2, w3};
         __builtin_amdgcn_raw_buffer_store_b128(v, rrs, 16u * u, 0, 0);
       }
       // the group's TileStats, one 128-B store at its last tile (lanes past it dropped)
@@ -1307,7 +1359,7 @@ __global__ __launch_bounds__(kThreads, MODE == kScanGen ? 3 : KLF_SCAN_OCC) void
       const bool gend = gk == kScanGroup - 1 || tile + 1 >= a.ntiles;
       const uint32_t ng = a.ntiles - g0 < kScanGroup ? a.ntiles - g0 : kScanGroup;
       const __amdgpu_buffer_rsrc_t srs =
-          __builtin_amdgcn_make_buffer_rsrc(a.tstat + g0, 0, (gend && !abl) ? (int)(16u * ng) : 0, 0x00020000);
+          __builtin_amdgcn_make_buffer_rsrc(a.tstat + g0, 0, (gend && (!abl || (KLF_ABL & 65536))) && !ABL(131072) ? (int)(16u * ng) : 0, 0x00020000);
       const uint4 gs = GEN ? stv : s_gstat[GEN ? 0 : wv][lane & (kScanGroup - 1)];
       __builtin_amdgcn_raw_buffer_store_b128(u32x4v{gs.x, gs.y, gs.z, gs.w}, srs, 16u * (uint32_t)lane, 0, 0);
     }
@@ -1403,9 +1455,15 @@ __device__ bool general_count(const RunArgs& a, const uint8_t* p, int64_t n, uin
 // TileStat's pool_base word (kTsInline, round 6: no 128-B record store for it; C5's most
 // common tile), every other tile in its record region.
 __device__ __forceinline__ uint32_t* slot_list(const RunArgs& a, const TileStat& ts, uint32_t tile) {
+  // (a.slots is null with the wave pool: a tile left with neither belongs to a run whose
+  // pool overflowed, which is redone -- its readers get in-bounds garbage)
   return (ts.flags & 1u) ? a.pool + ts.pool_base
          : (ts.flags & kTsInline) ? reinterpret_cast<uint32_t*>(a.tstat + tile) + 1
-                                  : a.slots + (size_t)tile * kRecStride + kRecHead;
+         : a.slots ? a.slots + (size_t)tile * kRecStride + kRecHead : a.pool;
+}
+// slot j of a tile whose TileStat is at hand: an inline slot without a second load
+__device__ __forceinline__ uint32_t slot_at(const RunArgs& a, const TileStat& ts, uint32_t tile, uint32_t j) {
+  return (ts.flags & kTsInline) ? ts.pool_base : slot_list(a, ts, tile)[j];
 }
 
 // One wave: the deferred lines of `tile` (TileStat ts) through the general parse; their
@@ -1626,7 +1684,17 @@ __global__ __launch_bounds__(256) void k_tindex(RunArgs a) {
     }
     uint32_t j = k - (lo ? s_hpre[lo - 1] : 0u), r = 0;
     while (j >= s_thit[lo * R + r]) j -= s_thit[lo * R + r++];
-    if (hb + k < a.hflat_cap) a.hflat[hb + k] = (t0 + lo * R + r) * kHitSlots + j;
+    if (hb + k < a.hflat_cap) {
+      // {tile, its hit's tile offset << 32}: inline hits from the TileStat (L2: this kernel
+      // just read it), the others from the tile's hit slots
+      const uint32_t tile = t0 + lo * R + r;
+      const TileStat& tsh = a.tstat[tile];
+      const uint32_t off = (tsh.flags & kTsHitInline) ? ((tsh.pool_base >> (16u * j)) & 0xFFFFu)
+                                                      : (uint32_t)a.hslots[(size_t)tile * kHitSlots + j];
+      // (+ the tile's stream in bits 48..63 when it fits: k_verify skips its tile_seg load)
+      const uint32_t hs = a.tile_seg[tile];
+      a.hflat[hb + k] = (uint64_t)tile | ((uint64_t)off << 32) | ((uint64_t)(hs < 0xFFFFu ? hs : 0xFFFFu) << 48);
+    }
   }
   if (t == 0 && (bid + 1) * (256u * R) >= a.ntiles) {  // the last block knows the totals
     // More lines than the line index holds: raised here, before any kernel that indexes
@@ -1741,8 +1809,7 @@ __device__ __forceinline__ void scatter_body(RunArgs& a, uint32_t bid, uint32_t 
           const uint32_t pk0 = prel == 0 ? 0 : 1;
           const uint32_t pn = pst.events + 1 > pk0 ? pst.events + 1 - pk0 : 0;  // never the stream's last tile
           if (pn == 0) continue;
-          const uint32_t* psrc = slot_list(a, pst, pt);
-          const uint32_t v = psrc[pn - 1];
+          const uint32_t v = slot_at(a, pst, pt, pn - 1);
           const uint32_t mt = v >> 16;
           // a deferred line had its whole content searched by k_fixup
           if ((mt & Meta::kParsed) && !(v & kSlotDefer)) cs = prel + (int64_t)(v & kSlotOff) + (mt >> 2);
@@ -1781,7 +1848,7 @@ __device__ __forceinline__ void scatter_body(RunArgs& a, uint32_t bid, uint32_t 
           const uint32_t src = s_ent[wv][lo].src;
           const uint32_t* sp = (src & 0x80000000u) ? a.pool + (src & 0x7FFFFFFFu)
                                : (src & 0x40000000u) ? reinterpret_cast<const uint32_t*>(a.tstat + g * kScatterGroup + lo) + 1
-                                                     : a.slots + (size_t)(g * kScatterGroup + lo) * kRecStride + kRecHead;
+                               : a.slots ? a.slots + (size_t)(g * kScatterGroup + lo) * kRecStride + kRecHead : a.pool;
           sl[u] = sp[j];
           kk[u] = lo;
           jj[u] = j;
@@ -1914,7 +1981,10 @@ __device__ void verify_hit_from(const RunArgs& a, uint32_t tile, uint32_t s, con
     // the rest of a needle longer than 32 bytes dword by dword
     const uint8_t* q = segp + rel_lo + x;
     bool eq = (((gword(q) | lm) ^ E.w) & msk_of(0)) == 0;
-    if (eq && m > 4) {
+    if (!KLF_VERIFY_PAR) {  // A/B: dword by dword, each load after the previous compare
+      for (uint32_t k = 4; k < m && eq; k += 4)
+        eq = (((gword(q + k) | lm) ^ P.qf_nbytes[E.x + (k >> 2)]) & msk_of(k)) == 0;
+    } else if (eq && m > 4) {
       const uintptr_t qa = reinterpret_cast<uintptr_t>(q);
       const uint32_t* qw = reinterpret_cast<const uint32_t*>(qa & ~(uintptr_t)3);
       const uint32_t sh = (uint32_t)(qa & 3);
@@ -1940,11 +2010,10 @@ __device__ void verify_hit_from(const RunArgs& a, uint32_t tile, uint32_t s, con
     const bool first = rel_lo == 0, last = rel_lo + kTile >= (int64_t)sd.len;
     const uint32_t k0 = first ? 0 : 1, k1 = last ? ts.events : ts.events + 1;
     const uint32_t nl = k1 > k0 ? k1 - k0 : 0;
-    const uint32_t* list = slot_list(a, ts, tile);
     int lo = 0, hi = x < 0 ? 0 : (int)nl;  // starts <= x
     while (lo < hi) {
       const int mid = (lo + hi) >> 1;
-      if ((int32_t)(list[mid] & kSlotOff) <= x) lo = mid + 1; else hi = mid;
+      if ((int32_t)(slot_at(a, ts, tile, (uint32_t)mid) & kSlotOff) <= x) lo = mid + 1; else hi = mid;
     }
     const uint64_t l = a.tile_base[tile] + (lo > 0 ? k0 + (uint32_t)lo - 1 : 0);
     if (l >= a.cap_lines) {  // (k_tindex raises the overflow first; never index past the arrays)
@@ -1957,7 +2026,7 @@ __device__ void verify_hit_from(const RunArgs& a, uint32_t tile, uint32_t s, con
     uint32_t v = 0;
     int64_t vrel = rel_lo;
     if (lo > 0) {
-      v = list[lo - 1];
+      v = slot_at(a, ts, tile, (uint32_t)lo - 1);
     } else {
       for (uint32_t pt = tile; pt > sd.tile0;) {  // the stream's first tile lists line 0
         --pt;
@@ -1966,8 +2035,7 @@ __device__ void verify_hit_from(const RunArgs& a, uint32_t tile, uint32_t s, con
         const uint32_t pk0 = prel == 0 ? 0u : 1u;
         const uint32_t pn = pst.events + 1 - pk0;  // an earlier tile is never the stream's last
         if (pn == 0) continue;
-        const uint32_t* psrc = slot_list(a, pst, pt);
-        v = psrc[pn - 1];
+        v = slot_at(a, pst, pt, pn - 1);
         vrel = prel;
         break;
       }
@@ -1992,15 +2060,14 @@ __device__ void verify_hit_from(const RunArgs& a, uint32_t tile, uint32_t s, con
       // these entries writes the same values)
       uint64_t le = sd.len;
       if ((uint32_t)lo < nl) {
-        le = (uint64_t)rel_lo + (list[lo] & kSlotOff);
+        le = (uint64_t)rel_lo + (slot_at(a, ts, tile, (uint32_t)lo) & kSlotOff);
       } else {
         for (uint32_t pt = tile + 1; pt < sd.tile0 + sd.ntiles; ++pt) {
           const TileStat pst = a.tstat[pt];
           const int64_t prel = (int64_t)(pt - sd.tile0) * kTile;
           const uint32_t pk1 = prel + kTile >= (int64_t)sd.len ? pst.events : pst.events + 1;
           if (pk1 <= 1u) continue;  // (k0 = 1: no line starts in tile pt)
-          const uint32_t* psrc = slot_list(a, pst, pt);
-          le = (uint64_t)prel + (psrc[0] & kSlotOff);
+          le = (uint64_t)prel + (slot_at(a, pst, pt, 0) & kSlotOff);
           break;
         }
       }
@@ -2049,10 +2116,11 @@ __device__ __forceinline__ void verify_body(RunArgs& a, uint32_t bid, uint32_t n
 #pragma unroll
     for (int u = 0; u < kVerifyBatch; ++u) {
       const uint32_t i = i0 + (uint32_t)u * stride;
-      const uint32_t slot = a.hflat[i < nf ? i : i0];
-      tile[u] = slot / kHitSlots;
-      pp[u] = a.hslots[slot];
-      sg[u] = a.tile_seg[tile[u]];
+      const uint64_t hf = a.hflat[i < nf ? i : i0];
+      tile[u] = (uint32_t)hf;
+      pp[u] = (int32_t)((hf >> 32) & 0xFFFFu);
+      sg[u] = (uint32_t)(hf >> 48);
+      if (sg[u] == 0xFFFFu) sg[u] = a.tile_seg[tile[u]];  // (streams past 65,534)
     }
 #pragma unroll
     for (int u = 0; u < kVerifyBatch; ++u) sd[u] = a.segs[sg[u]];
@@ -4343,7 +4411,9 @@ hipError_t launch_pipeline(const RunArgs& a0, hipStream_t st, hipEvent_t* ev, in
     }
     KLF_TRY(hipGetLastError());
   }
-  if (a.grep_mode == kGrepGeneral || a.grep_mode == kGrepAll) {
+  // (skip_match: a prefiltered set launches no k_match; an overflowed hit list or NFA queue,
+  // whose lines k_match would decide, makes the host redo the run with it)
+  if ((a.grep_mode == kGrepGeneral || a.grep_mode == kGrepAll) && !a.skip_match) {
     hipLaunchKernelGGL(k_match, dim3(num_cus * 8), dim3(256), 0, st, a);
     KLF_TRY(hipGetLastError());
   }
@@ -4396,29 +4466,33 @@ static hipError_t launch_tail_stage(const RunArgs& a, hipStream_t st, hipEvent_t
     hipLaunchKernelGGL(k_cmove, dim3(nb > gg ? nb : gg), dim3(kThreads), 0, st, a);
     KLF_TRY(hipGetLastError());
   }
-  if (a.compact_mode != 1) {
-    const uint32_t gk = (a.ntiles + kTcWaves - 1) / kTcWaves;
-    // persistent grid: one resident generation of blocks, so every wave's prefetch
-    // pipeline runs over its whole share of tiles
-    static int occ = 0;
-    if (occ == 0) {
-      (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_tcopy, 64 * kTcWaves, 0);
-      occ = occ < 1 ? 1 : (occ > 32 ? 32 : occ);
-      if (getenv("KLF_DIAG")) fprintf(stderr, "[klf] k_tcopy: %d blocks of %d waves per CU\n", occ, kTcWaves);
-    }
-    const uint32_t gc = (uint32_t)num_cus * (uint32_t)occ;
-    if (ev && !env_off("KLF_SCAN_EVENTS")) {  // ev[9] / ev[10]: the dispatch's own timestamps
-      hipExtLaunchKernelGGL(k_tcopy, dim3(gk < gc ? gk : gc), dim3(64 * kTcWaves), 0, st, ev[9], ev[10], 0, a,
-                            reinterpret_cast<const uint4*>(a.trec), a.kbase, a.truns);
-      m |= (1u << 9) | (1u << 10);
-    } else {
-      hipLaunchKernelGGL(k_tcopy, dim3(gk < gc ? gk : gc), dim3(64 * kTcWaves), 0, st, a,
-                         reinterpret_cast<const uint4*>(a.trec), a.kbase, a.truns);
-    }
-    KLF_TRY(hipGetLastError());
-  }
+  // (skip_tcopy: a --tail run that has not taken the dense path before launches no k_tcopy;
+  // the host launches it after the fact when this one did, launch_tcopy)
+  if (a.compact_mode != 1 && !a.skip_tcopy) KLF_TRY(launch_tcopy(a, st, ev, num_cus, &m));
 #undef KLF_TRY
   return hipSuccess;
+}
+
+hipError_t launch_tcopy(const RunArgs& a, hipStream_t st, hipEvent_t* ev, int num_cus, uint32_t* ev_mask) {
+  const uint32_t gk = (a.ntiles + kTcWaves - 1) / kTcWaves;
+  // persistent grid: one resident generation of blocks, so every wave's prefetch
+  // pipeline runs over its whole share of tiles
+  static int occ = 0;
+  if (occ == 0) {
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_tcopy, 64 * kTcWaves, 0);
+    occ = occ < 1 ? 1 : (occ > 32 ? 32 : occ);
+    if (getenv("KLF_DIAG")) fprintf(stderr, "[klf] k_tcopy: %d blocks of %d waves per CU\n", occ, kTcWaves);
+  }
+  const uint32_t gc = (uint32_t)num_cus * (uint32_t)occ;
+  if (ev && !env_off("KLF_SCAN_EVENTS")) {  // ev[9] / ev[10]: the dispatch's own timestamps
+    hipExtLaunchKernelGGL(k_tcopy, dim3(gk < gc ? gk : gc), dim3(64 * kTcWaves), 0, st, ev[9], ev[10], 0, a,
+                          reinterpret_cast<const uint4*>(a.trec), a.kbase, a.truns);
+    if (ev_mask) *ev_mask |= (1u << 9) | (1u << 10);
+  } else {
+    hipLaunchKernelGGL(k_tcopy, dim3(gk < gc ? gk : gc), dim3(64 * kTcWaves), 0, st, a,
+                       reinterpret_cast<const uint4*>(a.trec), a.kbase, a.truns);
+  }
+  return hipGetLastError();
 }
 
 hipError_t launch_retail(const RunArgs& a, hipStream_t st, hipEvent_t* ev, int num_cus, uint32_t* ev_mask) {

@@ -184,7 +184,8 @@ struct TileStat {
   uint16_t parsed, since_ok;
   uint16_t flags;      // bit0 dense (slots in the pool), bit1 literal hit in the carried-in line,
                        // bit2 some line deferred to k_fixup, bit3 literal hit in a line starting here,
-                       // bit4 the tile's single slot is pool_base (no record region written)
+                       // bit4 the tile's single slot is pool_base (no record region written),
+                       // bit5 (general sets) its 1-2 prefilter hits are pool_base's u16 halves
   uint16_t carry_off;  // literal: 1 + kCarryBias + tile offset of the furthest hit in the
                        // carried-in line (0 = none); general sets: hit slots used
 };
@@ -278,8 +279,11 @@ struct RunArgs {
   // workspace (device)
   TileStat* tstat;      // [ntiles]
   uint32_t* slots;      // [ntiles * kRecStride] per-tile records: TileStat, then staged line slots
-  uint32_t* pool;       // [pool_cap] slots of dense tiles
+  uint32_t* pool;       // [pool_cap] slots of dense tiles, and (wave_pool) of every tile where two or
+                        // more lines start, appended to per-wave chunks of pool_chunk slots
   uint64_t pool_cap;
+  uint32_t wave_pool;   // 1: slots in the pool (a.slots unused, null); 0: per-tile record regions
+  uint32_t pool_chunk;  // slots a wave reserves at a time (counters[kCtrPool] is the allocator)
   uint64_t* tile_base;  // [ntiles] global line index of each tile's line 0
   uint64_t* bsum;       // [4 * (ntiles / 1024 + 1)] scan block sums (events, parsed, since_ok, hits)
   uint64_t* mpart;      // [cap_lines / kMatchChunk + 1] matched-line partial per line chunk
@@ -307,7 +311,7 @@ struct RunArgs {
                         //  stream offset of the factor occurrence | stream << 40}
   uint32_t cand_cap;
   uint16_t* hslots;     // [ntiles * kHitSlots] prefilter hits (tile offsets of the samples)
-  uint32_t* hflat;      // [hflat_cap] hit slot ids (tile * kHitSlots + j), flattened by k_tbase
+  uint64_t* hflat;      // [hflat_cap] prefilter hits {tile | tile offset << 32 | stream << 48 (0xFFFF: look it up)}, by k_tindex
   uint64_t hflat_cap;
   uint64_t* qhits;      // [qhits_cap] spilled hits (batch byte offsets of the samples)
   uint32_t qhits_cap;
@@ -330,6 +334,8 @@ struct RunArgs {
   uint32_t win_index;
   uint32_t scatter_mode;  // k_scatter: 0 every tile, 1 tiles with deferred lines, 2 tiles meeting a window
   uint32_t scatter_split; // k_scatter: waves per 64-tile group (small batches: a group's lines split over them; 0 = 1)
+  uint32_t skip_match;    // prefiltered set: k_match not launched (an overflow redoes the run with it)
+  uint32_t skip_tcopy;    // --tail run: k_tcopy not launched (the host launches it when the run went dense)
   // per-pattern counts (KLF_FILTER_PATTERN_COUNTS): pcount[segment * n_cids + cid] lines,
   // each (line, cid) counted once through the `pairs` hash set (open addressing, u64 keys)
   uint32_t count_pats;
@@ -373,6 +379,7 @@ hipError_t launch_retail(const RunArgs& a, hipStream_t stream, hipEvent_t* ev, i
 // Diagnostic: reps back-to-back launches of a VALU loop (num_cus x 4 workgroups); out
 // (2 num_cus x 4 + 1 u64) gets the last launch's per-workgroup shader / real-time deltas.
 hipError_t clock_probe(int num_cus, uint32_t iters, uint32_t reps, uint64_t* out, hipStream_t stream);
+hipError_t launch_tcopy(const RunArgs& a, hipStream_t st, hipEvent_t* ev, int num_cus, uint32_t* ev_mask);
 hipError_t launch_nlsample(const uint8_t* bytes, const SegDesc* segs, uint32_t nsegs, uint32_t ntiles, uint32_t blocks,
                            uint32_t* out, hipStream_t st);
 hipError_t launch_gramhist(const uint8_t* bytes, const SegDesc* segs, uint32_t nsegs, uint64_t sample, uint32_t fold,

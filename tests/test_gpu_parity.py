@@ -514,6 +514,28 @@ def test_first_run_line_sample(gpu, monkeypatch, mode):
     check_against_c(streams, None, 20, synth.c4_literals(1024)[:100] + [b" x"])
 
 
+@pytest.mark.parametrize("mode", ["pool", "records", "overflow"])
+def test_line_slot_storage(gpu, monkeypatch, mode):
+    """Where the scan keeps each tile's line slots (round 6): one line start in the tile's
+    TileStat, two or more appended to the wave's chunk of the pool (the default), or the
+    per-tile record regions of earlier rounds (KLF_WAVE_POOL=0); a first attempt whose pool
+    is far too small (KLF_DEBUG_POOL_CAP) overflows and is redone.  Every reader of the
+    slots runs: the whole index, windows, deferred lines, literal and regex verification,
+    the dense compaction and the one-pass compaction, against the oracles."""
+    if mode == "records":
+        monkeypatch.setenv("KLF_WAVE_POOL", "0")
+    if mode == "overflow":
+        monkeypatch.setenv("KLF_DEBUG_POOL_CAP", "64")
+    streams = [synth.generate(synth.LONGJSON, 91, 0, 2_000_000, permille=30),
+               synth.generate(synth.ADVERSARIAL, 92, 1, 3000, drop_final_nl=True, permille=40), b"",
+               synth.generate(synth.TEXT, 93, 3, 1_500_000)]
+    for tail in (-1, 40):
+        check_against_c(streams, None, tail, [])
+        check_against_c(streams, (synth.T0 + 1800, 0), tail, [synth.NEEDLE])
+    check_against_c(streams, None, 25, synth.c4_literals(1024)[:300])
+    check_against_py(streams, (synth.T0 + 1800, 0), 15, match=synth.c5_regexes())
+
+
 @pytest.mark.parametrize("split", ["3", "8"])
 def test_scatter_split(gpu, monkeypatch, split):
     """k_scatter with each 64-tile group's lines split over several waves (small batches
