@@ -197,6 +197,8 @@ struct klf_engine {
   DevBuf d_cmap, d_cseg;
   DevBuf d_block;  // the first run's workspace buffers (ensure_all), freed last
   std::vector<DevBuf*> block_users;  // the buffers still mapped into d_block
+  DevBuf d_block2;  // the first run's line arrays, slot pool / records and output (sized after its sample)
+  std::vector<DevBuf*> block2_users;
   DevBuf d_batch, d_segs, d_tstat, d_slots, d_pool, d_tile_base, d_bsum, d_cstatus, d_counters, d_line_off,
       d_meta, d_bits, d_segout, d_wpre, d_out, d_mpart, d_trec, d_truns, d_kbase;
   // one-pass compaction (RunArgs::fuse): range table, extents, range states; d_out2 the
@@ -707,6 +709,7 @@ extern "C" void klf_close(klf_engine* e) {
   e->h_stage.release();
   for (DevBuf* b : {&e->d_ac_out, &e->d_ac_dict, &e->d_pcount, &e->d_pairs}) b->release();
   e->d_block.release();
+  e->d_block2.release();
   e->d_acblk.release();
   e->copier.reset();
   {
@@ -1109,7 +1112,11 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
   // scan's time plus the host's array setup in series: C2's first run 1.16 ms vs 1.01 warm)
   bool nl_pending = false;
   uint32_t nl_blocks = 0;
-  if (!tune_pending && e->line_density == 0.0 && !getenv("KLF_TWO_PHASE")) {
+  // (a first batch whose 32-B-rule line arrays take at most ~2 GB maps them as they are: no
+  // sample, no sync before the scan -- C1 / C2; lines under 32 B overflow and rerun exactly)
+  const bool small_first = e->line_density == 0.0 && cap * 11 <= (2ull << 30) && !getenv("KLF_TWO_PHASE") &&
+                           !getenv("KLF_DEBUG_NL_SCALE");
+  if (!tune_pending && e->line_density == 0.0 && !small_first && !getenv("KLF_TWO_PHASE")) {
     nl_blocks = (uint32_t)std::min<uint64_t>(ntiles, 64);
     HIPCHK(e, e->d_hist.ensure((size_t)nl_blocks * 8), "alloc line sample");
     HIPCHK(e, e->h_hist.ensure((size_t)nl_blocks * 8), "alloc line sample readback");
@@ -1153,7 +1160,7 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
       {&e->d_tstat, ntiles * sizeof(klf::TileStat)},
       {&e->d_tile_base, ntiles * 8}, {&e->d_bsum, (ntiles / 1024 + 2) * 4 * 8},
       {&e->d_counters, klf::kNumCounters * 4}, {&e->d_segout, nsegs * sizeof(SegOut)},
-      {&e->d_wpre, (3 * (size_t)nsegs + 2) * 8} /* + wgrp */, {&e->d_trec, ntiles * sizeof(klf::TRec)}, {&e->d_kbase, ntiles * 16}};
+      {&e->d_wpre, (3 * (size_t)nsegs + 2) * 8} /* + wgrp */};
   // the dense compaction's per-tile run table (512 B per tile: 2.1 GB for 32 GiB) only for
   // runs without a --tail limit or after a --tail run took the dense path (k_tcopy lists
   // the runs itself without it)
@@ -1161,6 +1168,14 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
   if (want_truns) ws.push_back({&e->d_truns, ntiles * klf::kRunSlots * 4});
   uint32_t compact_mode = 0;  // tests: force either compaction path
   if (const char* v = getenv("KLF_COMPACT")) compact_mode = !strcmp(v, "sparse") ? 1u : !strcmp(v, "dense") ? 2u : 0u;
+  // A --tail run selects at most S (N + 1) lines: up to 2^20 of them the line gather is the
+  // path (round 6; it copies any selection, long lines spread over copy chunks), so the tile
+  // copy's per-tile tables (32 B per tile: 134 MB for 32 GiB) are neither mapped nor walked
+  else if (f->tail >= 0 && (uint64_t)nsegs * ((uint64_t)f->tail + 1) <= (1ull << 20)) compact_mode = 1;
+  if (compact_mode != 1) {
+    ws.push_back({&e->d_trec, ntiles * sizeof(klf::TRec)});
+    ws.push_back({&e->d_kbase, ntiles * 16});
+  }
   // One-pass compaction (no patterns, --tail -1): the fused scan compacts each wave's tile
   // range in place.  The ranges (a multiple of kScanGroup tiles each, one per wave of a
   // full-occupancy launch) and each range's first extent (one extent per stream it touches).
@@ -1216,21 +1231,23 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
   // on demand -- the compaction skips a copy that would not fit, the host grows the buffer
   // to the run's output and reruns the tail stage (first runs only: the buffer is kept).
   // A --tail run then never maps an input-sized buffer (34 GB for C4 / C5).
-  if (f->tail < 0) HIPCHK(e, e->d_out.ensure(std::max<uint64_t>(total_bytes, fuse_try ? seg_end : 0) + 64), "alloc out");
+  uint64_t out_need = 0;  // the output buffer (mapped below, with a first run's line arrays)
+  if (f->tail < 0) out_need = std::max<uint64_t>(total_bytes, fuse_try ? seg_end : 0) + 64;
   else if (!e->d_out.p) {  // a first --tail run: room for a typical tail window (no rerun to grow)
     uint64_t first = 64ull << 20;
     if (const char* v = getenv("KLF_DEBUG_OUT_INIT")) first = (uint64_t)std::max(1L, atol(v));  // tests: force growth
-    HIPCHK(e, e->d_out.ensure(std::min<uint64_t>(total_bytes + 64, first)), "alloc out");
+    out_need = std::min<uint64_t>(total_bytes + 64, first);
   }
   const bool need_cand = mode == klf::CompiledSet::kGeneral && e->cs.qf_on && e->cs.rx_count;
   if (need_cand) ws.push_back({&e->d_cand, (size_t)e->cand_cap * 16});
   const bool need_hits = mode == klf::CompiledSet::kGeneral && e->cs.qf_on;
-  // bitmap hits: < 1 per 8 KiB tile on log text, kHitSlots per tile recorded in place;
-  // spills beyond 1 per 1 KiB of input -> k_match decides
-  const uint32_t qhits_cap = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(total_bytes / 1024, 1u << 16),
+  // bitmap hits: < 1 per 8 KiB tile on log text (C4's 1,024 literals: 0.41, C5 0.02),
+  // kHitSlots per tile recorded in place; spills beyond 1 per 8 KiB of input -> k_match decides
+  const uint32_t qhits_cap = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(total_bytes / 8192, 1u << 16),
                                                           e->hits_cap_max);
-  // flattened hit slots: up to 1 per 512 B of input (~16 per tile); more -> k_match decides
-  const uint64_t hflat_cap = std::min<uint64_t>(std::max<uint64_t>(total_bytes / 512, 1u << 20),
+  // flattened hit slots: up to 1 per 4 KiB of input (2 per tile); more -> k_match decides
+  // (round 5 mapped 1 per 512 B: 537 MB for 32 GiB, in every first run's workspace)
+  const uint64_t hflat_cap = std::min<uint64_t>(std::max<uint64_t>(total_bytes / 4096, 1u << 20),
                                                 (uint64_t)ntiles * klf::kHitSlots);
   if (need_hits) {
     ws.push_back({&e->d_qhits, (size_t)qhits_cap * 8});
@@ -1266,9 +1283,42 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
   const double dens = e->line_density > 0.0 ? e->line_density : est_density;
   const char* wpv = getenv("KLF_WAVE_POOL");
   const bool wave_pool = wpv ? strcmp(wpv, "0") != 0 : (dens > 0.0 && dens * 1024.0 < 1.0);
-  if (!wave_pool) HIPCHK(e, e->d_slots.ensure(ntiles * klf::kRecStride * 4), "alloc line records");
   if (density_cap)
     cap = std::min<uint64_t>(cap, (uint64_t)(est_density * (double)total_bytes * 2.0) + 2ull * nsegs + 65536);
+  // the buffers indexed by global line (and the compaction's per-block tables) for capacity c
+  auto line_sizes = [&](uint64_t c) {
+    const uint64_t mcb = c / klf::kCompactLines + 2;
+    // >= sum over blocks of ceil(bytes / chunk) (>= 1 each): the block prefix's chunk keeps
+    // the output within kCopyChunksTarget chunks unless it is the largest, kCopyChunk
+    const uint64_t cmc = mcb + std::max<uint64_t>(total_bytes / klf::kCopyChunk, klf::kCopyChunksTarget) + 2;
+    return std::vector<std::pair<DevBuf*, size_t>>{
+        {&e->d_line_off, (c + nsegs + 1) * 8}, {&e->d_meta, c * 2 + 16}, {&e->d_bits, (c / 32 + 1) * 4},
+        {&e->d_cstatus, (mcb + 1) * 3 * 8}, {&e->d_cmap, cmc * 4}, {&e->d_cseg, (mcb + 1) * 4},
+        {&e->d_mpart, (c / klf::kMatchChunk + 2) * 8}};
+  };
+  auto pool_need = [&](uint64_t c, uint32_t& chunk) -> uint64_t {  // the slot pool (wave_pool: see the scan)
+    chunk = 256;
+    if (!wave_pool) return e->pool_cap;
+    const uint64_t nwaves = (uint64_t)e->num_cus * 16;
+    const uint64_t per_wave = (c + 2 * ntiles) / nwaves;
+    while (chunk < 4096 && chunk * 4 < per_wave) chunk *= 2;
+    return std::max<uint64_t>(e->pool_cap, c + 3 * ntiles + nwaves * chunk + 1024);
+  };
+  {
+    // A first run maps its line arrays, slot pool / records and output buffer as one more
+    // allocation, now that their sizes are known (each hipMalloc costs 1-26 us of host time
+    // with the GPU idle: ~10 of them per first run); later runs grow single buffers
+    std::vector<std::pair<DevBuf*, size_t>> ws2;
+    if (out_need) ws2.push_back({&e->d_out, out_need});
+    if (!wave_pool) ws2.push_back({&e->d_slots, ntiles * klf::kRecStride * 4});
+    if (e->line_density == 0.0) {
+      for (auto& x : line_sizes(cap)) ws2.push_back(x);
+      uint32_t ch = 0;
+      ws2.push_back({&e->d_pool, pool_need(cap, ch) * 4});
+    }
+    HIPCHK(e, ensure_all(e->d_block2, e->block2_users, ws2), "alloc line arrays / output");
+    mark("line arrays / output");
+  }
   uint32_t pool_chunk = 256;  // (per attempt, below: the wave pool's chunk size)
   bool force_match = false;   // an overflowed hit list / NFA queue: redo the run with k_match
   // every RunArgs field but the line arrays (alloc_lines) of a run over the whole batch
@@ -1367,21 +1417,14 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
     // An engine's first run sizes its line arrays from its own line count: the pipeline
     // runs up to the tile index, the count is read back, the arrays are allocated, the
     // rest follows (one extra sync, first runs only).
-    const bool two_phase = attempt == 0 && e->line_density == 0.0 && !density_cap && !getenv("KLF_ONE_PHASE");
+    const bool two_phase = attempt == 0 && e->line_density == 0.0 && !density_cap && !small_first && !getenv("KLF_ONE_PHASE");
     // the arrays indexed by global line (and the compaction's per-block tables)
     auto alloc_lines = [&](klf::RunArgs& x, uint64_t c) -> hipError_t {
       const uint64_t mcb = c / klf::kCompactLines + 2;
-      // >= sum over blocks of ceil(bytes / chunk) (>= 1 each): the block prefix's chunk keeps
-      // the output within kCopyChunksTarget chunks unless it is the largest, kCopyChunk
       const uint64_t cmc = mcb + std::max<uint64_t>(total_bytes / klf::kCopyChunk, klf::kCopyChunksTarget) + 2;
       hipError_t h;
-      if ((h = e->d_line_off.ensure((c + nsegs + 1) * 8)) != hipSuccess) return h;
-      if ((h = e->d_meta.ensure(c * 2 + 16)) != hipSuccess) return h;
-      if ((h = e->d_bits.ensure((c / 32 + 1) * 4)) != hipSuccess) return h;
-      if ((h = e->d_cstatus.ensure((mcb + 1) * 3 * 8)) != hipSuccess) return h;
-      if ((h = e->d_cmap.ensure(cmc * 4)) != hipSuccess) return h;
-      if ((h = e->d_cseg.ensure((mcb + 1) * 4)) != hipSuccess) return h;
-      if ((h = e->d_mpart.ensure((c / klf::kMatchChunk + 2) * 8)) != hipSuccess) return h;
+      for (auto& q : line_sizes(c))
+        if ((h = q.first->ensure(q.second)) != hipSuccess) return h;
       x.line_off = e->d_line_off.as<uint64_t>();
       x.meta = e->d_meta.as<uint16_t>();
       x.bits = e->d_bits.as<uint32_t>();
@@ -1397,14 +1440,8 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
     // the pool: every tile where two or more lines start (16-B aligned: <= 3 spare slots each),
     // dense tiles, and the waves' partly used last chunks (wave_pool); an overflow reruns
     // with the count the scan reserved
-    pool_chunk = 256;
-    if (wave_pool) {
-      const uint64_t nwaves = (uint64_t)e->num_cus * 16;
-      const uint64_t per_wave = (cap + 2 * ntiles) / nwaves;
-      while (pool_chunk < 4096 && pool_chunk * 4 < per_wave) pool_chunk *= 2;
-      e->pool_cap = std::max<uint64_t>(e->pool_cap, cap + 3 * ntiles + nwaves * pool_chunk + 1024);
-      if (e->pool_cap >= (1ull << 31)) return set_err(e, KLF_EINVAL, "batch too large (line slot pool)");
-    }
+    e->pool_cap = pool_need(cap, pool_chunk);
+    if (e->pool_cap >= (1ull << 31)) return set_err(e, KLF_EINVAL, "batch too large (line slot pool)");
     HIPCHK(e, e->d_pool.ensure(e->pool_cap * 4), "alloc pool");
     klf::RunArgs a;
     fill_args(a, attempt);

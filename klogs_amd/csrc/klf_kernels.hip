@@ -40,6 +40,14 @@ __device__ uint32_t g_lb_rounds, g_lb_spins;
 #else
 #define KLF_STAMP(tile, k) do { } while (0)
 #endif
+// Diagnostic build only (KLF_TIMELINE): k_verify's phases per hit thread, slot k of its global
+// thread id (s_memtime; 0 = phase not reached)
+#if KLF_TIMELINE
+#define KLF_VSTAMP(k) do { const uint32_t vg_ = (blockIdx.x * blockDim.x + threadIdx.x) % 300000u; \
+  g_timeline[(size_t)vg_ * 8 + (k)] = __builtin_amdgcn_s_memtime(); } while (0)
+#else
+#define KLF_VSTAMP(k) do { } while (0)
+#endif
 
 // ------------------------------------------------------------------ small helpers ---
 
@@ -1645,6 +1653,7 @@ __global__ __launch_bounds__(256) void k_tindex(RunArgs a) {
   // tile bases and hit counts go through LDS so that both outputs are written coalesced
   __shared__ uint32_t s_tbl[256 * R];   // block-local tile line base (< 2^32)
   __shared__ uint8_t s_thit[256 * R];   // tile hit slots (<= kHitSlots)
+  __shared__ uint32_t s_tseg[256 * R];  // tile -> stream (for the flattened hits)
   __shared__ uint32_t s_hpre[256];      // inclusive prefix of the threads' hit slots
   s_hpre[t] = oh + h;
   uint32_t lv = ov;
@@ -1654,6 +1663,7 @@ __global__ __launch_bounds__(256) void k_tindex(RunArgs a) {
     const uint32_t tile = tb + r;
     s_tbl[t * R + r] = lv;
     s_thit[t * R + r] = (uint8_t)(tile < a.ntiles ? tile_hits(a, ts[r]) : 0u);
+    s_tseg[t * R + r] = sg[r];
     if (tile < a.ntiles) {
       const uint32_t s = sg[r];
       const uint32_t sp = r ? sg[r - 1] : s_prev, sn = r + 1 < R ? sg[r + 1] : s_next;
@@ -1688,11 +1698,17 @@ __global__ __launch_bounds__(256) void k_tindex(RunArgs a) {
       // {tile, its hit's tile offset << 32}: inline hits from the TileStat (L2: this kernel
       // just read it), the others from the tile's hit slots
       const uint32_t tile = t0 + lo * R + r;
-      const TileStat& tsh = a.tstat[tile];
-      const uint32_t off = (tsh.flags & kTsHitInline) ? ((tsh.pool_base >> (16u * j)) & 0xFFFFu)
-                                                      : (uint32_t)a.hslots[(size_t)tile * kHitSlots + j];
-      // (+ the tile's stream in bits 48..63 when it fits: k_verify skips its tile_seg load)
-      const uint32_t hs = a.tile_seg[tile];
+      uint32_t off;
+      if (KLF_HIT_INLINE) {
+        const TileStat& tsh = a.tstat[tile];
+        off = (tsh.flags & kTsHitInline) ? ((tsh.pool_base >> (16u * j)) & 0xFFFFu)
+                                         : (uint32_t)a.hslots[(size_t)tile * kHitSlots + j];
+      } else {
+        off = a.hslots[(size_t)tile * kHitSlots + j];
+      }
+      // (+ the tile's stream in bits 48..63 when it fits: k_verify skips its tile_seg load;
+      // the owning thread's registers hold it, passed through LDS)
+      const uint32_t hs = s_tseg[lo * R + r];
       a.hflat[hb + k] = (uint64_t)tile | ((uint64_t)off << 32) | ((uint64_t)(hs < 0xFFFFu ? hs : 0xFFFFu) << 48);
     }
   }
@@ -2005,6 +2021,7 @@ __device__ void verify_hit_from(const RunArgs& a, uint32_t tile, uint32_t s, con
     atomicOr(&a.counters[13], x);  // timing build: bucket walk only
     continue;
 #endif
+    KLF_VSTAMP(2);  // (a matching entry)
     // the occurrence's line: global index, start (stream offset), meta
     const TileStat ts = a.tstat[tile];
     const bool first = rel_lo == 0, last = rel_lo + kTile >= (int64_t)sd.len;
@@ -2020,13 +2037,14 @@ __device__ void verify_hit_from(const RunArgs& a, uint32_t tile, uint32_t s, con
       atomicOr(&a.counters[2], 1u);
       continue;
     }
+    KLF_VSTAMP(3);  // (its tile's line search done)
     // the line's meta and start from its slot: the tile's own, or for the line carried in
     // from an earlier tile the last one listed by the nearest earlier tile that lists one
     // (k_scatter may still be running: the global line index is not read here)
     uint32_t v = 0;
     int64_t vrel = rel_lo;
-    if (lo > 0) {
-      v = slot_at(a, ts, tile, (uint32_t)lo - 1);
+    if (lo > 0 || (KLF_ABL & 524288)) {  // (timing build 524288: no walk back, a wrong slot)
+      v = slot_at(a, ts, tile, lo > 0 ? (uint32_t)lo - 1 : 0u);
     } else {
       for (uint32_t pt = tile; pt > sd.tile0;) {  // the stream's first tile lists line 0
         --pt;
@@ -2042,6 +2060,7 @@ __device__ void verify_hit_from(const RunArgs& a, uint32_t tile, uint32_t s, con
     }
     const uint16_t mt = (uint16_t)(v >> 16);
     const uint64_t ls = (uint64_t)vrel + (v & kSlotOff);
+    KLF_VSTAMP(4);  // (the line's start slot, walked back to)
     if (!(mt & Meta::kParsed)) continue;
     if (!(E.y & kQfRegex)) {  // literal: a match when it starts inside the content
       // (a parsed line's first space ends its prefix: the stream end bounds the search)
@@ -2053,6 +2072,7 @@ __device__ void verify_hit_from(const RunArgs& a, uint32_t tile, uint32_t s, con
       continue;
     }
     if (!a.count_pats && ((a.bits[l >> 5] >> (l & 31)) & 1u)) continue;  // counting: every regex decides
+    KLF_VSTAMP(5);  // (bitmap checked)
     if (a.win_index) {
       // windowed line index (no full k_scatter): the candidate line's start, end and meta for
       // k_nfa_win / k_nfa.  Its end is the next line start: this tile's next slot, else the
@@ -2061,7 +2081,7 @@ __device__ void verify_hit_from(const RunArgs& a, uint32_t tile, uint32_t s, con
       uint64_t le = sd.len;
       if ((uint32_t)lo < nl) {
         le = (uint64_t)rel_lo + (slot_at(a, ts, tile, (uint32_t)lo) & kSlotOff);
-      } else {
+      } else if (!(KLF_ABL & 262144)) {  // (timing build 262144: no walk forward)
         for (uint32_t pt = tile + 1; pt < sd.tile0 + sd.ntiles; ++pt) {
           const TileStat pst = a.tstat[pt];
           const int64_t prel = (int64_t)(pt - sd.tile0) * kTile;
@@ -2075,6 +2095,7 @@ __device__ void verify_hit_from(const RunArgs& a, uint32_t tile, uint32_t s, con
       a.line_off[l + s + 1] = le;
       a.meta[l] = mt;
     }
+    KLF_VSTAMP(6);  // (the line's bounds written)
     // {line | regex << 40, the occurrence (stream offset) | stream << 40}
     push_candidate(a, vq, l | ((uint64_t)E.z << 40), (uint64_t)(rel_lo + x) | ((uint64_t)s << 40));
   }
@@ -2109,6 +2130,7 @@ __device__ __forceinline__ void verify_body(RunArgs& a, uint32_t bid, uint32_t n
   const uint32_t gid = bid * blockDim.x + threadIdx.x, stride = nb * blockDim.x;
   const uint32_t nf = a.counters[kCtrFlatHits];
   const DevPatterns& P = a.pats;
+  KLF_VSTAMP(0);
   for (uint32_t i0 = gid; i0 < nf; i0 += kVerifyBatch * stride) {
     uint32_t tile[kVerifyBatch], sg[kVerifyBatch], e0[kVerifyBatch], e1[kVerifyBatch];
     int32_t pp[kVerifyBatch];
@@ -2136,6 +2158,7 @@ __device__ __forceinline__ void verify_body(RunArgs& a, uint32_t bid, uint32_t n
       e0[u] = P.qf_head[b];
       e1[u] = P.qf_head[b + 1];
     }
+    KLF_VSTAMP(1);  // (the batch's hits, streams, grams and buckets loaded)
 #pragma unroll
     for (int u = 0; u < kVerifyBatch; ++u)
       if (i0 + (uint32_t)u * stride < nf) {
@@ -2159,6 +2182,7 @@ __device__ __forceinline__ void verify_body(RunArgs& a, uint32_t bid, uint32_t n
     verify_hit(a, tile, lo, (int32_t)(rel % kTile), vq);
   }
   if (gid == 0) a.counters[kCtrVerified] = nf + nh;
+  KLF_VSTAMP(7);
   // the wave's staged candidates: one queue reservation, then coalesced stores
   wave_lds_sync();
   const uint32_t nq = s_qn[wv] < kVerifyQ ? s_qn[wv] : kVerifyQ;
@@ -4432,7 +4456,9 @@ static hipError_t launch_tail_stage(const RunArgs& a, hipStream_t st, hipEvent_t
 #define KLF_TRY(x) do { e = (x); if (e != hipSuccess) return e; } while (0)
   if (a.grep_mode != kGrepNone) {
     const uint64_t nchunks = a.cap_lines / kMatchChunk + 1;
-    const uint32_t g = (uint32_t)(nchunks < (uint64_t)num_cus * 4 ? nchunks : (uint64_t)num_cus * 4);
+    // (16 blocks per CU: each 8,192-line chunk is a load, a block reduction and two barriers,
+    // latency more than bytes -- C4's 11,700 chunks took 12 rounds of 4 blocks per CU, 24 us)
+    const uint32_t g = (uint32_t)(nchunks < (uint64_t)num_cus * 16 ? nchunks : (uint64_t)num_cus * 16);
     hipLaunchKernelGGL(k_mcount, dim3(g), dim3(256), 0, st, a);
     KLF_TRY(hipGetLastError());
   }

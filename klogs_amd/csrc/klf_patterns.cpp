@@ -12,6 +12,7 @@
 #include <set>
 #include <unordered_map>
 #include <queue>
+#include <thread>
 
 #include "../../include/klf.h"
 #include "klf_kernels.hpp"
@@ -973,6 +974,60 @@ bool compile_set(const std::vector<std::vector<uint8_t>>& pats, const std::vecto
                               [](const std::string& f) { return f.find('\n') != std::string::npos; }),
                alts.end());
   };
+  // Each regex compiled on its own (parse, Glushkov tables, required factors), then gathered
+  // in pattern order, the first error by pattern index.  KLF_COMPILE_THREADS=n spreads them
+  // over n host threads (measured: slower than one thread for C5's 64 regexes -- thread
+  // start-up outweighs ~5 us per regex -- so one by default)
+  struct RxOut {
+    bool ok = false, always = false, never = false, have_fac = false;
+    std::string err;
+    int code = 0;
+    int root = -1;
+    std::vector<RNode> pool;
+    GlushkovTables g;
+    std::vector<std::string> alts;
+    bool loose = false;
+    uint32_t pre = kRxPreUnbounded;
+  };
+  std::vector<RxOut> rxo(pats.size());
+  auto compile_rx = [&](size_t k) {
+    RxOut& o = rxo[k];
+    // parsed once: the factor analyses read the tree, the Glushkov build rewrites a copy
+    Parser ps(pats[k].data(), pats[k].size());
+    o.root = ps.parse();
+    if (o.root < 0) {
+      o.err = "pattern " + std::to_string(k) + ": " + ps.err;
+      o.code = KLF_EPATTERN;
+      return;
+    }
+    {
+      std::vector<RNode> work = ps.pool;
+      if (!build_glushkov(work, o.root, o.g, o.err, o.code)) {
+        o.err = "pattern " + std::to_string(k) + ": " + o.err;
+        return;
+      }
+    }
+    o.ok = true;
+    if (o.g.accept_at_start && o.g.accept_empty) { o.always = true; return; }
+    o.pool = std::move(ps.pool);
+    if (factors_of(o.pool, o.root, o.alts, o.loose, &o.pre, SIZE_MAX)) {
+      // such alternatives cannot occur; none left = no match ever
+      drop_nl(o.alts);
+      if (o.alts.empty()) o.never = true;
+    }
+  };
+  {
+    std::vector<size_t> rk;
+    for (size_t k = 0; k < pats.size(); ++k)
+      if (kinds[k] == KLF_PAT_REGEX) rk.push_back(k);
+    size_t nthr = 1;
+    if (const char* v = getenv("KLF_COMPILE_THREADS")) nthr = std::max<size_t>(1, (size_t)atol(v));
+    std::vector<std::thread> th;
+    for (size_t t = 1; t < nthr; ++t)
+      th.emplace_back([&, t]() { for (size_t i = t; i < rk.size(); i += nthr) compile_rx(rk[i]); });
+    for (size_t i = 0; i < rk.size(); i += nthr) compile_rx(rk[i]);
+    for (auto& x : th) x.join();
+  }
   for (size_t k = 0; k < pats.size(); ++k) {
     if (kinds[k] == KLF_PAT_LITERAL) {
       const auto& l = pats[k];
@@ -980,37 +1035,20 @@ bool compile_set(const std::vector<std::vector<uint8_t>>& pats, const std::vecto
       if (std::find(l.begin(), l.end(), (uint8_t)'\n') != l.end()) continue;  // never in content
       lits.push_back(l);
     } else if (kinds[k] == KLF_PAT_REGEX) {
-      // parsed once: the factor analyses read the tree, the Glushkov build rewrites a copy
-      Parser ps(pats[k].data(), pats[k].size());
-      const int root = ps.parse();
-      if (root < 0) {
-        err = "pattern " + std::to_string(k) + ": " + ps.err;
-        err_code = KLF_EPATTERN;
+      RxOut& o = rxo[k];
+      if (!o.ok) {
+        err = o.err;
+        err_code = o.code;
         return false;
       }
-      GlushkovTables g;
-      {
-        std::vector<RNode> work = ps.pool;
-        if (!build_glushkov(work, root, g, err, err_code)) {
-          err = "pattern " + std::to_string(k) + ": " + err;
-          return false;
-        }
-      }
-      if (g.accept_at_start && g.accept_empty) { always_rx.push_back(k); always = true; continue; }
-      rxs.push_back(std::move(g));
-      std::vector<std::string> alts;
-      bool loose = false;
-      uint32_t pre = kRxPreUnbounded;
-      rx_tree.push_back(std::move(ps.pool));
-      rx_root.push_back(root);
-      if (factors_of(rx_tree.back(), root, alts, loose, &pre, SIZE_MAX)) {
-        // such alternatives cannot occur; none left = no match ever
-        drop_nl(alts);
-        if (alts.empty()) { rxs.pop_back(); rx_tree.pop_back(); rx_root.pop_back(); continue; }
-      }
-      rx_fac.push_back(alts);
-      rx_loose.push_back(loose);
-      rx_pre.push_back(pre);
+      if (o.always) { always_rx.push_back(k); always = true; continue; }
+      if (o.never) continue;
+      rxs.push_back(std::move(o.g));
+      rx_tree.push_back(std::move(o.pool));
+      rx_root.push_back(o.root);
+      rx_fac.push_back(std::move(o.alts));
+      rx_loose.push_back(o.loose);
+      rx_pre.push_back(o.pre);
       rx_src.push_back(k);
     } else {
       err = "unknown pattern kind";
