@@ -693,11 +693,17 @@ def committed(cfg: str, scan_ms: float):
     """The committed rocprofv3 evidence for cfg's roofline kernel (profiles/<round>/[<box>/]
     traffic.json and summary.json, scripts/collect_profiles.py): the per-launch HBM traffic
     and the rocprof-trace fraction of the profile whose steady kernel time is nearest this
-    run's (newest round first among equals), and how far apart the two times are; a match
-    is a profile within 3 %, else the nearest is cited with match false.  (Round 5 always
-    cited the newest summary, from a different board than the driver's run.)"""
+    run's, and how far apart the two times are; a match is a profile within 3 %, else the
+    nearest is cited with match false.  Only the newest round holding cfg is searched: an
+    older round profiled older code, whose time matching would be a coincidence.  (Round 5
+    always cited the newest summary, from a different board than the driver's run.)"""
     best = None
-    for sm in sorted(ROOT.glob("profiles/r*/**/summary.json"), reverse=True):
+    rounds = sorted({p.relative_to(ROOT / "profiles").parts[0]
+                     for p in ROOT.glob("profiles/r*/**/summary.json")
+                     if (json.loads(p.read_text()).get(cfg) or {}).get("steady_us")}, reverse=True)
+    if not rounds:
+        return {}
+    for sm in sorted(ROOT.glob(f"profiles/{rounds[0]}/**/summary.json"), reverse=True):
         s = json.loads(sm.read_text()).get(cfg)
         if not s or not s.get("steady_us"):
             continue

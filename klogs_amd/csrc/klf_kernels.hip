@@ -1981,23 +1981,26 @@ __device__ __forceinline__ void push_candidate(const RunArgs& a, const VerifyQ& 
   }
 }
 __device__ void verify_hit_from(const RunArgs& a, uint32_t tile, uint32_t s, const SegDesc& sd, int32_t p,
-                                uint32_t e0, uint32_t e1, const VerifyQ& vq) {
+                                uint32_t gs, uint32_t e0, uint32_t e1, const VerifyQ& vq) {
   const DevPatterns& P = a.pats;
   const uint8_t* segp = a.bytes + sd.base;
   const int64_t rel_lo = (int64_t)(tile - sd.tile0) * kTile;
   for (uint32_t e = e0; e < e1; ++e) {
     const uint4 E = P.qf_ent[e];
-    const uint32_t m = E.y & 0xFFFFu;
-    const int32_t x = p - (int32_t)((E.y >> 16) & 0xFFu);
-    if (rel_lo + x < 0 || rel_lo + x + (int64_t)m > (int64_t)sd.len) continue;
+    const uint32_t m = E.y & 0xFFFFu, ko = (E.y >> 16) & 0xFFu;
     const uint32_t lm = (E.y & kQfLoose) ? 0x20202020u : 0u;
     auto msk_of = [&](uint32_t k) { return m - k >= 4 ? 0xFFFFFFFFu : ((1u << (8 * (m - k))) - 1u); };
-    // the first dword (from the entry: most prefilter false hits end here), then dwords 1..7
-    // with every load in flight at once (one memory round trip, not one per dword), then
+    // the pre-check (round 6): the needle's bytes at its sampled offset against the sample
+    // dword gs already in a register -- entries of other grams sharing the bucket (C4: a
+    // bucket of common grams lists dozens of needles) end here without a memory access
+    if ((((gs | lm) ^ E.w) & msk_of(ko)) != 0u) continue;
+    const int32_t x = p - (int32_t)ko;
+    if (rel_lo + x < 0 || rel_lo + x + (int64_t)m > (int64_t)sd.len) continue;
+    // the needle's dwords, then dwords 1..7 with every load in flight at once (KLF_VERIFY_PAR),
     // the rest of a needle longer than 32 bytes dword by dword
     const uint8_t* q = segp + rel_lo + x;
-    bool eq = (((gword(q) | lm) ^ E.w) & msk_of(0)) == 0;
-    if (!KLF_VERIFY_PAR) {  // A/B: dword by dword, each load after the previous compare
+    bool eq = (((gword(q) | lm) ^ P.qf_nbytes[E.x]) & msk_of(0)) == 0;
+    if (!KLF_VERIFY_PAR) {  // dword by dword, each load after the previous compare
       for (uint32_t k = 4; k < m && eq; k += 4)
         eq = (((gword(q + k) | lm) ^ P.qf_nbytes[E.x + (k >> 2)]) & msk_of(k)) == 0;
     } else if (eq && m > 4) {
@@ -2105,9 +2108,10 @@ __device__ void verify_hit(const RunArgs& a, uint32_t tile, uint32_t s, int32_t 
   const DevPatterns& P = a.pats;
   const SegDesc sd = a.segs[s];
   const int64_t rel_lo = (int64_t)(tile - sd.tile0) * kTile;
-  const uint32_t g = (gword(a.bytes + sd.base + rel_lo + p) | P.qf_fold) & P.qf_mask;
+  const uint32_t gs = gword(a.bytes + sd.base + rel_lo + p);
+  const uint32_t g = (gs | P.qf_fold) & P.qf_mask;
   const uint32_t b = qf_bucket(g, P.qf_w24, P.qf_k);
-  verify_hit_from(a, tile, s, sd, p, P.qf_head[b], P.qf_head[b + 1], vq);
+  verify_hit_from(a, tile, s, sd, p, gs, P.qf_head[b], P.qf_head[b + 1], vq);
 }
 
 // Thread per hit: the flattened tile hit slots (k_tindex), then the spilled hits.  The
@@ -2130,7 +2134,7 @@ __device__ __forceinline__ void verify_body(RunArgs& a, uint32_t bid, uint32_t n
   const uint32_t gid = bid * blockDim.x + threadIdx.x, stride = nb * blockDim.x;
   const uint32_t nf = a.counters[kCtrFlatHits];
   const DevPatterns& P = a.pats;
-  KLF_VSTAMP(0);
+  if (gid < nf) KLF_VSTAMP(0);
   for (uint32_t i0 = gid; i0 < nf; i0 += kVerifyBatch * stride) {
     uint32_t tile[kVerifyBatch], sg[kVerifyBatch], e0[kVerifyBatch], e1[kVerifyBatch];
     int32_t pp[kVerifyBatch];
@@ -2166,7 +2170,7 @@ __device__ __forceinline__ void verify_body(RunArgs& a, uint32_t bid, uint32_t n
         if (pp[u] == 0x7FFF) atomicOr(&a.counters[13], sg[u]);  // timing build: no verification work
         continue;
 #endif
-        verify_hit_from(a, tile[u], sg[u], sd[u], pp[u], e0[u], e1[u], vq);
+        verify_hit_from(a, tile[u], sg[u], sd[u], pp[u], gg[u], e0[u], e1[u], vq);
       }
   }
   const uint32_t nh = a.counters[kCtrHits] < a.qhits_cap ? a.counters[kCtrHits] : a.qhits_cap;
@@ -2182,7 +2186,7 @@ __device__ __forceinline__ void verify_body(RunArgs& a, uint32_t bid, uint32_t n
     verify_hit(a, tile, lo, (int32_t)(rel % kTile), vq);
   }
   if (gid == 0) a.counters[kCtrVerified] = nf + nh;
-  KLF_VSTAMP(7);
+  if (gid < nf) KLF_VSTAMP(7);
   // the wave's staged candidates: one queue reservation, then coalesced stores
   wave_lds_sync();
   const uint32_t nq = s_qn[wv] < kVerifyQ ? s_qn[wv] : kVerifyQ;

@@ -1660,7 +1660,14 @@ void place_tables(CompiledSet& out, const DataStats* st) {
     en[1] = (uint32_t)out.qf_needle[i].size() | (v & 0xFFu) << 16 | out.qf_nflags[i] |
             (out.qf_nshort[i] ? kQfAnchored : 0u);
     en[2] = out.qf_nrx[i];
-    en[3] = out.qf_nbytes[noff[i]];  // first dword: the pre-check
+    {  // the pre-check (round 6): the needle's four bytes at its sampled offset k, which k_verify
+       // compares with the data's sample dword already in a register (bytes past the needle: 0)
+      const auto& nd = out.qf_needle[i];
+      const uint32_t k = v & 0xFFu;
+      uint32_t w = 0;
+      for (uint32_t j = 0; j < 4 && k + j < nd.size(); ++j) w |= (uint32_t)(uint8_t)nd[k + j] << (8 * j);
+      en[3] = w;
+    }
   }
 }
 
