@@ -1502,8 +1502,10 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
       HIPCHK(e, klf::launch_pipeline(a, st, e->ev, e->num_cus, 4, &ev_mask), "launch");
     } else {
       HIPCHK(e, alloc_lines(a, cap), "alloc line arrays");
+      mark("line arrays");
       HIPCHK(e, klf::launch_pipeline(a, st, e->ev, e->num_cus, 0, &ev_mask), "launch");
     }
+    mark("launched");
     uint8_t* rb = e->h_rb.as<uint8_t>();
     HIPCHK(e, hipMemcpyAsync(rb, e->d_counters.p, sizeof(counters), hipMemcpyDeviceToHost, st), "D2H counters");
     HIPCHK(e, hipMemcpyAsync(rb + sizeof(counters), e->d_segout.p, nsegs * sizeof(SegOut), hipMemcpyDeviceToHost, st),

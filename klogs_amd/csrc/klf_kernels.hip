@@ -1980,22 +1980,22 @@ __device__ __forceinline__ void push_candidate(const RunArgs& a, const VerifyQ& 
     atomicOr(&a.counters[kCtrQOver], 1u);
   }
 }
+#ifndef KLF_VERIFY_ENT
+#define KLF_VERIFY_ENT 4  // bucket entries loaded at once by the walk (1: one at a time)
+#endif
+constexpr int kVerifyEnt = KLF_VERIFY_ENT;
 __device__ void verify_hit_from(const RunArgs& a, uint32_t tile, uint32_t s, const SegDesc& sd, int32_t p,
                                 uint32_t gs, uint32_t e0, uint32_t e1, const VerifyQ& vq) {
   const DevPatterns& P = a.pats;
   const uint8_t* segp = a.bytes + sd.base;
   const int64_t rel_lo = (int64_t)(tile - sd.tile0) * kTile;
-  for (uint32_t e = e0; e < e1; ++e) {
-    const uint4 E = P.qf_ent[e];
+  // one bucket entry past its pre-check (below): the full compare, the line, the candidate
+  auto entry = [&](const uint4 E) {
     const uint32_t m = E.y & 0xFFFFu, ko = (E.y >> 16) & 0xFFu;
     const uint32_t lm = (E.y & kQfLoose) ? 0x20202020u : 0u;
     auto msk_of = [&](uint32_t k) { return m - k >= 4 ? 0xFFFFFFFFu : ((1u << (8 * (m - k))) - 1u); };
-    // the pre-check (round 6): the needle's bytes at its sampled offset against the sample
-    // dword gs already in a register -- entries of other grams sharing the bucket (C4: a
-    // bucket of common grams lists dozens of needles) end here without a memory access
-    if ((((gs | lm) ^ E.w) & msk_of(ko)) != 0u) continue;
     const int32_t x = p - (int32_t)ko;
-    if (rel_lo + x < 0 || rel_lo + x + (int64_t)m > (int64_t)sd.len) continue;
+    if (rel_lo + x < 0 || rel_lo + x + (int64_t)m > (int64_t)sd.len) return;
     // the needle's dwords, then dwords 1..7 with every load in flight at once (KLF_VERIFY_PAR),
     // the rest of a needle longer than 32 bytes dword by dword
     const uint8_t* q = segp + rel_lo + x;
@@ -2019,10 +2019,10 @@ __device__ void verify_hit_from(const RunArgs& a, uint32_t tile, uint32_t s, con
       for (uint32_t k = 32; k < m && eq; k += 4)
         eq = (((gword(q + k) | lm) ^ P.qf_nbytes[E.x + (k >> 2)]) & msk_of(k)) == 0;
     }
-    if (!eq) continue;
+    if (!eq) return;
 #if KLF_ABL & 32
     atomicOr(&a.counters[13], x);  // timing build: bucket walk only
-    continue;
+    return;
 #endif
     KLF_VSTAMP(2);  // (a matching entry)
     // the occurrence's line: global index, start (stream offset), meta
@@ -2038,7 +2038,7 @@ __device__ void verify_hit_from(const RunArgs& a, uint32_t tile, uint32_t s, con
     const uint64_t l = a.tile_base[tile] + (lo > 0 ? k0 + (uint32_t)lo - 1 : 0);
     if (l >= a.cap_lines) {  // (k_tindex raises the overflow first; never index past the arrays)
       atomicOr(&a.counters[2], 1u);
-      continue;
+      return;
     }
     KLF_VSTAMP(3);  // (its tile's line search done)
     // the line's meta and start from its slot: the tile's own, or for the line carried in
@@ -2064,7 +2064,7 @@ __device__ void verify_hit_from(const RunArgs& a, uint32_t tile, uint32_t s, con
     const uint16_t mt = (uint16_t)(v >> 16);
     const uint64_t ls = (uint64_t)vrel + (v & kSlotOff);
     KLF_VSTAMP(4);  // (the line's start slot, walked back to)
-    if (!(mt & Meta::kParsed)) continue;
+    if (!(mt & Meta::kParsed)) return;
     if (!(E.y & kQfRegex)) {  // literal: a match when it starts inside the content
       // (a parsed line's first space ends its prefix: the stream end bounds the search)
       const uint32_t plen = (mt >> 2) == kPlenEscape ? line_plen(a, mt, segp, ls, sd.len) : mt >> 2;
@@ -2072,9 +2072,9 @@ __device__ void verify_hit_from(const RunArgs& a, uint32_t tile, uint32_t s, con
         atomicOr(&a.bits[l >> 5], 1u << (l & 31));
         if (a.count_pats) count_pair(a, l, s, E.z);
       }
-      continue;
+      return;
     }
-    if (!a.count_pats && ((a.bits[l >> 5] >> (l & 31)) & 1u)) continue;  // counting: every regex decides
+    if (!a.count_pats && ((a.bits[l >> 5] >> (l & 31)) & 1u)) return;  // counting: every regex decides
     KLF_VSTAMP(5);  // (bitmap checked)
     if (a.win_index) {
       // windowed line index (no full k_scatter): the candidate line's start, end and meta for
@@ -2101,6 +2101,33 @@ __device__ void verify_hit_from(const RunArgs& a, uint32_t tile, uint32_t s, con
     KLF_VSTAMP(6);  // (the line's bounds written)
     // {line | regex << 40, the occurrence (stream offset) | stream << 40}
     push_candidate(a, vq, l | ((uint64_t)E.z << 40), (uint64_t)(rel_lo + x) | ((uint64_t)s << 40));
+  };
+  // the bucket walk, four entries loaded at once: the pre-check (round 6) compares the
+  // needle's bytes at its sampled offset with the sample dword gs already in a register, so
+  // entries of other grams sharing the bucket (C4: a bucket of a common gram lists dozens of
+  // needles) end without a further access -- the walk's cost is its entry loads, in flight
+  // together instead of one after the other
+  for (uint32_t eb = e0; eb < e1; eb += kVerifyEnt) {
+    uint4 Eb[kVerifyEnt];
+    uint32_t pass = 0;
+#pragma unroll
+    for (int j = 0; j < kVerifyEnt; ++j) Eb[j] = eb + (uint32_t)j < e1 ? P.qf_ent[eb + (uint32_t)j] : make_uint4(0, 0, 0, 0);
+#pragma unroll
+    for (int j = 0; j < kVerifyEnt; ++j) {
+      const uint32_t m = Eb[j].y & 0xFFFFu, ko = (Eb[j].y >> 16) & 0xFFu;
+      const uint32_t lm = (Eb[j].y & kQfLoose) ? 0x20202020u : 0u;
+      const uint32_t mk = m - ko >= 4 ? 0xFFFFFFFFu : ((1u << (8 * (m - ko))) - 1u);
+      if (eb + (uint32_t)j < e1 && (((gs | lm) ^ Eb[j].w) & mk) == 0u) pass |= 1u << j;
+    }
+    while (pass) {  // (register select, no dynamic index into Eb: that would go to scratch)
+      const int j = __builtin_ctz(pass);
+      pass &= pass - 1u;
+      uint4 E = Eb[0];
+#pragma unroll
+      for (int i = 1; i < kVerifyEnt; ++i)
+        if (j == i) E = Eb[i];
+      entry(E);
+    }
   }
 }
 
