@@ -115,7 +115,7 @@ typedef struct klf_filter {
 
 /* klf_result_index_mode: how much of the u64 line index the run wrote itself. */
 #define KLF_INDEX_FULL 0       /* every line of every stream                                  */
-#define KLF_INDEX_WINDOWS 1    /* the lines of each stream's --tail window (literal patterns)  */
+#define KLF_INDEX_WINDOWS 1    /* the lines of each stream's --tail window (prefiltered sets)  */
 #define KLF_INDEX_ON_DEMAND 2  /* none (no patterns, --tail -1, the dense copy path)          */
 
 typedef struct klf_counts {
@@ -209,7 +209,10 @@ int klf_result_write(klf_result* r, const int* fds, uint32_t n_fds, uint64_t* wr
  * [5] workspace memsets (KLF_FILTER_STAGE_TIMES, else 0), [6] the k_scan kernel alone
  * (part of [0]): the start / end timestamps of its own dispatch (hipExtLaunchKernel
  * events, no event record beside it), [7] the dense copy kernel k_tcopy alone, the same way
- * (part of [3]; it exits at once when the run takes the sparse gather path).  n = entries written. */
+ * (part of [3]; it exits at once when the run takes the sparse gather path).  With
+ * KLF_GRAPH=1 a batch of at most KLF_GRAPH_MAX_MB (default 256) MiB whose run repeats the
+ * previous run's arguments replays its launch sequence as a HIP graph: such a run reports
+ * [4] only, a graph's replays recording no per-kernel events.  n = entries written. */
 int klf_result_timing(const klf_result* r, double* ms, uint32_t cap, uint32_t* n);
 /* Totals across streams. */
 int klf_result_totals(const klf_result* r, klf_counts* totals);

@@ -200,7 +200,7 @@ struct klf_engine {
   DevBuf d_block2;  // the first run's line arrays, slot pool / records and output (sized after its sample)
   std::vector<DevBuf*> block2_users;
   DevBuf d_batch, d_segs, d_tstat, d_slots, d_pool, d_tile_base, d_bsum, d_cstatus, d_counters, d_line_off,
-      d_meta, d_bits, d_segout, d_wpre, d_out, d_mpart, d_trec, d_truns, d_kbase;
+      d_meta, d_bits, d_wpre, d_out, d_mpart, d_trec, d_truns, d_kbase;
   // one-pass compaction (RunArgs::fuse): range table, extents, range states; d_out2 the
   // contiguous device copy klf_result_device_out makes of a fused result on demand
   DevBuf d_fext0, d_fext, d_frinfo, d_out2;
@@ -214,7 +214,7 @@ struct klf_engine {
   // runs (the first run sizes them from its own tile index, between two launch phases)
   double line_density = 0.0;
   bool dense_tail_seen = false;  // a --tail run took the dense compaction (keep its run table)
-  HostBuf h_rb;  // run readback: counters (64 B), then the SegOut table
+  HostBuf h_rb;  // run readback: the counters (kCtrBytes), the SegOut table, a one-pass run's extents
   HostBuf h_stage;  // pinned staging of the prefilter tables (upload_prefilter)
   HostBuf h_acblk;  // the automaton thread's tables (pinned), uploaded on the launch stream at the join
   size_t ac_total = 0, ac_off[5] = {0, 0, 0, 0, 0}, ac_cap[5] = {0, 0, 0, 0, 0};
@@ -230,6 +230,16 @@ struct klf_engine {
   DevBuf d_acblk;
   hipEvent_t stage_ev = nullptr;  // the staged copies have drained
   bool stage_ev_pending = false;
+  // KLF_GRAPH=1: small batches replay their launch sequence as a HIP graph (round 6): ~12
+  // launches cost ~35-45 us of host time.  Opt-in: measured on C1 (64 MiB) the run went
+  // 104 -> ~95 us, the device being the bound, while the first capture costs 5-7 ms (most
+  // of it creating cap_stream), which a short-lived engine pays in full.  A sequence is
+  // captured (on cap_stream: the engine's own stream may be the null stream) the second
+  // time the same arguments run; graph_off after a capture that failed.
+  hipStream_t cap_stream = nullptr;
+  hipGraphExec_t gexec = nullptr;
+  std::vector<uint8_t> gkey, gprev;  // the captured arguments; the previous eager run's
+  bool graph_off = false;
   hipEvent_t ev[11] = {};  // [7], [8]: k_scan's dispatch (hipExtLaunchKernel start / stop); [9], [10]: k_tcopy's; [6] unused
   klf::RunArgs last_args{};  // arguments of the latest completed run (klf_retail)
   // the latest run's global line index is still to be built (lazy index, dense path): the
@@ -268,6 +278,13 @@ struct klf_result {
   std::vector<uint64_t> fx;
   std::vector<uint32_t> fx_first;
 };
+
+// The run's counters and its per-stream records share one allocation (d_counters: the
+// counters, then the records from byte kCtrBytes on), so that one D2H copy reads both back.
+constexpr size_t kCtrBytes = klf::kNumCounters * 4;
+static SegOut* segout_of(klf_engine* e) {
+  return reinterpret_cast<SegOut*>(e->d_counters.as<uint8_t>() + kCtrBytes);
+}
 
 static int set_err(klf_engine* e, int code, const std::string& m) {
   if (e) e->err = m;
@@ -698,7 +715,7 @@ extern "C" void klf_close(klf_engine* e) {
                     &e->d_rx_follow, &e->d_rx_vec, &e->d_rx_flags, &e->d_rx_pre, &e->d_qf_bitmap, &e->d_qf_head,
                     &e->d_qf_ent, &e->d_qf_nbytes, &e->d_qf_anc, &e->d_rx_vec4, &e->d_qhits, &e->d_hslots, &e->d_hist, &e->d_hflat, &e->d_cand, &e->d_batch, &e->d_segs, &e->d_tstat,
                     &e->d_slots, &e->d_pool, &e->d_tile_base, &e->d_bsum, &e->d_cstatus, &e->d_counters, &e->d_cmap, &e->d_cseg,
-                    &e->d_line_off, &e->d_meta, &e->d_bits, &e->d_segout, &e->d_wpre, &e->d_out, &e->d_tile_seg, &e->d_mpart, &e->d_trec, &e->d_truns, &e->d_kbase,
+                    &e->d_line_off, &e->d_meta, &e->d_bits, &e->d_wpre, &e->d_out, &e->d_tile_seg, &e->d_mpart, &e->d_trec, &e->d_truns, &e->d_kbase,
                     &e->d_fext0, &e->d_fext, &e->d_frinfo, &e->d_out2})
     b->release();
   e->d_asm.release();
@@ -726,6 +743,8 @@ extern "C" void klf_close(klf_engine* e) {
     if (x) (void)hipEventDestroy(x);
   if (e->copy_done) (void)hipEventDestroy(e->copy_done);
   if (e->copy_stream) (void)hipStreamDestroy(e->copy_stream);
+  if (e->gexec) (void)hipGraphExecDestroy(e->gexec);
+  if (e->cap_stream) (void)hipStreamDestroy(e->cap_stream);
   if (e->stage_ev) (void)hipEventDestroy(e->stage_ev);
   delete e;
   (void)hipGetLastError();  // nothing above reports: leave no sticky error for the next engine
@@ -965,6 +984,7 @@ static hipError_t wait_stream(hipStream_t st, uint64_t spin_us) {
 static hipError_t grow_out_retail(klf_engine* e, klf::RunArgs& a, std::vector<SegOut>& so) {
   a.plan_runs = 0;  // the tile plans were consumed (k_cmove rewrote them): list the runs again
   a.skip_tcopy = 0;
+  a.plan_mode = 0;  // (k_cplan / k_cmid / k_cmove, whichever path the window takes)
   for (int k = 0; k < 2; ++k) {
     uint64_t need = 0;
     for (auto& s : so) need = std::max(need, s.out_hi);
@@ -974,14 +994,67 @@ static hipError_t grow_out_retail(klf_engine* e, klf::RunArgs& a, std::vector<Se
     a.out_cap = e->d_out.cap;
     if ((h = klf::launch_retail(a, e->stream, e->ev, e->num_cus)) != hipSuccess) return h;
     uint32_t* rb = static_cast<uint32_t*>(e->h_rb.p);  // counters, then the stream records
-    if ((h = hipMemcpyAsync(rb, e->d_counters.p, 32 * 4, hipMemcpyDeviceToHost, e->stream)) != hipSuccess) return h;
-    if ((h = hipMemcpyAsync(so.data(), e->d_segout.p, so.size() * sizeof(SegOut), hipMemcpyDeviceToHost,
+    if ((h = hipMemcpyAsync(rb, e->d_counters.p, kCtrBytes + so.size() * sizeof(SegOut), hipMemcpyDeviceToHost,
                             e->stream)) != hipSuccess)
       return h;
     if ((h = hipStreamSynchronize(e->stream)) != hipSuccess) return h;
+    memcpy(so.data(), reinterpret_cast<uint8_t*>(rb) + kCtrBytes, so.size() * sizeof(SegOut));
     if (!rb[klf::kCtrOutShort]) return hipSuccess;
   }
   return hipErrorOutOfMemory;  // the ranges did not settle (cannot happen: they do not depend on the buffer)
+}
+
+// One steady run's launch sequence (launch_pipeline, phase 0, no events inside: a graph's
+// event nodes are not re-recorded by a replay) as a replayed graph, bracketed by ev[0] /
+// ev[5] on the engine stream.  Returns false when the run should launch eagerly instead:
+// a first sighting of these arguments, or a capture that failed (then never again).
+static bool launch_graph(klf_engine* e, const klf::RunArgs& a, uint32_t& ev_mask) {
+  const uint8_t* k = reinterpret_cast<const uint8_t*>(&a);
+  std::vector<uint8_t> key(k, k + sizeof(a));
+  key.insert(key.end(), reinterpret_cast<const uint8_t*>(&e->num_cus),
+             reinterpret_cast<const uint8_t*>(&e->num_cus) + sizeof(e->num_cus));
+  if (!e->gexec || key != e->gkey) {
+    if (key != e->gprev) {  // first sighting: eager, remembered
+      e->gprev = std::move(key);
+      return false;
+    }
+    if (e->gexec) {
+      (void)hipGraphExecDestroy(e->gexec);
+      e->gexec = nullptr;
+      e->gkey.clear();
+    }
+    if (!e->cap_stream && hipStreamCreateWithFlags(&e->cap_stream, hipStreamNonBlocking) != hipSuccess) {
+      (void)hipGetLastError();
+      e->graph_off = true;
+      return false;
+    }
+    hipGraph_t g = nullptr;
+    bool ok = hipStreamBeginCapture(e->cap_stream, hipStreamCaptureModeRelaxed) == hipSuccess;
+    if (ok) {
+      const hipError_t h = klf::launch_pipeline(a, e->cap_stream, nullptr, e->num_cus, 0, nullptr);
+      ok = hipStreamEndCapture(e->cap_stream, &g) == hipSuccess && h == hipSuccess && g;
+    }
+    if (ok) ok = hipGraphInstantiate(&e->gexec, g, nullptr, nullptr, 0) == hipSuccess;
+    if (g) (void)hipGraphDestroy(g);
+    if (!ok) {
+      (void)hipGetLastError();
+      if (e->gexec) (void)hipGraphExecDestroy(e->gexec);
+      e->gexec = nullptr;
+      e->graph_off = true;
+      if (getenv("KLF_DIAG")) fprintf(stderr, "[klf] graph capture failed: eager launches from here on\n");
+      return false;
+    }
+    e->gkey = std::move(key);
+  }
+  if (hipEventRecord(e->ev[0], e->stream) != hipSuccess) return false;
+  if (hipGraphLaunch(e->gexec, e->stream) != hipSuccess) {
+    (void)hipGetLastError();
+    e->graph_off = true;
+    return false;
+  }
+  ev_mask = 1u;
+  if (hipEventRecord(e->ev[5], e->stream) == hipSuccess) ev_mask |= 1u << 5;
+  return true;
 }
 
 static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_streams, const uint64_t* seg_base,
@@ -1159,7 +1232,7 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
   std::vector<std::pair<DevBuf*, size_t>> ws = {
       {&e->d_tstat, ntiles * sizeof(klf::TileStat)},
       {&e->d_tile_base, ntiles * 8}, {&e->d_bsum, (ntiles / 1024 + 2) * 4 * 8},
-      {&e->d_counters, klf::kNumCounters * 4}, {&e->d_segout, nsegs * sizeof(SegOut)},
+      {&e->d_counters, kCtrBytes + nsegs * sizeof(SegOut)} /* + the stream records */,
       {&e->d_wpre, (3 * (size_t)nsegs + 2) * 8} /* + wgrp */};
   // the dense compaction's per-tile run table (512 B per tile: 2.1 GB for 32 GiB) only for
   // runs without a --tail limit or after a --tail run took the dense path (k_tcopy lists
@@ -1353,7 +1426,7 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
     a.tile_base = e->d_tile_base.as<uint64_t>();
     a.bsum = e->d_bsum.as<uint64_t>();
     a.counters = e->d_counters.as<uint32_t>();
-    a.segout = e->d_segout.as<SegOut>();
+    a.segout = segout_of(e);
     a.wpre = e->d_wpre.as<uint64_t>();
     a.wgrp = a.wpre + nsegs + 1;
     a.out = e->d_out.as<uint8_t>();
@@ -1391,6 +1464,20 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
                     !(getenv("KLF_SKIP_IDLE") && !strcmp(getenv("KLF_SKIP_IDLE"), "0"))) ? 1u : 0u;
     // waves per scatter group (0: k_scatter picks it from its grid; tests force a split)
     a.scatter_split = getenv("KLF_SCATTER_SPLIT") ? (uint32_t)std::max(0L, atol(getenv("KLF_SCATTER_SPLIT"))) : 0u;
+    // a --tail run's sparse gather with fewer launches (RunArgs::plan_mode), without patterns
+    // (a window of at most S (N + 1) lines, the line index built before k_tailw): k_tailw
+    // plans a window of at most 4 compaction blocks itself (C1: k_tailw +4.7 us for k_cplan
+    // 4.8 + k_cmid 5.0), else k_cplan's last block runs the prefix (7.5 us).  A grep run's
+    // window spans every line between its N + 1 matches: its block sums need k_cplan's
+    // whole grid (C5 with the prefix in k_cplan's last block: 15.9 -> 24.1 us, r6t).
+    // (KLF_PLAN_MODE=0 / 1 / 2 forces one, tests)
+    a.plan_mode = 0;
+    if (compact_mode == 1 && f->tail >= 0 && (mode == klf::CompiledSet::kNone || getenv("KLF_PLAN_MODE"))) {
+      const bool index_first = !a.win_index && !lazy_index;
+      a.plan_mode = index_first && mode == klf::CompiledSet::kNone &&
+                    (uint64_t)nsegs * ((uint64_t)f->tail + 1) <= 4ull * klf::kCompactLines ? 2u : 1u;
+      if (const char* v = getenv("KLF_PLAN_MODE")) a.plan_mode = std::min<uint32_t>((uint32_t)atoi(v), index_first ? 2u : 1u);
+    }
     a.count_pats = count ? 1u : 0u;
     a.pcount = count ? e->d_pcount.as<uint32_t>() : nullptr;
     a.pairs = count ? e->d_pairs.as<uint64_t>() : nullptr;
@@ -1407,6 +1494,8 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
   };
   bool overflow = false, pairs_over = false;
   uint32_t ev_mask = 0;
+  const bool graph_on = getenv("KLF_GRAPH") && strcmp(getenv("KLF_GRAPH"), "0") != 0;  // (opt-in)
+  const uint64_t graph_max = (getenv("KLF_GRAPH_MAX_MB") ? (uint64_t)std::max(0L, atol(getenv("KLF_GRAPH_MAX_MB"))) : 256ull) << 20;
   for (int attempt = 0, line_reruns = 0, pair_reruns = 0; attempt < 4; ++attempt) {
     if (count) {
       HIPCHK(e, e->d_pcount.ensure((size_t)nsegs * e->cs.n_cids * 4), "alloc pcount");
@@ -1452,7 +1541,7 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
     uint32_t counters[32];
     // (+ a one-pass run's extents, read back with the counters: one sync on e->stream)
     const size_t rb_ext = fuse_ok ? (size_t)e->fuse_next * 16 : 0;
-    HIPCHK(e, e->h_rb.ensure(sizeof(counters) + nsegs * sizeof(SegOut) + rb_ext), "alloc readback");
+    HIPCHK(e, e->h_rb.ensure(kCtrBytes + nsegs * sizeof(SegOut) + rb_ext), "alloc readback");
     // the literal automaton (klf_open's thread) is read from k_tindex on (deferred lines)
     auto join_ac = [&]() -> int {
       if (const int rc = ensure_ac(e); rc != KLF_OK) return rc;
@@ -1465,13 +1554,12 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
       a.cap_lines = 1ull << 40;  // phase 1 indexes no line array (k_tindex: no overflow, no bitmap)
       HIPCHK(e, klf::launch_pipeline(a, st, e->ev, e->num_cus, 1, &ev_mask), "launch");
       uint8_t* rb1 = e->h_rb.as<uint8_t>();
-      HIPCHK(e, hipMemcpyAsync(rb1, e->d_counters.p, sizeof(counters), hipMemcpyDeviceToHost, st), "D2H counters");
-      HIPCHK(e, hipMemcpyAsync(rb1 + sizeof(counters), e->d_segout.p, nsegs * sizeof(SegOut), hipMemcpyDeviceToHost, st),
-             "D2H segout");
+      HIPCHK(e, hipMemcpyAsync(rb1, e->d_counters.p, kCtrBytes + nsegs * sizeof(SegOut), hipMemcpyDeviceToHost, st),
+             "D2H counters + records");
       HIPCHK(e, hipStreamSynchronize(st), "sync phase 1");
       mark("phase 1 (launch + sync)");
       memcpy(counters, rb1, sizeof(counters));
-      memcpy(r->so.data(), rb1 + sizeof(counters), nsegs * sizeof(SegOut));
+      memcpy(r->so.data(), rb1 + kCtrBytes, nsegs * sizeof(SegOut));
       if (counters[2]) {  // the dense-tile pool overflowed: a whole rerun (as below)
         e->pool_cap = std::max<uint64_t>(e->pool_cap, (uint64_t)counters[klf::kCtrPool] + (uint64_t)e->num_cus * 16 * 4096);
         e->line_density = (double)(r->so[nsegs - 1].line_hi + 1) / (double)total_bytes;
@@ -1503,20 +1591,22 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
     } else {
       HIPCHK(e, alloc_lines(a, cap), "alloc line arrays");
       mark("line arrays");
-      HIPCHK(e, klf::launch_pipeline(a, st, e->ev, e->num_cus, 0, &ev_mask), "launch");
+      // KLF_GRAPH=1: a small batch (KLF_GRAPH_MAX_MB, default 256) replays a graph
+      const bool graph = !e->graph_off && !a.stage_times && total_bytes <= graph_max && graph_on;
+      if (!(graph && launch_graph(e, a, ev_mask)))
+        HIPCHK(e, klf::launch_pipeline(a, st, e->ev, e->num_cus, 0, &ev_mask), "launch");
     }
     mark("launched");
     uint8_t* rb = e->h_rb.as<uint8_t>();
-    HIPCHK(e, hipMemcpyAsync(rb, e->d_counters.p, sizeof(counters), hipMemcpyDeviceToHost, st), "D2H counters");
-    HIPCHK(e, hipMemcpyAsync(rb + sizeof(counters), e->d_segout.p, nsegs * sizeof(SegOut), hipMemcpyDeviceToHost, st),
-           "D2H segout");
+    HIPCHK(e, hipMemcpyAsync(rb, e->d_counters.p, kCtrBytes + nsegs * sizeof(SegOut), hipMemcpyDeviceToHost, st),
+           "D2H counters + records");
     if (a.fuse)
-      HIPCHK(e, hipMemcpyAsync(rb + sizeof(counters) + nsegs * sizeof(SegOut), e->d_fext.p, rb_ext,
+      HIPCHK(e, hipMemcpyAsync(rb + kCtrBytes + nsegs * sizeof(SegOut), e->d_fext.p, rb_ext,
                                hipMemcpyDeviceToHost, st), "D2H extents");
     HIPCHK(e, wait_stream(st, 1000 + total_bytes / 2000000), "sync");
     mark("pipeline done");
     memcpy(counters, rb, sizeof(counters));
-    memcpy(r->so.data(), rb + sizeof(counters), nsegs * sizeof(SegOut));
+    memcpy(r->so.data(), rb + kCtrBytes, nsegs * sizeof(SegOut));
     e->last_segs = segs;
     if (getenv("KLF_DIAG"))
       fprintf(stderr, "[klf] hits=%u spilled=%u hits_over=%u nfa_queue=%u queue_over=%u deferred=%u\n",
@@ -1566,7 +1656,7 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
     if (a.fuse) {  // the extents, in stream order (ranges ascend, and so do a range's streams)
       r->fused = true;
       r->fx.resize((size_t)e->fuse_next * 2);
-      memcpy(r->fx.data(), rb + sizeof(counters) + nsegs * sizeof(SegOut), (size_t)e->fuse_next * 16);
+      memcpy(r->fx.data(), rb + kCtrBytes + nsegs * sizeof(SegOut), (size_t)e->fuse_next * 16);
       r->fx_first.assign(nsegs + 1, e->fuse_next);
       for (uint32_t q = e->fuse_nranges; q-- > 0;) {
         const uint32_t s0 = seg_of_tile((uint64_t)q * e->fuse_range);
@@ -1637,9 +1727,13 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
       fprintf(stderr, "[klf] timing events %d/%d unreadable: %s\n", k0, k1, hipGetErrorString(h));
   };
   static const int kPairs[6][3] = {{1, 2, 0}, {2, 3, 1}, {3, 4, 2}, {4, 5, 3}, {0, 5, 4}, {0, 1, 5}};
+  const auto t_q0 = std::chrono::steady_clock::now();
   for (const auto& q : kPairs) elapsed(q[0], q[1], q[2]);
   elapsed(7, 8, 6);   // k_scan's dispatch alone
   elapsed(9, 10, 7);  // k_tcopy's dispatch alone (dense copy)
+  if (diag_marks)
+    fprintf(stderr, "[klf] timing queries %.1f us\n",
+            std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t_q0).count());
   r->ev_mask = ev_mask;
   r->total_lines = r->so[nsegs - 1].line_hi;
   for (auto& s : r->so) r->total_out = std::max(r->total_out, s.out_hi);
@@ -1680,14 +1774,17 @@ extern "C" int klf_retail(klf_engine* e, klf_result* prev, int64_t tail, klf_res
     a.fuse = 0;  // (the two-pass compaction, over the line index)
     a.plan_runs = 0;  // (plans assume --tail -1 and are consumed by the run)
     a.skip_tcopy = 0;  // (another window may take the dense path)
+    a.plan_mode = 0;   // (and may be larger: the gather's plan over the whole grid)
     hipStream_t st = e->stream;
     uint32_t rmask = 0;
     hipError_t h = klf::launch_retail(a, st, e->ev, e->num_cus, &rmask);
     uint32_t short_out = 0;
-    if (h == hipSuccess) h = hipMemcpyAsync(r->so.data(), e->d_segout.p, nsegs * sizeof(SegOut), hipMemcpyDeviceToHost, st);
-    if (h == hipSuccess) h = hipMemcpyAsync(e->h_rb.p, e->d_counters.p, 32 * 4, hipMemcpyDeviceToHost, st);
+    if (h == hipSuccess) h = e->h_rb.ensure(kCtrBytes + nsegs * sizeof(SegOut));
+    if (h == hipSuccess)
+      h = hipMemcpyAsync(e->h_rb.p, e->d_counters.p, kCtrBytes + nsegs * sizeof(SegOut), hipMemcpyDeviceToHost, st);
     if (h == hipSuccess) h = hipStreamSynchronize(st);
     if (h == hipSuccess) {
+      memcpy(r->so.data(), e->h_rb.as<uint8_t>() + kCtrBytes, nsegs * sizeof(SegOut));
       short_out = static_cast<uint32_t*>(e->h_rb.p)[klf::kCtrOutShort];
       r->compaction = static_cast<uint32_t*>(e->h_rb.p)[klf::kCtrDense] ? KLF_COMPACT_TILES : KLF_COMPACT_GATHER;
     }

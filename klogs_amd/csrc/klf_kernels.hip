@@ -2762,6 +2762,7 @@ __device__ __forceinline__ void wprefix_body(RunArgs& a) {
 __global__ __launch_bounds__(256) void k_retail_init(RunArgs a) {
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     a.counters[kCtrTailDone] = 0;  // k_tailw's tickets
+    a.counters[kCtrPlanDone] = 0;  // k_cplan's
     a.counters[kCtrOutShort] = 0;
   }
   for (uint32_t s = blockIdx.x * 256 + threadIdx.x; s < a.nsegs; s += gridDim.x * 256) {
@@ -2840,14 +2841,15 @@ __device__ __forceinline__ void window_lines(const RunArgs& a, uint64_t w0, uint
 
 constexpr uint32_t kCsegBoundary = 0x80000000u;  // cseg flag: block holds a stream's first/last window line
 
-__device__ __forceinline__ void csum_body(RunArgs& a) {
+// (compaction blocks b0, b0 + bstep, ...: k_cplan's grid, or all of them in one block)
+__device__ __forceinline__ void csum_body(RunArgs& a, uint32_t b0, uint32_t bstep) {
   __shared__ uint64_t s_wb[4], s_wc[4];
   __shared__ uint32_t s_wf[4];
   if (a.counters[2] || a.counters[kCtrDense]) return;
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const uint64_t W = a.wpre[a.nsegs];
   const uint32_t nblocks = a.counters[3];
-  for (uint32_t blk = blockIdx.x; blk < nblocks; blk += gridDim.x) {
+  for (uint32_t blk = b0; blk < nblocks; blk += bstep) {
     WinLines r;
     window_lines(a, (uint64_t)blk * kCompactLines + (uint64_t)t * 4, W, r);
     const uint64_t b = wave_sum(r.bytes), c = wave_sum((uint64_t)r.nsel);
@@ -3710,6 +3712,12 @@ __global__ __launch_bounds__(256) void k_tailw(RunArgs a) {
       __syncthreads();
       win_groups_prefix(a);
     }
+    if (a.plan_mode == 2) {  // a small --tail selection: the gather's block sums and prefix here
+      __syncthreads();
+      csum_body(a, 0, 1);
+      __syncthreads();
+      cscan_body(a);
+    }
   }
 }
 // Then three launches serve either compaction path (k_wprefix's choice, counters[kCtrDense]):
@@ -3721,7 +3729,20 @@ __global__ __launch_bounds__(256) void k_cplan(RunArgs a, const uint32_t* __rest
                                                const SegDesc* __restrict__ segs, const TileStat* __restrict__ tstat,
                                                const uint64_t* __restrict__ tbase, const SegOut* __restrict__ sout) {
   if (a.counters[kCtrDense]) tkeep_body(a, tseg, segs, tstat, tbase, sout);
-  else csum_body(a);
+  else csum_body(a, blockIdx.x, gridDim.x);
+  if (a.plan_mode == 1) {  // the last block to finish runs k_cmid's prefix (not launched)
+    __shared__ uint32_t s_last;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      __threadfence();  // this block's sums (thread 0 wrote them) before its ticket
+      s_last = atomicAdd(&a.counters[kCtrPlanDone], 1u) == gridDim.x - 1 ? 1u : 0u;
+    }
+    __syncthreads();
+    if (s_last) {
+      __threadfence();
+      cscan_body(a);
+    }
+  }
 }
 __global__ __launch_bounds__(256) void k_cmid(RunArgs a) {
   if (a.counters[kCtrDense]) ksum_body<16>(a);
@@ -4512,13 +4533,24 @@ static hipError_t launch_tail_stage(const RunArgs& a, hipStream_t st, hipEvent_t
   }
   {
     const uint32_t gt = (a.ntiles + 4 * kTkBatch - 1) / (4 * kTkBatch);
-    const uint32_t gp = (uint32_t)num_cus * 8;
-    hipLaunchKernelGGL(k_cplan, dim3(a.compact_mode != 1 && gt < gp ? gt : gp), dim3(256), 0, st, a, a.tile_seg,
-                       a.segs, a.tstat, a.tile_base, a.segout);
-    KLF_TRY(hipGetLastError());
+    uint32_t gp = (uint32_t)num_cus * 8;
+    if (a.plan_mode == 1) {  // one ticket per block: a grid of one block per CU at most
+      gp = (uint32_t)num_cus;
+      if (a.grep_mode == kGrepNone && a.tail >= 0) {  // (<= S (N + 1) window lines without patterns)
+        const uint64_t wmax = (uint64_t)a.nsegs * ((uint64_t)a.tail + 1) / kCompactLines + 1;
+        gp = wmax < gp ? (uint32_t)wmax : gp;
+      }
+    }
+    if (a.plan_mode != 2) {
+      hipLaunchKernelGGL(k_cplan, dim3(a.compact_mode != 1 && gt < gp ? gt : gp), dim3(256), 0, st, a, a.tile_seg,
+                         a.segs, a.tstat, a.tile_base, a.segout);
+      KLF_TRY(hipGetLastError());
+    }
     const uint32_t nb = (a.ntiles + 4095) / 4096;
-    hipLaunchKernelGGL(k_cmid, dim3(nb), dim3(256), 0, st, a);
-    KLF_TRY(hipGetLastError());
+    if (a.plan_mode == 0) {
+      hipLaunchKernelGGL(k_cmid, dim3(nb), dim3(256), 0, st, a);
+      KLF_TRY(hipGetLastError());
+    }
     const uint32_t gg = (uint32_t)num_cus * KLF_CG_GRID;
     hipLaunchKernelGGL(k_cmove, dim3(nb > gg ? nb : gg), dim3(kThreads), 0, st, a);
     KLF_TRY(hipGetLastError());

@@ -61,6 +61,7 @@ constexpr uint32_t kCopyChunkMinLog2 = 12;
 constexpr uint32_t kCopyChunksTarget = KLF_COPY_CHUNKS_TARGET;  // one resident generation of k_cmove workgroups (4 per CU)
 constexpr uint32_t kCtrChunkLog2 = 16;               // counters[16]: log2 of this run's copy chunk
 constexpr uint32_t kCtrTailDone = 18;                // counters[18]: k_tailw blocks done
+constexpr uint32_t kCtrPlanDone = 26;                // counters[26]: k_cplan blocks done (plan_mode 1)
 constexpr uint32_t kCtrVerified = 10;                // counters[10]: hits k_verify walked (diagnostics)
 constexpr uint32_t kCtrDense = 14;                   // counters[14]: dense compaction (k_tkeep / k_tcopy)
 constexpr uint32_t kCtrFuseBad = 24;                 // counters[24]: the one-pass compaction was voided (rerun)
@@ -336,6 +337,10 @@ struct RunArgs {
   uint32_t scatter_split; // k_scatter: waves per 64-tile group (small batches: a group's lines split over them; 0 = 1)
   uint32_t skip_match;    // prefiltered set: k_match not launched (an overflow redoes the run with it)
   uint32_t skip_tcopy;    // --tail run: k_tcopy not launched (the host launches it when the run went dense)
+  // line gather's block sums / prefix (a --tail run, always the sparse path): 0 k_cplan,
+  // k_cmid, k_cmove; 1 k_cplan's last block runs the prefix (no k_cmid); 2 k_tailw's last
+  // block runs both (no k_cplan, no k_cmid: the line index exists before k_tailw)
+  uint32_t plan_mode;
   // per-pattern counts (KLF_FILTER_PATTERN_COUNTS): pcount[segment * n_cids + cid] lines,
   // each (line, cid) counted once through the `pairs` hash set (open addressing, u64 keys)
   uint32_t count_pats;

@@ -599,3 +599,68 @@ def test_literal_automaton_thread(gpu, monkeypatch):
     check_against_c([d], None, 40, lits)
     monkeypatch.setenv("KLF_HITS_CAP", "1")
     check_against_c([d, synth.generate(synth.ADVERSARIAL, 32, 1, 30_000, permille=40)], (synth.T0 + 1800, 0), -1, lits)
+
+
+@pytest.mark.parametrize("pats", ["none", "literal", "regex"])
+def test_graph_replay(gpu, monkeypatch, pats):
+    """Small batches replay their launch sequence as a HIP graph (round 6): captured the
+    second time the same arguments run, replayed from the third, recaptured when they
+    change.  Every run of an alternating sequence against the C / Python oracle, and the
+    replays carry no scan dispatch events (the mark that the graph ran, not eager launches)."""
+    import torch
+    monkeypatch.setenv("KLF_GRAPH", "1")
+    streams = [synth.generate(synth.TEXT, 81, 0, 2_000_000), b"",
+               synth.generate(synth.JSON, 82, 1, 700_000, permille=20),
+               synth.generate(synth.ADVERSARIAL, 83, 2, 2000, drop_final_nl=True, permille=40)]
+    lens = [len(s) for s in streams]
+    base, total = E.layout(lens)
+    host = np.zeros(total, dtype=np.uint8)
+    for b, s in zip(base, streams):
+        host[b:b + len(s)] = np.frombuffer(s, dtype=np.uint8)
+    dev = torch.from_numpy(host).to("cuda")
+    torch.cuda.synchronize()
+    kw = {"none": {}, "literal": {"grep": [synth.NEEDLE, b"ms"]},
+          "regex": {"grep": [synth.NEEDLE], "match": synth.c5_regexes()[:8]}}[pats]
+    A = ((synth.T0 + 1800, 0), 100)
+    B = (None, -1)
+    seq = [A, A, A, A, B, B, B, A, A, B]
+    replays = 0
+    pp = po.compile_patterns(kw.get("grep", []), kw.get("match", [])) if pats == "regex" else None
+    with E.Engine(0, **kw) as eng:
+        for since, tail in seq:
+            r = eng.run_device(dev.data_ptr(), base, lens, since=since, tail=tail)
+            tm = r.timing()
+            replays += tm[6] == 0
+            for i, s in enumerate(streams):
+                so = r.stream(i)
+                if pats == "regex":
+                    ref = po.filter_stream(s, since or GZ, tail, pp)
+                    assert so.out == ref.out, (i, since, tail)
+                    assert so.counts["matched"] == ref.n_matched, (i, since, tail)
+                else:
+                    out, lo, bits, c = co.filter_stream(s, since or GZ, tail, list(kw.get("grep", [])))
+                    assert so.out == out, (i, since, tail)
+                    assert np.array_equal(r.lines(i), lo), (i, since, tail)
+                    for k in ("lines", "parsed", "since_ok", "selected", "out_bytes"):
+                        assert so.counts[k] == c[k], (i, k, since, tail)
+            r.free()
+    # replays: runs 3, 4 (A), 7 (B), 9 (A) -- each the third or later sighting in a row
+    assert replays >= 4, replays
+
+
+@pytest.mark.parametrize("plan", ["0", "1", "2"])
+def test_gather_plan_modes(gpu, monkeypatch, plan):
+    """A --tail run's line gather with its block sums and prefix in k_cplan / k_cmid (0), in
+    k_cplan's last block (1) or in k_tailw's last block (2; runs whose line index precedes
+    k_tailw, i.e. no patterns): selections of one to many compaction blocks, empty streams,
+    windows with a fragment, literal and regex sets (which fall back to 1)."""
+    monkeypatch.setenv("KLF_PLAN_MODE", plan)
+    streams = [synth.generate(synth.TEXT, 91, 0, 2_000_000), b"",
+               synth.generate(synth.ADVERSARIAL, 92, 1, 3000, drop_final_nl=True, permille=40),
+               synth.generate(synth.JSON, 93, 2, 900_000, permille=20),
+               synth.generate(synth.LONGJSON, 94, 3, 1_500_000, permille=5)]
+    for since, tail in ((None, 0), (None, 1), ((synth.T0 + 1800, 0), 100), (None, 999), (None, 5000)):
+        check_against_c(streams, since, tail, [])
+    check_against_c(streams, (synth.T0 + 1800, 0), 100, [synth.NEEDLE])
+    check_against_c(streams, None, 3000, synth.c4_literals(1024)[:100])
+    check_against_py(streams[:3], None, 50, match=synth.c5_regexes()[:16])

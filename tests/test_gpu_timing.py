@@ -1,7 +1,9 @@
 """klf_result_timing through the C ABI: which device times a run reports, and that a run
 without dispatch events (KLF_SCAN_EVENTS=0) followed by a stage-times run on the SAME
 engine neither fails nor reports stale times (round-4 review: an event pair a run never
-recorded left a sticky HIP error that the next launch check reported)."""
+recorded left a sticky HIP error that the next launch check reported).  These runs launch
+eagerly (KLF_GRAPH=0): a small batch's graph replay records only the run's bracket [4]
+(test_gpu_parity.py::test_graph_replay)."""
 import numpy as np
 import pytest
 import torch
@@ -25,6 +27,7 @@ def _device_batch(streams):
 
 @pytest.mark.parametrize("grep", [[], [synth.NEEDLE]])
 def test_events_off_then_stage_times_same_engine(gpu, monkeypatch, grep):
+    monkeypatch.setenv("KLF_GRAPH", "0")
     streams = [synth.generate(synth.TEXT, 21, i, 2_000_000) for i in range(3)]
     dev, seg_base, lens = _device_batch(streams)
     since = (synth.T0 + 1800, 0)
@@ -57,6 +60,7 @@ def test_dense_copy_kernel_timed(gpu, monkeypatch):
     dense copy (k_tcopy): timing [7] is its dispatch alone, inside the compaction stage [3];
     on a --tail run (the sparse gather) k_tcopy exits at once.  The one-pass run has no
     k_tcopy."""
+    monkeypatch.setenv("KLF_GRAPH", "0")
     streams = [synth.generate(synth.TEXT, 22, i, 16_000_000) for i in range(4)]
     dev, seg_base, lens = _device_batch(streams)
     with E.Engine(0, hip_stream=torch.cuda.current_stream().cuda_stream) as eng:
