@@ -2231,7 +2231,10 @@ __device__ __forceinline__ void verify_body(RunArgs& a, uint32_t bid, uint32_t n
     }
   }
 }
-__global__ __launch_bounds__(256) void k_verify(RunArgs a) {
+#ifndef KLF_VERIFY_WAVES
+#define KLF_VERIFY_WAVES 1  // k_verify / k_scatter_verify: minimum waves per SIMD (4: <= 128 VGPRs)
+#endif
+__global__ __launch_bounds__(256, KLF_VERIFY_WAVES) void k_verify(RunArgs a) {
   __shared__ VerifyLds L;
   verify_body(a, blockIdx.x, gridDim.x, L);
 }
@@ -2239,7 +2242,7 @@ __global__ __launch_bounds__(256) void k_verify(RunArgs a) {
 // loads per hit) as one launch, blocks [0, nsb) scattering, the rest verifying, so the two
 // overlap on the chip without a second stream (k_verify reads the line slots, not the
 // global line index).
-__global__ __launch_bounds__(256) void k_scatter_verify(RunArgs a, uint32_t nsb) {
+__global__ __launch_bounds__(256, KLF_VERIFY_WAVES) void k_scatter_verify(RunArgs a, uint32_t nsb) {
   __shared__ union {
     ScatterLds s;
     VerifyLds v;
