@@ -1537,6 +1537,9 @@ __device__ __forceinline__ uint32_t tile_hits(const RunArgs& a, const TileStat& 
   return (a.grep_mode == kGrepGeneral && a.pats.qf_on) ? ts.carry_off : 0u;
 }
 
+#ifndef KLF_FLAT_BATCH
+#define KLF_FLAT_BATCH 1  // k_tindex<R, 1>: hits flattened per thread at once (4: C4 71.6 -> 85.5 us, its
+#endif                    // VGPRs past 128 cost the kernel a wave per SIMD, r6v)
 template <int R, int PASS>
 __global__ __launch_bounds__(256) void k_tindex(RunArgs a) {
   __shared__ uint32_t s_wt[4][4];
@@ -1685,32 +1688,50 @@ __global__ __launch_bounds__(256) void k_tindex(RunArgs a) {
   for (uint32_t k = (uint32_t)t; k < 256u * R; k += 256)
     if (t0 + k < a.ntiles) a.tile_base[t0 + k] = blk_lo + s_tbl[k];
   // the block's hit slots, in tile order: hit k -> its thread (prefix search), then tile
+  // (KLF_FLAT_BATCH hits per thread at once: their hit-slot loads in flight together)
   const uint64_t hb = s_base[3];
-  for (uint32_t k = (uint32_t)t; k < blk_h; k += 256) {
-    uint32_t lo = 0, hi = 255;  // the first thread whose inclusive prefix exceeds k
-    while (lo < hi) {
-      const uint32_t mid = (lo + hi) >> 1;
-      if (s_hpre[mid] > k) hi = mid; else lo = mid + 1;
-    }
-    uint32_t j = k - (lo ? s_hpre[lo - 1] : 0u), r = 0;
-    while (j >= s_thit[lo * R + r]) j -= s_thit[lo * R + r++];
-    if (hb + k < a.hflat_cap) {
-      // {tile, its hit's tile offset << 32}: inline hits from the TileStat (L2: this kernel
-      // just read it), the others from the tile's hit slots
-      const uint32_t tile = t0 + lo * R + r;
-      uint32_t off;
-      if (KLF_HIT_INLINE) {
-        const TileStat& tsh = a.tstat[tile];
-        off = (tsh.flags & kTsHitInline) ? ((tsh.pool_base >> (16u * j)) & 0xFFFFu)
-                                         : (uint32_t)a.hslots[(size_t)tile * kHitSlots + j];
-      } else {
-        off = a.hslots[(size_t)tile * kHitSlots + j];
+  constexpr int FB = KLF_FLAT_BATCH;
+  for (uint32_t k0 = (uint32_t)t; k0 < blk_h; k0 += 256u * FB) {
+    uint32_t ftile[FB], fj[FB], fseg[FB], off[FB];
+#pragma unroll
+    for (int u = 0; u < FB; ++u) {
+      const uint32_t k = k0 + 256u * (uint32_t)u;
+      ftile[u] = ~0u;
+      fj[u] = 0;
+      fseg[u] = 0;
+      if (k >= blk_h || hb + k >= a.hflat_cap) continue;
+      uint32_t lo = 0, hi = 255;  // the first thread whose inclusive prefix exceeds k
+      while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (s_hpre[mid] > k) hi = mid; else lo = mid + 1;
       }
+      uint32_t j = k - (lo ? s_hpre[lo - 1] : 0u), r = 0;
+      while (j >= s_thit[lo * R + r]) j -= s_thit[lo * R + r++];
+      ftile[u] = t0 + lo * R + r;
+      fj[u] = j;
       // (+ the tile's stream in bits 48..63 when it fits: k_verify skips its tile_seg load;
       // the owning thread's registers hold it, passed through LDS)
-      const uint32_t hs = s_tseg[lo * R + r];
-      a.hflat[hb + k] = (uint64_t)tile | ((uint64_t)off << 32) | ((uint64_t)(hs < 0xFFFFu ? hs : 0xFFFFu) << 48);
+      fseg[u] = s_tseg[lo * R + r];
     }
+#pragma unroll
+    for (int u = 0; u < FB; ++u) {
+      // {tile, its hit's tile offset << 32}: inline hits from the TileStat (L2: this kernel
+      // just read it), the others from the tile's hit slots
+      off[u] = 0;
+      if (ftile[u] == ~0u) continue;
+      if (KLF_HIT_INLINE) {
+        const TileStat& tsh = a.tstat[ftile[u]];
+        off[u] = (tsh.flags & kTsHitInline) ? ((tsh.pool_base >> (16u * fj[u])) & 0xFFFFu)
+                                            : (uint32_t)a.hslots[(size_t)ftile[u] * kHitSlots + fj[u]];
+      } else {
+        off[u] = a.hslots[(size_t)ftile[u] * kHitSlots + fj[u]];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < FB; ++u)
+      if (ftile[u] != ~0u)
+        a.hflat[hb + k0 + 256u * (uint32_t)u] = (uint64_t)ftile[u] | ((uint64_t)off[u] << 32) |
+                                                 ((uint64_t)(fseg[u] < 0xFFFFu ? fseg[u] : 0xFFFFu) << 48);
   }
   if (t == 0 && (bid + 1) * (256u * R) >= a.ntiles) {  // the last block knows the totals
     // More lines than the line index holds: raised here, before any kernel that indexes
@@ -2232,7 +2253,7 @@ __device__ __forceinline__ void verify_body(RunArgs& a, uint32_t bid, uint32_t n
   }
 }
 #ifndef KLF_VERIFY_WAVES
-#define KLF_VERIFY_WAVES 1  // k_verify / k_scatter_verify: minimum waves per SIMD (4: <= 128 VGPRs)
+#define KLF_VERIFY_WAVES 4  // k_verify / k_scatter_verify: min waves per SIMD (<= 128 VGPRs; 1 -> 129: C4 339 vs 295 us)
 #endif
 __global__ __launch_bounds__(256, KLF_VERIFY_WAVES) void k_verify(RunArgs a) {
   __shared__ VerifyLds L;
