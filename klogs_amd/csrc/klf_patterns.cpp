@@ -631,18 +631,29 @@ struct FactorCtx {
   size_t want = SIZE_MAX;  // shortest string the stride needs
 };
 
-void consider(const FactorCtx& cx, FInfo& f, const std::vector<std::string>& r, bool loose, uint32_t pre) {
-  const size_t a = req_score(r), b = req_score(f.req);
-  if (a == 0) return;
-  auto key = [&](size_t len, uint32_t p, size_t n) {
+// (the analysis runs ~4 times per regex at klf_open: candidate sets are moved, not copied,
+// and a single-string candidate is only materialised when it wins -- allocations were most
+// of the compile's time)
+bool better(const FactorCtx& cx, const FInfo& f, size_t a, uint32_t pre, size_t n) {
+  const size_t b = req_score(f.req);
+  if (a == 0) return false;
+  auto key = [&](size_t len, uint32_t p, size_t k) {
     return std::make_tuple(len >= cx.want ? 1 : 0, (len >= cx.want && p != kUnbounded) ? 1 : 0, len,
-                           -(long)n);
+                           -(long)k);
   };
-  if (b == 0 || key(a, pre, r.size()) > key(b, f.req_pre, f.req.size())) {
-    f.req = r;
-    f.req_loose = loose;
-    f.req_pre = pre;
-  }
+  return b == 0 || key(a, pre, n) > key(b, f.req_pre, f.req.size());
+}
+void consider(const FactorCtx& cx, FInfo& f, std::vector<std::string>&& r, bool loose, uint32_t pre) {
+  if (!better(cx, f, req_score(r), pre, r.size())) return;
+  f.req = std::move(r);
+  f.req_loose = loose;
+  f.req_pre = pre;
+}
+void consider_one(const FactorCtx& cx, FInfo& f, const std::string& run, bool loose, uint32_t pre) {
+  if (!better(cx, f, run.size(), pre, 1)) return;
+  f.req.assign(1, run);
+  f.req_loose = loose;
+  f.req_pre = pre;
 }
 
 std::vector<std::string> req_or_exact(const FInfo& f, bool& loose, uint32_t* pre = nullptr) {
@@ -654,6 +665,19 @@ std::vector<std::string> req_or_exact(const FInfo& f, bool& loose, uint32_t* pre
   loose = f.req_loose;
   if (pre) *pre = f.req_pre;
   return f.req;
+}
+// req_or_exact of a node result no longer needed: its strings moved out
+std::vector<std::string> take_req_or_exact(FInfo&& f, bool& loose, uint32_t* pre = nullptr) {
+  if (f.has_exact) {
+    loose = f.exact_loose;
+    if (pre) *pre = 0;
+    std::vector<std::string> v(1);
+    v[0] = std::move(f.exact);
+    return v;
+  }
+  loose = f.req_loose;
+  if (pre) *pre = f.req_pre;
+  return std::move(f.req);
 }
 
 FInfo factor_of(const FactorCtx& cx, const std::vector<RNode>& pool, int x) {
@@ -686,21 +710,21 @@ FInfo factor_of(const FactorCtx& cx, const std::vector<RNode>& pool, int x) {
       bool run_loose = false, all = true;
       uint32_t off = 0, run_pre = 0;  // offset of the kid (bound), of the current exact run
       for (int k : n.kids) {
-        const FInfo kf = factor_of(cx, pool, k);
-        consider(cx, f, kf.req, kf.req_loose, sat_add(off, kf.req_pre));
+        FInfo kf = factor_of(cx, pool, k);
+        consider(cx, f, std::move(kf.req), kf.req_loose, sat_add(off, kf.req_pre));
         if (kf.has_exact) {
           if (run.empty()) run_pre = off;
           run += kf.exact;
           run_loose |= kf.exact_loose;
         } else {
-          if (!run.empty()) consider(cx, f, {run}, run_loose, run_pre);
+          if (!run.empty()) consider_one(cx, f, run, run_loose, run_pre);
           run.clear();
           run_loose = false;
           all = false;
         }
         off = sat_add(off, kf.maxlen);
       }
-      if (!run.empty()) consider(cx, f, {run}, run_loose, run_pre);
+      if (!run.empty()) consider_one(cx, f, run, run_loose, run_pre);
       if (all) { f.has_exact = true; f.exact = run; f.exact_loose = run_loose; }
       f.maxlen = off;
       return f;
@@ -713,9 +737,9 @@ FInfo factor_of(const FactorCtx& cx, const std::vector<RNode>& pool, int x) {
       for (int k : n.kids) {
         bool l = false;
         uint32_t p = 0;
-        const FInfo kf = factor_of(cx, pool, k);
+        FInfo kf = factor_of(cx, pool, k);
         f.maxlen = std::max(f.maxlen, kf.maxlen);
-        const std::vector<std::string> r = req_or_exact(kf, l, &p);
+        const std::vector<std::string> r = take_req_or_exact(std::move(kf), l, &p);
         if (req_score(r) == 0) { none = true; continue; }  // some branch needs no byte at all
         loose |= l;
         pre = std::max(pre, p);
@@ -726,13 +750,13 @@ FInfo factor_of(const FactorCtx& cx, const std::vector<RNode>& pool, int x) {
       return f;
     }
     case RNode::kPlus: {
-      const FInfo kf = factor_of(cx, pool, n.kids[0]);
-      f.req = req_or_exact(kf, f.req_loose, &f.req_pre);  // the first repetition holds one
+      FInfo kf = factor_of(cx, pool, n.kids[0]);
       f.maxlen = kf.maxlen == 0 ? 0 : kUnbounded;
+      f.req = take_req_or_exact(std::move(kf), f.req_loose, &f.req_pre);  // the first repetition holds one
       return f;
     }
     case RNode::kRepeat: {
-      const FInfo kf = factor_of(cx, pool, n.kids[0]);
+      FInfo kf = factor_of(cx, pool, n.kids[0]);
       f.maxlen = n.hi < 0 ? (kf.maxlen == 0 ? 0 : kUnbounded)
                           : (kf.maxlen == kUnbounded ? kUnbounded : kf.maxlen * (uint32_t)n.hi);
       if (n.lo == 0) return f;
@@ -743,7 +767,7 @@ FInfo factor_of(const FactorCtx& cx, const std::vector<RNode>& pool, int x) {
         else { f.req = {rep}; f.req_loose = kf.exact_loose; f.req_pre = 0; }
         if (rep.empty()) f.req.clear();
       } else {
-        f.req = kf.req;
+        f.req = std::move(kf.req);
         f.req_loose = kf.req_loose;
         f.req_pre = kf.req_pre;
       }
@@ -990,6 +1014,14 @@ bool compile_set(const std::vector<std::vector<uint8_t>>& pats, const std::vecto
     uint32_t pre = kRxPreUnbounded;
   };
   std::vector<RxOut> rxo(pats.size());
+  // KLF_DIAG: the compile's phases (klf_open's "pattern compile" mark is their sum)
+  static const bool cdiag = getenv("KLF_DIAG") != nullptr;
+  const auto ct0 = std::chrono::steady_clock::now();
+  auto cmark = [&](const char* what) {
+    if (cdiag)
+      fprintf(stderr, "[klf] compile: %s at %.1f us\n", what,
+              std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - ct0).count());
+  };
   auto compile_rx = [&](size_t k) {
     RxOut& o = rxo[k];
     // parsed once: the factor analyses read the tree, the Glushkov build rewrites a copy
@@ -1061,6 +1093,7 @@ bool compile_set(const std::vector<std::vector<uint8_t>>& pats, const std::vecto
     err_code = KLF_ETOOBIG;
     return false;
   }
+  cmark("regexes parsed");
   // Second pass: two factor choices per regex for the layout to pick from (place_needles,
   // with the data's statistics at the first batch).  [0]: the sampling stride follows the
   // shortest needle of the first pass; keep it, and per regex prefer factor sets with a
@@ -1105,6 +1138,7 @@ bool compile_set(const std::vector<std::vector<uint8_t>>& pats, const std::vecto
     }
   }
   out.rx_pre = pre_v[0];
+  cmark("factor choices");
   // dedupe literals
   std::sort(lits.begin(), lits.end());
   lits.erase(std::unique(lits.begin(), lits.end()), lits.end());
@@ -1167,6 +1201,7 @@ bool compile_set(const std::vector<std::vector<uint8_t>>& pats, const std::vecto
   }
 
   // ---- regexes: shared byte classes by partition refinement ----
+  cmark("automaton");
   out.rx_count = (uint32_t)rxs.size();
   if (!rxs.empty()) {
     // a byte's signature = the positions (per regex) whose set holds it; equal signatures
@@ -1202,7 +1237,9 @@ bool compile_set(const std::vector<std::vector<uint8_t>>& pats, const std::vecto
       out.rx_flags.push_back((rxs[r].accept_at_start ? 1u : 0u) | (rxs[r].accept_empty ? 2u : 0u));
     }
   }
+  cmark("byte classes");
   build_prefilter(lits, fac_v, loose_v, pre_v, out, place);
+  cmark("prefilter");
   return true;
 }
 
