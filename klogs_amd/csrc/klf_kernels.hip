@@ -1540,8 +1540,11 @@ __device__ __forceinline__ uint32_t tile_hits(const RunArgs& a, const TileStat& 
 #ifndef KLF_FLAT_BATCH
 #define KLF_FLAT_BATCH 1  // k_tindex<R, 1>: hits flattened per thread at once (4: C4 71.6 -> 85.5 us, its
 #endif                    // VGPRs past 128 cost the kernel a wave per SIMD, r6v)
+#ifndef KLF_TINDEX_WAVES
+#define KLF_TINDEX_WAVES 4  // k_tindex: min waves per SIMD (<16, 1>: 130 -> 128 VGPRs, C4 75 -> 63 us, C5 38 -> 30, r6y)
+#endif
 template <int R, int PASS>
-__global__ __launch_bounds__(256) void k_tindex(RunArgs a) {
+__global__ __launch_bounds__(256, KLF_TINDEX_WAVES) void k_tindex(RunArgs a) {
   __shared__ uint32_t s_wt[4][4];
   __shared__ uint64_t s_w64[4][4];
   __shared__ uint64_t s_base[4];
