@@ -717,6 +717,8 @@ def committed(cfg: str, scan_ms: float):
            "rocprof_source": str(sm.relative_to(ROOT)), "rocprof_steady_ms": round(s["steady_us"] / 1e3, 4),
            "rocprof_vs_this_run": round(rel, 4), "rocprof_match_3pct": bool(rel <= 0.03)}
     tr = sm.parent / "traffic.json"
+    if not tr.exists():  # (a trace-only profile of another board: the round's counter passes, same build)
+        tr = ROOT / "profiles" / rounds[0] / "traffic.json"
     if tr.exists():
         t = json.loads(tr.read_text()).get(cfg)
         if t:
