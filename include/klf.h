@@ -112,6 +112,11 @@ typedef struct klf_filter {
 /* klf_filter.flags: write every line's u64 offset inside the run (KLF_INDEX_FULL), also where
  * the run needs only part of the index (see klf_result_index_mode). */
 #define KLF_FILTER_FULL_INDEX 4u
+/* klf_filter.flags: record no timing events (klf_result_timing then reports zeros; it
+ * overrides KLF_FILTER_STAGE_TIMES).  The k_scan dispatch's own events and the run's
+ * bracket cost a few microseconds of device time per run (C1: ~5 of ~75 us), which a
+ * caller that never reads the timing need not pay. */
+#define KLF_FILTER_NO_TIMING 8u
 
 /* klf_result_index_mode: how much of the u64 line index the run wrote itself. */
 #define KLF_INDEX_FULL 0       /* every line of every stream                                  */

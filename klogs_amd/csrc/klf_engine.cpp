@@ -1295,6 +1295,8 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
   e->index_pending.clear();
   // lazy line index (grep none, --tail -1; KLF_LAZY_INDEX=0 turns it off)
   const bool full_index = (f->flags & KLF_FILTER_FULL_INDEX) != 0;
+  // KLF_FILTER_NO_TIMING: no event in the launch sequence (launch_pipeline records none)
+  hipEvent_t* const evs = (f->flags & KLF_FILTER_NO_TIMING) ? nullptr : e->ev;
   const bool lazy_index = mode == klf::CompiledSet::kNone && f->tail < 0 && !full_index &&
                           !(getenv("KLF_LAZY_INDEX") && !strcmp(getenv("KLF_LAZY_INDEX"), "0"));
   // (a run that needs every line's index -- k_match's fallback -- turns it off)
@@ -1431,7 +1433,7 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
     a.wgrp = a.wpre + nsegs + 1;
     a.out = e->d_out.as<uint8_t>();
     a.out_cap = e->d_out.p ? e->d_out.cap : 0;
-    a.stage_times = (f->flags & KLF_FILTER_STAGE_TIMES) ? 1u : 0u;
+    a.stage_times = (f->flags & KLF_FILTER_STAGE_TIMES) && evs ? 1u : 0u;
     a.cand = need_cand ? e->d_cand.as<uint64_t>() : nullptr;
     a.cand_cap = need_cand ? e->cand_cap : 0;
     a.qhits = need_hits ? e->d_qhits.as<uint64_t>() : nullptr;
@@ -1552,7 +1554,7 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
     if (two_phase) {
       if (const int rc = join_ac(); rc != KLF_OK) return rc;
       a.cap_lines = 1ull << 40;  // phase 1 indexes no line array (k_tindex: no overflow, no bitmap)
-      HIPCHK(e, klf::launch_pipeline(a, st, e->ev, e->num_cus, 1, &ev_mask), "launch");
+      HIPCHK(e, klf::launch_pipeline(a, st, evs, e->num_cus, 1, &ev_mask), "launch");
       uint8_t* rb1 = e->h_rb.as<uint8_t>();
       HIPCHK(e, hipMemcpyAsync(rb1, e->d_counters.p, kCtrBytes + nsegs * sizeof(SegOut), hipMemcpyDeviceToHost, st),
              "D2H counters + records");
@@ -1581,20 +1583,20 @@ static int run_device_impl(klf_engine* e, const uint8_t* d_bytes, uint32_t n_str
       mark("line arrays");
       if (a.grep_mode != klf::CompiledSet::kNone)  // (phase 1's k_tindex zeroes it otherwise)
         HIPCHK(e, hipMemsetAsync(a.bits, 0, (cap / 32 + 1) * 4, st), "zero bits");
-      HIPCHK(e, klf::launch_pipeline(a, st, e->ev, e->num_cus, 2, &ev_mask), "launch");
+      HIPCHK(e, klf::launch_pipeline(a, st, evs, e->num_cus, 2, &ev_mask), "launch");
       mark("phase 2 launched");
     } else if (e->ac_pending) {  // joined while the scan runs
       HIPCHK(e, alloc_lines(a, cap), "alloc line arrays");
-      HIPCHK(e, klf::launch_pipeline(a, st, e->ev, e->num_cus, 3, &ev_mask), "launch");
+      HIPCHK(e, klf::launch_pipeline(a, st, evs, e->num_cus, 3, &ev_mask), "launch");
       if (const int rc = join_ac(); rc != KLF_OK) return rc;
-      HIPCHK(e, klf::launch_pipeline(a, st, e->ev, e->num_cus, 4, &ev_mask), "launch");
+      HIPCHK(e, klf::launch_pipeline(a, st, evs, e->num_cus, 4, &ev_mask), "launch");
     } else {
       HIPCHK(e, alloc_lines(a, cap), "alloc line arrays");
       mark("line arrays");
       // KLF_GRAPH=1: a small batch (KLF_GRAPH_MAX_MB, default 256) replays a graph
       const bool graph = !e->graph_off && !a.stage_times && total_bytes <= graph_max && graph_on;
       if (!(graph && launch_graph(e, a, ev_mask)))
-        HIPCHK(e, klf::launch_pipeline(a, st, e->ev, e->num_cus, 0, &ev_mask), "launch");
+        HIPCHK(e, klf::launch_pipeline(a, st, evs, e->num_cus, 0, &ev_mask), "launch");
     }
     mark("launched");
     uint8_t* rb = e->h_rb.as<uint8_t>();

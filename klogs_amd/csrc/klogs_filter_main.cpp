@@ -103,6 +103,7 @@ int main(int argc, char** argv) {
   int rejected = 0;
   char err[512] = {0};
   if (klh_lop_opts(since.c_str(), tail, now, &filter, &rejected, err, sizeof(err)) != KLH_OK) panic_exit(err);
+  filter.flags |= KLF_FILTER_NO_TIMING;  // (the CLI reads no device timing)
 
   // the pod selection, grouped by pod in first-appearance order
   std::vector<PodEnt> pods;

@@ -174,18 +174,19 @@ def _patterns(grep: Sequence[bytes], match: Sequence[bytes]):
 KLF_FILTER_STAGE_TIMES = 1
 KLF_FILTER_PATTERN_COUNTS = 2
 KLF_FILTER_FULL_INDEX = 4
+KLF_FILTER_NO_TIMING = 8
 INDEX_MODES = {0: "full", 1: "windowed", 2: "on_demand"}  # klf_result_index_mode
 COMPACTIONS = {0: "gather", 1: "tiles", 2: "one_pass"}  # klf_result_compaction
 
 
 def _filter(since: Optional[Tuple[int, int]], tail: int, stage_times: bool = False,
-            pattern_counts: bool = False, full_index: bool = False) -> _Filter:
+            pattern_counts: bool = False, full_index: bool = False, timing: bool = True) -> _Filter:
     f = _Filter()
     s = GO_ZERO_TIME if since is None else since
     f.since.sec, f.since.nsec = int(s[0]), int(s[1])
     f.tail = int(tail)
     f.flags = ((KLF_FILTER_STAGE_TIMES if stage_times else 0) | (KLF_FILTER_PATTERN_COUNTS if pattern_counts else 0)
-               | (KLF_FILTER_FULL_INDEX if full_index else 0))
+               | (KLF_FILTER_FULL_INDEX if full_index else 0) | (0 if timing else KLF_FILTER_NO_TIMING))
     return f
 
 
@@ -446,19 +447,19 @@ class Engine:
         _check(_lib.klf_reset(self._h), self._h)
 
     def run(self, since=None, tail: int = -1, n_streams: Optional[int] = None, stage_times: bool = False,
-            pattern_counts: bool = False, full_index: bool = False) -> Result:
-        f = _filter(since, tail, stage_times, pattern_counts, full_index)
+            pattern_counts: bool = False, full_index: bool = False, timing: bool = True) -> Result:
+        f = _filter(since, tail, stage_times, pattern_counts, full_index, timing)
         r = C.c_void_p()
         _check(_lib.klf_run(self._h, C.byref(f), C.byref(r)), self._h)
         return Result(r.value or 0, n_streams if n_streams is not None else 0, self)
 
     def run_device(self, d_ptr: int, seg_base: Sequence[int], lens: Sequence[int], since=None,
                    tail: int = -1, stage_times: bool = False, pattern_counts: bool = False,
-                   full_index: bool = False) -> Result:
+                   full_index: bool = False, timing: bool = True) -> Result:
         n = len(lens)
         B = (C.c_uint64 * max(1, n))(*[int(x) for x in seg_base])
         L = (C.c_uint64 * max(1, n))(*[int(x) for x in lens])
-        f = _filter(since, tail, stage_times, pattern_counts, full_index)
+        f = _filter(since, tail, stage_times, pattern_counts, full_index, timing)
         r = C.c_void_p()
         _check(_lib.klf_run_device(self._h, C.c_void_p(d_ptr), n, B, L, C.byref(f), C.byref(r)), self._h)
         return Result(r.value or 0, n, self)

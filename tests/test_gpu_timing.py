@@ -79,3 +79,25 @@ def test_dense_copy_kernel_timed(gpu, monkeypatch):
         r = eng.run_device(dev.data_ptr(), seg_base, lens, tail=10)
         assert r.timing()[7] < dense_ms, (r.timing(), dense_ms)
         r.free()
+
+
+def test_no_timing_flag(gpu, monkeypatch):
+    """KLF_FILTER_NO_TIMING: the run records no event (timing all zeros, even with stage
+    times asked for) and its output is the same; the next default run times again."""
+    monkeypatch.setenv("KLF_GRAPH", "0")
+    streams = [synth.generate(synth.TEXT, 23, i, 2_000_000) for i in range(2)]
+    dev, seg_base, lens = _device_batch(streams)
+    since = (synth.T0 + 1800, 0)
+    for grep in ([], [synth.NEEDLE]):
+        want = [co.filter_stream(s, since, 50, grep, want_lines=False, want_bits=False)[0] for s in streams]
+        with E.Engine(0, grep=grep, hip_stream=torch.cuda.current_stream().cuda_stream) as eng:
+            for stage in (False, True):
+                r = eng.run_device(dev.data_ptr(), seg_base, lens, since=since, tail=50, stage_times=stage, timing=False)
+                assert r.timing() == [0.0] * 8, r.timing()
+                assert [r.stream(i).out for i in range(2)] == want
+                r.free()
+            r = eng.run_device(dev.data_ptr(), seg_base, lens, since=since, tail=50)
+            tm = r.timing()
+            assert tm[4] > 0.0 and tm[6] > 0.0, tm
+            assert [r.stream(i).out for i in range(2)] == want
+            r.free()
